@@ -1,0 +1,361 @@
+// Boundary codec kernels: importance-ranked token selection and the
+// quantize/pack / unpack/dequantize of the hidden state that crosses a pipeline-stage boundary.
+//
+// Wire message (offsets computed on the host, codec/wire.py, every section 16-byte aligned):
+//   [header 32 B][class bitmask B x MW u32][scales][hi-class rows][lo-class rows]
+// A token whose bit is set belongs to the low-precision ("lo") class.  Rows of each class are stored in
+// token order; a row's slot is the popcount of the mask bits before it, so the receiver needs nothing
+// but the mask.  Row formats: 0 bf16, 1 int8, 2 int4 (two's-complement nibbles, even element in the low
+// nibble), 3 int2 (ternary, 4 per byte).  Scale modes: 0 per token (fp32 [B*S]), 1 per window for the
+// lo class (fp32 [B], reference Q1 "one global max-abs" int4), 2 per channel (fp32 [B*H]; reference
+// channel_8/4/1_max store max|x_c|, channel_1_mean stores mean_c + 1e-8).
+#include "common.h"
+
+enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3 };
+enum { SC_TOKEN = 0, SC_WINDOW = 1, SC_CHANNEL = 2 };
+enum { CH_MAXABS = 0, CH_MEAN = 1 };
+
+struct CodecArgs {
+  bf16_t* x; uint8_t* msg;
+  long long off_mask, off_scale, off_hi, off_lo;
+  int B, S, H, k, mw;           // mw: mask words per window
+  int hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo, ch_kind;
+};
+
+__device__ __forceinline__ int fmt_row_bytes(int fmt, int H) {
+  return fmt == FMT_BF16 ? 2 * H : fmt == FMT_INT8 ? H : fmt == FMT_INT4 ? H / 2 : H / 4;
+}
+
+__device__ __forceinline__ int wave_isum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// number of lo-class tokens before token j in window b, and the class of j
+__device__ __forceinline__ int lo_prefix(const uint32_t* __restrict__ mask, int mw, int j, bool& is_lo) {
+  const int lane = threadIdx.x & 63;
+  const int wj = j >> 5;
+  int cnt = 0;
+  for (int w = lane; w < wj; w += 64) cnt += __popc(mask[w]);
+  cnt = wave_isum(cnt);
+  const uint32_t word = mask[wj];
+  is_lo = (word >> (j & 31)) & 1u;
+  return cnt + __popc(word & ((1u << (j & 31)) - 1u));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Rank tokens by importance (ascending, ties by index) and mark the k least important as lo.
+__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ imp, int S, int k, int mw,
+                                                     uint32_t* __restrict__ mask_out, int mask_stride,
+                                                     int* __restrict__ rank_out) {
+  extern __shared__ float v[];
+  const int b = blockIdx.x;
+  const float* ib = imp + (size_t)b * S;
+  for (int j = threadIdx.x; j < S; j += 256) v[j] = ib[j];
+  __syncthreads();
+  uint32_t* mb = mask_out + (size_t)b * mask_stride;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int base = 0; base < mw * 32; base += 256) {
+    const int j = base + threadIdx.x;
+    bool lo = false;
+    if (j < S) {
+      const float vj = v[j];
+      int r = 0;
+      for (int i = 0; i < S; ++i) {
+        const float vi = v[i];
+        r += (vi < vj) || (vi == vj && i < j);
+      }
+      if (rank_out) rank_out[(size_t)b * S + j] = r;
+      lo = r < k;
+    }
+    const unsigned long long bal = __ballot(lo);
+    const int w0 = (base + wave * 64) >> 5;
+    if (lane == 0 && w0 < mw) mb[w0] = (uint32_t)bal;
+    if (lane == 1 && w0 + 1 < mw) mb[w0 + 1] = (uint32_t)(bal >> 32);
+  }
+}
+
+// Per-(window, channel) statistics over the window's rows (optionally only lo-class rows).
+// mode 0: max|x|, mode 1: mean(x) + 1e-8.   grid (B, ceil(H/64)), 256 threads = 4 row groups x 64 ch.
+__global__ __launch_bounds__(256) void channel_stats_kernel(const bf16_t* __restrict__ x,
+                                                            const uint32_t* __restrict__ mask, int mask_stride,
+                                                            float* __restrict__ out, int S, int H, int mode,
+                                                            int only_lo) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  const uint32_t* mb = mask + (size_t)b * mask_stride;
+  float acc = 0.f;
+  if (c < H) {
+    for (int j = rg; j < S; j += 4) {
+      if (only_lo && !((mb[j >> 5] >> (j & 31)) & 1u)) continue;
+      const float xv = bf2f(x[((size_t)b * S + j) * H + c]);
+      acc = mode == 0 ? fmaxf(acc, fabsf(xv)) : acc + xv;
+    }
+  }
+  red[rg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rg == 0 && c < H) {
+    const int l = threadIdx.x;
+    float r = mode == 0 ? fmaxf(fmaxf(red[0][l], red[1][l]), fmaxf(red[2][l], red[3][l]))
+                        : (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    out[(size_t)b * H + c] = mode == 0 ? r : r / (float)S + 1e-8f;
+  }
+}
+
+__global__ __launch_bounds__(256) void rowmax_kernel(const float* __restrict__ in, float* __restrict__ out, int H) {
+  __shared__ float red[4];
+  const float* r = in + (size_t)blockIdx.x * H;
+  float m = 0.f;
+  for (int c = threadIdx.x; c < H; c += 256) m = fmaxf(m, r[c]);
+  m = block_max<256>(m, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = m;
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int NCH>
+__device__ __forceinline__ void load_row8(const bf16_t* __restrict__ src, int H, float (&v)[NCH][8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < H) {
+      const u32x4_t w = *(const u32x4_t*)(src + col);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[c][2 * e] = bf_lo(w[e]); v[c][2 * e + 1] = bf_hi(w[e]); }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ float qround(float t, float qmax, float qmin) { return fminf(fmaxf(rintf(t), qmin), qmax); }
+
+template <int NCH>
+__global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.B * a.S) return;
+  const int lane = threadIdx.x & 63;
+  const int b = row / a.S, j = row - b * a.S;
+  const uint32_t* mask = (const uint32_t*)(a.msg + a.off_mask) + (size_t)b * a.mw;
+  bool is_lo;
+  const int slot_lo = lo_prefix(mask, a.mw, j, is_lo);
+  const int fmt = is_lo ? a.lo_fmt : a.hi_fmt;
+  const int qmax = is_lo ? a.qmax_lo : a.qmax_hi;
+  const int rb = fmt_row_bytes(fmt, a.H);
+  uint8_t* dst = is_lo ? a.msg + a.off_lo + ((size_t)b * a.k + slot_lo) * rb
+                       : a.msg + a.off_hi + ((size_t)b * (a.S - a.k) + (j - slot_lo)) * rb;
+  float v[NCH][8];
+  load_row8<NCH>(a.x + (size_t)row * a.H, a.H, v);
+  float* scales = (float*)(a.msg + a.off_scale);
+
+  // scale / quantiser for this row
+  float inv = 0.f, mul = 0.f;  // code = round(x * inv) for token & channel; window mode uses ref formula
+  if (fmt == FMT_BF16 && a.scale_mode == SC_TOKEN && lane == 0) scales[row] = 0.f;
+  if (fmt != FMT_BF16) {
+    if (a.scale_mode == SC_TOKEN) {
+      float am = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[c][e]));
+      am = wave_max(am);
+      const float s = am / (float)qmax;
+      if (lane == 0) scales[row] = s;
+      inv = am > 0.f ? 1.f / s : 0.f;
+    } else if (a.scale_mode == SC_WINDOW) {
+      mul = scales[b];  // max|x| over the window's lo rows
+    }
+  }
+  const float qmaxf = (float)qmax;
+  const float qminf = a.scale_mode == SC_WINDOW ? -(float)(qmax + 1) : -(float)qmax;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col >= a.H) continue;
+    int q[8];
+    if (fmt == FMT_BF16) {
+      u32x4_t w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = pack_bf2(v[c][2 * e], v[c][2 * e + 1]);
+      *(u32x4_t*)(dst + col * 2) = w;
+      continue;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xv = v[c][e];
+      float t;
+      if (a.scale_mode == SC_TOKEN) {
+        t = qround(xv * inv, qmaxf, qminf);
+      } else if (a.scale_mode == SC_WINDOW) {
+        // reference Q1: round(clamp(x / m * 7, -8, 7))
+        t = mul > 0.f ? rintf(fminf(fmaxf(xv / mul * qmaxf, qminf), qmaxf)) : 0.f;
+      } else {
+        const float sc = scales[(size_t)b * a.H + col + e];
+        if (a.ch_kind == CH_MEAN || qmax == 1) {
+          t = sc != 0.f ? fminf(fmaxf(rintf(xv / sc), -1.f), 1.f) : 0.f;       // ternary (reference clamps)
+        } else {
+          t = sc > 0.f ? rintf(xv / sc * qmaxf) : 0.f;                         // reference: no clamp
+        }
+      }
+      q[e] = (int)t;
+    }
+    if (fmt == FMT_INT8) {
+      u32x2_t w;
+      w[0] = (q[0] & 255) | ((q[1] & 255) << 8) | ((q[2] & 255) << 16) | ((uint32_t)(q[3] & 255) << 24);
+      w[1] = (q[4] & 255) | ((q[5] & 255) << 8) | ((q[6] & 255) << 16) | ((uint32_t)(q[7] & 255) << 24);
+      *(u32x2_t*)(dst + col) = w;
+    } else if (fmt == FMT_INT4) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w |= (uint32_t)(q[e] & 15) << (4 * e);
+      *(uint32_t*)(dst + col / 2) = w;
+    } else {
+      uint32_t w = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w |= (uint32_t)(q[e] & 3) << (2 * e);
+      *(uint16_t*)(dst + col / 4) = (uint16_t)w;
+    }
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.B * a.S) return;
+  const int lane = threadIdx.x & 63;
+  const int b = row / a.S, j = row - b * a.S;
+  const uint32_t* mask = (const uint32_t*)(a.msg + a.off_mask) + (size_t)b * a.mw;
+  bool is_lo;
+  const int slot_lo = lo_prefix(mask, a.mw, j, is_lo);
+  const int fmt = is_lo ? a.lo_fmt : a.hi_fmt;
+  const int qmax = is_lo ? a.qmax_lo : a.qmax_hi;
+  const int rb = fmt_row_bytes(fmt, a.H);
+  const uint8_t* src = is_lo ? a.msg + a.off_lo + ((size_t)b * a.k + slot_lo) * rb
+                             : a.msg + a.off_hi + ((size_t)b * (a.S - a.k) + (j - slot_lo)) * rb;
+  const float* scales = (const float*)(a.msg + a.off_scale);
+  float s = 0.f;
+  if (fmt != FMT_BF16) {
+    if (a.scale_mode == SC_TOKEN) s = scales[row];
+    else if (a.scale_mode == SC_WINDOW) s = scales[b];
+  }
+  bf16_t* out = a.x + (size_t)row * a.H;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col >= a.H) continue;
+    if (fmt == FMT_BF16) {
+      *(u32x4_t*)(out + col) = *(const u32x4_t*)(src + col * 2);
+      continue;
+    }
+    int q[8];
+    if (fmt == FMT_INT8) {
+      const u32x2_t w = *(const u32x2_t*)(src + col);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        q[e] = (int)(int8_t)((w[0] >> (8 * e)) & 255);
+        q[4 + e] = (int)(int8_t)((w[1] >> (8 * e)) & 255);
+      }
+    } else if (fmt == FMT_INT4) {
+      const uint32_t w = *(const uint32_t*)(src + col / 2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = ((int)(w << (28 - 4 * e))) >> 28;
+    } else {
+      const uint32_t w = *(const uint16_t*)(src + col / 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = ((int)(w << (30 - 2 * e))) >> 30;
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float qf = (float)q[e];
+      if (a.scale_mode == SC_TOKEN) o[e] = qf * s;
+      else if (a.scale_mode == SC_WINDOW) o[e] = qf / (float)qmax * s;            // reference: q / 7 * m
+      else {
+        const float sc = scales[(size_t)b * a.H + col + e];
+        o[e] = (a.ch_kind == CH_MEAN || qmax == 1) ? qf * sc : qf * sc / (float)qmax;
+      }
+    }
+    u32x4_t w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = pack_bf2(o[2 * e], o[2 * e + 1]);
+    *(u32x4_t*)(out + col) = w;
+  }
+}
+
+#define DISPATCH_NCH(H, ...)                                          \
+  do {                                                                \
+    const int _nch = ((H) / 8 + 63) / 64;                             \
+    if (_nch <= 1) { constexpr int NCH = 1; __VA_ARGS__; }            \
+    else if (_nch <= 2) { constexpr int NCH = 2; __VA_ARGS__; }       \
+    else if (_nch <= 4) { constexpr int NCH = 4; __VA_ARGS__; }       \
+    else if (_nch <= 8) { constexpr int NCH = 8; __VA_ARGS__; }       \
+    else return (int)hipErrorInvalidValue;                            \
+  } while (0)
+
+static CodecArgs make_args(void* x, void* msg, long long om, long long os, long long oh, long long ol, int B, int S,
+                           int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo,
+                           int ch_kind) {
+  CodecArgs a;
+  a.x = (bf16_t*)x; a.msg = (uint8_t*)msg;
+  a.off_mask = om; a.off_scale = os; a.off_hi = oh; a.off_lo = ol;
+  a.B = B; a.S = S; a.H = H; a.k = k; a.mw = ((S + 63) / 64) * 2;
+  a.hi_fmt = hi_fmt; a.lo_fmt = lo_fmt; a.scale_mode = scale_mode; a.qmax_hi = qmax_hi; a.qmax_lo = qmax_lo;
+  a.ch_kind = ch_kind;
+  return a;
+}
+
+EDGE_API int edge_select(const float* imp, int B, int S, int k, void* msg, long long off_mask, int* rank_out,
+                         hipStream_t st) {
+  if (B <= 0) return 0;
+  const int mw = ((S + 63) / 64) * 2;
+  hipLaunchKernelGGL(select_kernel, dim3(B), dim3(256), S * sizeof(float), st, imp, S, k, mw,
+                     (uint32_t*)((uint8_t*)msg + off_mask), mw, rank_out);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_set_mask(void* msg, long long off_mask, int B, int S, int all_lo, hipStream_t st) {
+  const int mw = ((S + 63) / 64) * 2;
+  return (int)hipMemsetAsync((uint8_t*)msg + off_mask, all_lo ? 0xff : 0, (size_t)B * mw * 4, st);
+}
+
+// channel_stats: mode 0 max|x|, 1 mean+1e-8; only_lo restricts to lo-class rows.  out: [B, H] fp32
+EDGE_API int edge_channel_stats(const void* x, const void* msg, long long off_mask, float* out, int B, int S, int H,
+                                int mode, int only_lo, hipStream_t st) {
+  if (B <= 0) return 0;
+  const int mw = ((S + 63) / 64) * 2;
+  hipLaunchKernelGGL(channel_stats_kernel, dim3(B, (H + 63) / 64), dim3(256), 0, st, (const bf16_t*)x,
+                     (const uint32_t*)((const uint8_t*)msg + off_mask), mw, out, S, H, mode, only_lo);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_rowmax(const float* in, float* out, int R, int H, hipStream_t st) {
+  if (R <= 0) return 0;
+  rowmax_kernel<<<R, 256, 0, st>>>(in, out, H);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_pack(const void* x, void* msg, long long om, long long os, long long oh, long long ol, int B, int S,
+                       int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo, int ch_kind,
+                       hipStream_t st) {
+  if (H % 32) return (int)hipErrorInvalidValue;
+  CodecArgs a = make_args((void*)x, msg, om, os, oh, ol, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
+                          ch_kind);
+  const int rows = B * S;
+  if (rows <= 0) return 0;
+  DISPATCH_NCH(H, hipLaunchKernelGGL(pack_kernel<NCH>, dim3((rows + 3) / 4), dim3(256), 0, st, a));
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_unpack(void* x, const void* msg, long long om, long long os, long long oh, long long ol, int B,
+                         int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo,
+                         int ch_kind, hipStream_t st) {
+  if (H % 32) return (int)hipErrorInvalidValue;
+  CodecArgs a = make_args(x, (void*)msg, om, os, oh, ol, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
+                          ch_kind);
+  const int rows = B * S;
+  if (rows <= 0) return 0;
+  DISPATCH_NCH(H, hipLaunchKernelGGL(unpack_kernel<NCH>, dim3((rows + 3) / 4), dim3(256), 0, st, a));
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,379 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues: C[M,N] = epilogue(A[M,K] . B[N,K]^T).
+//
+// Both operands are K-contiguous (activations [T,K], nn.Linear weights [N,K]).  128x128 block tile,
+// BK = 64, 4 waves (2x2), each wave a 64x64 sub-tile of 4x4 v_mfma_f32_16x16x32_bf16 accumulators.
+// Tiles are staged global->LDS with 16-byte global_load_lds (LDS image lane-linear, the XOR swizzle is
+// applied to the per-lane SOURCE address and to the ds_read_b128 address), double-buffered.
+// The MFMA is issued "swapped" (weights as the A operand) so every lane owns 4 consecutive output
+// columns of one row: epilogues are lane-local and stores are 8-byte vectors.
+//
+// Epilogues:
+//   NONE, BIAS, RESID (+residual, may alias C), BIAS_RESID, BIAS_GELU, SWIGLU (gate/up interleaved in
+//   16-row blocks -> silu(g)*u, output N/2 columns), QKV_ROPE (bias + RoPE + head-major q/k + V^T
+//   scatter + q pre-scale: replaces three reference ops), LSE (LM head: per-row partial max/sum-exp and
+//   target logit, logits are never written to memory).
+#include "common.h"
+
+enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_GELU = 4, EPI_SWIGLU = 5,
+       EPI_QKV_ROPE = 6, EPI_LSE = 7 };
+
+struct GemmArgs {
+  const bf16_t* A; const bf16_t* B; bf16_t* C;
+  int M, N, K, lda, ldb, ldc;
+  const bf16_t* bias; const bf16_t* resid; int ldr;
+  // QKV_ROPE
+  bf16_t* qout; bf16_t* kout; bf16_t* vtout;
+  const float* cosT; const float* sinT;
+  int S, Hq, Hkv, s_pad; float q_scale;
+  // LSE
+  const int64_t* targets; float* part_max; float* part_sum; float* tgt_logit; int nparts;
+};
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_BYTES = BM * BK * 2;          // 16 KiB per operand per stage
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;      // A + B
+constexpr int GROUP_M = 8;
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int ld, int row0, int row_max, int k0,
+                                           char* lds, int wave, int lane) {
+  // 16 wave-instructions cover the 128x64 tile (8 rows x 128 B each); this wave issues 4 of them.
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = i * 4 + wave;
+    const int r = blk * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz(r);
+    int gr = row0 + r;
+    gr = gr < row_max ? gr : row_max - 1;
+    glds16(src + (size_t)gr * ld + k0 + c * 8, lds + blk * 1024);
+  }
+}
+
+__device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
+  return *(const bf16x8_t*)(lds + r * 128 + ((c ^ swz(r)) << 4));
+}
+
+template <int EPI, int RH = 0>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- tile scheduling: XCD remap, then grouped-M order ---------------------------------------
+  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
+  const int nwg = tm * tn;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int group = id / (GROUP_M * tn);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tm - first_m, GROUP_M);
+  const int in_g = id - group * GROUP_M * tn;
+  const int tile_m = first_m + in_g % gsz;
+  const int tile_n = in_g / gsz;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / BK;
+  stage_tile(a.A, a.lda, m0, a.M, 0, smem, wave, lane);
+  stage_tile(a.B, a.ldb, n0, a.N, 0, smem + TILE_BYTES, wave, lane);
+  wait_vmcnt0();
+  __syncthreads();
+
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) {
+      char* nxt = smem + ((t + 1) & 1) * STAGE_BYTES;
+      stage_tile(a.A, a.lda, m0, a.M, (t + 1) * BK, nxt, wave, lane);
+      stage_tile(a.B, a.ldb, n0, a.N, (t + 1) * BK, nxt + TILE_BYTES, wave, lane);
+    }
+    const char* la = cur;
+    const char* lb = cur + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[4], bfr[4];
+      const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag(la, wm * 64 + i * 16 + (lane & 15), c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag(lb, wn * 64 + j * 16 + (lane & 15), c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  // ---- epilogue -------------------------------------------------------------------------------
+  const int g = lane >> 4;
+  const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
+
+  if constexpr (EPI == EPI_LSE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[i][j][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) se += __expf(acc[i][j][r] - mx);
+      se += __shfl_xor(se, 16, 64);
+      se += __shfl_xor(se, 32, 64);
+      if (m < a.M) {
+        if (g == 0) {
+          a.part_max[(size_t)m * a.nparts + nw / 64] = mx;
+          a.part_sum[(size_t)m * a.nparts + nw / 64] = se;
+        }
+        const int64_t tg = a.targets[m];
+        const int64_t off = tg - nw;
+        if (off >= 0 && off < 64) {
+          const int j = (int)(off >> 4), rr = (int)(off & 3), gg = (int)((off >> 2) & 3);
+          if (gg == g) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (jj == j && r == rr) a.tgt_logit[m] = acc[i][jj][r];
+          }
+        }
+      }
+    }
+    return;
+  }
+
+  if constexpr (EPI == EPI_QKV_ROPE) {
+    const int head = nw / 64;  // global head slot in [q heads | k heads | v heads]
+    const bool is_v = head >= a.Hq + a.Hkv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      const int mm = m < a.M ? m : a.M - 1;
+      const int b = mm / a.S, pos = mm - b * a.S;
+      float v[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nw + j * 16 + g * 4;
+        const u32x2_t bw = *(const u32x2_t*)(a.bias + n);
+        v[j][0] = acc[i][j][0] + bf_lo(bw[0]);
+        v[j][1] = acc[i][j][1] + bf_hi(bw[0]);
+        v[j][2] = acc[i][j][2] + bf_lo(bw[1]);
+        v[j][3] = acc[i][j][3] + bf_hi(bw[1]);
+      }
+      if constexpr (RH >= 16) {
+        // rotate_half partner of column d is d +- RH: register j +- RH/16, same lane.
+        constexpr int DJ = RH / 16;
+        if (!is_v) {
+          float o[4][4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (j * 16 >= 2 * RH) { o[j][r] = v[j][r]; continue; }
+              const bool lo = j * 16 < RH;
+              const int d = j * 16 + g * 4 + r;
+              const int fi = lo ? d : d - RH;
+              const float c = a.cosT[pos * RH + fi], s = a.sinT[pos * RH + fi];
+              const float y = lo ? v[(j + DJ) & 3][r] : v[(j - DJ) & 3][r];
+              o[j][r] = lo ? (v[j][r] * c - y * s) : (v[j][r] * c + y * s);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][r] = o[j][r];
+        }
+      } else if constexpr (RH > 0) {
+        // rotated dims live in register group j == 0; partner lane = lane ^ (4*RH)
+        float p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[r] = __shfl_xor(v[0][r], 4 * RH, 64);
+        if (!is_v) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int d = g * 4 + r;
+            if (d < 2 * RH) {
+              const bool lo = d < RH;
+              const int fi = lo ? d : d - RH;
+              const float c = a.cosT[pos * RH + fi], s = a.sinT[pos * RH + fi];
+              v[0][r] = lo ? (v[0][r] * c - p[r] * s) : (v[0][r] * c + p[r] * s);
+            }
+          }
+        }
+      }
+      if (m >= a.M) continue;
+      if (head < a.Hq) {
+        bf16_t* dst = a.qout + (((size_t)b * a.Hq + head) * a.S + pos) * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          u32x2_t w;
+          w[0] = pack_bf2(v[j][0] * a.q_scale, v[j][1] * a.q_scale);
+          w[1] = pack_bf2(v[j][2] * a.q_scale, v[j][3] * a.q_scale);
+          *(u32x2_t*)(dst + j * 16 + g * 4) = w;
+        }
+      } else if (!is_v) {
+        bf16_t* dst = a.kout + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          u32x2_t w;
+          w[0] = pack_bf2(v[j][0], v[j][1]);
+          w[1] = pack_bf2(v[j][2], v[j][3]);
+          *(u32x2_t*)(dst + j * 16 + g * 4) = w;
+        }
+      } else {
+        bf16_t* dst = a.vtout + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dst[(size_t)(j * 16 + g * 4 + r) * a.s_pad] = f2bf(v[j][r]);
+      }
+    }
+    return;
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= a.M) continue;
+    if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int n = nw / 2 + p * 16 + g * 4;
+        u32x2_t w;
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = silu(acc[i][2 * p][r]) * acc[i][2 * p + 1][r];
+        w[0] = pack_bf2(o[0], o[1]);
+        w[1] = pack_bf2(o[2], o[3]);
+        *(u32x2_t*)(a.C + (size_t)m * a.ldc + n) = w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nw + j * 16 + g * 4;
+        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU) {
+          const u32x2_t bw = *(const u32x2_t*)(a.bias + n);
+          o[0] += bf_lo(bw[0]); o[1] += bf_hi(bw[0]); o[2] += bf_lo(bw[1]); o[3] += bf_hi(bw[1]);
+        }
+        if constexpr (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
+        }
+        if constexpr (EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
+          const u32x2_t rw = *(const u32x2_t*)(a.resid + (size_t)m * a.ldr + n);
+          o[0] += bf_lo(rw[0]); o[1] += bf_hi(rw[0]); o[2] += bf_lo(rw[1]); o[3] += bf_hi(rw[1]);
+        }
+        u32x2_t w;
+        w[0] = pack_bf2(o[0], o[1]);
+        w[1] = pack_bf2(o[2], o[3]);
+        *(u32x2_t*)(a.C + (size_t)m * a.ldc + n) = w;
+      }
+    }
+  }
+}
+
+template <int EPI, int RH = 0>
+static int launch(const GemmArgs& a, hipStream_t st) {
+  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, RH>), dim3(tm * tn), dim3(256), 2 * STAGE_BYTES, st, a);
+  return (int)hipGetLastError();
+}
+
+static int check_shapes(const GemmArgs& a) {
+  if (a.M <= 0) return -1;
+  if (a.N % BN || a.K % BK || a.N <= 0 || a.K <= 0) return (int)hipErrorInvalidValue;
+  if (a.lda % 8 || a.ldb % 8) return (int)hipErrorInvalidValue;
+  return 0;
+}
+
+EDGE_API int edge_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                       const void* bias, const void* resid, int ldr, int act, hipStream_t st) {
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = (bf16_t*)C;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ldr = ldr;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  // act: 0 none, 1 gelu, 2 swiglu-interleaved
+  if (act == 2) return bias || resid ? (int)hipErrorInvalidValue : launch<EPI_SWIGLU>(a, st);
+  if (act == 1) return resid || !bias ? (int)hipErrorInvalidValue : launch<EPI_BIAS_GELU>(a, st);
+  if (bias && resid) return launch<EPI_BIAS_RESID>(a, st);
+  if (bias) return launch<EPI_BIAS>(a, st);
+  if (resid) return launch<EPI_RESID>(a, st);
+  return launch<EPI_NONE>(a, st);
+}
+
+EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, void* q, void* k, void* vt,
+                                const float* cosT, const float* sinT, int M, int K, int S, int Hq, int Hkv,
+                                int rot_dim, int s_pad, float q_scale, hipStream_t st) {
+  GemmArgs a{};
+  a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
+  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = K; a.lda = K; a.ldb = K;
+  a.bias = (const bf16_t*)bias;
+  a.qout = (bf16_t*)q; a.kout = (bf16_t*)k; a.vtout = (bf16_t*)vt;
+  a.cosT = cosT; a.sinT = sinT; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.s_pad = s_pad;
+  a.q_scale = q_scale;
+  if (!bias || M % S) return (int)hipErrorInvalidValue;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  switch (rot_dim) {
+    case 0: return launch<EPI_QKV_ROPE, 0>(a, st);
+    case 8: return launch<EPI_QKV_ROPE, 4>(a, st);
+    case 16: return launch<EPI_QKV_ROPE, 8>(a, st);
+    case 32: return launch<EPI_QKV_ROPE, 16>(a, st);
+    case 64: return launch<EPI_QKV_ROPE, 32>(a, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+EDGE_API int edge_gemm_lse(const void* X, const void* W, const int64_t* targets, float* part_max, float* part_sum,
+                           float* tgt_logit, int M, int N, int K, hipStream_t st) {
+  GemmArgs a{};
+  a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
+  a.M = M; a.N = N; a.K = K; a.lda = K; a.ldb = K;
+  a.targets = targets; a.part_max = part_max; a.part_sum = part_sum; a.tgt_logit = tgt_logit; a.nparts = N / 64;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  return launch<EPI_LSE>(a, st);
+}
+
+// Combine the LSE partials: nll[m] = logsumexp_m - logit[target_m].
+__global__ __launch_bounds__(256) void lse_reduce_kernel(const float* __restrict__ pmax, const float* __restrict__ psum,
+                                                         const float* __restrict__ tgt, float* __restrict__ nll,
+                                                         int nparts) {
+  __shared__ float red[4];
+  const int m = blockIdx.x;
+  const float* pm = pmax + (size_t)m * nparts;
+  const float* ps = psum + (size_t)m * nparts;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < nparts; i += 256) mx = fmaxf(mx, pm[i]);
+  mx = block_max<256>(mx, red);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += ps[i] * __expf(pm[i] - mx);
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) nll[m] = mx + logf(s) - tgt[m];
+}
+
+EDGE_API int edge_lse_reduce(const float* pmax, const float* psum, const float* tgt, float* nll, int M, int nparts,
+                             hipStream_t st) {
+  if (M <= 0) return 0;
+  lse_reduce_kernel<<<M, 256, 0, st>>>(pmax, psum, tgt, nll, nparts);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,170 @@
+// Memory-bound row kernels: embedding gather, RMSNorm, LayerNorm (single and dual-output), with an
+// optional row-gather so the final norm runs only on the rows that are scored (K1, K3, K9 of SURVEY §2.4).
+// One wave64 per row, 16-byte vector loads (8 bf16 per lane per chunk), fp32 statistics.
+#include "common.h"
+
+template <int NCH>
+__device__ __forceinline__ void load_row(const bf16_t* __restrict__ src, int H, float (&v)[NCH][8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < H) {
+      u32x4_t w = *(const u32x4_t*)(src + col);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[c][2 * j] = bf_lo(w[j]); v[c][2 * j + 1] = bf_hi(w[j]); }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+}
+
+template <int NCH>
+__device__ __forceinline__ void store_row(bf16_t* __restrict__ dst, int H, const float (&v)[NCH][8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < H) {
+      u32x4_t w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = pack_bf2(v[c][2 * j], v[c][2 * j + 1]);
+      *(u32x4_t*)(dst + col) = w;
+    }
+  }
+}
+
+template <int NCH>
+__device__ __forceinline__ void load_vec(const bf16_t* __restrict__ p, int H, float (&v)[NCH][8]) { load_row<NCH>(p, H, v); }
+
+// ---------------------------------------------------------------------------------------------
+template <int NCH>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                      bf16_t* __restrict__ y, const int* __restrict__ rows, int R,
+                                                      int H, float eps) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int src_row = rows ? rows[r] : r;
+  float v[NCH][8], g[NCH][8];
+  load_row<NCH>(x + (size_t)src_row * H, H, v);
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+  ss = wave_sum(ss);
+  const float rs = rsqrtf(ss / (float)H + eps);
+  load_vec<NCH>(w, H, g);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      // HF: (x * rsqrt(var+eps)).to(bf16) then * weight  -> round twice like the reference.
+      const float n = bf2f(f2bf(v[c][j] * rs));
+      v[c][j] = n * g[c][j];
+    }
+  store_row<NCH>(y + (size_t)r * H, H, v);
+}
+
+template <int NCH, bool DUAL>
+__global__ __launch_bounds__(256) void layernorm_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
+                                                        const bf16_t* __restrict__ b1, const bf16_t* __restrict__ w2,
+                                                        const bf16_t* __restrict__ b2, bf16_t* __restrict__ y1,
+                                                        bf16_t* __restrict__ y2, const int* __restrict__ rows, int R,
+                                                        int H, float eps) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int src_row = rows ? rows[r] : r;
+  float v[NCH][8], g[NCH][8], b[NCH][8], o[NCH][8];
+  load_row<NCH>(x + (size_t)src_row * H, H, v);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[c][j];
+  const float mean = wave_sum(s) / (float)H;
+  const int lane = threadIdx.x & 63;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const bool ok = (c * 64 + lane) * 8 < H;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = v[c][j] - mean;
+      v[c][j] = d;
+      ss += ok ? d * d : 0.f;
+    }
+  }
+  const float rs = rsqrtf(wave_sum(ss) / (float)H + eps);
+  load_vec<NCH>(w1, H, g);
+  load_vec<NCH>(b1, H, b);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[c][j] = v[c][j] * rs * g[c][j] + b[c][j];
+  store_row<NCH>(y1 + (size_t)r * H, H, o);
+  if (DUAL) {
+    load_vec<NCH>(w2, H, g);
+    load_vec<NCH>(b2, H, b);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[c][j] = v[c][j] * rs * g[c][j] + b[c][j];
+    store_row<NCH>(y2 + (size_t)r * H, H, o);
+  }
+}
+
+__global__ __launch_bounds__(256) void embedding_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ table,
+                                                        bf16_t* __restrict__ out, int T, int H, int V) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= T) return;
+  int64_t id = ids[r];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+  const u32x4_t* src = (const u32x4_t*)(table + (size_t)id * H);
+  u32x4_t* dst = (u32x4_t*)(out + (size_t)r * H);
+  for (int c = threadIdx.x & 63; c < H / 8; c += 64) dst[c] = src[c];
+}
+
+// ---------------------------------------------------------------------------------------------
+#define DISPATCH_NCH(H, ...)                       \
+  do {                                             \
+    const int _nch = ((H) / 8 + 63) / 64;          \
+    if (_nch <= 1) { constexpr int NCH = 1; __VA_ARGS__; } \
+    else if (_nch <= 2) { constexpr int NCH = 2; __VA_ARGS__; } \
+    else if (_nch <= 4) { constexpr int NCH = 4; __VA_ARGS__; } \
+    else if (_nch <= 8) { constexpr int NCH = 8; __VA_ARGS__; } \
+    else return (int)hipErrorInvalidValue;        \
+  } while (0)
+
+EDGE_API int edge_rmsnorm(const void* x, const void* w, void* y, const int* rows, int R, int H, float eps,
+                          hipStream_t st) {
+  if (H % 8 || R <= 0) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+  dim3 grid((R + 3) / 4);
+  DISPATCH_NCH(H, rmsnorm_kernel<NCH><<<grid, 256, 0, st>>>((const bf16_t*)x, (const bf16_t*)w, (bf16_t*)y, rows, R,
+                                                           H, eps));
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_layernorm(const void* x, const void* w1, const void* b1, const void* w2, const void* b2, void* y1,
+                            void* y2, const int* rows, int R, int H, float eps, hipStream_t st) {
+  if (H % 8 || R <= 0) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+  dim3 grid((R + 3) / 4);
+  if (y2) {
+    DISPATCH_NCH(H, (layernorm_kernel<NCH, true><<<grid, 256, 0, st>>>(
+                        (const bf16_t*)x, (const bf16_t*)w1, (const bf16_t*)b1, (const bf16_t*)w2, (const bf16_t*)b2,
+                        (bf16_t*)y1, (bf16_t*)y2, rows, R, H, eps)));
+  } else {
+    DISPATCH_NCH(H, (layernorm_kernel<NCH, false><<<grid, 256, 0, st>>>(
+                        (const bf16_t*)x, (const bf16_t*)w1, (const bf16_t*)b1, nullptr, nullptr, (bf16_t*)y1,
+                        nullptr, rows, R, H, eps)));
+  }
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_embedding(const int64_t* ids, const void* table, void* out, int T, int H, int V, hipStream_t st) {
+  if (H % 8) return (int)hipErrorInvalidValue;
+  if (T <= 0) return 0;
+  embedding_kernel<<<(T + 3) / 4, 256, 0, st>>>(ids, (const bf16_t*)table, (bf16_t*)out, T, H, V);
+  return (int)hipGetLastError();
+}

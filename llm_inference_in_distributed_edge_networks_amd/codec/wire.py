@@ -1,0 +1,408 @@
+"""Wire format of a boundary message and the encode/decode entry points.
+
+Message for a micro-batch of ``B`` windows of ``S`` tokens, hidden size ``H``,
+``k`` lo-class tokens per window (all sections 16-byte aligned)::
+
+    header   32 B   int32[8] = magic 'EDGB', version, codec id, B, S, H, k, hi-row format
+    mask     B * MW uint32        bit j of window b set <=> token j is in the lo class (MW = 2*ceil(S/64))
+    scales   fp32                 per token [B*S] | per window [B] | per channel [B*H]
+    hi rows  B*(S-k) rows         token order within each window
+    lo rows  B*k rows             token order within each window
+
+The size depends only on (codec, B, S, H, k, native dtype), so sender and
+receiver agree on it without a handshake and the receiver can post its
+``irecv`` before the sender has produced anything.
+
+``encode``/``decode`` run the gfx950 kernels of ``csrc/codec.hip`` for CUDA
+tensors and a bit-identical PyTorch implementation for CPU tensors.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from functools import lru_cache
+
+import torch
+
+from ..ops._native import call, ptr, stream
+
+MAGIC = 0x45444742
+VERSION = 1
+FMT_BF16, FMT_INT8, FMT_INT4, FMT_INT2, FMT_F32 = 0, 1, 2, 3, 4
+SC_TOKEN, SC_WINDOW, SC_CHANNEL = 0, 1, 2
+CH_MAXABS, CH_MEAN = 0, 1
+NATIVE = -1  # "keep in the activation dtype" (bf16 on GPU, fp32 in the CPU reference mode)
+
+
+@dataclass(frozen=True)
+class CodecSpec:
+    name: str
+    cid: int
+    hi_fmt: int
+    lo_fmt: int
+    scale_mode: int
+    qmax_hi: int = 0
+    qmax_lo: int = 0
+    ch_kind: int = CH_MAXABS
+    uses_ratio: bool = True      # lo class = int(ratio*S) least important tokens
+    needs_importance: bool = True
+
+
+CODECS = {c.name: c for c in [
+    CodecSpec("passthrough", 0, NATIVE, NATIVE, SC_TOKEN, uses_ratio=False, needs_importance=False),
+    CodecSpec("ref_int4_global", 1, NATIVE, FMT_INT4, SC_WINDOW, 0, 7),
+    CodecSpec("int4_token", 2, NATIVE, FMT_INT4, SC_TOKEN, 0, 7),
+    CodecSpec("int8_token", 3, FMT_INT8, FMT_INT8, SC_TOKEN, 127, 127, uses_ratio=False, needs_importance=False),
+    CodecSpec("mixed_int4_int8", 4, FMT_INT8, FMT_INT4, SC_TOKEN, 127, 7),
+    CodecSpec("mixed_int2_int8", 5, FMT_INT8, FMT_INT2, SC_TOKEN, 127, 1),
+    CodecSpec("channel_8", 6, FMT_INT8, FMT_INT8, SC_CHANNEL, 127, 127, CH_MAXABS, False, False),
+    CodecSpec("channel_4", 7, FMT_INT4, FMT_INT4, SC_CHANNEL, 7, 7, CH_MAXABS, False, False),
+    CodecSpec("channel_1_mean", 8, FMT_INT2, FMT_INT2, SC_CHANNEL, 1, 1, CH_MEAN, False, False),
+    CodecSpec("channel_1_max", 9, FMT_INT2, FMT_INT2, SC_CHANNEL, 1, 1, CH_MAXABS, False, False),
+]}
+
+
+def get_codec(name: str) -> CodecSpec:
+    if name not in CODECS:
+        raise KeyError(f"unknown codec {name!r}; known: {sorted(CODECS)}")
+    return CODECS[name]
+
+
+def _a16(n: int) -> int:
+    return (n + 15) // 16 * 16
+
+
+def _row_bytes(fmt: int, H: int) -> int:
+    return {FMT_BF16: 2 * H, FMT_INT8: H, FMT_INT4: H // 2, FMT_INT2: H // 4, FMT_F32: 4 * H}[fmt]
+
+
+@dataclass(frozen=True)
+class Layout:
+    B: int
+    S: int
+    H: int
+    k: int
+    mw: int
+    hi_fmt: int
+    lo_fmt: int
+    off_mask: int
+    off_scale: int
+    off_hi: int
+    off_lo: int
+    total: int
+
+    @property
+    def payload_bytes_per_token(self) -> float:
+        return self.total / (self.B * self.S)
+
+
+def native_fmt(dtype: torch.dtype) -> int:
+    if dtype == torch.bfloat16:
+        return FMT_BF16
+    if dtype == torch.float32:
+        return FMT_F32
+    raise TypeError(f"unsupported activation dtype {dtype}")
+
+
+def num_lo(spec: CodecSpec, ratio: float, S: int) -> int:
+    """Reference truncation: ``int(ratio * S)`` (qwen_layer_wise.py:57)."""
+    if not spec.uses_ratio:
+        return 0
+    return max(0, min(S, int(ratio * S)))
+
+
+@lru_cache(maxsize=256)
+def layout(spec: CodecSpec, B: int, S: int, H: int, k: int, dtype: torch.dtype = torch.bfloat16) -> Layout:
+    if H % 32:
+        raise ValueError("hidden size must be a multiple of 32 for the packed formats")
+    nf = native_fmt(dtype)
+    hi = nf if spec.hi_fmt == NATIVE else spec.hi_fmt
+    lo = nf if spec.lo_fmt == NATIVE else spec.lo_fmt
+    mw = 2 * ((S + 63) // 64)
+    off_mask = 32
+    n_scale = {SC_TOKEN: B * S, SC_WINDOW: B, SC_CHANNEL: B * H}[spec.scale_mode]
+    if spec.hi_fmt == NATIVE and spec.lo_fmt == NATIVE:
+        n_scale = 0
+    off_scale = off_mask + _a16(B * mw * 4)
+    off_hi = off_scale + _a16(n_scale * 4)
+    off_lo = off_hi + _a16(B * (S - k) * _row_bytes(hi, H))
+    total = off_lo + _a16(B * k * _row_bytes(lo, H))
+    return Layout(B, S, H, k, mw, hi, lo, off_mask, off_scale, off_hi, off_lo, total)
+
+
+def message_bytes(spec: CodecSpec, B: int, S: int, H: int, ratio: float, dtype=torch.bfloat16) -> int:
+    return layout(spec, B, S, H, num_lo(spec, ratio, S), dtype).total
+
+
+# --------------------------------------------------------------------------------------------
+# CPU (reference) implementation
+def _mask_words(lo: torch.Tensor, mw: int) -> torch.Tensor:
+    """bool [B, S] -> int32 [B, mw] little-endian bit words."""
+    B, S = lo.shape
+    bits = torch.zeros(B, mw * 32, dtype=torch.int64)
+    bits[:, :S] = lo.to(torch.int64)
+    w = (bits.view(B, mw, 32) << torch.arange(32, dtype=torch.int64)).sum(-1)
+    w = torch.where(w >= 2 ** 31, w - 2 ** 32, w)
+    return w.to(torch.int32)
+
+
+def _words_to_mask(words: torch.Tensor, S: int) -> torch.Tensor:
+    w = words.to(torch.int64) & 0xFFFFFFFF
+    bits = (w.unsqueeze(-1) >> torch.arange(32, dtype=torch.int64)) & 1
+    return bits.reshape(words.shape[0], -1)[:, :S].bool()
+
+
+def select_mask(imp: torch.Tensor, k: int) -> torch.Tensor:
+    """bool [B, S]: the k least important tokens (ascending, ties by position) of each window."""
+    B, S = imp.shape
+    lo = torch.zeros(B, S, dtype=torch.bool, device=imp.device)
+    if k <= 0:
+        return lo
+    if k >= S:
+        return ~lo
+    order = torch.sort(imp.float(), dim=1, stable=True).indices[:, :k]
+    lo.scatter_(1, order, True)
+    return lo
+
+
+def _qcodes(x: torch.Tensor, spec: CodecSpec, is_lo: bool, scale_row, ch_scale) -> torch.Tensor:
+    """Quantize fp32 rows [n, H] -> int codes, exactly as csrc/codec.hip does."""
+    qmax = spec.qmax_lo if is_lo else spec.qmax_hi
+    if spec.scale_mode == SC_TOKEN:
+        inv = torch.where(scale_row > 0, 1.0 / torch.where(scale_row > 0, scale_row, torch.ones_like(scale_row)),
+                          torch.zeros_like(scale_row))
+        return torch.round(x * inv[:, None]).clamp(-qmax, qmax)
+    if spec.scale_mode == SC_WINDOW:
+        m = scale_row  # [n] (window max broadcast per row)
+        safe = torch.where(m > 0, m, torch.ones_like(m))
+        t = torch.round((x / safe[:, None] * float(qmax)).clamp(-(qmax + 1), qmax))
+        return torch.where(m[:, None] > 0, t, torch.zeros_like(t))
+    sc = ch_scale  # [n, H]
+    if spec.ch_kind == CH_MEAN or qmax == 1:
+        safe = torch.where(sc != 0, sc, torch.ones_like(sc))
+        t = torch.round(x / safe).clamp(-1, 1)
+        return torch.where(sc != 0, t, torch.zeros_like(t))
+    safe = torch.where(sc > 0, sc, torch.ones_like(sc))
+    t = torch.round(x / safe * float(qmax))
+    return torch.where(sc > 0, t, torch.zeros_like(t))
+
+
+def _pack_rows(q: torch.Tensor, fmt: int) -> torch.Tensor:
+    n, H = q.shape
+    qi = q.to(torch.int64)
+    if fmt == FMT_INT8:
+        return (qi & 255).to(torch.uint8).reshape(-1)
+    if fmt == FMT_INT4:
+        p = qi.reshape(n, H // 2, 2) & 15
+        return (p[..., 0] | (p[..., 1] << 4)).to(torch.uint8).reshape(-1)
+    if fmt == FMT_INT2:
+        p = qi.reshape(n, H // 4, 4) & 3
+        return (p[..., 0] | (p[..., 1] << 2) | (p[..., 2] << 4) | (p[..., 3] << 6)).to(torch.uint8).reshape(-1)
+    raise ValueError(fmt)
+
+
+def _unpack_rows(b: torch.Tensor, fmt: int, n: int, H: int) -> torch.Tensor:
+    u = b.to(torch.int64)
+    if fmt == FMT_INT8:
+        v = u.reshape(n, H)
+        return torch.where(v >= 128, v - 256, v).float()
+    if fmt == FMT_INT4:
+        u = u.reshape(n, H // 2)
+        p = torch.stack([u & 15, (u >> 4) & 15], -1).reshape(n, H)
+        return torch.where(p >= 8, p - 16, p).float()
+    if fmt == FMT_INT2:
+        u = u.reshape(n, H // 4)
+        p = torch.stack([(u >> (2 * e)) & 3 for e in range(4)], -1).reshape(n, H)
+        return torch.where(p >= 2, p - 4, p).float()
+    raise ValueError(fmt)
+
+
+def _dequant(q: torch.Tensor, spec: CodecSpec, is_lo: bool, scale_row, ch_scale) -> torch.Tensor:
+    qmax = spec.qmax_lo if is_lo else spec.qmax_hi
+    if spec.scale_mode == SC_TOKEN:
+        return q * scale_row[:, None]
+    if spec.scale_mode == SC_WINDOW:
+        return q / float(qmax) * scale_row[:, None]
+    if spec.ch_kind == CH_MEAN or qmax == 1:
+        return q * ch_scale
+    return q * ch_scale / float(qmax)
+
+
+def _header(spec: CodecSpec, L: Layout) -> torch.Tensor:
+    return torch.tensor([MAGIC, VERSION, spec.cid, L.B, L.S, L.H, L.k, L.hi_fmt], dtype=torch.int32)
+
+
+def _encode_cpu(x, spec, L, lo_mask):
+    B, S, H, k = L.B, L.S, L.H, L.k
+    msg = torch.zeros(L.total, dtype=torch.uint8)
+    msg[:32] = _header(spec, L).view(torch.uint8)
+    mw_bytes = _mask_words(lo_mask, L.mw).view(torch.uint8).reshape(-1)
+    msg[L.off_mask:L.off_mask + mw_bytes.numel()] = mw_bytes
+    xf = x.float().reshape(B, S, H)
+    # statistics
+    scales = None
+    ch = None
+    if spec.scale_mode == SC_TOKEN and not (spec.hi_fmt == NATIVE and spec.lo_fmt == NATIVE):
+        scales = torch.zeros(B, S)
+        for is_lo, fmt, qmax in ((False, L.hi_fmt, spec.qmax_hi), (True, L.lo_fmt, spec.qmax_lo)):
+            if fmt in (FMT_BF16, FMT_F32):
+                continue
+            sel = lo_mask if is_lo else ~lo_mask
+            am = xf.abs().amax(-1)
+            scales = torch.where(sel, am / float(qmax), scales)
+        msg[L.off_scale:L.off_scale + B * S * 4] = scales.reshape(-1).view(torch.uint8)
+    elif spec.scale_mode == SC_WINDOW:
+        am = torch.where(lo_mask[..., None], xf.abs(), torch.zeros_like(xf)).amax(dim=(1, 2))
+        scales = am
+        msg[L.off_scale:L.off_scale + B * 4] = am.view(torch.uint8)
+    elif spec.scale_mode == SC_CHANNEL:
+        ch = xf.abs().amax(1) if spec.ch_kind == CH_MAXABS else xf.mean(1) + 1e-8   # [B, H]
+        msg[L.off_scale:L.off_scale + B * H * 4] = ch.reshape(-1).contiguous().view(torch.uint8)
+    # rows
+    for is_lo in (False, True):
+        fmt = L.lo_fmt if is_lo else L.hi_fmt
+        n_per = k if is_lo else S - k
+        if n_per == 0:
+            continue
+        sel = lo_mask if is_lo else ~lo_mask
+        rows = xf[sel]                                      # [B*n_per, H] in window/token order
+        off = L.off_lo if is_lo else L.off_hi
+        if fmt == FMT_F32:
+            data = rows.contiguous().view(torch.uint8).reshape(-1)
+        elif fmt == FMT_BF16:
+            data = rows.to(torch.bfloat16).contiguous().view(torch.uint8).reshape(-1)
+        else:
+            if spec.scale_mode == SC_TOKEN:
+                srow = scales[sel]
+                q = _qcodes(rows, spec, is_lo, srow, None)
+            elif spec.scale_mode == SC_WINDOW:
+                srow = scales.view(B, 1).expand(B, S)[sel]
+                q = _qcodes(rows, spec, is_lo, srow, None)
+            else:
+                chr_ = ch.view(B, 1, H).expand(B, S, H)[sel]
+                q = _qcodes(rows, spec, is_lo, None, chr_)
+            data = _pack_rows(q, fmt)
+        msg[off:off + data.numel()] = data
+    return msg
+
+
+def _decode_cpu(msg, spec, L, dtype):
+    B, S, H, k = L.B, L.S, L.H, L.k
+    words = msg[L.off_mask:L.off_mask + B * L.mw * 4].view(torch.int32).reshape(B, L.mw)
+    lo_mask = _words_to_mask(words, S)
+    out = torch.empty(B, S, H, dtype=torch.float32)
+    scales = None
+    ch = None
+    if spec.scale_mode == SC_TOKEN and not (spec.hi_fmt == NATIVE and spec.lo_fmt == NATIVE):
+        scales = msg[L.off_scale:L.off_scale + B * S * 4].view(torch.float32).reshape(B, S)
+    elif spec.scale_mode == SC_WINDOW:
+        scales = msg[L.off_scale:L.off_scale + B * 4].view(torch.float32)
+    elif spec.scale_mode == SC_CHANNEL:
+        ch = msg[L.off_scale:L.off_scale + B * H * 4].view(torch.float32).reshape(B, H)
+    for is_lo in (False, True):
+        fmt = L.lo_fmt if is_lo else L.hi_fmt
+        n = B * (k if is_lo else S - k)
+        if n == 0:
+            continue
+        sel = lo_mask if is_lo else ~lo_mask
+        off = L.off_lo if is_lo else L.off_hi
+        nb = n * _row_bytes(fmt, H)
+        raw = msg[off:off + nb]
+        if fmt == FMT_F32:
+            rows = raw.view(torch.float32).reshape(n, H)
+        elif fmt == FMT_BF16:
+            rows = raw.view(torch.bfloat16).reshape(n, H).float()
+        else:
+            q = _unpack_rows(raw, fmt, n, H)
+            if spec.scale_mode == SC_TOKEN:
+                rows = _dequant(q, spec, is_lo, scales[sel], None)
+            elif spec.scale_mode == SC_WINDOW:
+                rows = _dequant(q, spec, is_lo, scales.view(B, 1).expand(B, S)[sel], None)
+            else:
+                rows = _dequant(q, spec, is_lo, None, ch.view(B, 1, H).expand(B, S, H)[sel])
+        out[sel] = rows
+    return out.reshape(B * S, H).to(dtype)
+
+
+# --------------------------------------------------------------------------------------------
+# GPU implementation
+_HDR_CACHE: dict = {}
+
+
+def _gpu_header(spec, L, device):
+    key = (spec.cid, L, device)
+    h = _HDR_CACHE.get(key)
+    if h is None:
+        h = _header(spec, L).view(torch.uint8).to(device)
+        _HDR_CACHE[key] = h
+    return h
+
+
+def _args(spec, L):
+    return (L.off_mask, L.off_scale, L.off_hi, L.off_lo, L.B, L.S, L.H, L.k, L.hi_fmt, L.lo_fmt, spec.scale_mode,
+            spec.qmax_hi, spec.qmax_lo, spec.ch_kind)
+
+
+def _encode_gpu(x, spec, L, imp, msg):
+    if x.dtype != torch.bfloat16:
+        raise TypeError("GPU boundary codec expects bf16 activations")
+    st = stream()
+    msg[:32].copy_(_gpu_header(spec, L, x.device))
+    if 0 < L.k < L.S:
+        if imp is None:
+            raise ValueError(f"codec {spec.name} with 0 < k < S needs token importance")
+        call("edge_select", ptr(imp.float().contiguous()), L.B, L.S, L.k, ptr(msg), L.off_mask, None, st)
+    else:
+        call("edge_set_mask", ptr(msg), L.off_mask, L.B, L.S, 1 if L.k >= L.S else 0, st)
+    if spec.scale_mode == SC_WINDOW:
+        tmp = torch.empty(L.B, L.H, dtype=torch.float32, device=x.device)
+        call("edge_channel_stats", ptr(x), ptr(msg), L.off_mask, ptr(tmp), L.B, L.S, L.H, CH_MAXABS, 1, st)
+        call("edge_rowmax", ptr(tmp), msg.data_ptr() + L.off_scale, L.B, L.H, st)
+    elif spec.scale_mode == SC_CHANNEL:
+        call("edge_channel_stats", ptr(x), ptr(msg), L.off_mask, msg.data_ptr() + L.off_scale, L.B, L.S, L.H,
+             spec.ch_kind, 0, st)
+    call("edge_pack", ptr(x), ptr(msg), *_args(spec, L), st)
+    return msg
+
+
+def _decode_gpu(msg, spec, L, out):
+    call("edge_unpack", ptr(out), ptr(msg), *_args(spec, L), stream())
+    return out
+
+
+# --------------------------------------------------------------------------------------------
+def encode(x: torch.Tensor, spec: CodecSpec, B: int, S: int, ratio: float = 0.0, importance=None,
+           out: torch.Tensor | None = None) -> tuple[torch.Tensor, Layout]:
+    """Quantize and pack ``x`` ([B*S, H]) into one boundary message (uint8 tensor)."""
+    H = x.shape[-1]
+    k = num_lo(spec, ratio, S)
+    L = layout(spec, B, S, H, k, x.dtype)
+    if x.is_cuda:
+        if out is None:
+            out = torch.empty(L.total, dtype=torch.uint8, device=x.device)
+        return _encode_gpu(x.contiguous(), spec, L, importance, out), L
+    lo = select_mask(importance.float(), k) if (0 < k < S) else \
+        torch.full((B, S), k >= S and k > 0, dtype=torch.bool)
+    msg = _encode_cpu(x, spec, L, lo)
+    if out is not None:
+        out.copy_(msg)
+        return out, L
+    return msg, L
+
+
+def decode(msg: torch.Tensor, spec: CodecSpec, L: Layout, dtype=torch.bfloat16, out=None) -> torch.Tensor:
+    """Unpack and dequantize a boundary message into ``[B*S, H]`` activations."""
+    if msg.is_cuda:
+        if out is None:
+            out = torch.empty(L.B * L.S, L.H, dtype=dtype, device=msg.device)
+        return _decode_gpu(msg, spec, L, out)
+    y = _decode_cpu(msg, spec, L, dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def fake_quant(x: torch.Tensor, spec: CodecSpec, B: int, S: int, ratio: float = 0.0, importance=None):
+    """decode(encode(x)): what the receiving stage sees.  Returns (x_hat, message bytes)."""
+    msg, L = encode(x, spec, B, S, ratio, importance)
+    return decode(msg, spec, L, x.dtype), L.total

@@ -1,0 +1,117 @@
+"""``params.json`` configuration.
+
+The reference reads a bare ``params.json`` from the working directory with no
+schema, defaults or validation (``Experiments/Pythia-70M/main.py:24-25``,
+``Experiments/Qwen2-0.5B/main.py:108-116``, ``Experiments/Relevance/main.py:49-50``).
+This module keeps the same file format and keys and adds typed defaults for the
+new options (pipeline stages, codec, dtype, synthetic data ...).  Unknown keys
+are preserved in ``extra`` and never rejected, so every reference params file
+loads unchanged.
+"""
+from __future__ import annotations
+
+import dataclasses
+import hashlib
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Any
+
+
+@dataclass
+class Params:
+    # ---- reference keys ------------------------------------------------------
+    experiment: str = "last_row"            # Pythia: "last_row" | "initial"
+    ratios: list = field(default_factory=lambda: [0, 0.25, 0.5, 0.75, 1])
+    layers_of_interest: list = field(default_factory=lambda: [2])
+    methods: list = field(default_factory=lambda: ["last_row"])
+    stride: int = 32
+    max_length: int | None = None            # None -> model max_position (Pythia reference behaviour)
+    # ---- new keys (defaults reproduce the reference) -------------------------
+    model: str = ""                          # preset name, filled by the entry point
+    weights: str = ""                        # path to an HF safetensors dir; "" -> HF cache if present, else random
+    dataset: str = "wikitext"                # "wikitext" | "synthetic"
+    synthetic_tokens: int = 0                # length of the synthetic stream (0 -> 299,078, the WikiText-2 test size)
+    max_windows: int = 0                     # 0 = whole corpus
+    window_batch: int = 8                    # windows per forward batch
+    dtype: str = "auto"                      # "auto" (fp32 on CPU, bf16 on GPU) | "fp32" | "bf16"
+    device: str = "auto"                     # "auto" | "cpu" | "cuda"
+    codec: str = "ref_int4_global"           # boundary codec used for the ratio sweep (see codec/)
+    num_stages: int = 1                      # pipeline stages for the distributed runner
+    split_layers: list = field(default_factory=list)   # explicit stage boundaries (last layer of each stage but the last)
+    head_weights: str = ""                   # path to attention_head_weights.json (weighted_importance)
+    output_dir: str = "."
+    checkpoint_every: int = 1000             # windows between partial-result dumps (reference: 1000)
+    resume: bool = True
+    seed: int = 0
+    extra: dict = field(default_factory=dict)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "Params":
+        known = {f.name for f in dataclasses.fields(cls)}
+        kw = {k: v for k, v in d.items() if k in known and k != "extra"}
+        extra = {k: v for k, v in d.items() if k not in known}
+        p = cls(**kw)
+        p.extra = extra
+        p.validate()
+        return p
+
+    @classmethod
+    def load(cls, path: str = "params.json", **overrides) -> "Params":
+        with open(path) as f:
+            d = json.load(f)
+        d.update({k: v for k, v in overrides.items() if v is not None})
+        return cls.from_dict(d)
+
+    def to_dict(self) -> dict:
+        d = dataclasses.asdict(self)
+        extra = d.pop("extra")
+        d.update(extra)
+        return d
+
+    def config_hash(self) -> str:
+        d = self.to_dict()
+        for k in ("output_dir", "checkpoint_every", "resume"):
+            d.pop(k, None)
+        return hashlib.sha1(json.dumps(d, sort_keys=True, default=str).encode()).hexdigest()[:12]
+
+    def validate(self) -> None:
+        if self.stride <= 0:
+            raise ValueError("stride must be positive")
+        if self.max_length is not None and self.max_length <= 1:
+            raise ValueError("max_length must be > 1")
+        for r in self.ratios:
+            if not isinstance(r, (int, float)) or r < 0:
+                raise ValueError(f"bad ratio {r!r}")
+        if self.num_stages < 1:
+            raise ValueError("num_stages must be >= 1")
+
+
+def resolve_device(p: Params) -> str:
+    import torch
+    if p.device != "auto":
+        return p.device
+    return "cuda" if torch.cuda.is_available() else "cpu"
+
+
+def resolve_dtype(p: Params, device: str):
+    import torch
+    if p.dtype == "fp32":
+        return torch.float32
+    if p.dtype == "bf16":
+        return torch.bfloat16
+    return torch.bfloat16 if device.startswith("cuda") else torch.float32
+
+
+def env_flag(name: str, default: bool = False) -> bool:
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    return v not in ("0", "", "false", "False")
+
+
+def dump_json(obj: Any, path: str) -> None:
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f, indent=1, default=float)
+    os.replace(tmp, path)

@@ -1,0 +1,137 @@
+"""HF sliding-window perplexity recipe, batched.
+
+Reference loop (``Experiments/Qwen2-0.5B/main.py:151-180``, ``last_row_exp.py:85-113``)::
+
+    prev_end = 0
+    for begin in range(0, N, stride):
+        end = min(begin + max_length, N); trg_len = end - prev_end
+        target = ids[begin:end].clone(); target[:-trg_len] = -100
+        nll = CE(logits[:, :-1], target[:, 1:])            # mean over valid targets
+        total_nll += nll * (num_valid - batch)              # num_valid = trg_len, batch = 1
+        prev_end = end; if end == N: break
+    PPL = exp(total_nll / total_tokens)
+
+Windows are independent, so they are grouped into batches of equal length (all but
+the last window have ``S = max_length``).  For every window only the rows whose
+logits are scored are listed (``rows``/``targets``): the LM head runs on those
+rows only (a ~16x cut at stride 32 / length 512).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+
+@dataclass(frozen=True)
+class Window:
+    idx: int
+    begin: int
+    end: int
+    trg_len: int
+
+    @property
+    def length(self) -> int:
+        return self.end - self.begin
+
+    @property
+    def weight(self) -> int:
+        # num_loss_tokens = num_valid_tokens - batch_size (batch_size = 1 in the reference)
+        return self.trg_len - 1
+
+    @property
+    def first_scored(self) -> int:
+        return max(0, self.length - self.trg_len - 1)
+
+
+def sliding_windows(N: int, max_length: int, stride: int) -> list[Window]:
+    out, prev_end = [], 0
+    for i, begin in enumerate(range(0, N, stride)):
+        end = min(begin + max_length, N)
+        out.append(Window(i, begin, end, end - prev_end))
+        prev_end = end
+        if end == N:
+            break
+    return out
+
+
+@dataclass
+class WindowBatch:
+    ids: torch.Tensor          # [B, S] int64 (CPU)
+    windows: list
+    rows: torch.Tensor         # [R] flat row index b*S + p of every scored logit row
+    targets: torch.Tensor      # [R] target token ids
+    row_window: torch.Tensor   # [R] window slot (0..B-1) of each row
+    n_rows: torch.Tensor       # [B] number of CE terms per window
+    weights: torch.Tensor      # [B] float64 num_loss_tokens per window
+
+    @property
+    def B(self) -> int:
+        return self.ids.shape[0]
+
+    @property
+    def S(self) -> int:
+        return self.ids.shape[1]
+
+    @property
+    def tokens(self) -> int:
+        return self.ids.numel()
+
+    def to(self, device) -> "WindowBatch":
+        return WindowBatch(self.ids.to(device, non_blocking=True), self.windows, self.rows.to(device),
+                           self.targets.to(device), self.row_window.to(device), self.n_rows.to(device),
+                           self.weights)
+
+
+def make_batch(tokens: torch.Tensor, wins: list) -> WindowBatch:
+    ids = tokens.view(-1)
+    S = wins[0].length
+    assert all(w.length == S for w in wins)
+    rows, tgts, rw, nr = [], [], [], []
+    for b, w in enumerate(wins):
+        p = torch.arange(w.first_scored, S - 1)
+        rows.append(b * S + p)
+        tgts.append(ids[w.begin + p + 1])
+        rw.append(torch.full_like(p, b))
+        nr.append(p.numel())
+    return WindowBatch(
+        ids=torch.stack([ids[w.begin:w.end] for w in wins]).contiguous(),
+        windows=list(wins), rows=torch.cat(rows), targets=torch.cat(tgts), row_window=torch.cat(rw),
+        n_rows=torch.tensor(nr, dtype=torch.float32),
+        weights=torch.tensor([w.weight for w in wins], dtype=torch.float64))
+
+
+def batches(tokens: torch.Tensor, wins: list, batch_size: int):
+    """Group consecutive equal-length windows into batches of at most ``batch_size``."""
+    cur = []
+    for w in wins:
+        if cur and (len(cur) == batch_size or w.length != cur[0].length):
+            yield make_batch(tokens, cur)
+            cur = []
+        cur.append(w)
+    if cur:
+        yield make_batch(tokens, cur)
+
+
+def window_nll(row_nll: torch.Tensor, batch: WindowBatch) -> torch.Tensor:
+    """Per-window mean CE over its scored rows: [B] fp32 on the row_nll device."""
+    s = torch.zeros(batch.B, dtype=torch.float32, device=row_nll.device)
+    s.index_add_(0, batch.row_window, row_nll.float())
+    return s / batch.n_rows.to(row_nll.device)
+
+
+class PPLAccumulator:
+    """Token-weighted NLL accumulation, exactly the reference's ``total_nll``/``n_tokens``."""
+
+    def __init__(self):
+        self.total_nll = 0.0
+        self.n_tokens = 0.0
+
+    def add(self, wnll: torch.Tensor, batch: WindowBatch) -> None:
+        w = batch.weights
+        self.total_nll += float((wnll.double().cpu() * w).sum())
+        self.n_tokens += float(w.sum())
+
+    def ppl(self) -> float:
+        return math.exp(self.total_nll / self.n_tokens) if self.n_tokens else float("nan")

@@ -1,0 +1,288 @@
+"""Decoder-only LMs (Qwen2, GPT-NeoX/Pythia) with layer-range execution.
+
+Counterpart of the reference's layer-wise runners ``QwenPointFiveBModel``
+(``Experiments/Qwen2-0.5B/qwen_layer_wise.py:5-167``) and ``Pythia70Model``
+(``Experiments/Pythia-70M/pythia_model.py:13-206``), which drive HF modules
+one layer at a time so that a boundary can be inserted after any layer.  Here the
+model is our own: weights are stored in the layouts the gfx950 kernels want
+(fused QKV with q|k|v row order, interleaved gate/up, tied head) and each layer is
+a short sequence of fused kernels:
+
+Qwen2 layer (7 launches)::
+
+    rmsnorm -> QKV GEMM(+bias+RoPE+head-major scatter) -> flash attention
+            -> O GEMM(+residual) -> rmsnorm -> gate/up GEMM(+SiLU*up) -> down GEMM(+residual)
+
+GPT-NeoX layer (parallel residual, 6 launches)::
+
+    dual layernorm -> QKV GEMM(+RoPE on 16 dims) -> flash attention -> O GEMM(+bias+residual)
+                   -> fc GEMM(+bias+GELU) -> proj GEMM(+bias+residual)
+
+At a boundary layer the attention can additionally emit the statistics the
+importance scorers need (last-row probabilities, or row LSE + column sums), so
+the S x S attention map of the reference's second "eager" model copy
+(``Qwen2-0.5B/main.py:132-134``) is never materialised.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import math
+import os
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from .configs import ModelConfig
+
+
+@dataclass
+class AttnStats:
+    """Per-head attention statistics of one layer for the importance scorers."""
+    lastrow: torch.Tensor | None = None   # [B, Hq, S] P[S-1, j]
+    colsum: torch.Tensor | None = None    # [B, Hq, S] sum_i P[i, j]
+
+
+class DecoderLM:
+    def __init__(self, cfg: ModelConfig, weights: dict, device="cpu", dtype=torch.float32):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.w = weights
+        self.layers = weights["layers"]
+        cos, sin = ops.rope_tables(cfg.max_position, cfg.rotary_dim, cfg.rope_theta)
+        self.cos = cos.to(self.device).contiguous()
+        self.sin = sin.to(self.device).contiguous()
+        self.q_scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def random_init(cls, cfg: ModelConfig, seed: int = 0, device="cpu", dtype=torch.float32, std: float = 0.02,
+                    layers: range | None = None, with_embed: bool = True, with_head: bool = True):
+        """Seeded random weights of the given architecture (HF ``_init_weights`` style: N(0, 0.02)).
+
+        ``layers`` restricts allocation to a layer range (a pipeline stage only holds its own layers);
+        the generator is advanced identically so every stage sees the same weights as a full model.
+        """
+        g = torch.Generator().manual_seed(seed)
+        H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
+        keep = set(range(cfg.num_layers)) if layers is None else set(layers)
+
+        def rn(*shape, s=std):
+            return (torch.randn(*shape, generator=g) * s)
+
+        def fin(t):
+            return t.to(device=device, dtype=dtype).contiguous()
+
+        w: dict = {"layers": []}
+        emb = rn(V, H)
+        w["embed"] = fin(emb) if (with_embed or (with_head and cfg.tie_embeddings)) else None
+        for i in range(cfg.num_layers):
+            if cfg.arch == "qwen2":
+                shapes = dict(wqkv=(cfg.qkv_size, H), bqkv=(cfg.qkv_size,), wo=(H, cfg.q_size),
+                              wg=(I, H), wu=(I, H), wd=(H, I))
+            else:
+                shapes = dict(wqkv=(cfg.qkv_size, H), bqkv=(cfg.qkv_size,), wo=(H, cfg.q_size), bo=(H,),
+                              wfc=(I, H), bfc=(I,), wproj=(H, I), bproj=(H,))
+            raw = {k: rn(*s) for k, s in shapes.items()}
+            ln = {k: 1.0 + rn(H, s=0.05) for k in ("ln1_w", "ln2_w")}
+            if cfg.arch == "gpt_neox":
+                ln.update({k: rn(H, s=0.05) for k in ("ln1_b", "ln2_b")})
+            if i not in keep:
+                w["layers"].append(None)
+                continue
+            L = {k: fin(v) for k, v in ln.items()}
+            if cfg.arch == "qwen2":
+                L.update(wqkv=fin(raw["wqkv"]), bqkv=fin(raw["bqkv"]), wo=fin(raw["wo"]),
+                         wgu=fin(ops.interleave_gate_up(raw["wg"], raw["wu"])), wd=fin(raw["wd"]))
+            else:
+                L.update({k: fin(v) for k, v in raw.items()})
+            w["layers"].append(L)
+        w["norm_w"] = fin(1.0 + rn(H, s=0.05))
+        if cfg.arch == "gpt_neox":
+            w["norm_b"] = fin(rn(H, s=0.05))
+        if cfg.tie_embeddings:
+            w["head"] = w["embed"] if with_head else None
+        else:
+            hd = rn(V, H)
+            w["head"] = fin(hd) if with_head else None
+        if not with_embed and not cfg.tie_embeddings:
+            w["embed"] = None
+        return cls(cfg, w, device, dtype)
+
+    @classmethod
+    def from_state_dict(cls, cfg: ModelConfig, sd: dict, device="cpu", dtype=torch.float32,
+                        layers: range | None = None):
+        """Build from an HF-format state dict (transformers ``Qwen2ForCausalLM`` / ``GPTNeoXForCausalLM``)."""
+        keep = set(range(cfg.num_layers)) if layers is None else set(layers)
+
+        def fin(t):
+            return t.detach().to(device=device, dtype=dtype).contiguous()
+
+        def get(*names):
+            for n in names:
+                if n in sd:
+                    return sd[n]
+            raise KeyError(f"none of {names} in state dict")
+
+        w: dict = {"layers": []}
+        H, D = cfg.hidden_size, cfg.head_dim
+        if cfg.arch == "qwen2":
+            w["embed"] = fin(get("model.embed_tokens.weight"))
+            for i in range(cfg.num_layers):
+                if i not in keep:
+                    w["layers"].append(None)
+                    continue
+                p = f"model.layers.{i}."
+                wq, wk, wv = (get(p + f"self_attn.{n}_proj.weight") for n in "qkv")
+                bq, bk, bv = (get(p + f"self_attn.{n}_proj.bias") for n in "qkv")
+                w["layers"].append(dict(
+                    ln1_w=fin(get(p + "input_layernorm.weight")), ln2_w=fin(get(p + "post_attention_layernorm.weight")),
+                    wqkv=fin(torch.cat([wq, wk, wv], 0)), bqkv=fin(torch.cat([bq, bk, bv], 0)),
+                    wo=fin(get(p + "self_attn.o_proj.weight")),
+                    wgu=fin(ops.interleave_gate_up(get(p + "mlp.gate_proj.weight").float(),
+                                                   get(p + "mlp.up_proj.weight").float())),
+                    wd=fin(get(p + "mlp.down_proj.weight"))))
+            w["norm_w"] = fin(get("model.norm.weight"))
+            w["head"] = w["embed"] if cfg.tie_embeddings else fin(get("lm_head.weight"))
+        else:
+            Hh = cfg.num_heads
+            w["embed"] = fin(get("gpt_neox.embed_in.weight"))
+            for i in range(cfg.num_layers):
+                if i not in keep:
+                    w["layers"].append(None)
+                    continue
+                p = f"gpt_neox.layers.{i}."
+                wqkv = get(p + "attention.query_key_value.weight").reshape(Hh, 3, D, H).permute(1, 0, 2, 3)
+                bqkv = get(p + "attention.query_key_value.bias").reshape(Hh, 3, D).permute(1, 0, 2)
+                w["layers"].append(dict(
+                    ln1_w=fin(get(p + "input_layernorm.weight")), ln1_b=fin(get(p + "input_layernorm.bias")),
+                    ln2_w=fin(get(p + "post_attention_layernorm.weight")),
+                    ln2_b=fin(get(p + "post_attention_layernorm.bias")),
+                    wqkv=fin(wqkv.reshape(3 * Hh * D, H)), bqkv=fin(bqkv.reshape(-1)),
+                    wo=fin(get(p + "attention.dense.weight")), bo=fin(get(p + "attention.dense.bias")),
+                    wfc=fin(get(p + "mlp.dense_h_to_4h.weight")), bfc=fin(get(p + "mlp.dense_h_to_4h.bias")),
+                    wproj=fin(get(p + "mlp.dense_4h_to_h.weight")), bproj=fin(get(p + "mlp.dense_4h_to_h.bias"))))
+            w["norm_w"] = fin(get("gpt_neox.final_layer_norm.weight"))
+            w["norm_b"] = fin(get("gpt_neox.final_layer_norm.bias"))
+            w["head"] = fin(get("embed_out.weight", "lm_head.weight"))
+        return cls(cfg, w, device, dtype)
+
+    @classmethod
+    def from_pretrained_dir(cls, cfg: ModelConfig, path: str, device="cpu", dtype=torch.float32, layers=None):
+        """Load ``*.safetensors`` (or ``pytorch_model.bin`` with weights_only) from a local HF snapshot."""
+        files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+        sd = {}
+        if files:
+            from safetensors.torch import load_file
+            for f in files:
+                sd.update(load_file(f))
+        else:
+            binf = os.path.join(path, "pytorch_model.bin")
+            if not os.path.exists(binf):
+                raise FileNotFoundError(f"no safetensors / pytorch_model.bin under {path}")
+            sd = torch.load(binf, map_location="cpu", weights_only=True)
+        return cls.from_state_dict(cfg, sd, device, dtype, layers)
+
+    # ------------------------------------------------------------------ execution
+    def embed(self, ids: torch.Tensor) -> torch.Tensor:
+        """ids [B, S] -> hidden [B*S, H]."""
+        return ops.embedding(ids.to(self.device), self.w["embed"])
+
+    def layer(self, i: int, x: torch.Tensor, B: int, S: int, stats: str | None = None):
+        """Run decoder layer ``i`` on ``x`` ([B*S, H], not modified).  Returns (y, AttnStats|None).
+
+        ``stats``: None, "lastrow" (P[S-1, :] per head) or "colsum" (column sums of P per head).
+        """
+        cfg, L = self.cfg, self.layers[i]
+        if L is None:
+            raise RuntimeError(f"layer {i} is not resident on this stage")
+        Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
+        if cfg.arch == "qwen2":
+            h = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps)
+        else:
+            h, h2 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps)
+        q, k, vt = ops.qkv_rope(h, L["wqkv"], L["bqkv"], self.cos, self.sin, B, S, Hq, Hkv, D, cfg.rotary_dim,
+                                self.q_scale)
+        o, lse = ops.attention(q, k, vt, S, need_lse=(stats == "colsum"))
+        st = None
+        if stats == "lastrow":
+            st = AttnStats(lastrow=ops.attn_lastrow(q, k, S))
+        elif stats == "colsum":
+            st = AttnStats(colsum=ops.attn_colsum(q, k, lse, S))
+        elif stats is not None:
+            raise ValueError(stats)
+        if cfg.arch == "qwen2":
+            y = ops.linear(o, L["wo"], residual=x)
+            h = ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps)
+            a = ops.linear(h, L["wgu"], act="swiglu_il")
+            y = ops.linear(a, L["wd"], residual=y, out=y)
+        else:
+            y = ops.linear(o, L["wo"], L["bo"], residual=x)
+            f = ops.linear(h2, L["wfc"], L["bfc"], act="gelu")
+            y = ops.linear(f, L["wproj"], L["bproj"], residual=y, out=y)
+        return y, st
+
+    def final_norm(self, x: torch.Tensor, rows: torch.Tensor | None = None) -> torch.Tensor:
+        if self.cfg.arch == "qwen2":
+            return ops.rmsnorm(x, self.w["norm_w"], self.cfg.norm_eps, rows)
+        return ops.layernorm(x, self.w["norm_w"], self.w["norm_b"], self.cfg.norm_eps, rows)
+
+    def row_nll(self, x: torch.Tensor, rows: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+        """Per-row NLL of the scored rows only (final norm + LM head + CE fused)."""
+        h = self.final_norm(x, rows.to(self.device))
+        return ops.head_nll(h, self.w["head"], targets.to(self.device))
+
+    def logits(self, x: torch.Tensor) -> torch.Tensor:
+        """Full logits (tests / debugging only; the eval path never materialises them)."""
+        h = self.final_norm(x)
+        return ops.reference.linear(h, self.w["head"], out_dtype=torch.float32)
+
+    def forward_hidden(self, ids: torch.Tensor, start: int = 0, end: int | None = None) -> torch.Tensor:
+        B, S = ids.shape
+        x = self.embed(ids)
+        for i in range(start, self.cfg.num_layers if end is None else end):
+            x, _ = self.layer(i, x, B, S)
+        return x
+
+    def resident_bytes(self) -> int:
+        seen, n = set(), 0
+
+        def add(t):
+            nonlocal n
+            if t is not None and id(t) not in seen:
+                seen.add(id(t))
+                n += t.numel() * t.element_size()
+        for L in self.layers:
+            if L:
+                for t in L.values():
+                    add(t)
+        for k in ("embed", "head", "norm_w", "norm_b"):
+            add(self.w.get(k))
+        return n
+
+
+def find_hf_snapshot(hf_id: str) -> str | None:
+    """Locate a local HF-hub snapshot of ``hf_id`` (no network is ever used)."""
+    if not hf_id:
+        return None
+    roots = [os.environ.get("HF_HOME", os.path.expanduser("~/.cache/huggingface")), "/root/.cache/huggingface"]
+    for r in roots:
+        d = os.path.join(r, "hub", "models--" + hf_id.replace("/", "--"), "snapshots")
+        for snap in sorted(glob.glob(os.path.join(d, "*"))):
+            if glob.glob(os.path.join(snap, "*.safetensors")) or os.path.exists(os.path.join(snap, "pytorch_model.bin")):
+                return snap
+    return None
+
+
+def build_model(cfg: ModelConfig, device="cpu", dtype=torch.float32, weights: str = "", seed: int = 0,
+                layers: range | None = None, with_embed=True, with_head=True) -> tuple[DecoderLM, str]:
+    """Model from explicit weights dir, else a local HF snapshot, else seeded random init.
+
+    Returns (model, provenance string)."""
+    path = weights or find_hf_snapshot(cfg.hf_id)
+    if path and os.path.isdir(path):
+        return DecoderLM.from_pretrained_dir(cfg, path, device, dtype, layers), f"hf:{path}"
+    return (DecoderLM.random_init(cfg, seed, device, dtype, layers=layers, with_embed=with_embed,
+                                  with_head=with_head), f"random-init(seed={seed})")

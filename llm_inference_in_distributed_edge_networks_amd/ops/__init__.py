@@ -1,0 +1,187 @@
+"""Compute ops of the framework.
+
+Every op has exactly two implementations with identical layouts and semantics:
+
+* CUDA/HIP tensors -> the hand-written gfx950 kernel from ``csrc/`` (``_native``);
+  a missing library is an error, never a silent fallback;
+* CPU tensors -> the fp32 PyTorch oracle in ``reference.py`` (used for the
+  CPU WikiText-2 configuration and as the test oracle).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._native import call, ptr, stream
+
+IL_BLOCK = ref.IL_BLOCK
+s_pad = ref.s_pad
+rope_tables = ref.rope_tables
+interleave_gate_up = ref.interleave_gate_up
+deinterleave_gate_up = ref.deinterleave_gate_up
+
+_ACT = {None: 0, "gelu": 1, "swiglu_il": 2}
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _check_bf16(*ts):
+    for t in ts:
+        if t is not None and t.dtype != torch.bfloat16:
+            raise TypeError(f"HIP kernels take bf16 tensors, got {t.dtype}")
+        if t is not None and not t.is_contiguous():
+            raise ValueError("HIP kernels take contiguous tensors")
+
+
+# --------------------------------------------------------------------------------------------
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    if not _gpu(table):
+        return ref.embedding(ids, table)
+    _check_bf16(table)
+    ids = ids.reshape(-1).to(torch.int64).contiguous()
+    T, (V, H) = ids.numel(), table.shape
+    out = torch.empty(T, H, dtype=table.dtype, device=table.device)
+    call("edge_embedding", ptr(ids), ptr(table), ptr(out), T, H, V, stream())
+    return out
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, rows: torch.Tensor | None = None) -> torch.Tensor:
+    """RMSNorm of ``x[rows]`` (all rows if ``rows`` is None)."""
+    if not _gpu(x):
+        return ref.rmsnorm(x if rows is None else x.index_select(0, rows.long()), w, eps)
+    _check_bf16(x, w)
+    R = x.shape[0] if rows is None else rows.numel()
+    H = x.shape[1]
+    rows32 = None if rows is None else rows.to(torch.int32).contiguous()
+    y = torch.empty(R, H, dtype=x.dtype, device=x.device)
+    call("edge_rmsnorm", ptr(x), ptr(w), ptr(y), ptr(rows32), R, H, float(eps), stream())
+    return y
+
+
+def layernorm(x, w, b, eps, rows=None):
+    if not _gpu(x):
+        return ref.layernorm(x if rows is None else x.index_select(0, rows.long()), w, b, eps)
+    _check_bf16(x, w, b)
+    R = x.shape[0] if rows is None else rows.numel()
+    H = x.shape[1]
+    rows32 = None if rows is None else rows.to(torch.int32).contiguous()
+    y = torch.empty(R, H, dtype=x.dtype, device=x.device)
+    call("edge_layernorm", ptr(x), ptr(w), ptr(b), None, None, ptr(y), None, ptr(rows32), R, H, float(eps), stream())
+    return y
+
+
+def layernorm_dual(x, w1, b1, w2, b2, eps):
+    """Two LayerNorms of the same input (GPT-NeoX parallel residual reads ln1(x) and ln2(x))."""
+    if not _gpu(x):
+        return ref.layernorm_dual(x, w1, b1, w2, b2, eps)
+    _check_bf16(x, w1, b1, w2, b2)
+    R, H = x.shape
+    y1 = torch.empty_like(x)
+    y2 = torch.empty_like(x)
+    call("edge_layernorm", ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(y1), ptr(y2), None, R, H, float(eps),
+         stream())
+    return y1, y2
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, out=None) -> torch.Tensor:
+    """``act(x @ w.T + bias) + residual`` on MFMA (``residual`` may alias ``out``)."""
+    if not _gpu(x):
+        y = ref.linear(x, w, bias, residual, act)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _check_bf16(x, w, bias, residual)
+    M, K = x.shape
+    N = w.shape[0]
+    No = N // 2 if act == "swiglu_il" else N
+    if out is None:
+        out = torch.empty(M, No, dtype=x.dtype, device=x.device)
+    call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), ptr(bias),
+         ptr(residual), 0 if residual is None else residual.stride(0), _ACT[act], stream())
+    return out
+
+
+def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
+    """Fused QKV GEMM + bias + RoPE + head-major scatter.  Returns (q, k, vt)."""
+    if not _gpu(x):
+        return ref.qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
+    _check_bf16(x, wqkv, bqkv)
+    assert D == 64, "HIP attention path is specialised for head_dim 64"
+    M, K = x.shape
+    sp = s_pad(S)
+    q = torch.empty(B, Hq, S, D, dtype=x.dtype, device=x.device)
+    k = torch.empty(B, Hkv, S, D, dtype=x.dtype, device=x.device)
+    vt = torch.zeros(B, Hkv, D, sp, dtype=x.dtype, device=x.device) if sp != S else \
+        torch.empty(B, Hkv, D, sp, dtype=x.dtype, device=x.device)
+    call("edge_gemm_qkv_rope", ptr(x), ptr(wqkv), ptr(bqkv), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, K, S,
+         Hq, Hkv, rot_dim, sp, float(q_scale), stream())
+    return q, k, vt
+
+
+def attention(q, k, vt, S, need_lse=False):
+    if not _gpu(q):
+        return ref.attention(q, k, vt, S, need_lse)
+    _check_bf16(q, k, vt)
+    B, Hq, _, D = q.shape
+    Hkv = k.shape[1]
+    o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)
+    lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device) if need_lse else None
+    call("edge_flash_attn_fwd", ptr(q), ptr(k), ptr(vt), ptr(o), ptr(lse), B, Hq, Hkv, S, vt.shape[-1], stream())
+    return o, lse
+
+
+def attn_lastrow(q, k, S):
+    if not _gpu(q):
+        return ref.attn_lastrow(q, k, S)
+    B, Hq = q.shape[:2]
+    out = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
+    call("edge_attn_lastrow", ptr(q), ptr(k), ptr(out), B, Hq, k.shape[1], S, stream())
+    return out
+
+
+def attn_colsum(q, k, lse, S):
+    if not _gpu(q):
+        return ref.attn_colsum(q, k, lse, S)
+    B, Hq = q.shape[:2]
+    out = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
+    call("edge_attn_colsum", ptr(q), ptr(k), ptr(lse.contiguous()), ptr(out), B, Hq, k.shape[1], S, stream())
+    return out
+
+
+def head_combine(x, w=None, scale=1.0, out=None, beta=0.0):
+    """out = beta*out + scale * sum_h w[h] * x[:, h, :]   (x: [B, Hq, S] fp32)."""
+    if not _gpu(x):
+        wv = torch.ones(x.shape[1], dtype=torch.float32) if w is None else w.float().to(x.device)
+        r = scale * (x * wv.view(1, -1, 1)).sum(1)
+        if out is None:
+            return r
+        out.mul_(beta).add_(r) if beta != 0.0 else out.copy_(r)
+        return out
+    B, Hq, S = x.shape
+    if out is None:
+        out = torch.empty(B, S, dtype=torch.float32, device=x.device)
+        beta = 0.0
+    wv = None if w is None else w.to(device=x.device, dtype=torch.float32).contiguous()
+    call("edge_head_combine", ptr(x), ptr(wv), ptr(out), B, Hq, S, float(scale), float(beta), stream())
+    return out
+
+
+def head_nll(h, w, targets):
+    """Fused LM head + cross entropy on the scored rows only: per-row NLL (fp32)."""
+    if not _gpu(h):
+        return ref.head_nll(h, w, targets)
+    _check_bf16(h, w)
+    R, K = h.shape
+    V = w.shape[0]
+    nparts = V // 64
+    pmax = torch.empty(R, nparts, dtype=torch.float32, device=h.device)
+    psum = torch.empty_like(pmax)
+    tgt = torch.empty(R, dtype=torch.float32, device=h.device)
+    nll = torch.empty(R, dtype=torch.float32, device=h.device)
+    t64 = targets.to(torch.int64).contiguous()
+    call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, stream())
+    call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
+    return nll

@@ -1,0 +1,84 @@
+"""Loader for the in-tree gfx950 kernel library ``_native/libedge_kernels.so``.
+
+The library is plain HIP C ABI (no torch headers), built by ``build.py`` with
+``hipcc --offload-arch=gfx950``.  Kernels are launched on the current torch
+stream, so they compose with torch ops, CUDA-graph capture and RCCL streams.
+
+On a GPU process the library is mandatory: ``lib()`` raises instead of silently
+falling back to the PyTorch reference path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_native", "libedge_kernels.so")
+
+_lib = None
+
+c_p = ctypes.c_void_p
+c_i = ctypes.c_int
+c_f = ctypes.c_float
+c_ll = ctypes.c_longlong
+
+_SIGS = {
+    "edge_rmsnorm": [c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_p],
+    "edge_layernorm": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_p],
+    "edge_embedding": [c_p, c_p, c_p, c_i, c_i, c_i, c_p],
+    "edge_gemm": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p],
+    "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
+    "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
+    "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
+    "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_attn_lastrow": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    "edge_attn_colsum": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    "edge_head_combine": [c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p],
+    "edge_select": [c_p, c_i, c_i, c_i, c_p, c_ll, c_p, c_p],
+    "edge_set_mask": [c_p, c_ll, c_i, c_i, c_i, c_p],
+    "edge_channel_stats": [c_p, c_p, c_ll, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_rowmax": [c_p, c_p, c_i, c_i, c_p],
+    "edge_pack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_unpack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+}
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def available() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+def lib():
+    """Return the loaded ctypes library, loading it on first use (raises if absent)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not found: build the gfx950 kernels first "
+                "(python -c 'import __graft_entry__ as g; g.build()')")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, argt in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = c_i
+        _lib = L
+    return _lib
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with HIP error {rc}")

@@ -1,0 +1,174 @@
+"""Plain-PyTorch fp32 implementations of every op.
+
+These are the numerics oracle for the HIP kernels (tests compare each kernel
+against the function of the same name here) and the execution path on CPU
+(BASELINE config 1 "CPU WikiText-2 PPL").  They use exactly the tensor layouts
+of the HIP kernels so that the two are interchangeable op by op:
+
+* activations are token-major ``[T, H]`` with ``T = B * S``;
+* ``q`` is ``[B, Hq, S, D]`` with RoPE applied and pre-multiplied by ``q_scale``;
+* ``k`` is ``[B, Hkv, S, D]`` with RoPE applied;
+* ``vt`` is V transposed, ``[B, Hkv, D, S_pad]`` with ``S_pad = ceil(S/64)*64``
+  and zero padding (the attention kernel streams 64-key tiles of it);
+* gate/up weights of SwiGLU MLPs are interleaved in blocks of 16 rows
+  (``[g0..g15, u0..u15, g16..]``) so one GEMM tile holds matching gate and up
+  columns and the SiLU*up product is an epilogue.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+IL_BLOCK = 16  # gate/up interleave granularity (rows)
+
+
+def _f(x):
+    return x.float()
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    return table.index_select(0, ids.reshape(-1).long())
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    # HF Qwen2RMSNorm: fp32 variance, cast back to input dtype, then * weight.
+    xf = _f(x)
+    var = xf.pow(2).mean(-1, keepdim=True)
+    y = (xf * torch.rsqrt(var + eps)).to(x.dtype)
+    return (w * y).to(x.dtype)
+
+
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    return F.layer_norm(_f(x), (x.shape[-1],), _f(w), _f(b), eps).to(x.dtype)
+
+
+def layernorm_dual(x, w1, b1, w2, b2, eps):
+    return layernorm(x, w1, b1, eps), layernorm(x, w2, b2, eps)
+
+
+def gelu(x: torch.Tensor) -> torch.Tensor:
+    return F.gelu(x)  # exact (erf) GELU, HF "gelu"
+
+
+def deinterleave_gate_up(y: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Split the output of an interleaved gate/up GEMM into (gate, up)."""
+    T, N2 = y.shape
+    y4 = y.reshape(T, N2 // (2 * IL_BLOCK), 2, IL_BLOCK)
+    return y4[:, :, 0, :].reshape(T, N2 // 2), y4[:, :, 1, :].reshape(T, N2 // 2)
+
+
+def interleave_gate_up(wg: torch.Tensor, wu: torch.Tensor) -> torch.Tensor:
+    """[I,H] gate and up weights -> [2I,H] interleaved in blocks of IL_BLOCK rows."""
+    I, H = wg.shape
+    assert I % IL_BLOCK == 0
+    w = torch.stack([wg.reshape(I // IL_BLOCK, IL_BLOCK, H), wu.reshape(I // IL_BLOCK, IL_BLOCK, H)], 1)
+    return w.reshape(2 * I, H).contiguous()
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, out_dtype=None) -> torch.Tensor:
+    """y = act(x @ w.T + bias) (+ residual).  Accumulates in fp32."""
+    y = _f(x) @ _f(w).t()
+    if bias is not None:
+        y = y + _f(bias)
+    if act == "gelu":
+        y = gelu(y)
+    elif act == "swiglu_il":
+        g, u = deinterleave_gate_up(y)
+        y = F.silu(g) * u
+    elif act is not None:
+        raise ValueError(act)
+    if residual is not None:
+        y = y + _f(residual)
+    return y.to(out_dtype or x.dtype)
+
+
+def rope_tables(max_pos: int, rot_dim: int, theta: float, device=None):
+    """fp32 cos/sin tables ``[max_pos, rot_dim/2]`` (HF default rope recipe)."""
+    inv_freq = 1.0 / (theta ** (torch.arange(0, rot_dim, 2, dtype=torch.int64).float() / rot_dim))
+    pos = torch.arange(max_pos, dtype=torch.int64).float()
+    freqs = torch.outer(pos, inv_freq)
+    return freqs.cos().to(device), freqs.sin().to(device)
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, rot_dim: int) -> torch.Tensor:
+    """x: [..., S, D] fp32; cos/sin: [S, rot_dim/2]; rotate_half on the first rot_dim dims."""
+    half = rot_dim // 2
+    x1 = x[..., :half]
+    x2 = x[..., half:rot_dim]
+    c, s = cos, sin
+    r1 = x1 * c - x2 * s
+    r2 = x2 * c + x1 * s
+    return torch.cat([r1, r2, x[..., rot_dim:]], -1)
+
+
+def s_pad(S: int) -> int:
+    return ((S + 63) // 64) * 64
+
+
+def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
+    """Fused QKV projection + bias + RoPE + head-major scatter (+ q scaling)."""
+    y = linear(x, wqkv, bqkv, out_dtype=torch.float32)       # [T, (Hq+2Hkv)*D]
+    y = y.reshape(B, S, Hq + 2 * Hkv, D).permute(0, 2, 1, 3)  # [B, Htot, S, D]
+    q, k, v = y[:, :Hq], y[:, Hq:Hq + Hkv], y[:, Hq + Hkv:]
+    c, s_ = cos[:S], sin[:S]
+    q = apply_rope(q, c, s_, rot_dim) * q_scale
+    k = apply_rope(k, c, s_, rot_dim)
+    dt = x.dtype
+    vt = torch.zeros(B, Hkv, D, s_pad(S), dtype=dt, device=x.device)
+    vt[..., :S] = v.transpose(-1, -2).to(dt)
+    return q.to(dt).contiguous(), k.to(dt).contiguous(), vt
+
+
+def attention_probs(q, k, S):
+    """Full causal softmax probabilities [B, Hq, S, S] in fp32 (GQA expanded)."""
+    B, Hq = q.shape[:2]
+    Hkv = k.shape[1]
+    kk = _f(k).repeat_interleave(Hq // Hkv, dim=1)
+    sc = _f(q) @ kk.transpose(-1, -2)
+    mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+    sc = sc.masked_fill(mask, float("-inf"))
+    return torch.softmax(sc, -1)
+
+
+def attention(q, k, vt, S, need_lse=False):
+    """Causal GQA attention.  q is pre-scaled.  Returns (o [B*S, Hq*D], lse [B,Hq,S] or None)."""
+    B, Hq, _, D = q.shape
+    Hkv = k.shape[1]
+    kk = _f(k).repeat_interleave(Hq // Hkv, dim=1)
+    vv = _f(vt[..., :S]).transpose(-1, -2).repeat_interleave(Hq // Hkv, dim=1)
+    sc = _f(q) @ kk.transpose(-1, -2)
+    mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+    sc = sc.masked_fill(mask, float("-inf"))
+    lse = torch.logsumexp(sc, -1)
+    p = torch.exp(sc - lse[..., None])
+    o = p @ vv                                           # [B, Hq, S, D]
+    o = o.permute(0, 2, 1, 3).reshape(B * S, Hq * D).to(q.dtype)
+    return o, (lse if need_lse else None)
+
+
+def attn_lastrow(q, k, S):
+    """Per-head attention probabilities of the last query row: [B, Hq, S] fp32."""
+    B, Hq, _, D = q.shape
+    Hkv = k.shape[1]
+    kk = _f(k).repeat_interleave(Hq // Hkv, dim=1)
+    sc = (_f(q[:, :, S - 1:S]) @ kk.transpose(-1, -2))[:, :, 0]
+    return torch.softmax(sc, -1)
+
+
+def attn_colsum(q, k, lse, S):
+    """Per-head column sums of the causal attention probabilities: [B, Hq, S] fp32."""
+    B, Hq, _, D = q.shape
+    Hkv = k.shape[1]
+    kk = _f(k).repeat_interleave(Hq // Hkv, dim=1)
+    sc = _f(q) @ kk.transpose(-1, -2)
+    mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+    p = torch.exp(sc - lse[..., None]).masked_fill(mask, 0.0)
+    return p.sum(-2)
+
+
+def head_nll(h, w, targets):
+    """Fused final projection + cross entropy: per-row NLL (fp32) = lse(h @ w.T) - logit[target]."""
+    logits = _f(h) @ _f(w).t()
+    return torch.logsumexp(logits, -1) - logits.gather(1, targets.long().view(-1, 1)).squeeze(1)

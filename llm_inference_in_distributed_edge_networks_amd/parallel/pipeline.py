@@ -1,0 +1,221 @@
+"""Pipeline-stage runtime: layer-wise split inference with a quantized boundary.
+
+This is the real version of what the reference simulates in one process
+(``QwenPointFiveBModel.activation_quantization``, ``qwen_layer_wise.py:42-76``):
+stage ``s`` runs its contiguous layer range, scores the tokens at its last layer,
+encodes the hidden state with the boundary codec into one byte message and ships
+it to stage ``s+1`` (RCCL ``isend``/``irecv`` over xGMI between GPU processes,
+or a direct hand-off when all stages live in one process).  The last stage
+computes the per-window NLL of the scored rows.
+
+* ``StageRunner``      - executes one stage for one micro-batch (shared by both runtimes)
+* ``LocalPipeline``    - every stage in this process (1 GPU, CPU, tests, sweeps)
+* ``DistributedPipeline`` - one stage per rank, ``dp`` replicas of ``pp`` stages; the
+  receive for micro-batch i+1 is posted before micro-batch i is computed, so the
+  transfer overlaps compute, and consecutive micro-batches keep every stage busy
+  (forward-only GPipe fill/drain).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from .. import codec as C
+from ..eval.windows import PPLAccumulator, WindowBatch, window_nll
+from ..importance import ImportanceTracker, canonical
+from ..models.model import DecoderLM
+from .dist import Grid, all_reduce_sum
+from .plan import PipelinePlan
+
+
+@dataclass
+class BoundaryConfig:
+    codec: str = "passthrough"
+    ratio: float = 0.0
+    method: str = "last_row"
+    head_weights: torch.Tensor | None = None
+
+    @property
+    def spec(self) -> C.CodecSpec:
+        return C.get_codec(self.codec)
+
+    def needs_importance(self, S: int) -> bool:
+        k = C.wire.num_lo(self.spec, self.ratio, S)
+        return self.spec.needs_importance and 0 < k < S
+
+
+@dataclass
+class StageStats:
+    tokens: int = 0
+    windows: int = 0
+    wire_bytes: int = 0          # bytes this stage sent across its outgoing boundary
+    wire_tokens: int = 0
+    compute_s: float = 0.0
+
+    @property
+    def bytes_per_token(self) -> float:
+        return self.wire_bytes / self.wire_tokens if self.wire_tokens else 0.0
+
+
+class StageRunner:
+    def __init__(self, model: DecoderLM, plan: PipelinePlan, stage: int, bcfg: BoundaryConfig):
+        self.model, self.plan, self.stage, self.bcfg = model, plan, stage, bcfg
+        self.layers = plan.stage_layers(stage)
+        self.first = stage == 0
+        self.last = stage == plan.num_stages - 1
+        self.boundary = None if self.last else self.layers[-1]
+        self.stats = StageStats()
+
+    def _tracker(self, S: int):
+        if self.boundary is None or not self.bcfg.needs_importance(S):
+            return None
+        return ImportanceTracker(self.bcfg.method, [self.boundary], self.model.cfg.num_heads,
+                                 self.bcfg.head_weights)
+
+    def carries_state(self) -> bool:
+        return canonical(self.bcfg.method) in ("aggregate_till", "maximum_aggregation")
+
+    def run(self, batch: WindowBatch, x: torch.Tensor | None = None, carry: torch.Tensor | None = None):
+        """Returns (x_out, importance or None, carry_out or None)."""
+        m, B, S = self.model, batch.B, batch.S
+        if self.first:
+            x = m.embed(batch.ids)
+        tr = self._tracker(S)
+        if tr is not None and carry is not None:
+            tr.load_carry(carry, self.layers[0])
+        for i in self.layers:
+            need = tr.stats_for(i) if tr is not None else None
+            x, st = m.layer(i, x, B, S, stats=need)
+            if need is not None:
+                tr.observe(i, st, S)
+        imp = tr.importance(self.boundary) if tr is not None else None
+        return x, imp, (tr.carry() if tr is not None else None)
+
+    def encode(self, x, batch: WindowBatch, imp, out=None):
+        msg, L = C.encode(x, self.bcfg.spec, batch.B, batch.S, self.bcfg.ratio, imp, out=out)
+        self.stats.wire_bytes += L.total
+        self.stats.wire_tokens += batch.B * batch.S
+        return msg, L
+
+    def layout(self, batch: WindowBatch) -> C.Layout:
+        spec = self.bcfg.spec
+        k = C.wire.num_lo(spec, self.bcfg.ratio, batch.S)
+        return C.layout(spec, batch.B, batch.S, self.model.cfg.hidden_size, k, self.model.dtype)
+
+    def finish(self, x, batch: WindowBatch) -> torch.Tensor:
+        """Per-window mean NLL [B] (last stage)."""
+        nll = self.model.row_nll(x, batch.rows, batch.targets)
+        return window_nll(nll, batch)
+
+
+class LocalPipeline:
+    """All stages in one process.  ``run_batch`` is the split runner of the reference."""
+
+    def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig):
+        self.model, self.plan, self.bcfg = model, plan, bcfg
+        self.stages = [StageRunner(model, plan, s, bcfg) for s in range(plan.num_stages)]
+
+    def run_batch(self, batch: WindowBatch) -> torch.Tensor:
+        x, carry = None, None
+        for st in self.stages:
+            x, imp, c = st.run(batch, x, carry)
+            if st.last:
+                return st.finish(x, batch)
+            msg, L = st.encode(x, batch, imp)
+            x = C.decode(msg, self.bcfg.spec, L, self.model.dtype)
+            carry = c
+        raise AssertionError
+
+    def evaluate(self, batches, acc: PPLAccumulator | None = None, on_batch=None) -> PPLAccumulator:
+        acc = acc or PPLAccumulator()
+        for b in batches:
+            b = b.to(self.model.device)
+            wn = self.run_batch(b)
+            acc.add(wn, b)
+            if on_batch:
+                on_batch(b, wn)
+        return acc
+
+    def wire_bytes_per_token(self) -> list[float]:
+        return [s.stats.bytes_per_token for s in self.stages[:-1]]
+
+
+class DistributedPipeline:
+    """One pipeline stage per rank; ``grid.dp`` replicas share the window batches round-robin."""
+
+    def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig, grid: Grid, rank: int):
+        self.model, self.plan, self.bcfg, self.grid, self.rank = model, plan, bcfg, grid, rank
+        self.dp_idx, self.stage = grid.coords(rank)
+        if plan.num_stages != grid.pp:
+            raise ValueError("plan stages != grid pp")
+        self.runner = StageRunner(model, plan, self.stage, bcfg)
+        self.prev = grid.rank_of(self.dp_idx, self.stage - 1) if self.stage > 0 else None
+        self.next = grid.rank_of(self.dp_idx, self.stage + 1) if self.stage < grid.pp - 1 else None
+        self.device = model.device
+
+    def my_batches(self, batches):
+        for i, b in enumerate(batches):
+            if i % self.grid.dp == self.dp_idx:
+                yield b
+
+    def _recv_bufs(self, batch: WindowBatch):
+        r = self.runner
+        spec = self.bcfg.spec
+        k = C.wire.num_lo(spec, self.bcfg.ratio, batch.S)
+        L = C.layout(spec, batch.B, batch.S, self.model.cfg.hidden_size, k, self.model.dtype)
+        msg = torch.empty(L.total, dtype=torch.uint8, device=self.device)
+        carry = None
+        if r.carries_state() and self.bcfg.needs_importance(batch.S):
+            carry = torch.empty(batch.B, batch.S, dtype=torch.float32, device=self.device)
+        return L, msg, carry
+
+    def _post_recv(self, batch):
+        L, msg, carry = self._recv_bufs(batch)
+        reqs = [dist.irecv(msg, self.prev)]
+        if carry is not None:
+            reqs.append(dist.irecv(carry, self.prev))
+        return L, msg, carry, reqs
+
+    def evaluate(self, batches) -> tuple[PPLAccumulator, dict]:
+        """Run this rank's share.  Returns the globally reduced accumulator (valid on every rank)."""
+        mine = [b.to(self.device) for b in self.my_batches(batches)]
+        acc_local = torch.zeros(2, dtype=torch.float64, device=self.device)
+        pending_sends = []
+        recv_next = self._post_recv(mine[0]) if (self.prev is not None and mine) else None
+        t0 = time.perf_counter()
+        for i, b in enumerate(mine):
+            x = carry = None
+            if self.prev is not None:
+                L, msg, carry, reqs = recv_next
+                for r in reqs:
+                    r.wait()
+                if i + 1 < len(mine):
+                    recv_next = self._post_recv(mine[i + 1])  # prefetch: overlap next transfer with compute
+                x = C.decode(msg, self.bcfg.spec, L, self.model.dtype)
+            x, imp, c = self.runner.run(b, x, carry)
+            if self.next is not None:
+                msg, L = self.runner.encode(x, b, imp)
+                # keep at most two sends in flight so the buffers stay alive and memory bounded
+                pending_sends.append((msg, c, [dist.isend(msg, self.next)] +
+                                      ([dist.isend(c, self.next)] if c is not None else [])))
+                while len(pending_sends) > 2:
+                    for r in pending_sends.pop(0)[2]:
+                        r.wait()
+            else:
+                wn = self.runner.finish(x, b)
+                w = b.weights.to(self.device)
+                acc_local[0] += (wn.double() * w).sum()
+                acc_local[1] += w.sum()
+            self.runner.stats.windows += b.B
+            self.runner.stats.tokens += b.tokens
+        for _, _, reqs in pending_sends:
+            for r in reqs:
+                r.wait()
+        self.runner.stats.compute_s += time.perf_counter() - t0
+        all_reduce_sum(acc_local)
+        acc = PPLAccumulator()
+        acc.total_nll, acc.n_tokens = float(acc_local[0]), float(acc_local[1])
+        return acc, {"stage": self.stage, "dp": self.dp_idx, "wire_bytes_per_token": self.runner.stats.bytes_per_token}

@@ -1,0 +1,196 @@
+"""gfx950 kernels vs the plain-PyTorch fp32 oracle (ops/reference.py) of the same op."""
+import math
+
+import pytest
+import torch
+
+from llm_inference_in_distributed_edge_networks_amd import codec as C
+from llm_inference_in_distributed_edge_networks_amd import ops
+from llm_inference_in_distributed_edge_networks_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rnd(*shape, s=1.0, seed=0, dtype=torch.bfloat16):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * s).to(dtype)
+
+
+def close(a, b, atol, rtol=0.0):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    assert torch.isfinite(a).all(), "non-finite output"
+    assert (err <= tol).all(), f"max err {err.max().item():.4g} (atol {atol}, rtol {rtol})"
+
+
+def test_native_library_loaded():
+    from llm_inference_in_distributed_edge_networks_amd.ops import _native
+    assert _native.lib() is not None
+
+
+def test_embedding():
+    tab = rnd(1000, 256, seed=1)
+    ids = torch.randint(0, 1000, (3, 77))
+    out = ops.embedding(ids.to(DEV), tab.to(DEV))
+    assert torch.equal(out.cpu(), R.embedding(ids, tab))
+
+
+@pytest.mark.parametrize("H", [256, 896, 512, 2048])
+def test_rmsnorm(H):
+    x = rnd(300, H, seed=2)
+    w = rnd(H, s=0.2, seed=3) + 1
+    y = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6)
+    close(y, R.rmsnorm(x, w, 1e-6), atol=2e-2, rtol=1e-2)
+    rows = torch.tensor([5, 0, 299, 17])
+    y2 = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6, rows.to(DEV))
+    close(y2, R.rmsnorm(x[rows], w, 1e-6), atol=2e-2, rtol=1e-2)
+
+
+def test_layernorm_dual():
+    x = rnd(257, 512, seed=4) * 3 + 1
+    w1, b1, w2, b2 = (rnd(512, s=0.3, seed=s) for s in range(5, 9))
+    y1, y2 = ops.layernorm_dual(*(t.to(DEV) for t in (x, w1, b1, w2, b2)), 1e-5)
+    r1, r2 = R.layernorm_dual(x, w1, b1, w2, b2, 1e-5)
+    close(y1, r1, atol=3e-2, rtol=1e-2)
+    close(y2, r2, atol=3e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 1152, 896), (300, 896, 896), (1000, 256, 512), (64, 128, 4864)])
+@pytest.mark.parametrize("epi", ["none", "bias", "resid", "bias_resid", "gelu", "swiglu"])
+def test_gemm(M, N, K, epi):
+    x = rnd(M, K, seed=10)
+    w = rnd(N, K, s=1 / math.sqrt(K), seed=11)
+    b = rnd(N, s=0.5, seed=12)
+    No = N // 2 if epi == "swiglu" else N
+    r = rnd(M, No, seed=13)
+    kw = dict(bias=b if "bias" in epi or epi == "gelu" else None,
+              residual=r if "resid" in epi else None,
+              act={"gelu": "gelu", "swiglu": "swiglu_il"}.get(epi))
+    y = ops.linear(x.to(DEV), w.to(DEV), **{k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in kw.items()})
+    ref = R.linear(x, w, **kw, out_dtype=torch.float32)
+    close(y, ref, atol=3e-2, rtol=2e-2)
+
+
+def test_gemm_asymmetric_identity():
+    # A = I, asymmetric B: catches a transposed C-write
+    K = 128
+    x = torch.eye(K, dtype=torch.bfloat16)
+    w = torch.arange(256 * K, dtype=torch.float32).reshape(256, K).remainder(97).sub(48).to(torch.bfloat16)
+    y = ops.linear(x.to(DEV), w.to(DEV))
+    assert torch.equal(y.cpu().float(), w.t().float())
+
+
+def test_gemm_inplace_residual():
+    x = rnd(256, 512, seed=20)
+    w = rnd(512, 512, s=0.05, seed=21)
+    r = rnd(256, 512, seed=22)
+    ref = R.linear(x, w, residual=r, out_dtype=torch.float32)
+    rd = r.to(DEV)
+    ops.linear(x.to(DEV), w.to(DEV), residual=rd, out=rd)
+    close(rd, ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("S,Hq,Hkv,rot", [(512, 14, 2, 64), (100, 4, 2, 64), (130, 8, 8, 16), (64, 4, 4, 32)])
+def test_qkv_rope(S, Hq, Hkv, rot):
+    B, D, Hd = 2, 64, 256
+    cos, sin = R.rope_tables(1024, rot, 1e4 if rot < 64 else 1e6)
+    x = rnd(B * S, Hd, seed=30)
+    N = (Hq + 2 * Hkv) * D
+    w = rnd(N, Hd, s=0.06, seed=31)
+    b = rnd(N, s=0.3, seed=32)
+    q, k, vt = ops.qkv_rope(x.to(DEV), w.to(DEV), b.to(DEV), cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv, D, rot, 0.125)
+    rq, rk, rvt = R.qkv_rope(x, w, b, cos, sin, B, S, Hq, Hkv, D, rot, 0.125)
+    close(q, rq, atol=2e-2, rtol=2e-2)
+    close(k, rk, atol=3e-2, rtol=2e-2)
+    close(vt, rvt, atol=3e-2, rtol=2e-2)
+
+
+def _qkv(B, S, Hq, Hkv, seed):
+    q = rnd(B, Hq, S, 64, seed=seed) * 0.125 * 1.5
+    k = rnd(B, Hkv, S, 64, seed=seed + 1) * 1.5
+    v = rnd(B, Hkv, S, 64, seed=seed + 2)
+    vt = torch.zeros(B, Hkv, 64, ops.s_pad(S), dtype=torch.bfloat16)
+    vt[..., :S] = v.transpose(-1, -2)
+    return q, k, vt
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (1, 100, 4, 2), (3, 64, 8, 8), (1, 1000, 2, 1)])
+def test_flash_attention(B, S, Hq, Hkv):
+    q, k, vt = _qkv(B, S, Hq, Hkv, 40)
+    o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True)
+    ro, rlse = R.attention(q, k, vt, S, need_lse=True)
+    close(o, ro, atol=2e-2, rtol=2e-2)
+    close(lse, rlse, atol=2e-3, rtol=1e-3)
+
+
+def test_flash_attention_spike():
+    # force the online-softmax rescale: one key much larger for one query, late in the sequence
+    B, S, Hq, Hkv = 1, 256, 2, 1
+    q, k, vt = _qkv(B, S, Hq, Hkv, 50)
+    k[0, 0, 200] = q[0, 0, 230] * 400
+    o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True)
+    ro, rlse = R.attention(q, k, vt, S, need_lse=True)
+    close(o, ro, atol=3e-2, rtol=2e-2)
+    close(lse, rlse, atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (1, 100, 4, 2), (2, 2048, 8, 8)])
+def test_importance_kernels(B, S, Hq, Hkv):
+    q, k, vt = _qkv(B, S, Hq, Hkv, 60)
+    qd, kd = q.to(DEV), k.to(DEV)
+    _, lse = ops.attention(qd, kd, vt.to(DEV), S, need_lse=True)
+    lr = ops.attn_lastrow(qd, kd, S)
+    close(lr, R.attn_lastrow(q, k, S), atol=1e-4, rtol=2e-3)
+    cs = ops.attn_colsum(qd, kd, lse, S)
+    P = R.attention_probs(q, k, S)
+    close(cs, P.sum(-2), atol=2e-3, rtol=5e-3)
+    w = torch.randn(Hq)
+    hc = ops.head_combine(cs, w.to(DEV), 1.0 / S)
+    close(hc, (P.sum(-2) * w.view(1, -1, 1)).sum(1) / S, atol=1e-4, rtol=1e-2)
+
+
+@pytest.mark.parametrize("R_,V,K", [(96, 151936, 896), (33, 512, 256), (300, 50304, 512)])
+def test_head_nll(R_, V, K):
+    h = rnd(R_, K, seed=70)
+    w = rnd(V, K, s=2 / math.sqrt(K), seed=71)
+    t = torch.randint(0, V, (R_,))
+    nll = ops.head_nll(h.to(DEV), w.to(DEV), t.to(DEV))
+    close(nll, R.head_nll(h, w, t), atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("name", sorted(C.CODECS))
+@pytest.mark.parametrize("B,S,H,ratio", [(2, 512, 896, 0.5), (1, 100, 256, 0.25), (3, 64, 512, 1.0)])
+def test_codec_bytes_match_cpu(name, B, S, H, ratio):
+    spec = C.get_codec(name)
+    x = rnd(B * S, H, seed=80) * 3
+    x[5] *= 40  # an outlier token
+    imp = torch.rand(B, S, generator=torch.Generator().manual_seed(81))
+    msg_cpu, L = C.encode(x, spec, B, S, ratio, imp)
+    msg_gpu, L2 = C.encode(x.to(DEV), spec, B, S, ratio, imp.to(DEV))
+    assert L == L2
+    mg = msg_gpu.cpu()
+    if spec.scale_mode == C.wire.SC_CHANNEL and spec.ch_kind == C.wire.CH_MEAN:
+        # fp32 summation order differs for the channel mean: compare decoded values instead
+        close(C.decode(msg_gpu, spec, L), C.decode(msg_cpu, spec, L, torch.bfloat16), atol=1e-2, rtol=1e-2)
+    else:
+        assert torch.equal(mg, msg_cpu), f"{(mg != msg_cpu).sum().item()} bytes differ"
+        y_gpu = C.decode(msg_gpu, spec, L)
+        y_cpu = C.decode(msg_cpu, spec, L, torch.bfloat16)
+        assert torch.equal(y_gpu.cpu(), y_cpu)
+
+
+def test_tiny_model_gpu_vs_cpu():
+    from llm_inference_in_distributed_edge_networks_amd.models import TINY_QWEN2, TINY_NEOX, DecoderLM
+    for cfg in (TINY_QWEN2, TINY_NEOX):
+        mc = DecoderLM.random_init(cfg, seed=3, device="cpu", dtype=torch.float32, std=0.05)
+        mg = DecoderLM.random_init(cfg, seed=3, device=DEV, dtype=torch.bfloat16, std=0.05)
+        ids = torch.randint(0, cfg.vocab_size, (2, 200))
+        xc = mc.forward_hidden(ids)
+        xg = mg.forward_hidden(ids.to(DEV))
+        rows = torch.arange(0, 399)
+        tg = ids.view(-1)[1:400]
+        nc = mc.row_nll(xc, rows, tg)
+        ng = mg.row_nll(xg, rows.to(DEV), tg.to(DEV))
+        assert (nc - ng.cpu()).abs().mean() < 0.05 * nc.abs().mean() + 1e-2, cfg.name
