@@ -8,11 +8,11 @@
 // but the mask.  Row formats: 0 bf16, 1 int8, 2 int4 (two's-complement nibbles, even element in the low
 // nibble), 3 int2 (ternary, 4 per byte).  Scale modes: 0 per token (fp32 [B*S]), 1 per window for the
 // lo class (fp32 [B], reference Q1 "one global max-abs" int4), 2 per channel (fp32 [B*H]; reference
-// channel_8/4/1_max store max|x_c|, channel_1_mean stores mean_c + 1e-8).
+// channel_8/4/1_max store max|x_c|, channel_1_mean stores mean_c + 1e-8), 3 none (pass-through).
 #include "common.h"
 
 enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3 };
-enum { SC_TOKEN = 0, SC_WINDOW = 1, SC_CHANNEL = 2 };
+enum { SC_TOKEN = 0, SC_WINDOW = 1, SC_CHANNEL = 2, SC_NONE = 3 };
 enum { CH_MAXABS = 0, CH_MEAN = 1 };
 
 struct CodecArgs {

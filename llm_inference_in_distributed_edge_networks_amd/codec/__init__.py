@@ -21,6 +21,7 @@ mixed_int4_int8        int8            int4            per token    BASELINE con
 mixed_int2_int8        int8            int2 ternary    per token    extra compression point
 channel_8 / channel_4  int8 / int4     --              per channel  Q5
 channel_1_mean/_max    int2 ternary    --              per channel  Q6
+int8_token_keep        native dtype    int8            per token    Q2/Q4 (Pythia 'initial', intended semantics)
 =====================  ==============  ==============  ===========  ==================================
 
 "hi"/"lo" classes: the ``k = int(ratio * S)`` least important tokens of a

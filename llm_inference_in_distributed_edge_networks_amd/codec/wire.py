@@ -28,7 +28,7 @@ from ..ops._native import call, ptr, stream
 MAGIC = 0x45444742
 VERSION = 1
 FMT_BF16, FMT_INT8, FMT_INT4, FMT_INT2, FMT_F32 = 0, 1, 2, 3, 4
-SC_TOKEN, SC_WINDOW, SC_CHANNEL = 0, 1, 2
+SC_TOKEN, SC_WINDOW, SC_CHANNEL, SC_NONE = 0, 1, 2, 3
 CH_MAXABS, CH_MEAN = 0, 1
 NATIVE = -1  # "keep in the activation dtype" (bf16 on GPU, fp32 in the CPU reference mode)
 
@@ -48,7 +48,7 @@ class CodecSpec:
 
 
 CODECS = {c.name: c for c in [
-    CodecSpec("passthrough", 0, NATIVE, NATIVE, SC_TOKEN, uses_ratio=False, needs_importance=False),
+    CodecSpec("passthrough", 0, NATIVE, NATIVE, SC_NONE, uses_ratio=False, needs_importance=False),
     CodecSpec("ref_int4_global", 1, NATIVE, FMT_INT4, SC_WINDOW, 0, 7),
     CodecSpec("int4_token", 2, NATIVE, FMT_INT4, SC_TOKEN, 0, 7),
     CodecSpec("int8_token", 3, FMT_INT8, FMT_INT8, SC_TOKEN, 127, 127, uses_ratio=False, needs_importance=False),
@@ -58,6 +58,7 @@ CODECS = {c.name: c for c in [
     CodecSpec("channel_4", 7, FMT_INT4, FMT_INT4, SC_CHANNEL, 7, 7, CH_MAXABS, False, False),
     CodecSpec("channel_1_mean", 8, FMT_INT2, FMT_INT2, SC_CHANNEL, 1, 1, CH_MEAN, False, False),
     CodecSpec("channel_1_max", 9, FMT_INT2, FMT_INT2, SC_CHANNEL, 1, 1, CH_MAXABS, False, False),
+    CodecSpec("int8_token_keep", 10, NATIVE, FMT_INT8, SC_TOKEN, 0, 127),
 ]}
 
 
@@ -119,9 +120,7 @@ def layout(spec: CodecSpec, B: int, S: int, H: int, k: int, dtype: torch.dtype =
     lo = nf if spec.lo_fmt == NATIVE else spec.lo_fmt
     mw = 2 * ((S + 63) // 64)
     off_mask = 32
-    n_scale = {SC_TOKEN: B * S, SC_WINDOW: B, SC_CHANNEL: B * H}[spec.scale_mode]
-    if spec.hi_fmt == NATIVE and spec.lo_fmt == NATIVE:
-        n_scale = 0
+    n_scale = {SC_TOKEN: B * S, SC_WINDOW: B, SC_CHANNEL: B * H, SC_NONE: 0}[spec.scale_mode]
     off_scale = off_mask + _a16(B * mw * 4)
     off_hi = off_scale + _a16(n_scale * 4)
     off_lo = off_hi + _a16(B * (S - k) * _row_bytes(hi, H))
@@ -241,7 +240,7 @@ def _encode_cpu(x, spec, L, lo_mask):
     # statistics
     scales = None
     ch = None
-    if spec.scale_mode == SC_TOKEN and not (spec.hi_fmt == NATIVE and spec.lo_fmt == NATIVE):
+    if spec.scale_mode == SC_TOKEN:
         scales = torch.zeros(B, S)
         for is_lo, fmt, qmax in ((False, L.hi_fmt, spec.qmax_hi), (True, L.lo_fmt, spec.qmax_lo)):
             if fmt in (FMT_BF16, FMT_F32):
@@ -292,7 +291,7 @@ def _decode_cpu(msg, spec, L, dtype):
     out = torch.empty(B, S, H, dtype=torch.float32)
     scales = None
     ch = None
-    if spec.scale_mode == SC_TOKEN and not (spec.hi_fmt == NATIVE and spec.lo_fmt == NATIVE):
+    if spec.scale_mode == SC_TOKEN:
         scales = msg[L.off_scale:L.off_scale + B * S * 4].view(torch.float32).reshape(B, S)
     elif spec.scale_mode == SC_WINDOW:
         scales = msg[L.off_scale:L.off_scale + B * 4].view(torch.float32)
@@ -371,14 +370,16 @@ def _decode_gpu(msg, spec, L, out):
 
 # --------------------------------------------------------------------------------------------
 def encode(x: torch.Tensor, spec: CodecSpec, B: int, S: int, ratio: float = 0.0, importance=None,
-           out: torch.Tensor | None = None) -> tuple[torch.Tensor, Layout]:
-    """Quantize and pack ``x`` ([B*S, H]) into one boundary message (uint8 tensor)."""
+           out: torch.Tensor | None = None, k: int | None = None) -> tuple[torch.Tensor, Layout]:
+    """Quantize and pack ``x`` ([B*S, H]) into one boundary message (uint8 tensor).
+
+    The lo class is the ``k = int(ratio*S)`` least important tokens (``k`` may be given directly)."""
     H = x.shape[-1]
-    k = num_lo(spec, ratio, S)
+    k = num_lo(spec, ratio, S) if k is None else (k if spec.uses_ratio else 0)
     L = layout(spec, B, S, H, k, x.dtype)
     if x.is_cuda:
-        if out is None:
-            out = torch.empty(L.total, dtype=torch.uint8, device=x.device)
+        if out is None:  # zero-filled so the 16-byte section padding is deterministic on the wire
+            out = torch.zeros(L.total, dtype=torch.uint8, device=x.device)
         return _encode_gpu(x.contiguous(), spec, L, importance, out), L
     lo = select_mask(importance.float(), k) if (0 < k < S) else \
         torch.full((B, S), k >= S and k > 0, dtype=torch.bool)
@@ -402,7 +403,8 @@ def decode(msg: torch.Tensor, spec: CodecSpec, L: Layout, dtype=torch.bfloat16, 
     return y
 
 
-def fake_quant(x: torch.Tensor, spec: CodecSpec, B: int, S: int, ratio: float = 0.0, importance=None):
+def fake_quant(x: torch.Tensor, spec: CodecSpec, B: int, S: int, ratio: float = 0.0, importance=None,
+               k: int | None = None):
     """decode(encode(x)): what the receiving stage sees.  Returns (x_hat, message bytes)."""
-    msg, L = encode(x, spec, B, S, ratio, importance)
+    msg, L = encode(x, spec, B, S, ratio, importance, k=k)
     return decode(msg, spec, L, x.dtype), L.total

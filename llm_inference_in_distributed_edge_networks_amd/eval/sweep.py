@@ -1,0 +1,201 @@
+"""Importance x boundary-layer x ratio perplexity sweeps (the reference experiments).
+
+Reference drivers: ``Experiments/Qwen2-0.5B/main.py:100-207`` (4 methods x layers x ratios),
+``Experiments/Pythia-70M/last_row_exp.py:47-143`` and ``Experiments/Qwen2-0.5B/channel_wise.py:10-78``.
+Per window the reference runs one eager forward for attention maps and then one full split
+forward per (method, layer, ratio) - 101 forwards of 512 tokens per Qwen2 window.
+
+Here, per window batch:
+
+1. ONE unquantized forward: it yields the ratio-0 NLL, the hidden state after every boundary layer
+   of interest (kept on device) and every method's importance at those layers (fused attention
+   statistics, no S x S maps);
+2. per boundary layer L, the (method, ratio) variants are de-duplicated (ratio 0 and "all tokens
+   quantized" do not depend on the method), their fake-quantized copies of h_L are stacked along the
+   batch dimension and ONLY layers L+1.. are run, once, on the stacked batch (shared-prefix fork).
+
+Results keep the reference layouts: ``total_nll[method][layer][ratio]`` and
+``avg_ppl_results[method][layer][ratio]`` (ordered as in params.json), channel sweeps
+``[layer][method]``.  Progress is checkpointed every ``checkpoint_every`` windows and resumed.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import codec as C
+from ..importance import ImportanceTracker, canonical
+from ..models.model import DecoderLM
+from ..utils.checkpoint import SweepState
+from .windows import WindowBatch, window_nll
+
+
+@dataclass
+class SweepConfig:
+    methods: list
+    layers: list
+    ratios: list
+    codec: str = "ref_int4_global"
+    head_weights: torch.Tensor | None = None
+    max_fork_tokens: int = 1 << 17     # cap on tokens per stacked suffix forward
+    ratio_scale: float = 1.0           # Pythia 'initial' uses ratio in 0..10 meaning 0.1*ratio
+
+
+class SweepEngine:
+    def __init__(self, model: DecoderLM, sc: SweepConfig):
+        self.m, self.sc = model, sc
+        self.spec = C.get_codec(sc.codec)
+        self.methods = list(sc.methods)
+        self.layers = [int(l) for l in sc.layers]
+        self.ratios = list(sc.ratios)
+        shape = (len(self.methods), len(self.layers), len(self.ratios))
+        self.total_nll = torch.zeros(shape, dtype=torch.float64)
+        self.n_tokens = 0.0
+        self.windows_done = 0
+        self.forward_tokens = 0
+        self.wire_bytes = torch.zeros(shape, dtype=torch.float64)
+        self.tokens_done = 0
+
+    # -------------------------------------------------------------- one batch
+    def _prefix(self, batch: WindowBatch):
+        """Unquantized forward: base per-window NLL, h_L per boundary layer, importance per (method, L)."""
+        m, B, S = self.m, batch.B, batch.S
+        trackers = {meth: ImportanceTracker(meth, self.layers, m.cfg.num_heads, self.sc.head_weights)
+                    for meth in self.methods}
+        x = m.embed(batch.ids)
+        saved = {}
+        for i in range(m.cfg.num_layers):
+            kinds = set()
+            for tr in trackers.values():
+                k = tr.stats_for(i)
+                if k:
+                    kinds.add(k)
+            x, st = m.layer(i, x, B, S, stats=tuple(sorted(kinds)) or None)
+            for tr in trackers.values():
+                if tr.stats_for(i):
+                    tr.observe(i, st, S)
+            if i in self.layers:
+                saved[i] = x
+        base = window_nll(m.row_nll(x, batch.rows, batch.targets), batch)
+        self.forward_tokens += B * S
+        imp = {(meth, L): trackers[meth].importance(L) for meth in self.methods for L in self.layers}
+        return base, saved, imp
+
+    def _k(self, ratio, S):
+        return C.wire.num_lo(self.spec, float(ratio) * self.sc.ratio_scale, S)
+
+    def run_batch(self, batch: WindowBatch) -> torch.Tensor:
+        """Returns per-window NLL [M, Lc, R, B] for this batch (also accumulated)."""
+        m, B, S = self.m, batch.B, batch.S
+        base, saved, imp = self._prefix(batch)
+        M, Lc, R = len(self.methods), len(self.layers), len(self.ratios)
+        out = torch.empty(M, Lc, R, B, dtype=torch.float32, device=base.device)
+        for li, L in enumerate(self.layers):
+            # de-duplicate variants: key -> list of (mi, ri)
+            variants: dict = {}
+            for mi, meth in enumerate(self.methods):
+                for ri, r in enumerate(self.ratios):
+                    k = self._k(r, S)
+                    if k == 0 and self.spec.uses_ratio:
+                        out[mi, li, ri] = base
+                        self.wire_bytes[mi, li, ri] += C.message_bytes(C.get_codec("passthrough"), B, S,
+                                                                       m.cfg.hidden_size, 0.0, m.dtype)
+                        continue
+                    key = ("all", k) if (k >= S or not self.spec.needs_importance) else (meth, k)
+                    variants.setdefault(key, []).append((mi, ri))
+            keys = list(variants)
+            per_fork = max(1, self.sc.max_fork_tokens // (B * S))
+            for c0 in range(0, len(keys), per_fork):
+                chunk = keys[c0:c0 + per_fork]
+                xs = []
+                for key in chunk:
+                    meth, k = key
+                    im = None if meth == "all" else imp[(meth, L)]
+                    xq, nbytes = C.fake_quant(saved[L], self.spec, B, S, importance=im, k=k)
+                    xs.append(xq)
+                    for (mi, ri) in variants[key]:
+                        self.wire_bytes[mi, li, ri] += nbytes
+                V = len(chunk)
+                x = torch.cat(xs, 0)
+                for i in range(L + 1, m.cfg.num_layers):
+                    x, _ = m.layer(i, x, V * B, S)
+                self.forward_tokens += V * B * S
+                off = (torch.arange(V, device=batch.rows.device) * (B * S)).repeat_interleave(batch.rows.numel())
+                rows = batch.rows.repeat(V) + off
+                nll = m.row_nll(x, rows, batch.targets.repeat(V))
+                s = torch.zeros(V * B, dtype=torch.float32, device=nll.device)
+                s.index_add_(0, batch.row_window.repeat(V) + torch.arange(V, device=nll.device).repeat_interleave(
+                    batch.rows.numel()) * B, nll.float())
+                wn = (s.view(V, B) / batch.n_rows.to(nll.device).view(1, B))
+                for vi, key in enumerate(chunk):
+                    for (mi, ri) in variants[key]:
+                        out[mi, li, ri] = wn[vi]
+        w = batch.weights.to(out.device)
+        self.total_nll += (out.double() * w).sum(-1).cpu()
+        self.n_tokens += float(batch.weights.sum())
+        self.windows_done += B
+        self.tokens_done += B * S
+        return out
+
+    # -------------------------------------------------------------- results
+    def ppl(self) -> torch.Tensor:
+        return torch.exp(self.total_nll / self.n_tokens)
+
+    def results(self) -> dict:
+        p = self.ppl()
+        return {
+            "methods": self.methods, "layers_of_interest": self.layers, "ratios": self.ratios, "codec": self.sc.codec,
+            "avg_ppl_results": [[[float(p[mi, li, ri]) for ri in range(len(self.ratios))]
+                                 for li in range(len(self.layers))] for mi in range(len(self.methods))],
+            "total_nll": self.total_nll.tolist(), "n_tokens": self.n_tokens, "windows": self.windows_done,
+            "wire_bytes_per_token": (self.wire_bytes / max(1, self.tokens_done)).tolist(),
+        }
+
+    def state(self) -> dict:
+        return {"total_nll": self.total_nll.tolist(), "n_tokens": self.n_tokens, "windows_done": self.windows_done,
+                "wire_bytes": self.wire_bytes.tolist(), "tokens_done": self.tokens_done}
+
+    def load_state(self, st: dict) -> None:
+        self.total_nll = torch.tensor(st["total_nll"], dtype=torch.float64)
+        self.n_tokens = float(st["n_tokens"])
+        self.windows_done = int(st["windows_done"])
+        self.wire_bytes = torch.tensor(st["wire_bytes"], dtype=torch.float64)
+        self.tokens_done = int(st.get("tokens_done", 0))
+
+
+def run_sweep(engine: SweepEngine, batch_iter, state: SweepState | None = None, log_every: int = 1000,
+              progress=None, reduce_fn=None) -> dict:
+    """Drive ``engine`` over batches with periodic checkpoint/resume."""
+    start_windows = 0
+    if state is not None:
+        saved = state.load()
+        if saved is not None:
+            engine.load_state(saved["engine"])
+            start_windows = saved["windows_done"]
+    t0 = time.perf_counter()
+    seen = 0
+    next_log = (engine.windows_done // log_every + 1) * log_every
+    for b in batch_iter:
+        if seen + b.B <= start_windows:   # already accounted for in the checkpoint
+            seen += b.B
+            continue
+        seen += b.B
+        b = b.to(engine.m.device)
+        engine.run_batch(b)
+        if progress:
+            progress(b.B)
+        if engine.windows_done >= next_log:
+            next_log += log_every
+            if state is not None:
+                state.save({"engine": engine.state(), "windows_done": seen})
+    if reduce_fn is not None:
+        reduce_fn(engine)
+    res = engine.results()
+    res["seconds"] = time.perf_counter() - t0
+    res["forward_tokens"] = engine.forward_tokens
+    return res

@@ -193,7 +193,7 @@ class DecoderLM:
     def layer(self, i: int, x: torch.Tensor, B: int, S: int, stats: str | None = None):
         """Run decoder layer ``i`` on ``x`` ([B*S, H], not modified).  Returns (y, AttnStats|None).
 
-        ``stats``: None, "lastrow" (P[S-1, :] per head) or "colsum" (column sums of P per head).
+        ``stats``: None, "lastrow" (P[S-1, :] per head), "colsum" (column sums of P per head) or a tuple of both.
         """
         cfg, L = self.cfg, self.layers[i]
         if L is None:
@@ -205,14 +205,15 @@ class DecoderLM:
             h, h2 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps)
         q, k, vt = ops.qkv_rope(h, L["wqkv"], L["bqkv"], self.cos, self.sin, B, S, Hq, Hkv, D, cfg.rotary_dim,
                                 self.q_scale)
-        o, lse = ops.attention(q, k, vt, S, need_lse=(stats == "colsum"))
+        kinds = () if stats is None else ((stats,) if isinstance(stats, str) else tuple(stats))
+        for kd in kinds:
+            if kd not in ("lastrow", "colsum"):
+                raise ValueError(kd)
+        o, lse = ops.attention(q, k, vt, S, need_lse=("colsum" in kinds))
         st = None
-        if stats == "lastrow":
-            st = AttnStats(lastrow=ops.attn_lastrow(q, k, S))
-        elif stats == "colsum":
-            st = AttnStats(colsum=ops.attn_colsum(q, k, lse, S))
-        elif stats is not None:
-            raise ValueError(stats)
+        if kinds:
+            st = AttnStats(lastrow=ops.attn_lastrow(q, k, S) if "lastrow" in kinds else None,
+                           colsum=ops.attn_colsum(q, k, lse, S) if "colsum" in kinds else None)
         if cfg.arch == "qwen2":
             y = ops.linear(o, L["wo"], residual=x)
             h = ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps)

@@ -1,0 +1,203 @@
+"""AttnLRP per-head relevance calibration (reference C8: ``Experiments/Relevance/main.py``,
+``Notebooks/attention_head_weights_via_relevance.ipynb``).
+
+The reference monkey-patches HF Qwen2 with ``lxt.efficient`` rules (``Relevance/main.py:41``),
+embeds each window with ``requires_grad``, runs a forward that returns the attention
+probabilities, seeds the backward with the max logit at the last position
+(``max_logit.backward(max_logit)``, ``:87-88``) and takes per-head relevance
+``sum_{i,j} A * dA/d..`` (``:96-103``), accumulated over windows and normalised per layer so each
+layer's heads sum to 1 (signed, ``:111-118``).
+
+``lxt`` is not available here, so the rules are re-implemented as autograd functions on this
+framework's own model weights ("efficient" LRP = Input x modified-Gradient):
+
+* linear layers, residual adds, RoPE: plain gradient (epsilon-LRP / Gradient x Input);
+* RMSNorm / LayerNorm: identity rule - the normaliser is treated as a constant (detached);
+* SiLU / GELU: identity rule - backward multiplies by f(x)/x instead of f'(x);
+* element-wise gate*up and the two attention matmuls (Q K^T, A V): uniform rule - each input
+  receives half of the Gradient x Input relevance (backward scaled by 0.5);
+* softmax: Gradient x Input of the softmax (the bias-free Taylor rule), -inf logits zeroed.
+
+Conservation (sum of input relevance ~ seeded logit) is checked by the tests on tiny models.
+This is an offline calibration pass; it runs on PyTorch ops (hipBLASLt on the GPU) in fp32.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import reference as R
+
+
+class _IdentityAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kind: str):
+        y = F.silu(x) if kind == "silu" else F.gelu(x)
+        ctx.save_for_backward(x, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        ratio = torch.where(x.abs() > 1e-6, y / torch.where(x.abs() > 1e-6, x, torch.ones_like(x)),
+                            torch.full_like(x, 0.5))
+        return g * ratio, None
+
+
+class _UniformMul(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return a * b
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        return 0.5 * g * b, 0.5 * g * a
+
+
+class _UniformMatmul(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return a @ b
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        return 0.5 * (g @ b.transpose(-1, -2)), 0.5 * (a.transpose(-1, -2) @ g)
+
+
+class _Softmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        s = torch.softmax(x, -1)
+        ctx.save_for_backward(s)
+        return s
+
+    @staticmethod
+    def backward(ctx, g):
+        (s,) = ctx.saved_tensors
+        gi = s * (g - (s * g).sum(-1, keepdim=True))
+        return gi
+
+
+def _rmsnorm_id(x, w, eps):
+    rstd = torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps).detach()
+    return x * rstd * w
+
+
+def _layernorm_id(x, w, b, eps):
+    mu = x.mean(-1, keepdim=True)
+    xc = x - mu
+    rstd = torch.rsqrt(xc.pow(2).mean(-1, keepdim=True) + eps).detach()
+    return xc * rstd * w + b
+
+
+def _lin(x, w, b=None):
+    y = x @ w.t()
+    return y + b if b is not None else y
+
+
+def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32):
+    """Differentiable forward with AttnLRP rules.  Returns (logits_last [V], embeds, attn_probs list)."""
+    cfg = model.cfg
+    f = lambda t: None if t is None else t.to(dtype)  # noqa: E731
+    B, S = ids.shape
+    Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
+    emb = f(model.w["embed"]).index_select(0, ids.reshape(-1).to(model.device)).detach().requires_grad_(True)
+    x = emb
+    cos, sin = model.cos[:S].to(dtype), model.sin[:S].to(dtype)
+    probs = []
+    for L in model.layers:
+        if cfg.arch == "qwen2":
+            h = _rmsnorm_id(x, f(L["ln1_w"]), cfg.norm_eps)
+        else:
+            h = _layernorm_id(x, f(L["ln1_w"]), f(L["ln1_b"]), cfg.norm_eps)
+            h2 = _layernorm_id(x, f(L["ln2_w"]), f(L["ln2_b"]), cfg.norm_eps)
+        y = _lin(h, f(L["wqkv"]), f(L["bqkv"])).view(B, S, Hq + 2 * Hkv, D).permute(0, 2, 1, 3)
+        q, k, v = y[:, :Hq], y[:, Hq:Hq + Hkv], y[:, Hq + Hkv:]
+        q = R.apply_rope(q, cos, sin, cfg.rotary_dim) * model.q_scale
+        k = R.apply_rope(k, cos, sin, cfg.rotary_dim)
+        k = k.repeat_interleave(Hq // Hkv, 1)
+        v = v.repeat_interleave(Hq // Hkv, 1)
+        sc = _UniformMatmul.apply(q, k.transpose(-1, -2))
+        mask = torch.ones(S, S, dtype=torch.bool, device=sc.device).triu(1)
+        sc = sc.masked_fill(mask, float("-inf"))
+        A = _Softmax.apply(sc)
+        A.retain_grad()
+        probs.append(A)
+        o = _UniformMatmul.apply(A, v).permute(0, 2, 1, 3).reshape(B * S, Hq * D)
+        if cfg.arch == "qwen2":
+            x = x + _lin(o, f(L["wo"]))
+            h = _rmsnorm_id(x, f(L["ln2_w"]), cfg.norm_eps)
+            g, u = R.deinterleave_gate_up(_lin(h, f(L["wgu"])))
+            x = x + _lin(_UniformMul.apply(_IdentityAct.apply(g, "silu"), u), f(L["wd"]))
+        else:
+            a = _lin(o, f(L["wo"]), f(L["bo"]))
+            mlp = _lin(_IdentityAct.apply(_lin(h2, f(L["wfc"]), f(L["bfc"])), "gelu"), f(L["wproj"]), f(L["bproj"]))
+            x = x + a + mlp
+    last = x.view(B, S, -1)[:, -1]
+    if cfg.arch == "qwen2":
+        hN = _rmsnorm_id(last, f(model.w["norm_w"]), cfg.norm_eps)
+    else:
+        hN = _layernorm_id(last, f(model.w["norm_w"]), f(model.w["norm_b"]), cfg.norm_eps)
+    logits = _lin(hN, f(model.w["head"]))
+    return logits, emb, probs
+
+
+def head_relevance(model, ids: torch.Tensor, dtype=torch.float32):
+    """Per-(layer, head) relevance of one window (B=1): sum_{i,j} A * dA, after seeding the max logit.
+
+    Returns (rel [layers, heads], input relevance sum, seed logit)."""
+    logits, emb, probs = lrp_forward(model, ids, dtype)
+    mx = logits[0].max()
+    mx.backward(mx.detach())
+    rel = torch.stack([(A * A.grad).sum(dim=(0, 2, 3)) for A in probs]).detach()
+    in_rel = (emb * emb.grad).sum().detach()
+    return rel, in_rel, mx.detach()
+
+
+def normalize_per_layer(rel: torch.Tensor) -> torch.Tensor:
+    return rel / rel.sum(-1, keepdim=True)
+
+
+def relevance_main(p) -> list:
+    """Entry point of Experiments/Relevance/main.py: writes attention_head_weights.json."""
+    import json
+
+    from ..config import dump_json
+    from ..eval.data import token_stream
+    from ..eval.windows import sliding_windows
+    from ..models import build_model, get_config
+    from ..parallel.dist import all_reduce_sum, get_env, init_distributed
+    from ..utils.logging import log, progress_bar
+    env = init_distributed(p.device)
+    device = str(env.device)
+    cfg = get_config(p.model or "qwen2-0.5b")
+    model, prov = build_model(cfg, device, torch.float32, weights=p.weights, seed=p.seed)
+    ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed)
+    wins = sliding_windows(ids.shape[1], p.max_length or 512, p.stride)
+    if p.max_windows:
+        wins = wins[: p.max_windows]
+    log(f"relevance: model={cfg.name} weights={prov} data={data_prov} windows={len(wins)}")
+    acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=device)
+    pb = progress_bar(len(wins), env.is_main)
+    for wi, w in enumerate(wins):
+        if wi % env.world_size != env.rank:
+            continue
+        rel, _, _ = head_relevance(model, ids[:, w.begin:w.end].to(device))
+        acc += rel.double()
+        pb.update(env.world_size)
+    pb.close()
+    all_reduce_sum(acc)
+    weights = normalize_per_layer(acc).float().cpu().tolist()
+    if env.is_main:
+        out = os.path.join(p.output_dir, "attention_head_weights.json")
+        dump_json(weights, out)
+        log(f"wrote {out}")
+    return weights

@@ -1,0 +1,33 @@
+"""Worker for multi-process pipeline tests (gloo on CPU; same code path as RCCL on GPUs)."""
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+
+def run(rank, world, port, pp, codec, ratio, method, out_path, split):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
+    from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows
+    from llm_inference_in_distributed_edge_networks_amd.models import TINY_QWEN2, build_model
+    from llm_inference_in_distributed_edge_networks_amd.parallel import (BoundaryConfig, DistributedPipeline, Grid,
+                                                                          PipelinePlan, init_distributed, shutdown)
+    env = init_distributed("cpu", timeout_s=120)
+    cfg = TINY_QWEN2
+    grid = Grid(world, pp)
+    plan = PipelinePlan.from_split_layers(cfg.num_layers, split) if split else PipelinePlan.balanced(cfg, pp, 128)
+    _, stage = grid.coords(rank)
+    model, _ = build_model(cfg, "cpu", torch.float32, seed=0, layers=plan.stage_layers(stage),
+                           with_embed=stage == 0, with_head=stage == pp - 1)
+    hw = torch.linspace(-1, 2, cfg.num_layers * cfg.num_heads).view(cfg.num_layers, cfg.num_heads)
+    pipe = DistributedPipeline(model, plan, BoundaryConfig(codec, ratio, method, hw), grid, rank)
+    toks = synthetic_stream(1500, cfg.vocab_size, 2)
+    acc, info = pipe.evaluate(list(batches(toks, sliding_windows(1500, 128, 32), 3)))
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump({"ppl": acc.ppl(), "n": acc.n_tokens}, f)
+    shutdown()

@@ -1,0 +1,62 @@
+"""N-stage pipeline over processes (gloo) == single-process split runner == same PPL."""
+import json
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
+from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows
+from llm_inference_in_distributed_edge_networks_amd.models import TINY_QWEN2, DecoderLM
+from llm_inference_in_distributed_edge_networks_amd.parallel import (BoundaryConfig, Grid, LocalPipeline,
+                                                                      PipelinePlan)
+
+import dist_worker
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def local_ppl(plan, codec, ratio, method):
+    m = DecoderLM.random_init(TINY_QWEN2, 0)
+    hw = torch.linspace(-1, 2, 16).view(4, 4)
+    pipe = LocalPipeline(m, plan, BoundaryConfig(codec, ratio, method, hw))
+    toks = synthetic_stream(1500, 512, 2)
+    return pipe.evaluate(batches(toks, sliding_windows(1500, 128, 32), 3)).ppl()
+
+
+@pytest.mark.parametrize("world,pp,codec,ratio,method,split", [
+    (2, 2, "mixed_int4_int8", 0.5, "regular_importance", [1]),
+    (2, 2, "ref_int4_global", 0.25, "last_row", [2]),
+    (4, 2, "int8_token", 0.0, "last_row", [1]),                 # pp2 x dp2
+    (4, 4, "mixed_int4_int8", 0.75, "aggregate_till", None),    # 4 stages, running-aggregate carry
+    (3, 3, "int4_token", 0.5, "weighted_importance", [0, 2]),
+])
+def test_distributed_equals_local(tmp_path, world, pp, codec, ratio, method, split):
+    out = tmp_path / "res.json"
+    mp.spawn(dist_worker.run, args=(world, free_port(), pp, codec, ratio, method, str(out), split), nprocs=world,
+             join=True)
+    res = json.loads(out.read_text())
+    plan = PipelinePlan.from_split_layers(4, split) if split else PipelinePlan.balanced(TINY_QWEN2, pp, 128)
+    ref = local_ppl(plan, codec, ratio, method)
+    assert abs(res["ppl"] - ref) / ref < 1e-6
+
+
+def test_grid_and_plan():
+    g = Grid(8, 2)
+    assert g.dp == 4 and g.coords(5) == (2, 1) and g.rank_of(2, 1) == 5
+    from llm_inference_in_distributed_edge_networks_amd.models import QWEN2_0_5B
+    p = PipelinePlan.balanced(QWEN2_0_5B, 2)
+    assert p.num_stages == 2 and p.boundary_layers()[0] in (11, 12)
+    p8 = PipelinePlan.balanced(QWEN2_0_5B, 8)
+    sizes = [len(p8.stage_layers(s)) for s in range(8)]
+    assert sum(sizes) == 24 and max(sizes) - min(sizes) <= 1
+    assert PipelinePlan.from_split_layers(24, [11]).stage_layers(1) == range(12, 24)
+    with pytest.raises(ValueError):
+        PipelinePlan.from_split_layers(24, [23])

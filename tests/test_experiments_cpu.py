@@ -1,0 +1,68 @@
+"""Reference entry points (Experiments/*/main.py + params.json) run end-to-end on tiny models (CPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_main(exp, params, tmp_path):
+    d = tmp_path / exp
+    d.mkdir()
+    base = {"dataset": "synthetic", "synthetic_tokens": 1200, "max_windows": 8, "device": "cpu",
+            "window_batch": 4, "output_dir": str(d)}
+    base.update(params)
+    (d / "params.json").write_text(json.dumps(base))
+    env = dict(os.environ, EDGE_NO_PROGRESS="1", WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "Experiments", exp, "main.py")], cwd=d, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return d
+
+
+def test_pythia_last_row(tmp_path):
+    d = run_main("Pythia-70M", {"model": "tiny-neox", "experiment": "last_row", "max_length": 128,
+                                "ratios": [0, 0.5, 1], "layers_of_interest": [1, 2],
+                                "methods": ["regular_importance", "last_row", "aggregate_till"]}, tmp_path)
+    res = json.loads((d / "avg_ppl_results_pythia_70m.json").read_text())
+    p = res["avg_ppl_results"]
+    assert len(p) == 3 and len(p[0]) == 2 and len(p[0][0]) == 3
+    assert p[0][0][0] == p[1][1][0]
+
+
+def test_pythia_initial(tmp_path):
+    d = run_main("Pythia-70M", {"model": "tiny-neox", "experiment": "initial", "max_length": 128,
+                                "ratios": [0, 5, 10],
+                                "layers_of_interest": [1, "aggregate upto 2", "maximum aggregation", "upto ratio"]},
+                 tmp_path)
+    res = json.loads((d / "exp_1.json").read_text())["exp_1"]
+    assert set(res) == {"1", "aggregate upto 2", "maximum aggregation", "upto ratio"}
+    assert len({round(v["0"], 9) for v in res.values()}) == 1   # ratio 0 is method independent
+
+
+def test_pythia_unknown_experiment(tmp_path):
+    with pytest.raises(AssertionError):
+        run_main("Pythia-70M", {"model": "tiny-neox", "experiment": "bogus"}, tmp_path)
+
+
+def test_qwen2_importance_and_relevance(tmp_path):
+    d = run_main("Relevance", {"model": "tiny-qwen2", "max_length": 64, "max_windows": 3}, tmp_path)
+    hw = json.loads((d / "attention_head_weights.json").read_text())
+    assert len(hw) == 4 and len(hw[0]) == 4
+    d2 = run_main("Qwen2-0.5B", {"model": "tiny-qwen2", "max_length": 128, "ratios": [0, 0.25, 1],
+                                 "layers_of_interest": [1, 2],
+                                 "methods": ["regular_importance", "weighted_importance", "last_row",
+                                             "aggregate_till"],
+                                 "head_weights": str(d / "attention_head_weights.json")}, tmp_path)
+    res = json.loads((d2 / "avg_ppl_results.json").read_text())
+    assert len(res["avg_ppl_results"]) == 4 and res["wire_bytes_per_token"][0][0][2] < res["wire_bytes_per_token"][0][0][0]
+
+
+def test_qwen2_channel(tmp_path):
+    d = run_main("Qwen2-0.5B", {"model": "tiny-qwen2", "max_length": 128, "layers_of_interest": [1, 3],
+                                "methods": ["channel_8", "channel_4", "channel_1_mean", "channel_1_max"]}, tmp_path)
+    res = json.loads((d / "avg_ppl_results_channel.json").read_text())
+    assert len(res["avg_ppl_results"]) == 2 and len(res["avg_ppl_results"][0]) == 4

@@ -1,0 +1,71 @@
+"""Own model implementations vs HF transformers (random-init tiny configs, fp32, CPU)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from llm_inference_in_distributed_edge_networks_amd.models import TINY_NEOX, TINY_QWEN2, DecoderLM, get_config
+from llm_inference_in_distributed_edge_networks_amd.models.configs import PYTHIA_70M, QWEN2_0_5B
+
+from helpers import hf_neox, hf_qwen2, ours_from_hf
+
+
+@pytest.mark.parametrize("cfg,mk", [(TINY_QWEN2, hf_qwen2), (TINY_NEOX, hf_neox)])
+def test_logits_match_hf(cfg, mk):
+    hf = mk(cfg)
+    ours = ours_from_hf(cfg, hf)
+    ids = torch.randint(0, cfg.vocab_size, (2, 50), generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        ref = hf(ids).logits
+    got = ours.logits(ours.forward_hidden(ids)).view_as(ref)
+    assert (got - ref).abs().max() < 1e-4
+
+
+@pytest.mark.parametrize("cfg,mk", [(TINY_QWEN2, hf_qwen2), (TINY_NEOX, hf_neox)])
+def test_row_nll_matches_hf_ce(cfg, mk):
+    hf = mk(cfg)
+    ours = ours_from_hf(cfg, hf)
+    ids = torch.randint(0, cfg.vocab_size, (1, 64), generator=torch.Generator().manual_seed(2))
+    with torch.no_grad():
+        ref = F.cross_entropy(hf(ids).logits[0, :-1], ids[0, 1:], reduction="none")
+    got = ours.row_nll(ours.forward_hidden(ids), torch.arange(63), ids[0, 1:])
+    assert (got - ref).abs().max() < 1e-4
+
+
+def test_layer_range_equals_monolithic():
+    m = DecoderLM.random_init(TINY_QWEN2, 3)
+    ids = torch.randint(0, 512, (2, 40))
+    full = m.forward_hidden(ids)
+    x = m.embed(ids)
+    for i in range(2):
+        x, _ = m.layer(i, x, 2, 40)
+    for i in range(2, 4):
+        x, _ = m.layer(i, x, 2, 40)
+    assert torch.equal(x, full)
+
+
+@pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX])
+def test_partial_stage_weights_identical(cfg):
+    full = DecoderLM.random_init(cfg, 7)
+    s1 = DecoderLM.random_init(cfg, 7, layers=range(2, 4), with_embed=False)
+    for i in range(2, 4):
+        for k, v in full.layers[i].items():
+            assert torch.equal(v, s1.layers[i][k])
+    assert s1.layers[0] is None
+    assert torch.equal(full.w["head"], s1.w["head"])
+
+
+def test_layer_does_not_modify_input():
+    m = DecoderLM.random_init(TINY_NEOX, 0)
+    x = torch.randn(2 * 30, 256)
+    x0 = x.clone()
+    m.layer(0, x, 2, 30)
+    assert torch.equal(x, x0)
+
+
+def test_presets():
+    q = get_config("Qwen/Qwen2-0.5B")
+    assert q is QWEN2_0_5B and q.qkv_size == 1152 and q.group_size == 7
+    assert 490e6 < q.num_params() < 500e6    # 494M params
+    p = get_config("pythia")
+    assert p is PYTHIA_70M and p.rotary_dim == 16 and p.parallel_residual
+    assert 69e6 < p.num_params() < 72e6

@@ -1,0 +1,52 @@
+"""Shared-prefix sweep engine == independent split runs; checkpoint/resume."""
+import json
+import os
+
+import torch
+
+from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
+from llm_inference_in_distributed_edge_networks_amd.eval.sweep import SweepConfig, SweepEngine, run_sweep
+from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows
+from llm_inference_in_distributed_edge_networks_amd.models import TINY_QWEN2, DecoderLM
+from llm_inference_in_distributed_edge_networks_amd.parallel import BoundaryConfig, LocalPipeline, PipelinePlan
+from llm_inference_in_distributed_edge_networks_amd.utils.checkpoint import SweepState
+
+M = DecoderLM.random_init(TINY_QWEN2, 0, std=0.06)
+TOK = synthetic_stream(1200, 512, 1)
+WINS = sliding_windows(1200, 128, 32)
+
+
+def test_sweep_equals_split_runner():
+    methods = ["regular_importance", "last_row", "aggregate_till", "weighted_importance"]
+    hw = torch.randn(4, 4)
+    sc = SweepConfig(methods, [0, 2], [0, 0.25, 0.5, 1], codec="ref_int4_global", head_weights=hw, max_fork_tokens=512)
+    res = run_sweep(SweepEngine(M, sc), batches(TOK, WINS, 4))
+    for mi, meth in enumerate(methods):
+        for li, L in enumerate([0, 2]):
+            for ri, r in enumerate([0, 0.25, 0.5, 1]):
+                pipe = LocalPipeline(M, PipelinePlan.from_split_layers(4, [L]),
+                                     BoundaryConfig("ref_int4_global", r, meth, hw))
+                ppl = pipe.evaluate(batches(TOK, WINS, 4)).ppl()
+                assert abs(ppl - res["avg_ppl_results"][mi][li][ri]) / ppl < 1e-6, (meth, L, r)
+    # ratio 0 identical across methods/layers, ratio 1 identical across methods
+    p = res["avg_ppl_results"]
+    assert len({round(p[mi][li][0], 9) for mi in range(4) for li in range(2)}) == 1
+    assert len({round(p[mi][0][3], 9) for mi in range(4)}) == 1
+
+
+def test_resume(tmp_path):
+    sc = SweepConfig(["last_row"], [1], [0, 0.5], codec="mixed_int4_int8")
+    full = run_sweep(SweepEngine(M, sc), batches(TOK, WINS, 2))
+    st = SweepState(str(tmp_path / "ck.json"), "h1")
+    e1 = SweepEngine(M, sc)
+    # interrupt after 3 batches
+    it = batches(TOK, WINS, 2)
+    part = [next(it) for _ in range(3)]
+    run_sweep(e1, iter(part), st, log_every=2)
+    assert os.path.exists(tmp_path / "ck.json")
+    e2 = SweepEngine(M, sc)
+    res = run_sweep(e2, batches(TOK, WINS, 2), st, log_every=2)
+    assert abs(res["avg_ppl_results"][0][0][1] - full["avg_ppl_results"][0][0][1]) < 1e-9
+    assert res["windows"] == full["windows"]
+    # different config hash -> not resumed
+    assert SweepState(str(tmp_path / "ck.json"), "other").load() is None

@@ -1,0 +1,74 @@
+"""Time the gfx950 GEMM kernel (all model shapes/epilogues) against torch.matmul (hipBLASLt) on random data.
+
+Interleaved rounds in one process (guide §5.4 rule 24); prints median TFLOP/s per shape."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llm_inference_in_distributed_edge_networks_amd import ops  # noqa: E402
+
+SHAPES = {  # name: (M, N, K, act, bias, resid)
+    "qkv": (8192, 1152, 896, None, True, False),
+    "o_proj": (8192, 896, 896, None, False, True),
+    "gate_up": (8192, 9728, 896, "swiglu_il", False, False),
+    "down": (8192, 896, 4864, None, False, True),
+    "lm_head": (512, 151936, 896, None, False, False),
+    "big": (8192, 8192, 8192, None, False, False),
+}
+
+
+def timeit(fn, iters):
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(iters):
+        fn()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--m", type=int, default=0, help="override M")
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    dev = "cuda"
+    res = {}
+    for name, (M, N, K, act, bias, resid) in SHAPES.items():
+        M = a.m or M if name != "lm_head" else M
+        x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        b = torch.randn(N, device=dev).to(torch.bfloat16) if bias else None
+        No = N // 2 if act == "swiglu_il" else N
+        r = torch.randn(M, No, device=dev).to(torch.bfloat16) if resid else None
+        out = torch.empty(M, No, device=dev, dtype=torch.bfloat16)
+        ours = lambda: ops.linear(x, w, bias=b, residual=r, act=act, out=out)  # noqa: E731
+        lib = lambda: torch.matmul(x, w.t())  # noqa: E731
+        for _ in range(3):
+            ours(); lib()
+        t_o, t_l = [], []
+        for _ in range(a.rounds):
+            t_o.append(timeit(ours, a.iters))
+            t_l.append(timeit(lib, a.iters))
+        fl = 2.0 * M * N * K
+        res[name] = {"M": M, "N": N, "K": K, "ours_us": statistics.median(t_o) * 1e6,
+                     "hipblaslt_us": statistics.median(t_l) * 1e6,
+                     "ours_tflops": fl / statistics.median(t_o) / 1e12,
+                     "hipblaslt_tflops": fl / statistics.median(t_l) / 1e12}
+        print(f"{name:8s} M={M:6d} N={N:6d} K={K:5d}  ours {res[name]['ours_us']:8.1f}us "
+              f"{res[name]['ours_tflops']:7.1f} TF | hipBLASLt (plain, no epilogue) {res[name]['hipblaslt_us']:8.1f}us "
+              f"{res[name]['hipblaslt_tflops']:7.1f} TF", flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
