@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--model", default="qwen2-0.5b")
-    p.add_argument("--batch", type=int, default=16, help="windows per micro-batch")
+    p.add_argument("--batch", type=int, default=32, help="windows per micro-batch")
     p.add_argument("--microbatches", type=int, default=4, help="micro-batches per step per replica")
     p.add_argument("--max-length", type=int, default=512)
     p.add_argument("--stride", type=int, default=32)

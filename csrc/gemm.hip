@@ -29,39 +29,61 @@ struct GemmArgs {
   const int64_t* targets; float* part_max; float* part_sum; float* tgt_logit; int nparts;
 };
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int TILE_BYTES = BM * BK * 2;          // 16 KiB per operand per stage
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;      // A + B
+constexpr int BK = 64;
 constexpr int GROUP_M = 8;
+
+// Tile configurations: every wave owns a (MI*16) x 64 output slab (the 64-wide column slab is what
+// the QKV/RoPE (one head) and SwiGLU (gate/up pairs) epilogues rely on).
+template <int BM_, int BN_, int NWM_, int NWN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, NWM = NWM_, NWN = NWN_;
+  static constexpr int NW = NWM * NWN, NT = 64 * NW;
+  static constexpr int WTM = BM / NWM, MI = WTM / 16;
+  static_assert(BN / NWN == 64, "wave column slab must be 64");
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW;  // 1-KiB glds per wave per K-tile
+  static constexpr int LDS = 2 * STAGE;
+};
+using C128 = Cfg<128, 128, 2, 2>;   // 4 waves, 64 KiB LDS, 2 blocks/CU
+using C256 = Cfg<256, 256, 2, 4>;   // 8 waves, 128 KiB LDS, 1 block/CU
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
-__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int ld, int row0, int row_max, int k0,
-                                           char* lds, int wave, int lane) {
-  // 16 wave-instructions cover the 128x64 tile (8 rows x 128 B each); this wave issues 4 of them.
+// Per-lane source pointers of this wave's staging instructions (hoisted out of the K loop): instruction
+// i of wave w writes LDS rows [8*(i*NW+w), +8) of the tile, lane l -> row +l/8, physical 16-B chunk l%8,
+// which holds logical chunk (l%8) ^ swz(row) (swizzle applied on the source side, LDS image lane-linear).
+template <int NI, int NW>
+__device__ __forceinline__ void stage_ptrs(const bf16_t* __restrict__ src, int ld, int row0, int row_max, int wave,
+                                           int lane, const bf16_t* (&p)[NI]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int blk = i * 4 + wave;
+  for (int i = 0; i < NI; ++i) {
+    const int blk = i * NW + wave;
     const int r = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz(r);
     int gr = row0 + r;
     gr = gr < row_max ? gr : row_max - 1;
-    glds16(src + (size_t)gr * ld + k0 + c * 8, lds + blk * 1024);
+    p[i] = src + (size_t)gr * ld + c * 8;
   }
+}
+template <int NI, int NW>
+__device__ __forceinline__ void stage_issue(const bf16_t* const (&p)[NI], int k0, char* lds, int wave) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) glds16(p[i] + k0, lds + (i * NW + wave) * 1024);
 }
 
 __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
   return *(const bf16x8_t*)(lds + r * 128 + ((c ^ swz(r)) << 4));
 }
 
-template <int EPI, int RH = 0>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
+template <int EPI, int RH, class CF>
+__global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = CF::BM, BN = CF::BN, MI = CF::MI, NW = CF::NW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / CF::NWN, wn = wave % CF::NWN;
 
   // ---- tile scheduling: XCD remap, then grouped-M order ---------------------------------------
   const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
@@ -75,37 +97,55 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
   const int tile_n = in_g / gsz;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  const bf16_t* pa[CF::A_INSTR];
+  const bf16_t* pb[CF::B_INSTR];
+  stage_ptrs<CF::A_INSTR, NW>(a.A, a.lda, m0, a.M, wave, lane, pa);
+  stage_ptrs<CF::B_INSTR, NW>(a.B, a.ldb, n0, a.N, wave, lane, pb);
+  // fragment row offsets in the swizzled LDS image (loop invariant)
+  int aoff[2][MI], boff[2][4];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int r = wm * CF::WTM + i * 16 + (lane & 15);
+      aoff[ks][i] = r * 128 + ((c ^ swz(r)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = wn * 64 + j * 16 + (lane & 15);
+      boff[ks][j] = CF::A_BYTES + r * 128 + ((c ^ swz(r)) << 4);
+    }
+  }
+
   const int nk = a.K / BK;
-  stage_tile(a.A, a.lda, m0, a.M, 0, smem, wave, lane);
-  stage_tile(a.B, a.ldb, n0, a.N, 0, smem + TILE_BYTES, wave, lane);
+  stage_issue<CF::A_INSTR, NW>(pa, 0, smem, wave);
+  stage_issue<CF::B_INSTR, NW>(pb, 0, smem + CF::A_BYTES, wave);
   wait_vmcnt0();
   __syncthreads();
 
   for (int t = 0; t < nk; ++t) {
-    char* cur = smem + (t & 1) * STAGE_BYTES;
+    const char* cur = smem + (t & 1) * CF::STAGE;
     if (t + 1 < nk) {
-      char* nxt = smem + ((t + 1) & 1) * STAGE_BYTES;
-      stage_tile(a.A, a.lda, m0, a.M, (t + 1) * BK, nxt, wave, lane);
-      stage_tile(a.B, a.ldb, n0, a.N, (t + 1) * BK, nxt + TILE_BYTES, wave, lane);
+      char* nxt = smem + ((t + 1) & 1) * CF::STAGE;
+      stage_issue<CF::A_INSTR, NW>(pa, (t + 1) * BK, nxt, wave);
+      stage_issue<CF::B_INSTR, NW>(pb, (t + 1) * BK, nxt + CF::A_BYTES, wave);
     }
-    const char* la = cur;
-    const char* lb = cur + TILE_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8_t af[4], bfr[4];
-      const int c = ks * 4 + (lane >> 4);
+      bf16x8_t af[MI], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag(la, wm * 64 + i * 16 + (lane & 15), c);
+      for (int i = 0; i < MI; ++i) af[i] = *(const bf16x8_t*)(cur + aoff[ks][i]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag(lb, wn * 64 + j * 16 + (lane & 15), c);
+      for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8_t*)(cur + boff[ks][j]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
@@ -120,8 +160,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
 
   if constexpr (EPI == EPI_LSE) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
       float mx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -162,8 +202,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
     const int head = nw / 64;  // global head slot in [q heads | k heads | v heads]
     const bool is_v = head >= a.Hq + a.Hkv;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
       const int mm = m < a.M ? m : a.M - 1;
       const int b = mm / a.S, pos = mm - b * a.S;
       float v[4][4];
@@ -248,8 +288,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
   }
 
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+  for (int i = 0; i < MI; ++i) {
+    const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
     if (m >= a.M) continue;
     if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
@@ -289,16 +329,38 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs a) {
   }
 }
 
+static int g_tile_override = 0;  // 0 auto, 128 or 256 (tests / tuning)
+
+template <int EPI, int RH, class CF>
+static int launch_cfg(const GemmArgs& a, hipStream_t st) {
+  const int tm = (a.M + CF::BM - 1) / CF::BM, tn = a.N / CF::BN;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, RH, CF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        CF::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, RH, CF>), dim3(tm * tn), dim3(CF::NT), CF::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
 template <int EPI, int RH = 0>
 static int launch(const GemmArgs& a, hipStream_t st) {
-  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
-  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, RH>), dim3(tm * tn), dim3(256), 2 * STAGE_BYTES, st, a);
-  return (int)hipGetLastError();
+  // 256x256 tiles when the shape can fill the chip with them (halves L2->LDS traffic per FLOP),
+  // 128x128 otherwise (N not a multiple of 256, or too few 256-row panels).
+  const bool big = (a.N % 256 == 0) && ((long long)((a.M + 255) / 256) * (a.N / 256) >= 256);
+  const bool use256 = g_tile_override ? g_tile_override == 256 && a.N % 256 == 0 : big;
+  return use256 ? launch_cfg<EPI, RH, C256>(a, st) : launch_cfg<EPI, RH, C128>(a, st);
+}
+
+EDGE_API int edge_gemm_set_tile(int t) {
+  g_tile_override = t;
+  return 0;
 }
 
 static int check_shapes(const GemmArgs& a) {
   if (a.M <= 0) return -1;
-  if (a.N % BN || a.K % BK || a.N <= 0 || a.K <= 0) return (int)hipErrorInvalidValue;
+  if (a.N % 128 || a.K % BK || a.N <= 0 || a.K <= 0) return (int)hipErrorInvalidValue;
   if (a.lda % 8 || a.ldb % 8) return (int)hipErrorInvalidValue;
   return 0;
 }

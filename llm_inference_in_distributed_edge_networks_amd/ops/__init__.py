@@ -85,6 +85,11 @@ def layernorm_dual(x, w1, b1, w2, b2, eps):
     return y1, y2
 
 
+def set_gemm_tile(tile: int) -> None:
+    """Force the GEMM block tile (128 or 256; 0 = automatic by shape).  Tuning / tests only."""
+    call("edge_gemm_set_tile", int(tile))
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, out=None) -> torch.Tensor:
     """``act(x @ w.T + bias) + residual`` on MFMA (``residual`` may alias ``out``)."""
     if not _gpu(x):

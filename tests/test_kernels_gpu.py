@@ -57,9 +57,21 @@ def test_layernorm_dual():
     close(y2, r2, atol=3e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 1152, 896), (300, 896, 896), (1000, 256, 512), (64, 128, 4864)])
+@pytest.mark.parametrize("M,N,K", [(512, 1152, 896), (300, 896, 896), (1000, 256, 512), (64, 128, 4864),
+                                   (700, 1024, 640)])
 @pytest.mark.parametrize("epi", ["none", "bias", "resid", "bias_resid", "gelu", "swiglu"])
-def test_gemm(M, N, K, epi):
+@pytest.mark.parametrize("tile", [128, 256])
+def test_gemm(M, N, K, epi, tile):
+    if tile == 256 and N % 256:
+        pytest.skip("256 tile needs N % 256 == 0")
+    ops.set_gemm_tile(tile)
+    try:
+        _gemm_case(M, N, K, epi)
+    finally:
+        ops.set_gemm_tile(0)
+
+
+def _gemm_case(M, N, K, epi):
     x = rnd(M, K, seed=10)
     w = rnd(N, K, s=1 / math.sqrt(K), seed=11)
     b = rnd(N, s=0.5, seed=12)
@@ -73,12 +85,15 @@ def test_gemm(M, N, K, epi):
     close(y, ref, atol=3e-2, rtol=2e-2)
 
 
-def test_gemm_asymmetric_identity():
+@pytest.mark.parametrize("tile", [128, 256])
+def test_gemm_asymmetric_identity(tile):
     # A = I, asymmetric B: catches a transposed C-write
-    K = 128
+    K = 256
     x = torch.eye(K, dtype=torch.bfloat16)
-    w = torch.arange(256 * K, dtype=torch.float32).reshape(256, K).remainder(97).sub(48).to(torch.bfloat16)
+    w = torch.arange(512 * K, dtype=torch.float32).reshape(512, K).remainder(97).sub(48).to(torch.bfloat16)
+    ops.set_gemm_tile(tile)
     y = ops.linear(x.to(DEV), w.to(DEV))
+    ops.set_gemm_tile(0)
     assert torch.equal(y.cpu().float(), w.t().float())
 
 
@@ -92,7 +107,8 @@ def test_gemm_inplace_residual():
     close(rd, ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("S,Hq,Hkv,rot", [(512, 14, 2, 64), (100, 4, 2, 64), (130, 8, 8, 16), (64, 4, 4, 32)])
+@pytest.mark.parametrize("S,Hq,Hkv,rot", [(512, 14, 2, 64), (100, 4, 2, 64), (130, 8, 8, 16), (64, 4, 4, 32),
+                                          (256, 12, 2, 64)])
 def test_qkv_rope(S, Hq, Hkv, rot):
     B, D, Hd = 2, 64, 256
     cos, sin = R.rope_tables(1024, rot, 1e4 if rot < 64 else 1e6)

@@ -38,10 +38,15 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--m", type=int, default=0, help="override M")
     ap.add_argument("--json", default="")
+    ap.add_argument("--only", default="", help="comma list of shapes")
+    ap.add_argument("--tiles", default="0", help="comma list of forced tiles (0=auto,128,256)")
+    ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt comparison (profiling)")
     a = ap.parse_args()
     dev = "cuda"
     res = {}
     for name, (M, N, K, act, bias, resid) in SHAPES.items():
+        if a.only and name not in a.only.split(","):
+            continue
         M = a.m or M if name != "lm_head" else M
         x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
@@ -49,15 +54,29 @@ def main():
         No = N // 2 if act == "swiglu_il" else N
         r = torch.randn(M, No, device=dev).to(torch.bfloat16) if resid else None
         out = torch.empty(M, No, device=dev, dtype=torch.bfloat16)
-        ours = lambda: ops.linear(x, w, bias=b, residual=r, act=act, out=out)  # noqa: E731
+        tiles = [int(t) for t in a.tiles.split(",")]
+
+        def mk(tile):
+            def f():
+                ops.set_gemm_tile(tile)
+                ops.linear(x, w, bias=b, residual=r, act=act, out=out)
+            return f
+        variants = {t: mk(t) for t in tiles}
+        ours = variants[tiles[0]]
         lib = lambda: torch.matmul(x, w.t())  # noqa: E731
         for _ in range(3):
             ours(); lib()
         t_o, t_l = [], []
+        t_v = {t: [] for t in tiles}
         for _ in range(a.rounds):
-            t_o.append(timeit(ours, a.iters))
-            t_l.append(timeit(lib, a.iters))
+            for t, f in variants.items():
+                t_v[t].append(timeit(f, a.iters))
+            t_o.append(min(statistics.median(v) for v in t_v.values()))
+            t_l.append(timeit(lib, a.iters) if not a.no_lib else 1.0)
+        ops.set_gemm_tile(0)
         fl = 2.0 * M * N * K
+        for t, v in t_v.items():
+            print(f"   tile={t:3d}: {statistics.median(v)*1e6:8.1f}us {fl/statistics.median(v)/1e12:7.1f} TF", flush=True)
         res[name] = {"M": M, "N": N, "K": K, "ours_us": statistics.median(t_o) * 1e6,
                      "hipblaslt_us": statistics.median(t_l) * 1e6,
                      "ours_tflops": fl / statistics.median(t_o) / 1e12,
