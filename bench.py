@@ -89,9 +89,16 @@ def main():
     pool = [b.to(dev) for b in pool]
     nll_acc = torch.zeros(2, dtype=torch.float64, device=dev)
 
-    def step(si: int):
-        base = (si * a.microbatches * grid.dp) % max(1, len(pool) - a.microbatches * grid.dp)
-        mbs = pool[base: base + a.microbatches * grid.dp]
+    per_step = a.microbatches * grid.dp
+
+    def mbs_for(first_step: int, nsteps: int):
+        return [pool[(first_step * per_step + i) % len(pool)] for i in range(nsteps * per_step)]
+
+    def run_steps(first_step: int, nsteps: int):
+        """nsteps consecutive steps.  pp=1: micro-batch by micro-batch on the local 2-stage pipeline.
+        pp>1: one continuous pipeline over all nsteps*microbatches (stages stay busy across step
+        boundaries; the only fill/drain is at the ends of the timed region)."""
+        mbs = mbs_for(first_step, nsteps)
         if pp == 1:
             for b in mbs:
                 wn = runner.run_batch(b)
@@ -110,13 +117,11 @@ def main():
             if dev.type == "cuda":
                 torch.cuda.synchronize()
 
-    for i in range(a.warmup):
-        step(i)
+    run_steps(0, a.warmup)
     sync()
     nll_acc.zero_()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i)
+    run_steps(a.warmup, a.steps)
     sync()
     dt = time.perf_counter() - t0
     if env.is_dist:

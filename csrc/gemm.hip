@@ -43,6 +43,7 @@ struct Cfg {
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   static constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW;  // 1-KiB glds per wave per K-tile
   static constexpr int LDS = 2 * STAGE;
+  static constexpr bool PIPE = MI >= 8;  // register-pipelined fragments (1 block/CU configs)
 };
 using C128 = Cfg<128, 128, 2, 2>;   // 4 waves, 64 KiB LDS, 2 blocks/CU
 using C256 = Cfg<256, 256, 2, 4>;   // 8 waves, 128 KiB LDS, 1 block/CU
@@ -107,22 +108,38 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
   const bf16_t* pb[CF::B_INSTR];
   stage_ptrs<CF::A_INSTR, NW>(a.A, a.lda, m0, a.M, wave, lane, pa);
   stage_ptrs<CF::B_INSTR, NW>(a.B, a.ldb, n0, a.N, wave, lane, pb);
-  // fragment row offsets in the swizzled LDS image (loop invariant)
-  int aoff[2][MI], boff[2][4];
+  // Fragment addresses in the swizzled LDS image.  The swizzle of row r is (r>>1)&7 and every fragment
+  // row is lane&15 plus a multiple of 16, so it depends on the lane only: one base per k-half, the
+  // m/n tile offsets are immediates (2 KiB per 16 rows).
+  const int sw = ((lane & 15) >> 1) & 7;
+  int abase[2], bbase[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int c = ks * 4 + (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int r = wm * CF::WTM + i * 16 + (lane & 15);
-      aoff[ks][i] = r * 128 + ((c ^ swz(r)) << 4);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = wn * 64 + j * 16 + (lane & 15);
-      boff[ks][j] = CF::A_BYTES + r * 128 + ((c ^ swz(r)) << 4);
-    }
+    abase[ks] = (wm * CF::WTM + (lane & 15)) * 128 + ((c ^ sw) << 4);
+    bbase[ks] = CF::A_BYTES + (wn * 64 + (lane & 15)) * 128 + ((c ^ sw) << 4);
   }
+
+  // Sub-steps of a K-tile: s = (ks, mg) with ks the 32-wide k half and mg a group of 4 m-tiles, each
+  // 16 MFMAs.  Fragments are double-buffered in registers (sets X/Y): the LDS reads of sub-step s+1 are
+  // in flight while the MFMAs of sub-step s issue.  One barrier per K-tile (in the last sub-step) makes
+  // the next tile's DMA visible and retires every wave's reads of the current buffer before it is
+  // restaged (RAW: own vmcnt(0) + barrier; WAR: own lgkmcnt(0) + barrier).
+  constexpr int MG = MI / 4, NS = 2 * MG;
+  bf16x8_t XA[4], XB[4], YA[4], YB[4];
+  auto ld = [&](bf16x8_t(&FA)[4], bf16x8_t(&FB)[4], const char* buf, int ks, int mg) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) FA[i] = *(const bf16x8_t*)(buf + abase[ks] + (mg * 4 + i) * 2048);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) FB[j] = *(const bf16x8_t*)(buf + bbase[ks] + j * 2048);
+  };
+  auto mma = [&](const bf16x8_t(&FA)[4], const bf16x8_t(&FB)[4], int mg) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[mg * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[mg * 4 + i][j], 0, 0, 0);
+  };
 
   const int nk = a.K / BK;
   stage_issue<CF::A_INSTR, NW>(pa, 0, smem, wave);
@@ -130,28 +147,58 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
   wait_vmcnt0();
   __syncthreads();
 
-  for (int t = 0; t < nk; ++t) {
-    const char* cur = smem + (t & 1) * CF::STAGE;
-    if (t + 1 < nk) {
+  if constexpr (!CF::PIPE) {
+    // 2 sub-steps per K-tile, fragments read right before use (several blocks per CU hide the latency)
+    for (int t = 0; t < nk; ++t) {
+      const char* cur = smem + (t & 1) * CF::STAGE;
+      if (t + 1 < nk) {
+        char* nxt = smem + ((t + 1) & 1) * CF::STAGE;
+        stage_issue<CF::A_INSTR, NW>(pa, (t + 1) * BK, nxt, wave);
+        stage_issue<CF::B_INSTR, NW>(pb, (t + 1) * BK, nxt + CF::A_BYTES, wave);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int mg = 0; mg < MG; ++mg) {
+          ld(XA, XB, cur, ks, mg);
+          mma(XA, XB, mg);
+        }
+      }
+      wait_vmcnt0();
+      __syncthreads();
+    }
+  } else {
+    ld(XA, XB, smem, 0, 0);
+    for (int t = 0; t < nk; ++t) {
+      const char* cur = smem + (t & 1) * CF::STAGE;
       char* nxt = smem + ((t + 1) & 1) * CF::STAGE;
-      stage_issue<CF::A_INSTR, NW>(pa, (t + 1) * BK, nxt, wave);
-      stage_issue<CF::B_INSTR, NW>(pb, (t + 1) * BK, nxt + CF::A_BYTES, wave);
+      const bool more = t + 1 < nk;
+  #pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (s == 0 && more) {
+          stage_issue<CF::A_INSTR, NW>(pa, (t + 1) * BK, nxt, wave);
+          stage_issue<CF::B_INSTR, NW>(pb, (t + 1) * BK, nxt + CF::A_BYTES, wave);
+        }
+        const int mg = s % MG;
+        if (s + 1 < NS) {
+          const int ks1 = (s + 1) / MG, mg1 = (s + 1) % MG;
+          if (s & 1) ld(XA, XB, cur, ks1, mg1); else ld(YA, YB, cur, ks1, mg1);
+        } else {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          if (more) {
+            if (s & 1) ld(XA, XB, nxt, 0, 0); else ld(YA, YB, nxt, 0, 0);
+          }
+        }
+        // keep the next sub-step's LDS reads ahead of this sub-step's MFMAs (the scheduler would
+        // otherwise sink them below the MFMAs and wait lgkmcnt(0), serialising reads and math)
+        __builtin_amdgcn_sched_barrier(0);
+        // this sub-step's 8 fragments were issued one sub-step ago; leave the 8 just issued in flight
+        if (s + 1 < NS) __builtin_amdgcn_s_waitcnt(0xC87F);  // lgkmcnt(8)
+        if (s & 1) mma(YA, YB, mg); else mma(XA, XB, mg);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8_t af[MI], bfr[4];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = *(const bf16x8_t*)(cur + aoff[ks][i]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8_t*)(cur + boff[ks][j]);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-    wait_vmcnt0();
-    __syncthreads();
   }
 
   // ---- epilogue -------------------------------------------------------------------------------

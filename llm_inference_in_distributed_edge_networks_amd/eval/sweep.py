@@ -32,7 +32,7 @@ from .. import codec as C
 from ..importance import ImportanceTracker, canonical
 from ..models.model import DecoderLM
 from ..utils.checkpoint import SweepState
-from .windows import WindowBatch, window_nll
+from .windows import WindowBatch, segment_mean, window_nll
 
 
 @dataclass
@@ -101,12 +101,14 @@ class SweepEngine:
             for mi, meth in enumerate(self.methods):
                 for ri, r in enumerate(self.ratios):
                     k = self._k(r, S)
-                    if k == 0 and self.spec.uses_ratio:
+                    # no lo tokens and an exact hi class (reference Q1 "ratio 0"): the unquantized base
+                    if k == 0 and self.spec.uses_ratio and self.spec.hi_fmt == C.wire.NATIVE:
                         out[mi, li, ri] = base
                         self.wire_bytes[mi, li, ri] += C.message_bytes(C.get_codec("passthrough"), B, S,
                                                                        m.cfg.hidden_size, 0.0, m.dtype)
                         continue
-                    key = ("all", k) if (k >= S or not self.spec.needs_importance) else (meth, k)
+                    method_free = k >= S or k == 0 or not self.spec.needs_importance
+                    key = ("all", k) if method_free else (meth, k)
                     variants.setdefault(key, []).append((mi, ri))
             keys = list(variants)
             per_fork = max(1, self.sc.max_fork_tokens // (B * S))
@@ -128,10 +130,7 @@ class SweepEngine:
                 off = (torch.arange(V, device=batch.rows.device) * (B * S)).repeat_interleave(batch.rows.numel())
                 rows = batch.rows.repeat(V) + off
                 nll = m.row_nll(x, rows, batch.targets.repeat(V))
-                s = torch.zeros(V * B, dtype=torch.float32, device=nll.device)
-                s.index_add_(0, batch.row_window.repeat(V) + torch.arange(V, device=nll.device).repeat_interleave(
-                    batch.rows.numel()) * B, nll.float())
-                wn = (s.view(V, B) / batch.n_rows.to(nll.device).view(1, B))
+                wn = segment_mean(nll, batch.n_rows.to(nll.device).repeat(V)).view(V, B)
                 for vi, key in enumerate(chunk):
                     for (mi, ri) in variants[key]:
                         out[mi, li, ri] = wn[vi]

@@ -114,11 +114,19 @@ def batches(tokens: torch.Tensor, wins: list, batch_size: int):
         yield make_batch(tokens, cur)
 
 
+def segment_mean(values: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
+    """Mean of consecutive segments of ``values`` (lengths ``counts``), bitwise deterministic on GPU:
+    an fp64 prefix sum instead of float atomics (``index_add_``)."""
+    cs = torch.cumsum(values.double(), 0)
+    ends = torch.cumsum(counts.to(torch.int64), 0) - 1
+    tot = cs.index_select(0, ends)
+    prev = torch.cat([tot.new_zeros(1), tot[:-1]])
+    return ((tot - prev) / counts.double()).float()
+
+
 def window_nll(row_nll: torch.Tensor, batch: WindowBatch) -> torch.Tensor:
-    """Per-window mean CE over its scored rows: [B] fp32 on the row_nll device."""
-    s = torch.zeros(batch.B, dtype=torch.float32, device=row_nll.device)
-    s.index_add_(0, batch.row_window, row_nll.float())
-    return s / batch.n_rows.to(row_nll.device)
+    """Per-window mean CE over its scored rows (rows are grouped by window): [B] fp32."""
+    return segment_mean(row_nll, batch.n_rows.to(row_nll.device))
 
 
 class PPLAccumulator:

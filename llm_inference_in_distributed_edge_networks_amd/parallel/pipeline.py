@@ -27,6 +27,7 @@ from .. import codec as C
 from ..eval.windows import PPLAccumulator, WindowBatch, window_nll
 from ..importance import ImportanceTracker, canonical
 from ..models.model import DecoderLM
+from ..utils.graphs import GraphCache
 from .dist import Grid, all_reduce_sum
 from .plan import PipelinePlan
 
@@ -96,9 +97,33 @@ class StageRunner:
 
     def encode(self, x, batch: WindowBatch, imp, out=None):
         msg, L = C.encode(x, self.bcfg.spec, batch.B, batch.S, self.bcfg.ratio, imp, out=out)
-        self.stats.wire_bytes += L.total
-        self.stats.wire_tokens += batch.B * batch.S
         return msg, L
+
+    def account(self, batch: WindowBatch) -> None:
+        """Wire-byte accounting of the outgoing boundary (outside any captured graph)."""
+        if not self.last:
+            self.stats.wire_bytes += self.layout(batch).total
+            self.stats.wire_tokens += batch.B * batch.S
+        self.stats.windows += batch.B
+        self.stats.tokens += batch.tokens
+
+    def forward(self, ids, rows, targets, row_window, n_rows, msg_in=None, carry_in=None):
+        """Graph-capturable stage step on tensors only.
+
+        Non-last stage -> (msg_out, carry_out or empty); last stage -> per-window NLL [B]."""
+        b = WindowBatch(ids, None, rows, targets, row_window, n_rows, None)
+        x = None
+        if not self.first:
+            L = self.layout_in(b)
+            x = C.decode(msg_in, self.bcfg.spec, L, self.model.dtype)
+        x, imp, c = self.run(b, x, carry_in if (carry_in is not None and carry_in.numel()) else None)
+        if self.last:
+            return self.finish(x, b)
+        msg, _ = self.encode(x, b, imp)
+        return msg, (c if c is not None else torch.empty(0, device=msg.device))
+
+    def layout_in(self, batch) -> C.Layout:
+        return self.layout(batch)
 
     def layout(self, batch: WindowBatch) -> C.Layout:
         spec = self.bcfg.spec
@@ -112,22 +137,29 @@ class StageRunner:
 
 
 class LocalPipeline:
-    """All stages in one process.  ``run_batch`` is the split runner of the reference."""
+    """All stages in one process.  ``run_batch`` is the split runner of the reference.
 
-    def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig):
+    On a GPU the whole multi-stage step (all layers, importance, boundary encode/decode, head) is
+    captured into one HIP graph per batch signature (``use_graphs``)."""
+
+    def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig, use_graphs: bool = True):
         self.model, self.plan, self.bcfg = model, plan, bcfg
         self.stages = [StageRunner(model, plan, s, bcfg) for s in range(plan.num_stages)]
+        self.graphs = GraphCache(self._step, enabled=use_graphs and model.device.type == "cuda")
+
+    def _step(self, ids, rows, targets, row_window, n_rows):
+        msg = carry = None
+        for st in self.stages:
+            out = st.forward(ids, rows, targets, row_window, n_rows, msg, carry)
+            if st.last:
+                return out
+            msg, carry = out
+        raise AssertionError
 
     def run_batch(self, batch: WindowBatch) -> torch.Tensor:
-        x, carry = None, None
         for st in self.stages:
-            x, imp, c = st.run(batch, x, carry)
-            if st.last:
-                return st.finish(x, batch)
-            msg, L = st.encode(x, batch, imp)
-            x = C.decode(msg, self.bcfg.spec, L, self.model.dtype)
-            carry = c
-        raise AssertionError
+            st.account(batch)
+        return self.graphs(batch.ids, batch.rows, batch.targets, batch.row_window, batch.n_rows)
 
     def evaluate(self, batches, acc: PPLAccumulator | None = None, on_batch=None) -> PPLAccumulator:
         acc = acc or PPLAccumulator()
@@ -146,7 +178,8 @@ class LocalPipeline:
 class DistributedPipeline:
     """One pipeline stage per rank; ``grid.dp`` replicas share the window batches round-robin."""
 
-    def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig, grid: Grid, rank: int):
+    def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig, grid: Grid, rank: int,
+                 use_graphs: bool = True):
         self.model, self.plan, self.bcfg, self.grid, self.rank = model, plan, bcfg, grid, rank
         self.dp_idx, self.stage = grid.coords(rank)
         if plan.num_stages != grid.pp:
@@ -155,6 +188,10 @@ class DistributedPipeline:
         self.prev = grid.rank_of(self.dp_idx, self.stage - 1) if self.stage > 0 else None
         self.next = grid.rank_of(self.dp_idx, self.stage + 1) if self.stage < grid.pp - 1 else None
         self.device = model.device
+        self.graphs = GraphCache(self._stage_step, enabled=use_graphs and model.device.type == "cuda")
+
+    def _stage_step(self, ids, rows, targets, row_window, n_rows, msg_in=None, carry_in=None):
+        return self.runner.forward(ids, rows, targets, row_window, n_rows, msg_in, carry_in)
 
     def my_batches(self, batches):
         for i, b in enumerate(batches):
@@ -163,54 +200,53 @@ class DistributedPipeline:
 
     def _recv_bufs(self, batch: WindowBatch):
         r = self.runner
-        spec = self.bcfg.spec
-        k = C.wire.num_lo(spec, self.bcfg.ratio, batch.S)
-        L = C.layout(spec, batch.B, batch.S, self.model.cfg.hidden_size, k, self.model.dtype)
+        L = r.layout_in(batch)
         msg = torch.empty(L.total, dtype=torch.uint8, device=self.device)
-        carry = None
+        carry = torch.empty(0, dtype=torch.float32, device=self.device)
         if r.carries_state() and self.bcfg.needs_importance(batch.S):
             carry = torch.empty(batch.B, batch.S, dtype=torch.float32, device=self.device)
-        return L, msg, carry
+        return msg, carry
 
     def _post_recv(self, batch):
-        L, msg, carry = self._recv_bufs(batch)
+        msg, carry = self._recv_bufs(batch)
         reqs = [dist.irecv(msg, self.prev)]
-        if carry is not None:
+        if carry.numel():
             reqs.append(dist.irecv(carry, self.prev))
-        return L, msg, carry, reqs
+        return msg, carry, reqs
 
     def evaluate(self, batches) -> tuple[PPLAccumulator, dict]:
-        """Run this rank's share.  Returns the globally reduced accumulator (valid on every rank)."""
+        """Run this rank's share of ``batches`` as one continuous pipeline (no flush between batches).
+
+        Returns the globally reduced accumulator (valid on every rank)."""
         mine = [b.to(self.device) for b in self.my_batches(batches)]
         acc_local = torch.zeros(2, dtype=torch.float64, device=self.device)
         pending_sends = []
         recv_next = self._post_recv(mine[0]) if (self.prev is not None and mine) else None
         t0 = time.perf_counter()
         for i, b in enumerate(mine):
-            x = carry = None
+            msg_in = carry_in = None
             if self.prev is not None:
-                L, msg, carry, reqs = recv_next
+                msg_in, carry_in, reqs = recv_next
                 for r in reqs:
                     r.wait()
                 if i + 1 < len(mine):
                     recv_next = self._post_recv(mine[i + 1])  # prefetch: overlap next transfer with compute
-                x = C.decode(msg, self.bcfg.spec, L, self.model.dtype)
-            x, imp, c = self.runner.run(b, x, carry)
+            self.runner.account(b)
+            out = self.graphs(b.ids, b.rows, b.targets, b.row_window, b.n_rows,
+                              *(() if self.prev is None else (msg_in, carry_in)))
             if self.next is not None:
-                msg, L = self.runner.encode(x, b, imp)
-                # keep at most two sends in flight so the buffers stay alive and memory bounded
-                pending_sends.append((msg, c, [dist.isend(msg, self.next)] +
-                                      ([dist.isend(c, self.next)] if c is not None else [])))
-                while len(pending_sends) > 2:
+                msg, c = out
+                if self.graphs.enabled:      # graph outputs are static buffers: hand NCCL private copies
+                    msg, c = msg.clone(), c.clone()
+                reqs = [dist.isend(msg, self.next)] + ([dist.isend(c, self.next)] if c.numel() else [])
+                pending_sends.append((msg, c, reqs))
+                while len(pending_sends) > 2:   # bound in-flight sends (memory) without stalling compute
                     for r in pending_sends.pop(0)[2]:
                         r.wait()
             else:
-                wn = self.runner.finish(x, b)
                 w = b.weights.to(self.device)
-                acc_local[0] += (wn.double() * w).sum()
+                acc_local[0] += (out.double() * w).sum()
                 acc_local[1] += w.sum()
-            self.runner.stats.windows += b.B
-            self.runner.stats.tokens += b.tokens
         for _, _, reqs in pending_sends:
             for r in reqs:
                 r.wait()

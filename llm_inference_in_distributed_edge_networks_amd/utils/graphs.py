@@ -1,0 +1,66 @@
+"""HIP-graph capture of launch-bound stage compute (MI355X replacement for a tracing compiler).
+
+A pipeline stage's forward for a fixed micro-batch signature (B, S, number of scored rows) is a fixed
+sequence of ~170 kernel launches (7 per Qwen2 layer + boundary codec + head).  ``GraphCache`` captures
+it once per signature into a ``torch.cuda.CUDAGraph`` (hipGraph on ROCm) with static input/output
+buffers and replays it: one launch instead of hundreds, no Python or ctypes overhead per kernel.
+Kernels launched through the ctypes library go to the current (capturing) stream, so they are
+captured like any torch op.  Batches with a new signature (first / last window of a corpus) run
+eagerly the first time they are seen and are captured on the second sighting.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+
+
+class GraphCache:
+    def __init__(self, fn: Callable, enabled: bool = True, warmup: int = 1):
+        """``fn(*tensors) -> tensor or tuple of tensors``; every input must be a tensor."""
+        self.fn = fn
+        self.enabled = enabled and torch.cuda.is_available()
+        self.warmup = warmup
+        self.seen: dict = {}
+        self.graphs: dict = {}
+
+    @staticmethod
+    def _sig(args):
+        return tuple((tuple(a.shape), a.dtype, a.device) for a in args)
+
+    def __call__(self, *args):
+        if not self.enabled or not all(torch.is_tensor(a) and a.is_cuda for a in args):
+            return self.fn(*args)
+        key = self._sig(args)
+        g = self.graphs.get(key)
+        if g is None:
+            n = self.seen.get(key, 0)
+            self.seen[key] = n + 1
+            if n < self.warmup:
+                return self.fn(*args)      # also warms allocator / lazy kernel attributes
+            g = self._capture(args)
+            self.graphs[key] = g
+        graph, static_in, static_out = g
+        for s, a in zip(static_in, args):
+            s.copy_(a, non_blocking=True)
+        graph.replay()
+        return static_out
+
+    def _capture(self, args):
+        static_in = [a.clone() for a in args]
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.fn(*static_in)  # one more eager run on the capture stream
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph):
+            static_out = self.fn(*static_in)
+        torch.cuda.synchronize()
+        return graph, static_in, static_out
+
+    def clear(self):
+        self.graphs.clear()
+        self.seen.clear()

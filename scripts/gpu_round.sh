@@ -1,4 +1,4 @@
-# One gpurun session: build, GPU tests, smoke, GEMM microbench, bench variants.  Every GPU step has its own
+# One gpurun session: build, GPU tests, smoke, GEMM microbench, bench + profile.  Every GPU step has its own
 # time limit; a crash/timeout ends the script (no further GPU work).
 set -o pipefail
 mkdir -p gpurun_out
@@ -13,7 +13,8 @@ step() {  # name timeout cmd...
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD_FAIL; tail gpurun_out/build.log; exit 1; }
 TAIL=25 step pytest_gpu 900 python -m pytest tests -m gpu -q -rf; rc=$?; [ $rc -le 1 ] || exit $rc
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-step gemm_bench 300 python tools/gemm_bench.py --rounds 3 --iters 10 --json gpurun_out/gemm_bench.json || exit $?
-step bench_b16m4 300 python bench.py --steps 5 --warmup 2 || exit $?
-step bench_b32m4 300 python bench.py --steps 5 --warmup 2 --batch 32 || exit $?
-step bench_b8m8 300 python bench.py --steps 5 --warmup 2 --batch 8 --microbatches 8 || exit $?
+[ -n "$GEMM" ] && { step gemm_bench 300 python tools/gemm_bench.py --rounds 3 --iters 10 --tiles 128,256 || exit $?; }
+step bench 300 python bench.py --steps 10 --warmup 3 --json-out gpurun_out/bench.json || exit $?
+if [ -n "$PROF" ]; then
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1; echo "[prof] rc=$?"
+fi
