@@ -126,7 +126,8 @@ class SweepEngine:
                 x = torch.cat(xs, 0)
                 for i in range(L + 1, m.cfg.num_layers):
                     x, _ = m.layer(i, x, V * B, S)
-                self.forward_tokens += V * B * S
+                # layer-token work in units of full-model forward tokens
+                self.forward_tokens += V * B * S * (m.cfg.num_layers - L - 1) / m.cfg.num_layers
                 off = (torch.arange(V, device=batch.rows.device) * (B * S)).repeat_interleave(batch.rows.numel())
                 rows = batch.rows.repeat(V) + off
                 nll = m.row_nll(x, rows, batch.targets.repeat(V))

@@ -18,3 +18,4 @@ step bench 300 python bench.py --steps 10 --warmup 3 --json-out gpurun_out/bench
 if [ -n "$PROF" ]; then
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1; echo "[prof] rc=$?"
 fi
+[ -n "$SWEEP" ] && { step sweep_bench 600 python tools/sweep_bench.py --windows ${SWEEP_WINDOWS:-256} --batch 8 --json-out gpurun_out/sweep_bench.json || exit $?; }
