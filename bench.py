@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--ratio", type=float, default=0.5)
     p.add_argument("--method", default="regular_importance")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--transport", default="torch", choices=["torch", "rccl"],
+                   help="stage hand-off: torch.distributed p2p (RCCL) or the native RCCL wrapper")
+    p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--json-out", default="")
     return p.parse_args()
 
@@ -73,13 +76,14 @@ def main():
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     if pp == 1:
         model, prov = build_model(cfg, dev, dtype, seed=a.seed)
-        runner = LocalPipeline(model, plan2, BoundaryConfig(a.codec, a.ratio, a.method))
+        runner = LocalPipeline(model, plan2, BoundaryConfig(a.codec, a.ratio, a.method), use_graphs=not a.no_graphs)
     else:
         dp_idx, stage = grid.coords(env.rank)
         lay = plan2.stage_layers(stage)
         model, prov = build_model(cfg, dev, dtype, seed=a.seed, layers=lay, with_embed=(stage == 0),
                                   with_head=(stage == pp - 1))
-        runner = DistributedPipeline(model, plan2, BoundaryConfig(a.codec, a.ratio, a.method), grid, env.rank)
+        runner = DistributedPipeline(model, plan2, BoundaryConfig(a.codec, a.ratio, a.method), grid, env.rank,
+                                     use_graphs=not a.no_graphs, transport=a.transport)
 
     # ---- data: synthetic stream of WikiText-2 test length, HF sliding windows, staged on device
     tokens = synthetic_stream(299_078, cfg.vocab_size, a.seed)
@@ -148,7 +152,8 @@ def main():
         "data": "synthetic (WikiText-2-test-length Zipf token stream), random-init weights",
         "config": {"model": cfg.name, "global_batch": grid.dp * a.microbatches * a.batch, "seq_len": a.max_length,
                    "stride": a.stride, "parallelism": f"pp{pp}xdp{grid.dp}", "split_after_layer": a.split,
-                   "codec": a.codec, "ratio": a.ratio, "importance": a.method},
+                   "codec": a.codec, "ratio": a.ratio, "importance": a.method,
+                   "transport": a.transport if pp > 1 else "local", "hip_graphs": not a.no_graphs},
         "scored_tokens_per_s": round(scored_per_step * a.steps / dt, 1),
         "wire_bytes_per_token": round(wire, 2),
         "wire_compression_vs_bf16": round(2 * cfg.hidden_size / wire, 3),

@@ -31,6 +31,7 @@ import torch
 from .. import codec as C
 from ..importance import ImportanceTracker, canonical
 from ..models.model import DecoderLM
+from ..utils import trace
 from ..utils.checkpoint import SweepState
 from .windows import WindowBatch, segment_mean, window_nll
 
@@ -92,7 +93,8 @@ class SweepEngine:
     def run_batch(self, batch: WindowBatch) -> torch.Tensor:
         """Returns per-window NLL [M, Lc, R, B] for this batch (also accumulated)."""
         m, B, S = self.m, batch.B, batch.S
-        base, saved, imp = self._prefix(batch)
+        with trace.range("sweep/prefix"):
+            base, saved, imp = self._prefix(batch)
         M, Lc, R = len(self.methods), len(self.layers), len(self.ratios)
         out = torch.empty(M, Lc, R, B, dtype=torch.float32, device=base.device)
         for li, L in enumerate(self.layers):

@@ -35,7 +35,27 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
+COMM_LIB = os.path.join(os.path.dirname(LIB_PATH), "libedge_comm.so")
+COMM_SRC = os.path.join(CSRC, "comm", "rccl_comm.cpp")
+
+
+def build_comm(force: bool = False, verbose: bool = False) -> str:
+    """The native RCCL transport (links librccl; kept out of the kernel library)."""
+    if not force and os.path.exists(COMM_LIB) and os.path.getmtime(COMM_LIB) >= os.path.getmtime(COMM_SRC):
+        return COMM_LIB
+    tmp = COMM_LIB + ".tmp"
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-o", tmp, COMM_SRC,
+           f"-L{rocm}/lib", "-lrccl", f"-Wl,-rpath,{rocm}/lib"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, COMM_LIB)
+    return COMM_LIB
+
+
 def build_native(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
+    build_comm(force, verbose)
     if not force and up_to_date():
         return LIB_PATH
     os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)

@@ -27,7 +27,9 @@ from .. import codec as C
 from ..eval.windows import PPLAccumulator, WindowBatch, window_nll
 from ..importance import ImportanceTracker, canonical
 from ..models.model import DecoderLM
+from ..utils import trace
 from ..utils.graphs import GraphCache
+from ..utils.watchdog import from_env as watchdog_from_env
 from .dist import Grid, all_reduce_sum
 from .plan import PipelinePlan
 
@@ -159,7 +161,8 @@ class LocalPipeline:
     def run_batch(self, batch: WindowBatch) -> torch.Tensor:
         for st in self.stages:
             st.account(batch)
-        return self.graphs(batch.ids, batch.rows, batch.targets, batch.row_window, batch.n_rows)
+        with trace.range("local/step"):
+            return self.graphs(batch.ids, batch.rows, batch.targets, batch.row_window, batch.n_rows)
 
     def evaluate(self, batches, acc: PPLAccumulator | None = None, on_batch=None) -> PPLAccumulator:
         acc = acc or PPLAccumulator()
@@ -179,7 +182,7 @@ class DistributedPipeline:
     """One pipeline stage per rank; ``grid.dp`` replicas share the window batches round-robin."""
 
     def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig, grid: Grid, rank: int,
-                 use_graphs: bool = True):
+                 use_graphs: bool = True, transport: str = "torch"):
         self.model, self.plan, self.bcfg, self.grid, self.rank = model, plan, bcfg, grid, rank
         self.dp_idx, self.stage = grid.coords(rank)
         if plan.num_stages != grid.pp:
@@ -189,6 +192,14 @@ class DistributedPipeline:
         self.next = grid.rank_of(self.dp_idx, self.stage + 1) if self.stage < grid.pp - 1 else None
         self.device = model.device
         self.graphs = GraphCache(self._stage_step, enabled=use_graphs and model.device.type == "cuda")
+        if transport == "rccl":
+            from .rccl import RcclComm
+            self.tr = RcclComm(rank, grid.world, model.device.index or 0)
+        elif transport == "torch":
+            from .rccl import TorchP2P
+            self.tr = TorchP2P()
+        else:
+            raise ValueError(f"unknown transport {transport!r}")
 
     def _stage_step(self, ids, rows, targets, row_window, n_rows, msg_in=None, carry_in=None):
         return self.runner.forward(ids, rows, targets, row_window, n_rows, msg_in, carry_in)
@@ -209,9 +220,9 @@ class DistributedPipeline:
 
     def _post_recv(self, batch):
         msg, carry = self._recv_bufs(batch)
-        reqs = [dist.irecv(msg, self.prev)]
+        reqs = [self.tr.recv(msg, self.prev)]
         if carry.numel():
-            reqs.append(dist.irecv(carry, self.prev))
+            reqs.append(self.tr.recv(carry, self.prev))
         return msg, carry, reqs
 
     def evaluate(self, batches) -> tuple[PPLAccumulator, dict]:
@@ -220,25 +231,33 @@ class DistributedPipeline:
         Returns the globally reduced accumulator (valid on every rank)."""
         mine = [b.to(self.device) for b in self.my_batches(batches)]
         acc_local = torch.zeros(2, dtype=torch.float64, device=self.device)
+        wd = watchdog_from_env(f"stage{self.stage}")
+        tag = f"stage{self.stage}"
         pending_sends = []
         recv_next = self._post_recv(mine[0]) if (self.prev is not None and mine) else None
         t0 = time.perf_counter()
         for i, b in enumerate(mine):
             msg_in = carry_in = None
+            if wd:
+                wd.beat()
             if self.prev is not None:
                 msg_in, carry_in, reqs = recv_next
-                for r in reqs:
-                    r.wait()
+                with trace.range(f"{tag}/recv_wait"):
+                    for r in reqs:
+                        r.wait()
                 if i + 1 < len(mine):
                     recv_next = self._post_recv(mine[i + 1])  # prefetch: overlap next transfer with compute
             self.runner.account(b)
-            out = self.graphs(b.ids, b.rows, b.targets, b.row_window, b.n_rows,
-                              *(() if self.prev is None else (msg_in, carry_in)))
+            with trace.range(f"{tag}/compute"):
+                out = self.graphs(b.ids, b.rows, b.targets, b.row_window, b.n_rows,
+                                  *(() if self.prev is None else (msg_in, carry_in)))
             if self.next is not None:
                 msg, c = out
                 if self.graphs.enabled:      # graph outputs are static buffers: hand NCCL private copies
                     msg, c = msg.clone(), c.clone()
-                reqs = [dist.isend(msg, self.next)] + ([dist.isend(c, self.next)] if c.numel() else [])
+                trace.counter(f"{tag}/wire_bytes", msg.numel() + 4 * c.numel())
+                with trace.range(f"{tag}/send_post"):
+                    reqs = [self.tr.send(msg, self.next)] + ([self.tr.send(c, self.next)] if c.numel() else [])
                 pending_sends.append((msg, c, reqs))
                 while len(pending_sends) > 2:   # bound in-flight sends (memory) without stalling compute
                     for r in pending_sends.pop(0)[2]:
@@ -250,6 +269,8 @@ class DistributedPipeline:
         for _, _, reqs in pending_sends:
             for r in reqs:
                 r.wait()
+        if wd:
+            wd.stop()
         self.runner.stats.compute_s += time.perf_counter() - t0
         all_reduce_sum(acc_local)
         acc = PPLAccumulator()

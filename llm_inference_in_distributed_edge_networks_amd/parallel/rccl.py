@@ -1,0 +1,128 @@
+"""Native RCCL transport for boundary messages (``csrc/comm/rccl_comm.cpp``).
+
+An alternative to ``torch.distributed`` p2p for the stage hand-off: one communicator over all ranks
+(bootstrapped with a unique id broadcast through the default process group), a dedicated
+non-blocking HIP comm stream, and event-only ordering with the compute stream.  ``send``/``recv``
+return handles whose ``wait()`` makes the *current* stream wait on the GPU (no host blocking),
+mirroring ``torch.distributed.Work.wait`` for NCCL.  Buffers are tied to the comm stream with
+``record_stream`` so the caching allocator never recycles them while RCCL still uses them.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from ..ops._native import LIB_PATH as _KLIB
+
+COMM_LIB_PATH = os.path.join(os.path.dirname(_KLIB), "libedge_comm.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(COMM_LIB_PATH):
+            raise RuntimeError(f"{COMM_LIB_PATH} missing: run the build (__graft_entry__.build())")
+        L = ctypes.CDLL(COMM_LIB_PATH)
+        p, i, ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+        sig = {"edge_rccl_id_bytes": [], "edge_rccl_unique_id": [ctypes.c_char_p],
+               "edge_rccl_init": [ctypes.POINTER(p), i, ctypes.c_char_p, i, i], "edge_rccl_destroy": [p],
+               "edge_rccl_wait_for": [p, p], "edge_rccl_signal_to": [p, p], "edge_rccl_group_start": [],
+               "edge_rccl_group_end": [], "edge_rccl_send": [p, p, ll, i], "edge_rccl_recv": [p, p, ll, i],
+               "edge_rccl_allreduce_sum_f64": [p, p, ll], "edge_rccl_stream_sync": [p], "edge_rccl_stream": [p]}
+        for n, a in sig.items():
+            f = getattr(L, n)
+            f.argtypes = a
+            f.restype = ll if n == "edge_rccl_stream" else i
+        _lib = L
+    return _lib
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc}; >=1000 is an RCCL ncclResult_t + 1000)")
+
+
+class _Handle:
+    def __init__(self, comm, is_recv):
+        self.comm, self.is_recv = comm, is_recv
+
+    def wait(self):
+        if self.is_recv:   # compute stream waits for the receive (GPU-side)
+            _ok(lib().edge_rccl_signal_to(self.comm.h, torch.cuda.current_stream().cuda_stream), "signal_to")
+
+
+class RcclComm:
+    def __init__(self, rank: int, world: int, device: int, unique_id: bytes | None = None):
+        L = lib()
+        if unique_id is None:
+            unique_id = self.make_unique_id() if world == 1 else self._bootstrap_id(rank)
+        h = ctypes.c_void_p()
+        _ok(L.edge_rccl_init(ctypes.byref(h), world, unique_id, rank, device), "ncclCommInitRank")
+        self.h, self.rank, self.world = h, rank, world
+        self.stream = torch.cuda.ExternalStream(L.edge_rccl_stream(h), device=torch.device("cuda", device))
+
+    @staticmethod
+    def make_unique_id() -> bytes:
+        L = lib()
+        buf = ctypes.create_string_buffer(L.edge_rccl_id_bytes())
+        _ok(L.edge_rccl_unique_id(buf), "ncclGetUniqueId")
+        return buf.raw
+
+    @staticmethod
+    def _bootstrap_id(rank: int) -> bytes:
+        from .dist import broadcast_object
+        return broadcast_object(RcclComm.make_unique_id() if rank == 0 else None, src=0)
+
+    def _after_compute(self):
+        _ok(lib().edge_rccl_wait_for(self.h, torch.cuda.current_stream().cuda_stream), "wait_for")
+
+    def send(self, t: torch.Tensor, peer: int) -> _Handle:
+        self._after_compute()
+        t.record_stream(self.stream)
+        _ok(lib().edge_rccl_send(self.h, t.data_ptr(), t.numel() * t.element_size(), peer), "ncclSend")
+        return _Handle(self, False)
+
+    def recv(self, t: torch.Tensor, peer: int) -> _Handle:
+        self._after_compute()
+        t.record_stream(self.stream)
+        _ok(lib().edge_rccl_recv(self.h, t.data_ptr(), t.numel() * t.element_size(), peer), "ncclRecv")
+        return _Handle(self, True)
+
+    def sendrecv(self, send_t, recv_t, peer):
+        """Grouped send+recv with one peer (self-loopback when peer == rank)."""
+        L = lib()
+        self._after_compute()
+        send_t.record_stream(self.stream)
+        recv_t.record_stream(self.stream)
+        _ok(L.edge_rccl_group_start(), "group_start")
+        _ok(L.edge_rccl_send(self.h, send_t.data_ptr(), send_t.numel() * send_t.element_size(), peer), "send")
+        _ok(L.edge_rccl_recv(self.h, recv_t.data_ptr(), recv_t.numel() * recv_t.element_size(), peer), "recv")
+        _ok(L.edge_rccl_group_end(), "group_end")
+        return _Handle(self, True)
+
+    def all_reduce_sum_f64(self, t: torch.Tensor):
+        assert t.dtype == torch.float64
+        self._after_compute()
+        _ok(lib().edge_rccl_allreduce_sum_f64(self.h, t.data_ptr(), t.numel()), "allreduce")
+        _Handle(self, True).wait()
+        return t
+
+    def close(self):
+        if self.h:
+            lib().edge_rccl_destroy(self.h)
+            self.h = None
+
+
+class TorchP2P:
+    """The default transport: torch.distributed isend/irecv (RCCL via ProcessGroupNCCL, or gloo)."""
+
+    def send(self, t, peer):
+        import torch.distributed as dist
+        return dist.isend(t, peer)
+
+    def recv(self, t, peer):
+        import torch.distributed as dist
+        return dist.irecv(t, peer)

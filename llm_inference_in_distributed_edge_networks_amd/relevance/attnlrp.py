@@ -18,7 +18,8 @@ framework's own model weights ("efficient" LRP = Input x modified-Gradient):
   receives half of the Gradient x Input relevance (backward scaled by 0.5);
 * softmax: Gradient x Input of the softmax (the bias-free Taylor rule), -inf logits zeroed.
 
-Conservation (sum of input relevance ~ seeded logit) is checked by the tests on tiny models.
+The tests check per-rule conservation (Gradient x Input through each rule sums to the output relevance)
+and that the head relevance computed from the head outputs equals the literal S x S probability hook.
 This is an offline calibration pass; it runs on PyTorch ops (hipBLASLt on the GPU) in fp32.
 """
 from __future__ import annotations
@@ -103,8 +104,13 @@ def _lin(x, w, b=None):
     return y + b if b is not None else y
 
 
-def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32):
-    """Differentiable forward with AttnLRP rules.  Returns (logits_last [V], embeds, attn_probs list)."""
+def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32, keep_probs: bool = True):
+    """Differentiable forward with AttnLRP rules.
+
+    Returns (logits_last [V], embeds, per-layer tensors): the attention probabilities A (S x S per head,
+    ``keep_probs``) or the per-head attention outputs O = A V (S x D per head).  Under the uniform rule
+    on A V, dA = 0.5 dO V^T, hence sum_ij A_ij dA_ij = 0.5 sum_i dO_i . O_i: the head relevance needs
+    only O and its gradient - an S/D-times smaller tensor than A (8x at S=512)."""
     cfg = model.cfg
     f = lambda t: None if t is None else t.to(dtype)  # noqa: E731
     B, S = ids.shape
@@ -129,9 +135,14 @@ def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32):
         mask = torch.ones(S, S, dtype=torch.bool, device=sc.device).triu(1)
         sc = sc.masked_fill(mask, float("-inf"))
         A = _Softmax.apply(sc)
-        A.retain_grad()
-        probs.append(A)
-        o = _UniformMatmul.apply(A, v).permute(0, 2, 1, 3).reshape(B * S, Hq * D)
+        oh = _UniformMatmul.apply(A, v)          # [B, Hq, S, D]
+        if keep_probs:
+            A.retain_grad()
+            probs.append(A)
+        else:
+            oh.retain_grad()
+            probs.append(oh)
+        o = oh.permute(0, 2, 1, 3).reshape(B * S, Hq * D)
         if cfg.arch == "qwen2":
             x = x + _lin(o, f(L["wo"]))
             h = _rmsnorm_id(x, f(L["ln2_w"]), cfg.norm_eps)
@@ -150,14 +161,17 @@ def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32):
     return logits, emb, probs
 
 
-def head_relevance(model, ids: torch.Tensor, dtype=torch.float32):
+def head_relevance(model, ids: torch.Tensor, dtype=torch.float32, via_probs: bool = False):
     """Per-(layer, head) relevance of one window (B=1): sum_{i,j} A * dA, after seeding the max logit.
 
+    ``via_probs`` computes it literally from the retained S x S probabilities (the reference's hook,
+    ``Relevance/main.py:96-103``); the default uses the exact identity 0.5 * sum dO . O.
     Returns (rel [layers, heads], input relevance sum, seed logit)."""
-    logits, emb, probs = lrp_forward(model, ids, dtype)
+    logits, emb, probs = lrp_forward(model, ids, dtype, keep_probs=via_probs)
     mx = logits[0].max()
     mx.backward(mx.detach())
-    rel = torch.stack([(A * A.grad).sum(dim=(0, 2, 3)) for A in probs]).detach()
+    scale = 1.0 if via_probs else 0.5
+    rel = torch.stack([scale * (T * T.grad).sum(dim=(0, 2, 3)) for T in probs]).detach()
     in_rel = (emb * emb.grad).sum().detach()
     return rel, in_rel, mx.detach()
 

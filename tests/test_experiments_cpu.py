@@ -66,3 +66,10 @@ def test_qwen2_channel(tmp_path):
                                 "methods": ["channel_8", "channel_4", "channel_1_mean", "channel_1_max"]}, tmp_path)
     res = json.loads((d / "avg_ppl_results_channel.json").read_text())
     assert len(res["avg_ppl_results"]) == 2 and len(res["avg_ppl_results"][0]) == 4
+
+
+def test_analysis_js(tmp_path):
+    d = run_main("Analysis", {"model": "tiny-neox", "max_lines": 6}, tmp_path)
+    res = json.loads((d / "js_divergence.json").read_text())
+    m = res["js_divergence"]
+    assert len(m) == 4 and m[0][0] == 0 and abs(m[0][1] - m[1][0]) < 1e-12 and all(0 <= v <= 1 for r in m for v in r)

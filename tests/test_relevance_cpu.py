@@ -37,3 +37,12 @@ def test_head_relevance_shapes_and_normalisation():
         assert torch.allclose(w.sum(-1), torch.ones(cfg.num_layers), atol=1e-3)
         rel2, _, _ = head_relevance(m, ids)
         assert torch.allclose(rel, rel2)
+
+
+def test_output_identity_equals_probability_hook():
+    for cfg in (TINY_QWEN2, TINY_NEOX):
+        m = DecoderLM.random_init(cfg, 3, std=0.05)
+        ids = torch.randint(0, cfg.vocab_size, (1, 48), generator=torch.Generator().manual_seed(1))
+        r_probs, _, _ = head_relevance(m, ids, via_probs=True)
+        r_out, _, _ = head_relevance(m, ids)
+        assert torch.allclose(r_probs, r_out, rtol=1e-4, atol=1e-6)
