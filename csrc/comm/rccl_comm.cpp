@@ -73,7 +73,9 @@ EDGE_API int edge_rccl_destroy(void* handle) {
   (void)hipStreamSynchronize(c->stream);
   const ncclResult_t r = ncclCommDestroy(c->comm);
   for (int i = 0; i < NEV; ++i) (void)hipEventDestroy(c->ev[i]);
-  (void)hipStreamDestroy(c->stream);
+  // The comm stream is deliberately NOT destroyed: buffers handed to RCCL are tied to it through the
+  // torch caching allocator (record_stream), which records events on it when those blocks are freed,
+  // possibly at interpreter exit.  A stream per communicator for the process lifetime is harmless.
   delete c;
   return nccl_rc(r);
 }
