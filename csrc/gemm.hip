@@ -13,6 +13,7 @@
 //   scatter + q pre-scale: replaces three reference ops), LSE (LM head: per-row partial max/sum-exp and
 //   target logit, logits are never written to memory).
 #include "common.h"
+#include <algorithm>
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_GELU = 4, EPI_SWIGLU = 5,
        EPI_QKV_ROPE = 6, EPI_LSE = 7 };
@@ -79,129 +80,11 @@ __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
   return *(const bf16x8_t*)(lds + r * 128 + ((c ^ swz(r)) << 4));
 }
 
+// ---- epilogue: lane owns rows m0 + wm*WTM + i*16 + (lane&15), columns n0 + wn*64 + j*16 + 4*(lane>>4) + r
 template <int EPI, int RH, class CF>
-__global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kernel(GemmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BM = CF::BM, BN = CF::BN, MI = CF::MI, NW = CF::NW;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / CF::NWN, wn = wave % CF::NWN;
-
-  // ---- tile scheduling: XCD remap, then grouped-M order ---------------------------------------
-  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
-  const int nwg = tm * tn;
-  const int id = xcd_remap(blockIdx.x, nwg);
-  const int group = id / (GROUP_M * tn);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tm - first_m, GROUP_M);
-  const int in_g = id - group * GROUP_M * tn;
-  const int tile_m = first_m + in_g % gsz;
-  const int tile_n = in_g / gsz;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-
-  f32x4_t acc[MI][4];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const bf16_t* pa[CF::A_INSTR];
-  const bf16_t* pb[CF::B_INSTR];
-  stage_ptrs<CF::A_INSTR, NW>(a.A, a.lda, m0, a.M, wave, lane, pa);
-  stage_ptrs<CF::B_INSTR, NW>(a.B, a.ldb, n0, a.N, wave, lane, pb);
-  // Fragment addresses in the swizzled LDS image.  The swizzle of row r is (r>>1)&7 and every fragment
-  // row is lane&15 plus a multiple of 16, so it depends on the lane only: one base per k-half, the
-  // m/n tile offsets are immediates (2 KiB per 16 rows).
-  const int sw = ((lane & 15) >> 1) & 7;
-  int abase[2], bbase[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int c = ks * 4 + (lane >> 4);
-    abase[ks] = (wm * CF::WTM + (lane & 15)) * 128 + ((c ^ sw) << 4);
-    bbase[ks] = CF::A_BYTES + (wn * 64 + (lane & 15)) * 128 + ((c ^ sw) << 4);
-  }
-
-  // Sub-steps of a K-tile: s = (ks, mg) with ks the 32-wide k half and mg a group of 4 m-tiles, each
-  // 16 MFMAs.  Fragments are double-buffered in registers (sets X/Y): the LDS reads of sub-step s+1 are
-  // in flight while the MFMAs of sub-step s issue.  One barrier per K-tile (in the last sub-step) makes
-  // the next tile's DMA visible and retires every wave's reads of the current buffer before it is
-  // restaged (RAW: own vmcnt(0) + barrier; WAR: own lgkmcnt(0) + barrier).
-  constexpr int MG = MI / 4, NS = 2 * MG;
-  bf16x8_t XA[4], XB[4], YA[4], YB[4];
-  auto ld = [&](bf16x8_t(&FA)[4], bf16x8_t(&FB)[4], const char* buf, int ks, int mg) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) FA[i] = *(const bf16x8_t*)(buf + abase[ks] + (mg * 4 + i) * 2048);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) FB[j] = *(const bf16x8_t*)(buf + bbase[ks] + j * 2048);
-  };
-  auto mma = [&](const bf16x8_t(&FA)[4], const bf16x8_t(&FB)[4], int mg) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[mg * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[mg * 4 + i][j], 0, 0, 0);
-  };
-
-  const int nk = a.K / BK;
-  stage_issue<CF::A_INSTR, NW>(pa, 0, smem, wave);
-  stage_issue<CF::B_INSTR, NW>(pb, 0, smem + CF::A_BYTES, wave);
-  wait_vmcnt0();
-  __syncthreads();
-
-  if constexpr (!CF::PIPE) {
-    // 2 sub-steps per K-tile, fragments read right before use (several blocks per CU hide the latency)
-    for (int t = 0; t < nk; ++t) {
-      const char* cur = smem + (t & 1) * CF::STAGE;
-      if (t + 1 < nk) {
-        char* nxt = smem + ((t + 1) & 1) * CF::STAGE;
-        stage_issue<CF::A_INSTR, NW>(pa, (t + 1) * BK, nxt, wave);
-        stage_issue<CF::B_INSTR, NW>(pb, (t + 1) * BK, nxt + CF::A_BYTES, wave);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-        for (int mg = 0; mg < MG; ++mg) {
-          ld(XA, XB, cur, ks, mg);
-          mma(XA, XB, mg);
-        }
-      }
-      wait_vmcnt0();
-      __syncthreads();
-    }
-  } else {
-    ld(XA, XB, smem, 0, 0);
-    for (int t = 0; t < nk; ++t) {
-      const char* cur = smem + (t & 1) * CF::STAGE;
-      char* nxt = smem + ((t + 1) & 1) * CF::STAGE;
-      const bool more = t + 1 < nk;
-  #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        if (s == 0 && more) {
-          stage_issue<CF::A_INSTR, NW>(pa, (t + 1) * BK, nxt, wave);
-          stage_issue<CF::B_INSTR, NW>(pb, (t + 1) * BK, nxt + CF::A_BYTES, wave);
-        }
-        const int mg = s % MG;
-        if (s + 1 < NS) {
-          const int ks1 = (s + 1) / MG, mg1 = (s + 1) % MG;
-          if (s & 1) ld(XA, XB, cur, ks1, mg1); else ld(YA, YB, cur, ks1, mg1);
-        } else {
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          if (more) {
-            if (s & 1) ld(XA, XB, nxt, 0, 0); else ld(YA, YB, nxt, 0, 0);
-          }
-        }
-        // keep the next sub-step's LDS reads ahead of this sub-step's MFMAs (the scheduler would
-        // otherwise sink them below the MFMAs and wait lgkmcnt(0), serialising reads and math)
-        __builtin_amdgcn_sched_barrier(0);
-        // this sub-step's 8 fragments were issued one sub-step ago; leave the 8 just issued in flight
-        if (s + 1 < NS) __builtin_amdgcn_s_waitcnt(0xC87F);  // lgkmcnt(8)
-        if (s & 1) mma(YA, YB, mg); else mma(XA, XB, mg);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-
-  // ---- epilogue -------------------------------------------------------------------------------
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[CF::MI][4], int m0, int n0,
+                                              int lane, int wm, int wn) {
+  constexpr int MI = CF::MI;
   const int g = lane >> 4;
   const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
 
@@ -376,28 +259,203 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
   }
 }
 
+__device__ __forceinline__ void tile_origin(int id, int M, int N, int BM, int BN, int& m0, int& n0) {
+  // grouped-M order: GROUP_M consecutive m-panels sweep the n-panels together (A panels stay in L2)
+  const int tm = (M + BM - 1) / BM, tn = N / BN;
+  const int group = id / (GROUP_M * tn);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tm - first_m, GROUP_M);
+  const int in_g = id - group * GROUP_M * tn;
+  m0 = (first_m + in_g % gsz) * BM;
+  n0 = (in_g / gsz) * BN;
+}
+
+template <int EPI, int RH, class CF>
+__global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = CF::BM, BN = CF::BN, MI = CF::MI, NW = CF::NW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / CF::NWN, wn = wave % CF::NWN;
+  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
+  const int ntiles = tm * tn;
+
+  f32x4_t acc[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const bf16_t* pa[CF::A_INSTR];
+  const bf16_t* pb[CF::B_INSTR];
+  // Fragment addresses in the swizzled LDS image.  The swizzle of row r is (r>>1)&7 and every fragment
+  // row is lane&15 plus a multiple of 16, so it depends on the lane only: one base per k-half, the
+  // m/n tile offsets are immediates (2 KiB per 16 rows).
+  const int sw = ((lane & 15) >> 1) & 7;
+  int abase[2], bbase[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = ks * 4 + (lane >> 4);
+    abase[ks] = (wm * CF::WTM + (lane & 15)) * 128 + ((c ^ sw) << 4);
+    bbase[ks] = CF::A_BYTES + (wn * 64 + (lane & 15)) * 128 + ((c ^ sw) << 4);
+  }
+  constexpr int MG = MI / 4, NS = 2 * MG;
+  bf16x8_t XA[4], XB[4], YA[4], YB[4];
+  auto ld = [&](bf16x8_t(&FA)[4], bf16x8_t(&FB)[4], const char* buf, int ks, int mg) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) FA[i] = *(const bf16x8_t*)(buf + abase[ks] + (mg * 4 + i) * 2048);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) FB[j] = *(const bf16x8_t*)(buf + bbase[ks] + j * 2048);
+  };
+  auto mma = [&](const bf16x8_t(&FA)[4], const bf16x8_t(&FB)[4], int mg) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[mg * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[mg * 4 + i][j], 0, 0, 0);
+  };
+  auto stage = [&](int k0, char* buf) {
+    stage_issue<CF::A_INSTR, NW>(pa, k0, buf, wave);
+    stage_issue<CF::B_INSTR, NW>(pb, k0, buf + CF::A_BYTES, wave);
+  };
+  const int nk = a.K / BK;
+
+  if constexpr (!CF::PIPE) {
+    // One tile per workgroup (2 workgroups per CU hide each other's prologue/epilogue); fragments
+    // are read right before use.
+    int m0, n0;
+    tile_origin(xcd_remap(blockIdx.x, ntiles), a.M, a.N, BM, BN, m0, n0);
+    stage_ptrs<CF::A_INSTR, NW>(a.A, a.lda, m0, a.M, wave, lane, pa);
+    stage_ptrs<CF::B_INSTR, NW>(a.B, a.ldb, n0, a.N, wave, lane, pb);
+    stage(0, smem);
+    wait_vmcnt0();
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const char* cur = smem + (t & 1) * CF::STAGE;
+      if (t + 1 < nk) stage((t + 1) * BK, smem + ((t + 1) & 1) * CF::STAGE);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int mg = 0; mg < MG; ++mg) {
+          ld(XA, XB, cur, ks, mg);
+          mma(XA, XB, mg);
+        }
+      }
+      wait_vmcnt0();
+      __syncthreads();
+    }
+    gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn);
+  } else {
+    // Persistent (one workgroup per CU walks tiles v, v+G, v+2G, ... with v the XCD-grouped id of this
+    // workgroup, so the 32 CUs of an XCD work on 32 consecutive grouped-M tiles).  Sub-steps
+    // s = (ks, mg) of 16 MFMAs with register double-buffered fragments (sets X/Y): the LDS reads of
+    // sub-step s+1 are in flight while the MFMAs of sub-step s issue.  One barrier per K-tile (in the
+    // last sub-step): RAW - own vmcnt(0) + barrier makes the next K-tile's DMA visible; WAR - own
+    // lgkmcnt(0) + barrier retires every wave's reads of the buffer about to be restaged.  The last
+    // K-tile of a tile already stages (and reads fragments of) the NEXT tile's first K-tile, so the
+    // epilogue overlaps that DMA and the next tile starts with its operands in LDS.
+    const int G = gridDim.x;
+    int tile = xcd_remap(blockIdx.x, G);
+    if (tile >= ntiles) return;
+    int m0, n0;
+    tile_origin(tile, a.M, a.N, BM, BN, m0, n0);
+    stage_ptrs<CF::A_INSTR, NW>(a.A, a.lda, m0, a.M, wave, lane, pa);
+    stage_ptrs<CF::B_INSTR, NW>(a.B, a.ldb, n0, a.N, wave, lane, pb);
+    stage(0, smem);
+    wait_vmcnt0();
+    __syncthreads();
+    ld(XA, XB, smem, 0, 0);
+    int g = 0;  // K-tiles consumed by this workgroup (LDS buffer parity)
+    while (true) {
+      const int next = tile + G;
+      const bool has_next = next < ntiles;
+      int nm0 = 0, nn0 = 0;
+      if (has_next) tile_origin(next, a.M, a.N, BM, BN, nm0, nn0);
+      for (int t = 0; t < nk; ++t, ++g) {
+        const char* cur = smem + (g & 1) * CF::STAGE;
+        char* nxt = smem + ((g + 1) & 1) * CF::STAGE;
+        const bool more = t + 1 < nk;
+        const bool prefetch = more || has_next;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          if (s == 0) {
+            if (more) {
+              stage((t + 1) * BK, nxt);
+            } else if (has_next) {
+              stage_ptrs<CF::A_INSTR, NW>(a.A, a.lda, nm0, a.M, wave, lane, pa);
+              stage_ptrs<CF::B_INSTR, NW>(a.B, a.ldb, nn0, a.N, wave, lane, pb);
+              stage(0, nxt);
+            }
+          }
+          const int mg = s % MG;
+          if (s + 1 < NS) {
+            const int ks1 = (s + 1) / MG, mg1 = (s + 1) % MG;
+            if (s & 1) ld(XA, XB, cur, ks1, mg1); else ld(YA, YB, cur, ks1, mg1);
+          } else {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (prefetch) {
+              if (s & 1) ld(XA, XB, nxt, 0, 0); else ld(YA, YB, nxt, 0, 0);
+            }
+          }
+          // keep the next sub-step's LDS reads ahead of this sub-step's MFMAs (the scheduler would
+          // otherwise sink them below the MFMAs and wait lgkmcnt(0), serialising reads and math)
+          __builtin_amdgcn_sched_barrier(0);
+          if (s + 1 < NS) __builtin_amdgcn_s_waitcnt(0xC87F);  // lgkmcnt(8): this set was issued a sub-step ago
+          if (s & 1) mma(YA, YB, mg); else mma(XA, XB, mg);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn);
+      if (!has_next) break;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      tile = next;
+      m0 = nm0;
+      n0 = nn0;
+    }
+  }
+}
+
 static int g_tile_override = 0;  // 0 auto, 128 or 256 (tests / tuning)
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
 
 template <int EPI, int RH, class CF>
 static int launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int tm = (a.M + CF::BM - 1) / CF::BM, tn = a.N / CF::BN;
+  const int grid = CF::PIPE ? std::min(tm * tn, num_cus()) : tm * tn;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, RH, CF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         CF::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, RH, CF>), dim3(tm * tn), dim3(CF::NT), CF::LDS, st, a);
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, RH, CF>), dim3(grid), dim3(CF::NT), CF::LDS, st, a);
   return (int)hipGetLastError();
 }
 
 template <int EPI, int RH = 0>
 static int launch(const GemmArgs& a, hipStream_t st) {
-  // 256x256 tiles when the shape can fill the chip with them (halves L2->LDS traffic per FLOP),
-  // 128x128 otherwise (N not a multiple of 256, or too few 256-row panels).
-  const bool big = (a.N % 256 == 0) && ((long long)((a.M + 255) / 256) * (a.N / 256) >= 256);
-  const bool use256 = g_tile_override ? g_tile_override == 256 && a.N % 256 == 0 : big;
-  return use256 ? launch_cfg<EPI, RH, C256>(a, st) : launch_cfg<EPI, RH, C128>(a, st);
+  // 256x256 persistent tiles when the shape can fill the chip with them (halves L2->LDS traffic per
+  // FLOP), 128x128 otherwise (N not a multiple of 256, or too few 256-row panels).  The QKV/RoPE and
+  // LSE epilogues stay on 128x128 (register budget; their N is never a multiple of 256 in practice).
+  if constexpr (EPI == EPI_QKV_ROPE || EPI == EPI_LSE) {
+    return launch_cfg<EPI, RH, C128>(a, st);
+  } else {
+    const bool big = (a.N % 256 == 0) && ((long long)((a.M + 255) / 256) * (a.N / 256) >= 256);
+    const bool use256 = g_tile_override ? g_tile_override == 256 && a.N % 256 == 0 : big;
+    return use256 ? launch_cfg<EPI, RH, C256>(a, st) : launch_cfg<EPI, RH, C128>(a, st);
+  }
 }
 
 EDGE_API int edge_gemm_set_tile(int t) {
