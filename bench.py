@@ -48,8 +48,8 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--model", default="qwen2-0.5b")
-    p.add_argument("--batch", type=int, default=32, help="windows per micro-batch")
-    p.add_argument("--microbatches", type=int, default=4, help="micro-batches per step per replica")
+    p.add_argument("--batch", type=int, default=64, help="windows per micro-batch")
+    p.add_argument("--microbatches", type=int, default=2, help="micro-batches per step per replica")
     p.add_argument("--max-length", type=int, default=512)
     p.add_argument("--stride", type=int, default=32)
     p.add_argument("--split", type=int, default=11, help="last layer of stage 0 (reference layer_of_interest)")

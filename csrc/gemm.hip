@@ -28,6 +28,10 @@ struct GemmArgs {
   int S, Hq, Hkv, s_pad; float q_scale;
   // LSE
   const int64_t* targets; float* part_max; float* part_sum; float* tgt_logit; int nparts;
+  // fused RMSNorm: consumer side (row scale rscale[m] = rsqrt(mean(x_m^2) + eps), the norm weight is
+  // pre-folded into B) and producer side (per-row sum of squares of the stored bf16 outputs, one
+  // partial per 64-column slab: ssq_out[m, n/64])
+  const float* rscale; float* ssq_out;
 };
 
 constexpr int BK = 64;
@@ -83,10 +87,17 @@ __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
 // ---- epilogue: lane owns rows m0 + wm*WTM + i*16 + (lane&15), columns n0 + wn*64 + j*16 + 4*(lane>>4) + r
 template <int EPI, int RH, class CF>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[CF::MI][4], int m0, int n0,
-                                              int lane, int wm, int wn) {
+                                              int lane, int wm, int wn, const float (&rs)[CF::MI]) {
   constexpr int MI = CF::MI;
   const int g = lane >> 4;
   const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
+
+  if (a.rscale) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] *= rs[i];
+  }
 
   if constexpr (EPI == EPI_LSE) {
 #pragma unroll
@@ -150,6 +161,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
         // rotate_half partner of column d is d +- RH: register j +- RH/16, same lane.
         constexpr int DJ = RH / 16;
         if (!is_v) {
+          // cos/sin of the 4 consecutive frequencies this lane needs per 16-column group: one float4
+          // load each (the frequency index of column d is d mod RH, shared by the pair (d, d+RH))
+          constexpr int NJ = RH / 16;  // register groups in the low half
+          f32x4_t cs[NJ], sn[NJ];
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            cs[j] = *(const f32x4_t*)(a.cosT + pos * RH + j * 16 + g * 4);
+            sn[j] = *(const f32x4_t*)(a.sinT + pos * RH + j * 16 + g * 4);
+          }
           float o[4][4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -157,11 +177,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
             for (int r = 0; r < 4; ++r) {
               if (j * 16 >= 2 * RH) { o[j][r] = v[j][r]; continue; }
               const bool lo = j * 16 < RH;
-              const int d = j * 16 + g * 4 + r;
-              const int fi = lo ? d : d - RH;
-              const float c = a.cosT[pos * RH + fi], s = a.sinT[pos * RH + fi];
+              const int jf = lo ? j : j - DJ;
+              const float c = cs[jf][r], sv = sn[jf][r];
               const float y = lo ? v[(j + DJ) & 3][r] : v[(j - DJ) & 3][r];
-              o[j][r] = lo ? (v[j][r] * c - y * s) : (v[j][r] * c + y * s);
+              o[j][r] = lo ? (v[j][r] * c - y * sv) : (v[j][r] * c + y * sv);
             }
           }
 #pragma unroll
@@ -220,8 +239,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
-    if (m >= a.M) continue;
+    const bool ok = m < a.M;
     if constexpr (EPI == EPI_SWIGLU) {
+      if (!ok) continue;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int n = nw / 2 + p * 16 + g * 4;
@@ -234,29 +254,57 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
         *(u32x2_t*)(a.C + (size_t)m * a.ldc + n) = w;
       }
     } else {
+      float ss = 0.f;
+      if (ok) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = nw + j * 16 + g * 4;
-        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU) {
-          const u32x2_t bw = *(const u32x2_t*)(a.bias + n);
-          o[0] += bf_lo(bw[0]); o[1] += bf_hi(bw[0]); o[2] += bf_lo(bw[1]); o[3] += bf_hi(bw[1]);
-        }
-        if constexpr (EPI == EPI_BIAS_GELU) {
+        for (int j = 0; j < 4; ++j) {
+          const int n = nw + j * 16 + g * 4;
+          float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU) {
+            const u32x2_t bw = *(const u32x2_t*)(a.bias + n);
+            o[0] += bf_lo(bw[0]); o[1] += bf_hi(bw[0]); o[2] += bf_lo(bw[1]); o[3] += bf_hi(bw[1]);
+          }
+          if constexpr (EPI == EPI_BIAS_GELU) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
+            for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
+          }
+          if constexpr (EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
+            const u32x2_t rw = *(const u32x2_t*)(a.resid + (size_t)m * a.ldr + n);
+            o[0] += bf_lo(rw[0]); o[1] += bf_hi(rw[0]); o[2] += bf_lo(rw[1]); o[3] += bf_hi(rw[1]);
+          }
+          u32x2_t w;
+          w[0] = pack_bf2(o[0], o[1]);
+          w[1] = pack_bf2(o[2], o[3]);
+          *(u32x2_t*)(a.C + (size_t)m * a.ldc + n) = w;
+          const float q0 = bf_lo(w[0]), q1 = bf_hi(w[0]), q2 = bf_lo(w[1]), q3 = bf_hi(w[1]);
+          ss += q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;  // of the stored (rounded) values
         }
-        if constexpr (EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
-          const u32x2_t rw = *(const u32x2_t*)(a.resid + (size_t)m * a.ldr + n);
-          o[0] += bf_lo(rw[0]); o[1] += bf_hi(rw[0]); o[2] += bf_lo(rw[1]); o[3] += bf_hi(rw[1]);
-        }
-        u32x2_t w;
-        w[0] = pack_bf2(o[0], o[1]);
-        w[1] = pack_bf2(o[2], o[3]);
-        *(u32x2_t*)(a.C + (size_t)m * a.ldc + n) = w;
+      }
+      if (a.ssq_out) {  // uniform branch: every lane takes part in the shuffles
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        if (ok && g == 0) a.ssq_out[(size_t)m * (a.N / 64) + nw / 64] = ss;
       }
     }
   }
+}
+
+template <int MI, int WTM>
+__device__ __forceinline__ void load_rscale(const GemmArgs& a, int m0, int wm, int lane, float (&rs)[MI]) {
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    int m = m0 + wm * WTM + i * 16 + (lane & 15);
+    m = m < a.M ? m : a.M - 1;
+    rs[i] = a.rscale ? a.rscale[m] : 1.f;
+  }
+}
+
+template <int MI>
+__device__ __forceinline__ void zero_acc(f32x4_t (&acc)[MI][4]) {
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 }
 
 __device__ __forceinline__ void tile_origin(int id, int M, int N, int BM, int BN, int& m0, int& n0) {
@@ -324,6 +372,8 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
     // are read right before use.
     int m0, n0;
     tile_origin(xcd_remap(blockIdx.x, ntiles), a.M, a.N, BM, BN, m0, n0);
+    float rs[MI];
+    load_rscale<MI, CF::WTM>(a, m0, wm, lane, rs);
     stage_ptrs<CF::A_INSTR, NW>(a.A, a.lda, m0, a.M, wave, lane, pa);
     stage_ptrs<CF::B_INSTR, NW>(a.B, a.ldb, n0, a.N, wave, lane, pb);
     stage(0, smem);
@@ -343,7 +393,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
       wait_vmcnt0();
       __syncthreads();
     }
-    gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn);
+    gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
   } else {
     // Persistent (one workgroup per CU walks tiles v, v+G, v+2G, ... with v the XCD-grouped id of this
     // workgroup, so the 32 CUs of an XCD work on 32 consecutive grouped-M tiles).  Sub-steps
@@ -405,12 +455,14 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn);
+      {
+        // row scales loaded here, not across the K loop: this config runs at the 256-VGPR budget
+        float rs[MI];
+        load_rscale<MI, CF::WTM>(a, m0, wm, lane, rs);
+        gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
+      }
       if (!has_next) break;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      zero_acc<MI>(acc);
       tile = next;
       m0 = nm0;
       n0 = nn0;
@@ -471,8 +523,11 @@ static int check_shapes(const GemmArgs& a) {
 }
 
 EDGE_API int edge_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                       const void* bias, const void* resid, int ldr, int act, hipStream_t st) {
+                       const void* bias, const void* resid, int ldr, int act, const float* rscale, float* ssq_out,
+                       hipStream_t st) {
   GemmArgs a{};
+  a.rscale = rscale; a.ssq_out = ssq_out;
+  if (ssq_out && (N % 64 || act == 2)) return (int)hipErrorInvalidValue;
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = (bf16_t*)C;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ldr = ldr;
@@ -489,8 +544,9 @@ EDGE_API int edge_gemm(const void* A, const void* B, void* C, int M, int N, int 
 
 EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, void* q, void* k, void* vt,
                                 const float* cosT, const float* sinT, int M, int K, int S, int Hq, int Hkv,
-                                int rot_dim, int s_pad, float q_scale, hipStream_t st) {
+                                int rot_dim, int s_pad, float q_scale, const float* rscale, hipStream_t st) {
   GemmArgs a{};
+  a.rscale = rscale;
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
   a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = K; a.lda = K; a.ldb = K;
   a.bias = (const bf16_t*)bias;

@@ -168,3 +168,51 @@ EDGE_API int edge_embedding(const int64_t* ids, const void* table, void* out, in
   embedding_kernel<<<(T + 3) / 4, 256, 0, st>>>(ids, (const bf16_t*)table, (bf16_t*)out, T, H, V);
   return (int)hipGetLastError();
 }
+
+// Per-row sum of squares in 64-column slabs: ssq[r, s] = sum_{c in slab s} x[r, c]^2 (the partial layout the
+// residual GEMM epilogues produce; consumed by the fused-RMSNorm GEMMs).  Wave per row.
+template <int NCH>
+__global__ __launch_bounds__(256) void row_ssq_kernel(const bf16_t* __restrict__ x, float* __restrict__ ssq, int R,
+                                                      int H) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int lane = threadIdx.x & 63;
+  float v[NCH][8];
+  load_row<NCH>(x + (size_t)r * H, H, v);
+  const int P = H / 64;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[c][j] * v[c][j];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    const int slab = c * 8 + (lane >> 3);
+    if ((lane & 7) == 0 && slab < P) ssq[(size_t)r * P + slab] = s;
+  }
+}
+
+EDGE_API int edge_row_ssq(const void* x, float* ssq, int R, int H, hipStream_t st) {
+  if (H % 64) return (int)hipErrorInvalidValue;
+  if (R <= 0) return 0;
+  DISPATCH_NCH(H, row_ssq_kernel<NCH><<<(R + 3) / 4, 256, 0, st>>>((const bf16_t*)x, ssq, R, H));
+  return (int)hipGetLastError();
+}
+
+// rscale[r] = rsqrt(sum_p ssq[r, p] / H + eps): the per-row RMSNorm factor from the slab partials.
+__global__ __launch_bounds__(256) void row_rscale_kernel(const float* __restrict__ ssq, float* __restrict__ rs, int R,
+                                                         int P, int H, float eps) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  const float* p = ssq + (size_t)r * P;
+  float s = 0.f;
+  for (int i = 0; i < P; ++i) s += p[i];
+  rs[r] = rsqrtf(s / (float)H + eps);
+}
+
+EDGE_API int edge_row_rscale(const float* ssq, float* rs, int R, int P, int H, float eps, hipStream_t st) {
+  if (R <= 0) return 0;
+  row_rscale_kernel<<<(R + 255) / 256, 256, 0, st>>>(ssq, rs, R, P, H, eps);
+  return (int)hipGetLastError();
+}

@@ -55,6 +55,15 @@ class DecoderLM:
         self.cos = cos.to(self.device).contiguous()
         self.sin = sin.to(self.device).contiguous()
         self.q_scale = 1.0 / math.sqrt(cfg.head_dim)
+        # GPU fast path for RMSNorm models: the norm weight is folded into the consuming GEMM's weight and
+        # the row scale is applied in its epilogue, from sum-of-squares partials the residual GEMMs emit.
+        self.fuse_norm = (self.device.type == "cuda" and cfg.arch == "qwen2" and dtype == torch.bfloat16
+                          and cfg.hidden_size % 64 == 0)
+        if self.fuse_norm:
+            for L in self.layers:
+                if L is not None:
+                    L["wqkv_n"] = ops.reference.fold_norm_weight(L["wqkv"], L["ln1_w"]).contiguous()
+                    L["wgu_n"] = ops.reference.fold_norm_weight(L["wgu"], L["ln2_w"]).contiguous()
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -199,12 +208,19 @@ class DecoderLM:
         if L is None:
             raise RuntimeError(f"layer {i} is not resident on this stage")
         Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
-        if cfg.arch == "qwen2":
-            h = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps)
+        if self.fuse_norm:
+            ssq = getattr(x, "_edge_ssq", None)
+            if ssq is None:           # stage input / decoded boundary / embedding: one light kernel
+                ssq = ops.row_ssq(x)
+            q, k, vt = ops.qkv_rope(x, L["wqkv_n"], L["bqkv"], self.cos, self.sin, B, S, Hq, Hkv, D,
+                                    cfg.rotary_dim, self.q_scale, norm=(ssq, cfg.norm_eps))
         else:
-            h, h2 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps)
-        q, k, vt = ops.qkv_rope(h, L["wqkv"], L["bqkv"], self.cos, self.sin, B, S, Hq, Hkv, D, cfg.rotary_dim,
-                                self.q_scale)
+            if cfg.arch == "qwen2":
+                h = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps)
+            else:
+                h, h2 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps)
+            q, k, vt = ops.qkv_rope(h, L["wqkv"], L["bqkv"], self.cos, self.sin, B, S, Hq, Hkv, D,
+                                    cfg.rotary_dim, self.q_scale)
         kinds = () if stats is None else ((stats,) if isinstance(stats, str) else tuple(stats))
         for kd in kinds:
             if kd not in ("lastrow", "colsum"):
@@ -214,7 +230,11 @@ class DecoderLM:
         if kinds:
             st = AttnStats(lastrow=ops.attn_lastrow(q, k, S) if "lastrow" in kinds else None,
                            colsum=ops.attn_colsum(q, k, lse, S) if "colsum" in kinds else None)
-        if cfg.arch == "qwen2":
+        if self.fuse_norm:
+            y = ops.linear(o, L["wo"], residual=x, want_ssq=True)
+            a = ops.linear(y, L["wgu_n"], act="swiglu_il", norm=(y._edge_ssq, cfg.norm_eps))
+            y = ops.linear(a, L["wd"], residual=y, out=y, want_ssq=True)   # in place; fresh ssq attached
+        elif cfg.arch == "qwen2":
             y = ops.linear(o, L["wo"], residual=x)
             h = ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps)
             a = ops.linear(h, L["wgu"], act="swiglu_il")

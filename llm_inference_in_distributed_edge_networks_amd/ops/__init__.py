@@ -90,13 +90,62 @@ def set_gemm_tile(tile: int) -> None:
     call("edge_gemm_set_tile", int(tile))
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, out=None) -> torch.Tensor:
-    """``act(x @ w.T + bias) + residual`` on MFMA (``residual`` may alias ``out``)."""
+def row_ssq(x: torch.Tensor) -> torch.Tensor:
+    """Per-row sum of squares in 64-column slabs [T, H/64] (input of the fused-RMSNorm GEMMs)."""
     if not _gpu(x):
-        y = ref.linear(x, w, bias, residual, act)
+        return ref.row_ssq(x)
+    _check_bf16(x)
+    T, H = x.shape
+    out = torch.empty(T, H // 64, dtype=torch.float32, device=x.device)
+    call("edge_row_ssq", ptr(x), ptr(out), T, H, stream())
+    return out
+
+
+def row_rscale(ssq: torch.Tensor, K: int, eps: float) -> torch.Tensor:
+    """rsqrt(sum(ssq_parts)/K + eps) per row: the fused RMSNorm's row scale [T] fp32."""
+    if not ssq.is_cuda:
+        return ref.rownorm_scale(ssq, K, eps)
+    T, P = ssq.shape
+    out = torch.empty(T, dtype=torch.float32, device=ssq.device)
+    call("edge_row_rscale", ptr(ssq), ptr(out), T, P, K, float(eps), stream())
+    return out
+
+
+def _norm_scale(norm, K):
+    """norm = (ssq_parts, eps) -> per-row scale tensor (device side)."""
+    ssq, eps = norm
+    return row_rscale(ssq, K, eps)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, out=None, norm=None,
+           want_ssq: bool = False) -> torch.Tensor:
+    """``act(rowscale * (x @ w.T) + bias) + residual`` on MFMA (``residual`` may alias ``out``).
+
+    ``norm=(ssq, eps)``: fused RMSNorm of ``x`` - rows are scaled by rsqrt(sum(ssq)/K + eps) (``w`` must
+    carry the folded norm weight).  ``want_ssq``: the output's per-row 64-column sum-of-squares partials
+    are produced in the epilogue and attached as ``out._edge_ssq`` (for the next fused norm)."""
+    if not _gpu(x):
+        y = ref.linear(x, w, None, None, None, out_dtype=torch.float32) if norm is not None else None
+        if norm is not None:
+            ssq, eps = norm
+            y = y * ref.rownorm_scale(ssq, x.shape[1], eps).view(-1, 1)
+            if bias is not None:
+                y = y + bias.float()
+            if act == "swiglu_il":
+                g, u = ref.deinterleave_gate_up(y)
+                y = torch.nn.functional.silu(g) * u
+            elif act == "gelu":
+                y = ref.gelu(y)
+            if residual is not None:
+                y = y + residual.float()
+            y = y.to(x.dtype)
+        else:
+            y = ref.linear(x, w, bias, residual, act)
         if out is not None:
             out.copy_(y)
-            return out
+            y = out
+        if want_ssq:
+            y._edge_ssq = ref.row_ssq(y)
         return y
     _check_bf16(x, w, bias, residual)
     M, K = x.shape
@@ -104,14 +153,21 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None,
     No = N // 2 if act == "swiglu_il" else N
     if out is None:
         out = torch.empty(M, No, dtype=x.dtype, device=x.device)
+    rs = None if norm is None else _norm_scale(norm, K)
+    ssq_out = torch.empty(M, No // 64, dtype=torch.float32, device=x.device) if want_ssq else None
     call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), ptr(bias),
-         ptr(residual), 0 if residual is None else residual.stride(0), _ACT[act], stream())
+         ptr(residual), 0 if residual is None else residual.stride(0), _ACT[act], ptr(rs), ptr(ssq_out), stream())
+    if want_ssq:
+        out._edge_ssq = ssq_out
     return out
 
 
-def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
-    """Fused QKV GEMM + bias + RoPE + head-major scatter.  Returns (q, k, vt)."""
+def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=None):
+    """Fused QKV GEMM + bias + RoPE + head-major scatter (+ fused RMSNorm row scale).  Returns (q, k, vt)."""
     if not _gpu(x):
+        if norm is not None:
+            xs = (x.float() * ref.rownorm_scale(norm[0], x.shape[1], norm[1]).view(-1, 1))
+            return ref.qkv_rope(xs, wqkv.float(), bqkv.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
         return ref.qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
     _check_bf16(x, wqkv, bqkv)
     assert D == 64, "HIP attention path is specialised for head_dim 64"
@@ -121,8 +177,9 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
     k = torch.empty(B, Hkv, S, D, dtype=x.dtype, device=x.device)
     vt = torch.zeros(B, Hkv, D, sp, dtype=x.dtype, device=x.device) if sp != S else \
         torch.empty(B, Hkv, D, sp, dtype=x.dtype, device=x.device)
+    rs = None if norm is None else _norm_scale(norm, K)
     call("edge_gemm_qkv_rope", ptr(x), ptr(wqkv), ptr(bqkv), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, K, S,
-         Hq, Hkv, rot_dim, sp, float(q_scale), stream())
+         Hq, Hkv, rot_dim, sp, float(q_scale), ptr(rs), stream())
     return q, k, vt
 
 

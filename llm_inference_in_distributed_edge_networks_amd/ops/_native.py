@@ -28,9 +28,11 @@ _SIGS = {
     "edge_rmsnorm": [c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_p],
     "edge_layernorm": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_p],
     "edge_embedding": [c_p, c_p, c_p, c_i, c_i, c_i, c_p],
-    "edge_gemm": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p],
+    "edge_gemm": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p, c_p, c_p],
+    "edge_row_ssq": [c_p, c_p, c_i, c_i, c_p],
+    "edge_row_rscale": [c_p, c_p, c_i, c_i, c_i, c_f, c_p],
     "edge_gemm_set_tile": [c_i],
-    "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
+    "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p],
     "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],

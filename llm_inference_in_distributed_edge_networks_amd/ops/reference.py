@@ -172,3 +172,19 @@ def head_nll(h, w, targets):
     """Fused final projection + cross entropy: per-row NLL (fp32) = lse(h @ w.T) - logit[target]."""
     logits = _f(h) @ _f(w).t()
     return torch.logsumexp(logits, -1) - logits.gather(1, targets.long().view(-1, 1)).squeeze(1)
+
+
+# ---- fused RMSNorm (GPU fast path) semantics -------------------------------------------------------
+def row_ssq(x: torch.Tensor) -> torch.Tensor:
+    """Per-row sum of squares in 64-column slabs: [T, H/64] fp32."""
+    T, H = x.shape
+    return _f(x).pow(2).reshape(T, H // 64, 64).sum(-1)
+
+
+def rownorm_scale(ssq: torch.Tensor, K: int, eps: float) -> torch.Tensor:
+    return torch.rsqrt(ssq.sum(-1) / K + eps)
+
+
+def fold_norm_weight(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
+    """W' = W diag(norm_w): rmsnorm(x) @ W^T == (x @ W'^T) * rsqrt(mean(x^2) + eps) (up to rounding)."""
+    return (_f(w) * _f(norm_w).view(1, -1)).to(w.dtype)

@@ -210,3 +210,63 @@ def test_tiny_model_gpu_vs_cpu():
         nc = mc.row_nll(xc, rows, tg)
         ng = mg.row_nll(xg, rows.to(DEV), tg.to(DEV))
         assert (nc - ng.cpu()).abs().mean() < 0.05 * nc.abs().mean() + 1e-2, cfg.name
+
+
+# ---- fused RMSNorm path --------------------------------------------------------------------------
+@pytest.mark.parametrize("H", [256, 896])
+def test_row_ssq(H):
+    x = rnd(333, H, seed=90)
+    s = ops.row_ssq(x.to(DEV))
+    close(s, R.row_ssq(x), atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("act", [None, "swiglu_il"])
+def test_gemm_fused_norm_and_ssq_out(tile, act):
+    M, K, N = 700, 896, 1024
+    x = rnd(M, K, seed=91)
+    w = rnd(N, K, s=1 / math.sqrt(K), seed=92)
+    nw = rnd(K, s=0.1, seed=93) + 1
+    ssq = R.row_ssq(x)
+    wn = R.fold_norm_weight(w, nw)
+    ops.set_gemm_tile(tile)
+    try:
+        y = ops.linear(x.to(DEV), wn.to(DEV), act=act, norm=(ssq.to(DEV), 1e-6))
+    finally:
+        ops.set_gemm_tile(0)
+    ref = R.linear(R.rmsnorm(x, nw, 1e-6), w, act=act, out_dtype=torch.float32)
+    close(y, ref, atol=4e-2, rtol=3e-2)
+    # producer side: residual GEMM emits the ssq partials of its stored output
+    r = rnd(M, 896, seed=94)
+    w2 = rnd(896, K, s=1 / math.sqrt(K), seed=95)
+    y2 = ops.linear(x.to(DEV), w2.to(DEV), residual=r.to(DEV), want_ssq=True)
+    close(y2._edge_ssq, R.row_ssq(y2.cpu()), atol=1e-2, rtol=1e-4)
+
+
+def test_qkv_rope_fused_norm():
+    B, S, Hq, Hkv, Hd = 2, 256, 14, 2, 896
+    cos, sin = R.rope_tables(1024, 64, 1e6)
+    x = rnd(B * S, Hd, seed=96)
+    nw = rnd(Hd, s=0.1, seed=97) + 1
+    N = (Hq + 2 * Hkv) * 64
+    w = rnd(N, Hd, s=0.04, seed=98)
+    b = rnd(N, s=0.3, seed=99)
+    q, k, vt = ops.qkv_rope(x.to(DEV), R.fold_norm_weight(w, nw).to(DEV), b.to(DEV), cos.to(DEV), sin.to(DEV),
+                            B, S, Hq, Hkv, 64, 64, 0.125, norm=(R.row_ssq(x).to(DEV), 1e-6))
+    rq, rk, rvt = R.qkv_rope(R.rmsnorm(x, nw, 1e-6), w, b, cos, sin, B, S, Hq, Hkv, 64, 64, 0.125)
+    close(q, rq, atol=3e-2, rtol=3e-2)
+    close(k, rk, atol=4e-2, rtol=3e-2)
+    close(vt, rvt, atol=4e-2, rtol=3e-2)
+
+
+def test_fused_norm_model_matches_unfused():
+    from llm_inference_in_distributed_edge_networks_amd.models import QWEN2_0_5B, DecoderLM
+    cfg = QWEN2_0_5B.replace(num_layers=3, vocab_size=1024)
+    m = DecoderLM.random_init(cfg, 5, device=DEV, dtype=torch.bfloat16, std=0.03)
+    assert m.fuse_norm
+    ids = torch.randint(0, 1024, (2, 256)).to(DEV)
+    xf = m.forward_hidden(ids)
+    m.fuse_norm = False
+    xu = m.forward_hidden(ids)
+    rel = (xf.float() - xu.float()).norm() / xu.float().norm()
+    assert rel < 2e-2, rel
