@@ -91,6 +91,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
   constexpr int MI = CF::MI;
   const int g = lane >> 4;
   const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
+  if (nw >= a.N) return;        // slab beyond N in a partial last column tile (wave-uniform)
 
   if (a.rscale) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
 #pragma unroll
@@ -309,7 +310,7 @@ __device__ __forceinline__ void zero_acc(f32x4_t (&acc)[MI][4]) {
 
 __device__ __forceinline__ void tile_origin(int id, int M, int N, int BM, int BN, int& m0, int& n0) {
   // grouped-M order: GROUP_M consecutive m-panels sweep the n-panels together (A panels stay in L2)
-  const int tm = (M + BM - 1) / BM, tn = N / BN;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int group = id / (GROUP_M * tn);
   const int first_m = group * GROUP_M;
   const int gsz = min(tm - first_m, GROUP_M);
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
   constexpr int BM = CF::BM, BN = CF::BN, MI = CF::MI, NW = CF::NW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / CF::NWN, wn = wave % CF::NWN;
-  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
+  const int tm = (a.M + BM - 1) / BM, tn = (a.N + BN - 1) / BN;  // last column tile may be partial
   const int ntiles = tm * tn;
 
   f32x4_t acc[MI][4];
@@ -484,7 +485,7 @@ static int num_cus() {
 
 template <int EPI, int RH, class CF>
 static int launch_cfg(const GemmArgs& a, hipStream_t st) {
-  const int tm = (a.M + CF::BM - 1) / CF::BM, tn = a.N / CF::BN;
+  const int tm = (a.M + CF::BM - 1) / CF::BM, tn = (a.N + CF::BN - 1) / CF::BN;
   const int grid = CF::PIPE ? std::min(tm * tn, num_cus()) : tm * tn;
   static bool attr = false;
   if (!attr) {
@@ -504,8 +505,11 @@ static int launch(const GemmArgs& a, hipStream_t st) {
   if constexpr (EPI == EPI_QKV_ROPE || EPI == EPI_LSE) {
     return launch_cfg<EPI, RH, C128>(a, st);
   } else {
-    const bool big = (a.N % 256 == 0) && ((long long)((a.M + 255) / 256) * (a.N / 256) >= 256);
-    const bool use256 = g_tile_override ? g_tile_override == 256 && a.N % 256 == 0 : big;
+    // a partial last column tile (N % 256 == 128) wastes at most 1/(2*tn) of the MFMA work
+    const int tn = (a.N + 255) / 256;
+    const bool fits = a.N % 256 == 0 || (a.N % 128 == 0 && tn >= 4 && EPI != EPI_SWIGLU);
+    const bool big = fits && ((long long)((a.M + 255) / 256) * tn >= 256);
+    const bool use256 = g_tile_override ? g_tile_override == 256 && fits : big;
     return use256 ? launch_cfg<EPI, RH, C256>(a, st) : launch_cfg<EPI, RH, C128>(a, st);
   }
 }

@@ -58,12 +58,12 @@ def test_layernorm_dual():
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 1152, 896), (300, 896, 896), (1000, 256, 512), (64, 128, 4864),
-                                   (700, 1024, 640)])
+                                   (700, 1024, 640), (600, 896, 640)])
 @pytest.mark.parametrize("epi", ["none", "bias", "resid", "bias_resid", "gelu", "swiglu"])
 @pytest.mark.parametrize("tile", [128, 256])
 def test_gemm(M, N, K, epi, tile):
-    if tile == 256 and N % 256:
-        pytest.skip("256 tile needs N % 256 == 0")
+    if tile == 256 and (N % 256 and (N % 128 or N < 768 or epi == "swiglu")):
+        pytest.skip("256 tile needs N % 256 == 0, or N % 128 == 0 with >= 4 column tiles")
     ops.set_gemm_tile(tile)
     try:
         _gemm_case(M, N, K, epi)

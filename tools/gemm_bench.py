@@ -18,6 +18,9 @@ SHAPES = {  # name: (M, N, K, act, bias, resid)
     "gate_up": (8192, 9728, 896, "swiglu_il", False, False),
     "down": (8192, 896, 4864, None, False, True),
     "lm_head": (512, 151936, 896, None, False, False),
+    "down_b64": (32768, 896, 4864, None, False, True),
+    "o_proj_b64": (32768, 896, 896, None, False, True),
+    "gate_up_b64": (32768, 9728, 896, "swiglu_il", False, False),
     "big": (8192, 8192, 8192, None, False, False),
 }
 
