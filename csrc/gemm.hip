@@ -308,6 +308,14 @@ __device__ __forceinline__ void zero_acc(f32x4_t (&acc)[MI][4]) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 }
 
+// 32-bit LDS address of a pointer into dynamic shared memory
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// ds_read_b128 hidden from the compiler's waitcnt insertion: the caller owns the lgkmcnt accounting.
+#define DS_READ_B128(dst, vaddr, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(vaddr), "i"(off))
+
 __device__ __forceinline__ void tile_origin(int id, int M, int N, int BM, int BN, int& m0, int& n0) {
   // grouped-M order: GROUP_M consecutive m-panels sweep the n-panels together (A panels stay in L2)
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
@@ -319,7 +327,7 @@ __device__ __forceinline__ void tile_origin(int id, int M, int N, int BM, int BN
   n0 = (in_g / gsz) * BN;
 }
 
-template <int EPI, int RH, class CF>
+template <int EPI, int RH, class CF, bool AR = false>
 __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BM = CF::BM, BN = CF::BN, MI = CF::MI, NW = CF::NW;
@@ -350,10 +358,18 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
   constexpr int MG = MI / 4, NS = 2 * MG;
   bf16x8_t XA[4], XB[4], YA[4], YB[4];
   auto ld = [&](bf16x8_t(&FA)[4], bf16x8_t(&FB)[4], const char* buf, int ks, int mg) {
+    if constexpr (AR) {
+      const uint32_t va = lds_addr(buf) + abase[ks], vb = lds_addr(buf) + bbase[ks];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) FA[i] = *(const bf16x8_t*)(buf + abase[ks] + (mg * 4 + i) * 2048);
+      for (int i = 0; i < 4; ++i) DS_READ_B128(FA[i], va, (mg * 4 + i) * 2048);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) FB[j] = *(const bf16x8_t*)(buf + bbase[ks] + j * 2048);
+      for (int j = 0; j < 4; ++j) DS_READ_B128(FB[j], vb, j * 2048);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) FA[i] = *(const bf16x8_t*)(buf + abase[ks] + (mg * 4 + i) * 2048);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) FB[j] = *(const bf16x8_t*)(buf + bbase[ks] + j * 2048);
+    }
   };
   auto mma = [&](const bf16x8_t(&FA)[4], const bf16x8_t(&FB)[4], int mg) {
 #pragma unroll
@@ -415,6 +431,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
     wait_vmcnt0();
     __syncthreads();
     ld(XA, XB, smem, 0, 0);
+    if constexpr (AR) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     int g = 0;  // K-tiles consumed by this workgroup (LDS buffer parity)
     while (true) {
       const int next = tile + G;
@@ -451,7 +468,11 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
           // keep the next sub-step's LDS reads ahead of this sub-step's MFMAs (the scheduler would
           // otherwise sink them below the MFMAs and wait lgkmcnt(0), serialising reads and math)
           __builtin_amdgcn_sched_barrier(0);
-          if (s + 1 < NS) __builtin_amdgcn_s_waitcnt(0xC87F);  // lgkmcnt(8): this set was issued a sub-step ago
+          if (s + 1 < NS) {  // lgkmcnt(8): this set was issued a sub-step ago, the next set's 8 reads may fly
+            if constexpr (AR) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+            else __builtin_amdgcn_s_waitcnt(0xC87F);
+          }
+          if constexpr (AR) __builtin_amdgcn_sched_barrier(0);  // an asm wait does not fence the MFMAs
           if (s & 1) mma(YA, YB, mg); else mma(XA, XB, mg);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -472,6 +493,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
 }
 
 static int g_tile_override = 0;  // 0 auto, 128 or 256 (tests / tuning)
+static int g_asm_reads = 1;      // 256x256 main loop: fragment reads via inline asm (1) or plain loads (0)
 
 static int num_cus() {
   static int n = 0;
@@ -483,17 +505,17 @@ static int num_cus() {
   return n;
 }
 
-template <int EPI, int RH, class CF>
+template <int EPI, int RH, class CF, bool AR = false>
 static int launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int tm = (a.M + CF::BM - 1) / CF::BM, tn = (a.N + CF::BN - 1) / CF::BN;
   const int grid = CF::PIPE ? std::min(tm * tn, num_cus()) : tm * tn;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, RH, CF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        CF::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, RH, CF, AR>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, RH, CF>), dim3(grid), dim3(CF::NT), CF::LDS, st, a);
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, RH, CF, AR>), dim3(grid), dim3(CF::NT), CF::LDS, st, a);
   return (int)hipGetLastError();
 }
 
@@ -510,12 +532,18 @@ static int launch(const GemmArgs& a, hipStream_t st) {
     const bool fits = a.N % 256 == 0 || (a.N % 128 == 0 && tn >= 4 && EPI != EPI_SWIGLU);
     const bool big = fits && ((long long)((a.M + 255) / 256) * tn >= 256);
     const bool use256 = g_tile_override ? g_tile_override == 256 && fits : big;
-    return use256 ? launch_cfg<EPI, RH, C256>(a, st) : launch_cfg<EPI, RH, C128>(a, st);
+    if (!use256) return launch_cfg<EPI, RH, C128>(a, st);
+    return g_asm_reads ? launch_cfg<EPI, RH, C256, true>(a, st) : launch_cfg<EPI, RH, C256, false>(a, st);
   }
 }
 
 EDGE_API int edge_gemm_set_tile(int t) {
   g_tile_override = t;
+  return 0;
+}
+
+EDGE_API int edge_gemm_set_asm_reads(int on) {
+  g_asm_reads = on;
   return 0;
 }
 

@@ -90,6 +90,11 @@ def set_gemm_tile(tile: int) -> None:
     call("edge_gemm_set_tile", int(tile))
 
 
+def set_gemm_asm_reads(on: bool) -> None:
+    """256x256 GEMM main loop: hand-counted asm fragment reads (default) or compiler-waited loads.  A/B only."""
+    call("edge_gemm_set_asm_reads", int(bool(on)))
+
+
 def row_ssq(x: torch.Tensor) -> torch.Tensor:
     """Per-row sum of squares in 64-column slabs [T, H/64] (input of the fused-RMSNorm GEMMs)."""
     if not _gpu(x):

@@ -17,6 +17,7 @@ computes the per-window NLL of the scored rows.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -182,7 +183,7 @@ class DistributedPipeline:
     """One pipeline stage per rank; ``grid.dp`` replicas share the window batches round-robin."""
 
     def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig, grid: Grid, rank: int,
-                 use_graphs: bool = True, transport: str = "torch"):
+                 use_graphs: bool = True, transport: str = "torch", check: bool | None = None):
         self.model, self.plan, self.bcfg, self.grid, self.rank = model, plan, bcfg, grid, rank
         self.dp_idx, self.stage = grid.coords(rank)
         if plan.num_stages != grid.pp:
@@ -200,6 +201,11 @@ class DistributedPipeline:
             self.tr = TorchP2P()
         else:
             raise ValueError(f"unknown transport {transport!r}")
+        if check is None:
+            check = os.environ.get("EDGE_P2P_CHECK", "0") not in ("", "0")
+        if check:
+            from .rccl import CheckedTransport
+            self.tr = CheckedTransport(self.tr)
 
     def _stage_step(self, ids, rows, targets, row_window, n_rows, msg_in=None, carry_in=None):
         return self.runner.forward(ids, rows, targets, row_window, n_rows, msg_in, carry_in)

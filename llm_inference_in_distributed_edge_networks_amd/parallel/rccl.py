@@ -126,3 +126,65 @@ class TorchP2P:
     def recv(self, t, peer):
         import torch.distributed as dist
         return dist.irecv(t, peer)
+
+
+class P2PIntegrityError(RuntimeError):
+    """A boundary message arrived corrupted, truncated or out of order (checked transport only)."""
+
+
+def fingerprint(t: torch.Tensor, seq: int) -> torch.Tensor:
+    """[seq, nbytes, sum(b), sum(b * w)] int64 of a tensor's bytes, ``w = 1 + (pos mod 251)``.
+
+    The position weight catches swapped or shifted byte ranges, which a plain byte sum misses."""
+    b = t.detach().contiguous().view(-1).view(torch.uint8).to(torch.int64)
+    w = torch.arange(b.numel(), device=b.device, dtype=torch.int64).remainder_(251).add_(1)
+    head = torch.tensor([seq, b.numel()], dtype=torch.int64, device=b.device)
+    return torch.cat([head, b.sum().view(1), (b * w).sum().view(1)])
+
+
+class _CheckedRecv:
+    def __init__(self, tr, t, fp, reqs, seq, peer):
+        self.tr, self.t, self.fp, self.reqs, self.seq, self.peer = tr, t, fp, reqs, seq, peer
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+        got = self.fp.cpu().tolist()
+        want = fingerprint(self.t, self.seq).cpu().tolist()
+        if got != want:
+            raise P2PIntegrityError(f"message {self.seq} from rank {self.peer}: sender fingerprint "
+                                    f"[seq, bytes, sum, wsum]={got}, received data gives {want}")
+
+
+class _CheckedSend:
+    def __init__(self, reqs):
+        self.reqs = reqs
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+
+
+class CheckedTransport:
+    """Debug wrapper (SURVEY §5.2 "P2P ordering tests with payload checksums"): every message is followed by
+    a 32-byte fingerprint carrying a per-peer sequence number; the receiver recomputes it after the
+    transfer and raises :class:`P2PIntegrityError` on any mismatch.  Costs a host sync per receive, so it
+    is opt-in (``EDGE_P2P_CHECK=1`` or ``DistributedPipeline(..., check=True)``)."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.sent: dict[int, int] = {}
+        self.recvd: dict[int, int] = {}
+
+    def send(self, t, peer):
+        seq = self.sent.get(peer, 0)
+        self.sent[peer] = seq + 1
+        fp = fingerprint(t, seq)
+        return _CheckedSend([self.inner.send(t, peer), self.inner.send(fp, peer)])
+
+    def recv(self, t, peer):
+        seq = self.recvd.get(peer, 0)
+        self.recvd[peer] = seq + 1
+        fp = torch.empty(4, dtype=torch.int64, device=t.device)
+        reqs = [self.inner.recv(t, peer), self.inner.recv(fp, peer)]
+        return _CheckedRecv(self, t, fp, reqs, seq, peer)

@@ -31,3 +31,44 @@ def run(rank, world, port, pp, codec, ratio, method, out_path, split):
         with open(out_path, "w") as f:
             json.dump({"ppl": acc.ppl(), "n": acc.n_tokens}, f)
     shutdown()
+
+
+def run_checked(rank, world, port, out_path, corrupt):
+    """Fingerprinted p2p: rank 0 sends 3 messages (the 2nd corrupted in flight if ``corrupt``)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from llm_inference_in_distributed_edge_networks_amd.parallel import init_distributed, shutdown
+    from llm_inference_in_distributed_edge_networks_amd.parallel.rccl import (CheckedTransport, P2PIntegrityError,
+                                                                             TorchP2P)
+
+    class Flip(TorchP2P):  # flips one bit of the 2nd payload after the sender fingerprinted it
+        n = 0
+
+        def send(self, t, peer):
+            if t.dtype == torch.uint8:
+                Flip.n += 1
+                if corrupt and Flip.n == 2:
+                    t = t.clone()
+                    t[77] ^= 4
+            return super().send(t, peer)
+
+    init_distributed("cpu", timeout_s=60)
+    tr = CheckedTransport(Flip())
+    msgs = [torch.randint(0, 256, (1000 + 13 * i,), dtype=torch.uint8, generator=torch.Generator().manual_seed(i))
+            for i in range(3)]
+    if rank == 0:
+        for h in [tr.send(m, 1) for m in msgs]:
+            h.wait()
+    else:
+        res = {"ok": 0, "error": None}
+        for m in msgs:
+            buf = torch.empty_like(m)
+            try:
+                tr.recv(buf, 0).wait()
+                res["ok"] += int(torch.equal(buf, m))
+            except P2PIntegrityError as e:
+                res["error"] = str(e)
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+    shutdown()

@@ -60,3 +60,24 @@ def test_grid_and_plan():
     assert PipelinePlan.from_split_layers(24, [11]).stage_layers(1) == range(12, 24)
     with pytest.raises(ValueError):
         PipelinePlan.from_split_layers(24, [23])
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_checked_transport_detects_corruption(tmp_path, corrupt):
+    out = tmp_path / "res.json"
+    mp.spawn(dist_worker.run_checked, args=(2, free_port(), str(out), corrupt), nprocs=2, join=True)
+    res = json.loads(out.read_text())
+    if corrupt:
+        assert res["ok"] == 2 and "message 1 from rank 0" in res["error"]
+    else:
+        assert res == {"ok": 3, "error": None}
+
+
+def test_distributed_checked_pipeline(tmp_path, monkeypatch):
+    """EDGE_P2P_CHECK=1: every boundary message (payload + carry) is fingerprinted; results unchanged."""
+    monkeypatch.setenv("EDGE_P2P_CHECK", "1")
+    out = tmp_path / "res.json"
+    args = (3, free_port(), 3, "mixed_int4_int8", 0.5, "aggregate_till", str(out), [0, 2])
+    mp.spawn(dist_worker.run, args=args, nprocs=3, join=True)
+    ref = local_ppl(PipelinePlan.from_split_layers(4, [0, 2]), "mixed_int4_int8", 0.5, "aggregate_till")
+    assert abs(json.loads(out.read_text())["ppl"] - ref) / ref < 1e-6

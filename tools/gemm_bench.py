@@ -42,7 +42,8 @@ def main():
     ap.add_argument("--m", type=int, default=0, help="override M")
     ap.add_argument("--json", default="")
     ap.add_argument("--only", default="", help="comma list of shapes")
-    ap.add_argument("--tiles", default="0", help="comma list of forced tiles (0=auto,128,256)")
+    ap.add_argument("--tiles", default="0", help="comma list of forced tiles (0=auto,128,256); suffix p = 256x256 "
+                    "main loop with plain (compiler-waited) fragment loads instead of asm reads, e.g. 256,256p")
     ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt comparison (profiling)")
     a = ap.parse_args()
     dev = "cuda"
@@ -57,11 +58,14 @@ def main():
         No = N // 2 if act == "swiglu_il" else N
         r = torch.randn(M, No, device=dev).to(torch.bfloat16) if resid else None
         out = torch.empty(M, No, device=dev, dtype=torch.bfloat16)
-        tiles = [int(t) for t in a.tiles.split(",")]
+        tiles = a.tiles.split(",")
 
-        def mk(tile):
+        def mk(spec):
+            tile, asm_reads = int(spec.rstrip("p")), not spec.endswith("p")
+
             def f():
                 ops.set_gemm_tile(tile)
+                ops.set_gemm_asm_reads(asm_reads)
                 ops.linear(x, w, bias=b, residual=r, act=act, out=out)
             return f
         variants = {t: mk(t) for t in tiles}
@@ -77,9 +81,10 @@ def main():
             t_o.append(min(statistics.median(v) for v in t_v.values()))
             t_l.append(timeit(lib, a.iters) if not a.no_lib else 1.0)
         ops.set_gemm_tile(0)
+        ops.set_gemm_asm_reads(True)
         fl = 2.0 * M * N * K
         for t, v in t_v.items():
-            print(f"   tile={t:3d}: {statistics.median(v)*1e6:8.1f}us {fl/statistics.median(v)/1e12:7.1f} TF", flush=True)
+            print(f"   tile={t:>4s}: {statistics.median(v)*1e6:8.1f}us {fl/statistics.median(v)/1e12:7.1f} TF", flush=True)
         res[name] = {"M": M, "N": N, "K": K, "ours_us": statistics.median(t_o) * 1e6,
                      "hipblaslt_us": statistics.median(t_l) * 1e6,
                      "ours_tflops": fl / statistics.median(t_o) / 1e12,
