@@ -492,8 +492,193 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
   }
 }
 
+// ---- 256x256 persistent GEMM with a 4-slot K-half ring (counted vmcnt, loads in flight across barriers) ----
+// The K loop is cut into K-halves of 32 columns.  LDS holds a ring of 4 slots, each one K-half of the A and B
+// tiles (256 rows x 64 B each, 32 KiB).  A K-half is consumed in two phases of 16 MFMAs per wave (m-tiles
+// 0-3, then 4-7 of the wave's 128x64 slab), so a phase p works on K-half q = p/2 of a CTA-wide sequence that
+// runs through all of this workgroup's tiles (the next tile's operands stream in under the epilogue).
+// Per phase, after one barrier:
+//   stage   half of K-half q+3 (2 glds per thread: A rows at even phases, B rows at odd phases) into the
+//           slot K-half q-1 used (WAR: its last reads were retired by the previous phase's lgkmcnt);
+//   read    the fragments of phase p+1 (inline asm ds_read_b128, counted by hand);
+//   wait    lgkmcnt(#just issued) -> this phase's fragments, then 16 MFMAs;
+//   even p: s_waitcnt vmcnt(N) for K-half q+1 (N = the <= 6 glds issued after it), made visible by the
+//           next phase's barrier before phase p+1 reads it.
+// vmcnt never drains to 0 in the loop: every K-half has >= 3 phases (~1500 MFMA cycles per SIMD) to land.
+// LDS image: row r of a slot is 64 B, 16-B chunk c stored at position c ^ ring_swz((r >> 2) & 3); the swizzle
+// is applied to the glds source address and to the fragment read.
+//
+// ds_read_b128 is serviced in four 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59},
+// {36-43,48-51,60-63} (MI355X_MICROARCH.md §LDS).  A fragment lane reads row (lane & 15), chunk lane >> 4, so
+// a group holds rows R=r>>2 in {0,3} at one chunk and {1,2} at the next (or the reverse); its 16 addresses
+// fall on 16 distinct 16-B bank slots (r & 3, position) iff g maps each such pair apart: g = [0,2,3,1].
+__device__ __forceinline__ int ring_swz(int R) { return (R >> 1) | (((R ^ (R >> 1)) & 1) << 1); }
+
+template <int EPI, int RH, bool PRIO>
+__global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
+  using CF = C256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int SLOT = 32768, BOFF = 16384;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tm = (a.M + 255) / 256, tn = (a.N + 255) / 256, ntiles = tm * tn;
+  const int G = gridDim.x;
+  const int tile0 = xcd_remap(blockIdx.x, G);
+  if (tile0 >= ntiles) return;
+  const int nkh = a.K / 32;
+  const int total = ((ntiles - 1 - tile0) / G + 1) * nkh;  // K-halves this workgroup consumes
+
+  // staging: wave w issues instructions u = 2w, 2w+1 of the 16 per operand (16 rows x 64 B each);
+  // lane -> row (lane >> 2) of the instruction, physical chunk lane & 3 = logical chunk ^ ((row >> 2) & 3)
+  const int srow = lane >> 2, schunk = (lane & 3) ^ ring_swz((lane >> 4) & 3);
+  // saddr-form glds: uniform tile base (SGPRs, advanced per K-half) + per-lane 32-bit byte offset (VGPRs, fixed
+  // per tile).  Redefining a glds address VGPR makes the compiler wait vmcnt(0) first, so none is rewritten.
+  const char* sa = nullptr;
+  const char* sb = nullptr;
+  uint32_t oa[2], ob[2];
+  auto set_stage_tile = [&](int t) {
+    int m0, n0;
+    tile_origin(t, a.M, a.N, 256, 256, m0, n0);
+    sa = (const char*)(a.A + (size_t)m0 * a.lda);
+    sb = (const char*)(a.B + (size_t)n0 * a.ldb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (2 * wave + i) * 16 + srow;
+      const int ra = min(r, a.M - 1 - m0), rb = min(r, a.N - 1 - n0);
+      oa[i] = (uint32_t)(ra * a.lda + schunk * 8) * 2u;
+      ob[i] = (uint32_t)(rb * a.ldb + schunk * 8) * 2u;
+    }
+  };
+  int st_q = 0, st_kh = 0, st_tile = tile0;  // next K-half to stage, its index within its tile, its tile
+  set_stage_tile(tile0);
+  auto stage_part = [&](int part) {  // part 0: A rows, part 1: B rows of K-half st_q (then advance)
+    char* slot = smem + (st_q & 3) * SLOT;
+    const int kb = st_kh * 64;  // bytes
+    if (part == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(sa + kb + oa[i], slot + (2 * wave + i) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(sb + kb + ob[i], slot + BOFF + (2 * wave + i) * 1024);
+      ++st_q;
+      if (++st_kh == nkh && st_q < total) {
+        st_kh = 0;
+        st_tile += G;
+        set_stage_tile(st_tile);
+      }
+    }
+  };
+
+  // fragment addresses: row = base + (lane & 15) -> (row >> 2) & 3 == (lane >> 2) & 3; logical chunk lane >> 4
+  const int fpos = ((lane >> 4) ^ ring_swz((lane >> 2) & 3)) << 4;
+  const uint32_t abase = lds_addr(smem) + (wm * 128 + (lane & 15)) * 64 + fpos;
+  const uint32_t bbase = lds_addr(smem) + BOFF + (wn * 64 + (lane & 15)) * 64 + fpos;
+  bf16x8_t FA0[4], FA1[4], FB0[4], FB1[4];
+  auto read_a = [&](bf16x8_t(&FA)[4], int q, int sub) {
+    const uint32_t va = abase + (q & 3) * SLOT;
+    if (sub == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) DS_READ_B128(FA[i], va, i * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) DS_READ_B128(FA[i], va, (4 + i) * 1024);
+    }
+  };
+  auto read_b = [&](bf16x8_t(&FB)[4], int q) {
+    const uint32_t vb = bbase + (q & 3) * SLOT;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) DS_READ_B128(FB[j], vb, j * 1024);
+  };
+  f32x4_t acc[8][4];
+  zero_acc<8>(acc);
+  auto mma = [&](const bf16x8_t(&FA)[4], const bf16x8_t(&FB)[4], int sub) {
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+    if (sub == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[4 + i][j], 0, 0, 0);
+    }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: K-halves 0..2 in flight, wait for K-half 0, read phase 0's fragments
+#pragma unroll 1
+  for (int i = 0; i < 3; ++i)
+    if (st_q < total) { stage_part(0); stage_part(1); }
+  if (total >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (total == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  read_a(FA0, 0, 0);
+  read_b(FB0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+
+  int tile = tile0, kh = 0;  // compute side: current tile, K-half within it
+  int m0, n0;
+  tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
+  // K-half q: even phase (m-tiles 0-3, FA0) and odd phase (m-tiles 4-7, FA1), B fragments FBc; the odd
+  // phase reads K-half q+1's first A set and its B set FBn.  Unrolled by two K-halves (K % 64 == 0) so
+  // the B register set is static and a tile always ends after an odd K-half.
+  auto khalf = [&](int q, bf16x8_t(&FBc)[4], bf16x8_t(&FBn)[4]) {
+    // ---- even phase 2q
+    __builtin_amdgcn_s_barrier();
+    if (st_q == q + 3 && st_q < total) stage_part(0);
+    read_a(FA1, q, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(FA0, FBc, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    // K-half q+1 must have landed before the next phase's barrier (its reads follow that barrier)
+    if (q + 3 < total) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (q + 2 < total) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- odd phase 2q+1
+    __builtin_amdgcn_s_barrier();
+    if (st_q == q + 3 && st_q < total) stage_part(1);
+    if (q + 1 < total) {
+      read_a(FA0, q + 1, 0);
+      read_b(FBn, q + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mma(FA1, FBc, 1);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#pragma unroll 1
+  for (int q = 0; q < total; q += 2) {
+    khalf(q, FB0, FB1);
+    khalf(q + 1, FB1, FB0);
+    kh += 2;
+    if (kh == nkh) {  // tile done: epilogue (the next tile's first K-halves are already in flight)
+      if (n0 + wn * 64 < a.N) {  // (no row-scale loads left unconsumed on the skip path: they would
+        float rs[8];             //  make the compiler drain vmcnt at the loop head)
+        load_rscale<8, 128>(a, m0, wm, lane, rs);
+        gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
+      }
+      zero_acc<8>(acc);
+      kh = 0;
+      tile += G;
+      if (tile < ntiles) tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 static int g_tile_override = 0;  // 0 auto, 128 or 256 (tests / tuning)
-static int g_asm_reads = 1;      // 256x256 main loop: fragment reads via inline asm (1) or plain loads (0)
+// 256x256 main loop: 0 = K-tile double buffer, compiler-waited fragment loads; 1 = same with hand-counted asm
+// reads; 2 = K-half ring (gemm_ring_kernel); 3 = ring with s_setprio around the MFMA clusters
+static int g_c256_variant = 1;
 
 static int num_cus() {
   static int n = 0;
@@ -519,6 +704,20 @@ static int launch_cfg(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+template <int EPI, int RH, bool PRIO>
+static int launch_ring(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const int grid = std::min(tiles, num_cus());
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<EPI, RH, PRIO>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 32768);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_ring_kernel<EPI, RH, PRIO>), dim3(grid), dim3(512), 4 * 32768, st, a);
+  return (int)hipGetLastError();
+}
+
 template <int EPI, int RH = 0>
 static int launch(const GemmArgs& a, hipStream_t st) {
   // 256x256 persistent tiles when the shape can fill the chip with them (halves L2->LDS traffic per
@@ -533,7 +732,12 @@ static int launch(const GemmArgs& a, hipStream_t st) {
     const bool big = fits && ((long long)((a.M + 255) / 256) * tn >= 256);
     const bool use256 = g_tile_override ? g_tile_override == 256 && fits : big;
     if (!use256) return launch_cfg<EPI, RH, C128>(a, st);
-    return g_asm_reads ? launch_cfg<EPI, RH, C256, true>(a, st) : launch_cfg<EPI, RH, C256, false>(a, st);
+    switch (g_c256_variant) {
+      case 0: return launch_cfg<EPI, RH, C256, false>(a, st);
+      case 2: return launch_ring<EPI, RH, false>(a, st);
+      case 3: return launch_ring<EPI, RH, true>(a, st);
+      default: return launch_cfg<EPI, RH, C256, true>(a, st);
+    }
   }
 }
 
@@ -542,8 +746,8 @@ EDGE_API int edge_gemm_set_tile(int t) {
   return 0;
 }
 
-EDGE_API int edge_gemm_set_asm_reads(int on) {
-  g_asm_reads = on;
+EDGE_API int edge_gemm_set_variant(int v) {
+  g_c256_variant = v;
   return 0;
 }
 

@@ -90,9 +90,20 @@ def set_gemm_tile(tile: int) -> None:
     call("edge_gemm_set_tile", int(tile))
 
 
-def set_gemm_asm_reads(on: bool) -> None:
-    """256x256 GEMM main loop: hand-counted asm fragment reads (default) or compiler-waited loads.  A/B only."""
-    call("edge_gemm_set_asm_reads", int(bool(on)))
+GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3}
+
+
+def set_gemm_variant(v: int) -> None:
+    """256x256 GEMM main loop (A/B and tests): 0 K-tile double buffer with compiler-waited fragment loads,
+    1 the same with hand-counted asm reads, 2 the K-half ring, 3 the ring with s_setprio."""
+    call("edge_gemm_set_variant", int(v))
+
+
+def set_gemm_config(spec: str) -> None:
+    """'0' (automatic), '128', or '256' + variant suffix ('', 'p', 'r', 'rp'), e.g. '256r'."""
+    tile = int(spec.rstrip("pr"))
+    set_gemm_tile(tile)
+    set_gemm_variant(GEMM_VARIANTS[spec[len(str(tile)):]] if tile == 256 else GEMM_VARIANTS[""])
 
 
 def row_ssq(x: torch.Tensor) -> torch.Tensor:

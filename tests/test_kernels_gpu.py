@@ -60,15 +60,28 @@ def test_layernorm_dual():
 @pytest.mark.parametrize("M,N,K", [(512, 1152, 896), (300, 896, 896), (1000, 256, 512), (64, 128, 4864),
                                    (700, 1024, 640), (600, 896, 640)])
 @pytest.mark.parametrize("epi", ["none", "bias", "resid", "bias_resid", "gelu", "swiglu"])
-@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("tile", ["128", "256", "256p", "256r"])
 def test_gemm(M, N, K, epi, tile):
-    if tile == 256 and (N % 256 and (N % 128 or N < 768 or epi == "swiglu")):
+    if tile != "128" and (N % 256 and (N % 128 or N < 768 or epi == "swiglu")):
         pytest.skip("256 tile needs N % 256 == 0, or N % 128 == 0 with >= 4 column tiles")
-    ops.set_gemm_tile(tile)
+    ops.set_gemm_config(tile)
     try:
         _gemm_case(M, N, K, epi)
     finally:
-        ops.set_gemm_tile(0)
+        ops.set_gemm_config("0")
+
+
+@pytest.mark.parametrize("tile", ["256", "256r", "256rp"])
+@pytest.mark.parametrize("M,N,K,epi", [(4352 + 37, 4096, 192, "resid"), (4352, 4096, 64, "swiglu"),
+                                       (4400, 3968, 128, "bias_resid")])
+def test_gemm_persistent_multi_tile(M, N, K, epi, tile):
+    """More 256x256 tiles than CUs: workgroups walk several tiles, the K-half ring streams across tile
+    boundaries (K=64: two K-halves per tile, the shortest ring), partial last row/column tiles."""
+    ops.set_gemm_config(tile)
+    try:
+        _gemm_case(M, N, K, epi)
+    finally:
+        ops.set_gemm_config("0")
 
 
 def _gemm_case(M, N, K, epi):
@@ -85,15 +98,15 @@ def _gemm_case(M, N, K, epi):
     close(y, ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("tile", ["128", "256", "256r"])
 def test_gemm_asymmetric_identity(tile):
     # A = I, asymmetric B: catches a transposed C-write
     K = 256
     x = torch.eye(K, dtype=torch.bfloat16)
     w = torch.arange(512 * K, dtype=torch.float32).reshape(512, K).remainder(97).sub(48).to(torch.bfloat16)
-    ops.set_gemm_tile(tile)
+    ops.set_gemm_config(tile)
     y = ops.linear(x.to(DEV), w.to(DEV))
-    ops.set_gemm_tile(0)
+    ops.set_gemm_config("0")
     assert torch.equal(y.cpu().float(), w.t().float())
 
 
@@ -220,7 +233,7 @@ def test_row_ssq(H):
     close(s, R.row_ssq(x), atol=1e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("tile", ["128", "256", "256r"])
 @pytest.mark.parametrize("act", [None, "swiglu_il"])
 def test_gemm_fused_norm_and_ssq_out(tile, act):
     M, K, N = 700, 896, 1024
@@ -229,17 +242,17 @@ def test_gemm_fused_norm_and_ssq_out(tile, act):
     nw = rnd(K, s=0.1, seed=93) + 1
     ssq = R.row_ssq(x)
     wn = R.fold_norm_weight(w, nw)
-    ops.set_gemm_tile(tile)
+    ops.set_gemm_config(tile)
     try:
         y = ops.linear(x.to(DEV), wn.to(DEV), act=act, norm=(ssq.to(DEV), 1e-6))
+        r = rnd(M, 896, seed=94)
+        w2 = rnd(896, K, s=1 / math.sqrt(K), seed=95)
+        y2 = ops.linear(x.to(DEV), w2.to(DEV), residual=r.to(DEV), want_ssq=True)
     finally:
-        ops.set_gemm_tile(0)
+        ops.set_gemm_config("0")
     ref = R.linear(R.rmsnorm(x, nw, 1e-6), w, act=act, out_dtype=torch.float32)
     close(y, ref, atol=4e-2, rtol=3e-2)
     # producer side: residual GEMM emits the ssq partials of its stored output
-    r = rnd(M, 896, seed=94)
-    w2 = rnd(896, K, s=1 / math.sqrt(K), seed=95)
-    y2 = ops.linear(x.to(DEV), w2.to(DEV), residual=r.to(DEV), want_ssq=True)
     close(y2._edge_ssq, R.row_ssq(y2.cpu()), atol=1e-2, rtol=1e-4)
 
 

@@ -42,8 +42,8 @@ def main():
     ap.add_argument("--m", type=int, default=0, help="override M")
     ap.add_argument("--json", default="")
     ap.add_argument("--only", default="", help="comma list of shapes")
-    ap.add_argument("--tiles", default="0", help="comma list of forced tiles (0=auto,128,256); suffix p = 256x256 "
-                    "main loop with plain (compiler-waited) fragment loads instead of asm reads, e.g. 256,256p")
+    ap.add_argument("--tiles", default="0", help="comma list of GEMM configs: 0=auto, 128, 256 + main-loop variant "
+                    "suffix ('' asm reads, p plain loads, r K-half ring, rp ring + setprio), e.g. 256,256r")
     ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt comparison (profiling)")
     a = ap.parse_args()
     dev = "cuda"
@@ -61,11 +61,8 @@ def main():
         tiles = a.tiles.split(",")
 
         def mk(spec):
-            tile, asm_reads = int(spec.rstrip("p")), not spec.endswith("p")
-
             def f():
-                ops.set_gemm_tile(tile)
-                ops.set_gemm_asm_reads(asm_reads)
+                ops.set_gemm_config(spec)
                 ops.linear(x, w, bias=b, residual=r, act=act, out=out)
             return f
         variants = {t: mk(t) for t in tiles}
@@ -80,8 +77,7 @@ def main():
                 t_v[t].append(timeit(f, a.iters))
             t_o.append(min(statistics.median(v) for v in t_v.values()))
             t_l.append(timeit(lib, a.iters) if not a.no_lib else 1.0)
-        ops.set_gemm_tile(0)
-        ops.set_gemm_asm_reads(True)
+        ops.set_gemm_config("0")
         fl = 2.0 * M * N * K
         for t, v in t_v.items():
             print(f"   tile={t:>4s}: {statistics.median(v)*1e6:8.1f}us {fl/statistics.median(v)/1e12:7.1f} TF", flush=True)
