@@ -675,10 +675,200 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
   }
 }
 
+// ---- ping-pong variant of the K-half ring: wave groups alternate MFMA and LDS work on every SIMD ----------
+// Waves w and w+4 share a SIMD.  Group 1 (waves 4-7) runs one barrier behind group 0, and every phase p is
+// split by barriers into R_p (stage glds, ds_read this phase's fragments) and M_p (lgkmcnt(0), 16 MFMAs at
+// raised priority): while one wave of a SIMD is in M the other is in R.  Group 0 arrives at barrier 2p after
+// R_p and 2p+1 after M_p; group 1 at 2p+1 after R_p and 2p+2 after M_p (one extra barrier at the start for
+// group 1, at the end for group 0).  NS ring slots of one K-half each (32 KiB).
+//   RAW: every wave waits vmcnt for K-half q at the end of R_{2q-1}, i.e. before barrier 4q-1 at the latest;
+//        the first read of K-half q is group 0's R_{2q}, after barrier 4q-1.
+//   WAR: K-half j reuses the slot of K-half j-NS, last read in R_{2(j-NS)+1} and retired by the lgkmcnt(0)
+//        opening M_{2(j-NS)+1}, which for group 1 precedes barrier 4(j-NS)+4; the first R section after
+//        that barrier for both groups is R_{2j-2NS+3}: part 0 (A rows) of K-half j is staged there, part 1
+//        (B rows) one phase later.  At the wait for K-half q the younger glds are K-halves q+1 .. q+NS-3
+//        (both parts) and part 0 of q+NS-2: 2*(2*(NS-3)+1) = 6 (NS=4) or 10 (NS=5) when none is past the end.
+// Measured (ablation, gemm_bench 8192^3): without the in-loop vmcnt waits the loop runs ~20 % faster, so the
+// ring depth, not the glds issue, is what this parameter buys.
+template <int NS>
+__device__ __forceinline__ void pp_wait_vm(int q, int total) {  // K-half q+1 landed (see the header)
+  const int n = 2 * (2 * (min(total, q + NS - 1) - (q + 2) > 0 ? min(total, q + NS - 1) - (q + 2) : 0) +
+                     (q + NS - 1 < total ? 1 : 0));
+  if constexpr (NS == 5) {
+    if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// ABL (timing ablations only, wrong results): 1 no global staging, 2 also no LDS reads, 3 staging without the
+// in-loop vmcnt waits (races)
+template <int EPI, int RH, int ABL = 0, int NS = 4>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
+  using CF = C256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int SLOT = 32768, BOFF = 16384;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tm = (a.M + 255) / 256, tn = (a.N + 255) / 256, ntiles = tm * tn;
+  const int G = gridDim.x;
+  const int tile0 = xcd_remap(blockIdx.x, G);
+  if (tile0 >= ntiles) return;
+  const int nkh = a.K / 32;
+  const int total = ((ntiles - 1 - tile0) / G + 1) * nkh;
+
+  const int srow = lane >> 2, schunk = (lane & 3) ^ ring_swz((lane >> 4) & 3);
+  const char* sa = nullptr;
+  const char* sb = nullptr;
+  uint32_t oa[2], ob[2];
+  auto set_stage_tile = [&](int t) {
+    int m0, n0;
+    tile_origin(t, a.M, a.N, 256, 256, m0, n0);
+    sa = (const char*)(a.A + (size_t)m0 * a.lda);
+    sb = (const char*)(a.B + (size_t)n0 * a.ldb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (2 * wave + i) * 16 + srow;
+      const int ra = min(r, a.M - 1 - m0), rb = min(r, a.N - 1 - n0);
+      oa[i] = (uint32_t)(ra * a.lda + schunk * 8) * 2u;
+      ob[i] = (uint32_t)(rb * a.ldb + schunk * 8) * 2u;
+    }
+  };
+  int st_q = 0, st_kh = 0, st_tile = tile0;
+  set_stage_tile(tile0);
+  auto stage_part = [&](int part) {
+    char* slot = smem + (st_q % NS) * SLOT;
+    const int kb = st_kh * 64;
+    if (part == 0) {
+      if (ABL == 0 || ABL == 3)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) glds16(sa + kb + oa[i], slot + (2 * wave + i) * 1024);
+    } else {
+      if (ABL == 0 || ABL == 3)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) glds16(sb + kb + ob[i], slot + BOFF + (2 * wave + i) * 1024);
+      ++st_q;
+      if (++st_kh == nkh && st_q < total) {
+        st_kh = 0;
+        st_tile += G;
+        set_stage_tile(st_tile);
+      }
+    }
+  };
+
+  const int fpos = ((lane >> 4) ^ ring_swz((lane >> 2) & 3)) << 4;
+  const uint32_t abase = lds_addr(smem) + (wm * 128 + (lane & 15)) * 64 + fpos;
+  const uint32_t bbase = lds_addr(smem) + BOFF + (wn * 64 + (lane & 15)) * 64 + fpos;
+  bf16x8_t FA[4], FB[4];
+  if (ABL == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { FA[i] = bf16x8_t{}; FB[i] = bf16x8_t{}; }
+  }
+  f32x4_t acc[8][4];
+  zero_acc<8>(acc);
+  auto mma = [&](int sub) {
+    __builtin_amdgcn_s_setprio(1);
+    if (sub == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[4 + i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: K-halves 0..NS-2 in flight; K-half 0 landed and visible; group 1 takes its extra barrier
+#pragma unroll 1
+  for (int i = 0; i < NS - 1; ++i)
+    if (st_q < total) { stage_part(0); stage_part(1); }
+  {
+    const int more = min(total, NS - 1) - 1;  // K-halves staged after K-half 0
+    if (ABL == 1 || ABL == 2) {
+    } else if (more >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (more == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (more == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+
+  int tile = tile0, kh = 0, m0, n0;
+  tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
+#pragma unroll 1
+  for (int q = 0; q < total; ++q) {
+    const uint32_t so = (q % NS) * SLOT;
+    // ---- R_{2q}: B part of K-half q+NS-2 (not for q = 0: K-halves 0..NS-2 came with the prologue), sub 0
+    if (q >= 1 && st_q == q + NS - 2 && st_q < total) stage_part(1);
+    if (ABL < 2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) DS_READ_B128(FB[j], bbase + so, j * 1024);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) DS_READ_B128(FA[i], abase + so, i * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(FA[i]), "+v"(FB[i]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- M_{2q}
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- R_{2q+1}: A part of K-half q+NS-1, fragments of sub 1, then K-half q+1 must have landed
+    if (st_q == q + NS - 1 && st_q < total) stage_part(0);
+    if (ABL < 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) DS_READ_B128(FA[i], abase + so, (4 + i) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(FA[i]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!ABL) pp_wait_vm<NS>(q, total);
+    __builtin_amdgcn_s_barrier();
+    // ---- M_{2q+1}
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    if (++kh == nkh) {  // epilogue inside this wave's next R window (no barrier in it)
+      if (n0 + wn * 64 < a.N) {
+        float rs[8];
+        load_rscale<8, 128>(a, m0, wm, lane, rs);
+        gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
+      }
+      zero_acc<8>(acc);
+      kh = 0;
+      tile += G;
+      if (tile < ntiles) tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // group 0 matches group 1's extra barrier
+}
+
 static int g_tile_override = 0;  // 0 auto, 128 or 256 (tests / tuning)
 // 256x256 main loop: 0 = K-tile double buffer, compiler-waited fragment loads; 1 = same with hand-counted asm
-// reads; 2 = K-half ring (gemm_ring_kernel); 3 = ring with s_setprio around the MFMA clusters
-static int g_c256_variant = 1;
+// reads; 2 = K-half ring (gemm_ring_kernel); 3 = ring with s_setprio around the MFMA clusters; 4 = ring with
+// wave-group ping-pong (gemm_pp_kernel)
+// -1 = automatic: 4 for long K (>= 2048, e.g. the MLP down projection: +3-4 % there), 1 otherwise (equal or
+// better at K = 896, where a tile's K loop is only 28 phases and the ping-pong prologue/epilogue weigh more)
+static int g_c256_variant = -1;
 
 static int num_cus() {
   static int n = 0;
@@ -718,6 +908,20 @@ static int launch_ring(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+template <int EPI, int RH, int ABL = 0, int NS = 4>
+static int launch_pp(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const int grid = std::min(tiles, num_cus());
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, RH, ABL, NS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, NS * 32768);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, RH, ABL, NS>), dim3(grid), dim3(512), NS * 32768, st, a);
+  return (int)hipGetLastError();
+}
+
 template <int EPI, int RH = 0>
 static int launch(const GemmArgs& a, hipStream_t st) {
   // 256x256 persistent tiles when the shape can fill the chip with them (halves L2->LDS traffic per
@@ -732,10 +936,16 @@ static int launch(const GemmArgs& a, hipStream_t st) {
     const bool big = fits && ((long long)((a.M + 255) / 256) * tn >= 256);
     const bool use256 = g_tile_override ? g_tile_override == 256 && fits : big;
     if (!use256) return launch_cfg<EPI, RH, C128>(a, st);
-    switch (g_c256_variant) {
+    const int variant = g_c256_variant >= 0 ? g_c256_variant : (a.K >= 2048 ? 4 : 1);
+    switch (variant) {
       case 0: return launch_cfg<EPI, RH, C256, false>(a, st);
       case 2: return launch_ring<EPI, RH, false>(a, st);
       case 3: return launch_ring<EPI, RH, true>(a, st);
+      case 4: return launch_pp<EPI, RH>(a, st);
+      case 5: return launch_pp<EPI, RH, 1>(a, st);  // timing ablations (wrong results)
+      case 6: return launch_pp<EPI, RH, 2>(a, st);
+      case 7: return launch_pp<EPI, RH, 3>(a, st);
+      case 8: return launch_pp<EPI, RH, 0, 5>(a, st);
       default: return launch_cfg<EPI, RH, C256, true>(a, st);
     }
   }

@@ -90,20 +90,23 @@ def set_gemm_tile(tile: int) -> None:
     call("edge_gemm_set_tile", int(tile))
 
 
-GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3}
+GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8}  # s-a*: timing ablations
 
 
 def set_gemm_variant(v: int) -> None:
     """256x256 GEMM main loop (A/B and tests): 0 K-tile double buffer with compiler-waited fragment loads,
-    1 the same with hand-counted asm reads, 2 the K-half ring, 3 the ring with s_setprio."""
+    1 the same with hand-counted asm reads, 2 the K-half ring, 3 the ring with s_setprio, 4 the ring with
+    wave-group ping-pong."""
     call("edge_gemm_set_variant", int(v))
 
 
 def set_gemm_config(spec: str) -> None:
-    """'0' (automatic), '128', or '256' + variant suffix ('', 'p', 'r', 'rp'), e.g. '256r'."""
-    tile = int(spec.rstrip("pr"))
+    """'0' (automatic tile and main loop), '128', or '256' + main-loop suffix ('' asm-read K-tile loop, 'p', 'r',
+    'rp', 's' ping-pong ring, 's5'), e.g. '256s'.  '256' pins variant 1; '0' restores the automatic choice."""
+    digits = len(spec) - len(spec.lstrip("0123456789"))
+    tile, suffix = int(spec[:digits]), spec[digits:]
     set_gemm_tile(tile)
-    set_gemm_variant(GEMM_VARIANTS[spec[len(str(tile)):]] if tile == 256 else GEMM_VARIANTS[""])
+    set_gemm_variant(GEMM_VARIANTS[suffix] if (tile == 256 or suffix) else -1)
 
 
 def row_ssq(x: torch.Tensor) -> torch.Tensor:

@@ -71,6 +71,9 @@ def lib():
             fn.argtypes = argt
             fn.restype = c_i
         _lib = L
+        v = os.environ.get("EDGE_GEMM_VARIANT")  # A/B of the 256x256 main loop (see ops.set_gemm_variant)
+        if v:
+            L.edge_gemm_set_variant(int(v))
     return _lib
 
 

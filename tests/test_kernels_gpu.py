@@ -60,7 +60,7 @@ def test_layernorm_dual():
 @pytest.mark.parametrize("M,N,K", [(512, 1152, 896), (300, 896, 896), (1000, 256, 512), (64, 128, 4864),
                                    (700, 1024, 640), (600, 896, 640)])
 @pytest.mark.parametrize("epi", ["none", "bias", "resid", "bias_resid", "gelu", "swiglu"])
-@pytest.mark.parametrize("tile", ["128", "256", "256p", "256r"])
+@pytest.mark.parametrize("tile", ["128", "256", "256p", "256r", "256s", "256s5"])
 def test_gemm(M, N, K, epi, tile):
     if tile != "128" and (N % 256 and (N % 128 or N < 768 or epi == "swiglu")):
         pytest.skip("256 tile needs N % 256 == 0, or N % 128 == 0 with >= 4 column tiles")
@@ -71,7 +71,7 @@ def test_gemm(M, N, K, epi, tile):
         ops.set_gemm_config("0")
 
 
-@pytest.mark.parametrize("tile", ["256", "256r", "256rp"])
+@pytest.mark.parametrize("tile", ["256", "256r", "256rp", "256s", "256s5"])
 @pytest.mark.parametrize("M,N,K,epi", [(4352 + 37, 4096, 192, "resid"), (4352, 4096, 64, "swiglu"),
                                        (4400, 3968, 128, "bias_resid")])
 def test_gemm_persistent_multi_tile(M, N, K, epi, tile):
@@ -98,7 +98,7 @@ def _gemm_case(M, N, K, epi):
     close(y, ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("tile", ["128", "256", "256r"])
+@pytest.mark.parametrize("tile", ["128", "256", "256r", "256s", "256s5"])
 def test_gemm_asymmetric_identity(tile):
     # A = I, asymmetric B: catches a transposed C-write
     K = 256
@@ -233,7 +233,7 @@ def test_row_ssq(H):
     close(s, R.row_ssq(x), atol=1e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("tile", ["128", "256", "256r"])
+@pytest.mark.parametrize("tile", ["128", "256", "256r", "256s", "256s5"])
 @pytest.mark.parametrize("act", [None, "swiglu_il"])
 def test_gemm_fused_norm_and_ssq_out(tile, act):
     M, K, N = 700, 896, 1024

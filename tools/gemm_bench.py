@@ -68,14 +68,16 @@ def main():
         variants = {t: mk(t) for t in tiles}
         ours = variants[tiles[0]]
         lib = lambda: torch.matmul(x, w.t())  # noqa: E731
+        if resid:  # hipBLASLt with the residual as beta*C (what a library route for RESID GEMMs would run)
+            variants["libr"] = lambda: torch.addmm(r, x, w.t())
         for _ in range(3):
             ours(); lib()
         t_o, t_l = [], []
-        t_v = {t: [] for t in tiles}
+        t_v = {t: [] for t in variants}
         for _ in range(a.rounds):
             for t, f in variants.items():
                 t_v[t].append(timeit(f, a.iters))
-            t_o.append(min(statistics.median(v) for v in t_v.values()))
+            t_o.append(min(statistics.median(t_v[t]) for t in tiles))
             t_l.append(timeit(lib, a.iters) if not a.no_lib else 1.0)
         ops.set_gemm_config("0")
         fl = 2.0 * M * N * K
