@@ -32,6 +32,7 @@ struct GemmArgs {
   // pre-folded into B) and producer side (per-row sum of squares of the stored bf16 outputs, one
   // partial per 64-column slab: ssq_out[m, n/64])
   const float* rscale; float* ssq_out;
+  int walk;  // persistent tile walk: 1 = XCD-contiguous chunks (default), 0 = strided by the grid size
 };
 
 constexpr int BK = 64;
@@ -316,6 +317,23 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // ds_read_b128 hidden from the compiler's waitcnt insertion: the caller owns the lgkmcnt accounting.
 #define DS_READ_B128(dst, vaddr, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(vaddr), "i"(off))
 
+// Persistent tile walk of workgroup bid out of G.  Workgroups are dispatched round-robin over the 8 XCDs
+// (bid & 7), and xcd_remap numbers the workgroups of one XCD consecutively (base .. base+cx-1).
+//   chunked (default): XCD x owns the contiguous range [T*base/G, T*(base+cx)/G) of the grouped-M tile order
+//     and its cx workgroups take tiles lo+l, lo+l+cx, ...  Consecutive rounds of an XCD stay inside one
+//     GROUP_M band, so its 8 A panels stay in the XCD's L2 and only the next B panels are fetched (for the
+//     gate/up shape: 4 new panels per round of 32 tiles instead of 12).
+//   strided: tiles v, v+G, v+2G, ... with v = xcd_remap(bid): every round jumps to a new region of the order.
+struct TileWalk { int first, stride, end; };
+__device__ __forceinline__ TileWalk tile_walk(int bid, int G, int ntiles, int chunked) {
+  if (!chunked) return {xcd_remap(bid, G), G, ntiles};
+  const int x = bid & 7, l = bid >> 3, q = G >> 3, r = G & 7;
+  const int cx = q + (x < r ? 1 : 0);
+  const int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const int lo = (int)((long long)ntiles * base / G), hi = (int)((long long)ntiles * (base + cx) / G);
+  return {lo + l, cx, hi};
+}
+
 __device__ __forceinline__ void tile_origin(int id, int M, int N, int BM, int BN, int& m0, int& n0) {
   // grouped-M order: GROUP_M consecutive m-panels sweep the n-panels together (A panels stay in L2)
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
@@ -420,9 +438,9 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
     // lgkmcnt(0) + barrier retires every wave's reads of the buffer about to be restaged.  The last
     // K-tile of a tile already stages (and reads fragments of) the NEXT tile's first K-tile, so the
     // epilogue overlaps that DMA and the next tile starts with its operands in LDS.
-    const int G = gridDim.x;
-    int tile = xcd_remap(blockIdx.x, G);
-    if (tile >= ntiles) return;
+    const TileWalk walk = tile_walk(blockIdx.x, gridDim.x, ntiles, a.walk);
+    int tile = walk.first;
+    if (tile >= walk.end) return;
     int m0, n0;
     tile_origin(tile, a.M, a.N, BM, BN, m0, n0);
     stage_ptrs<CF::A_INSTR, NW>(a.A, a.lda, m0, a.M, wave, lane, pa);
@@ -434,8 +452,8 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
     if constexpr (AR) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     int g = 0;  // K-tiles consumed by this workgroup (LDS buffer parity)
     while (true) {
-      const int next = tile + G;
-      const bool has_next = next < ntiles;
+      const int next = tile + walk.stride;
+      const bool has_next = next < walk.end;
       int nm0 = 0, nn0 = 0;
       if (has_next) tile_origin(next, a.M, a.N, BM, BN, nm0, nn0);
       for (int t = 0; t < nk; ++t, ++g) {
@@ -522,11 +540,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int tm = (a.M + 255) / 256, tn = (a.N + 255) / 256, ntiles = tm * tn;
-  const int G = gridDim.x;
-  const int tile0 = xcd_remap(blockIdx.x, G);
-  if (tile0 >= ntiles) return;
+  const TileWalk walk = tile_walk(blockIdx.x, gridDim.x, ntiles, a.walk);
+  const int tile0 = walk.first, G = walk.stride;
+  if (tile0 >= walk.end) return;
   const int nkh = a.K / 32;
-  const int total = ((ntiles - 1 - tile0) / G + 1) * nkh;  // K-halves this workgroup consumes
+  const int total = ((walk.end - 1 - tile0) / G + 1) * nkh;  // K-halves this workgroup consumes
 
   // staging: wave w issues instructions u = 2w, 2w+1 of the 16 per operand (16 rows x 64 B each);
   // lane -> row (lane >> 2) of the instruction, physical chunk lane & 3 = logical chunk ^ ((row >> 2) & 3)
@@ -669,7 +687,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
       zero_acc<8>(acc);
       kh = 0;
       tile += G;
-      if (tile < ntiles) tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
+      if (tile < walk.end) tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -692,22 +710,19 @@ __global__ __launch_bounds__(512, 1) void gemm_ring_kernel(GemmArgs a) {
 // ring depth, not the glds issue, is what this parameter buys.
 template <int NS>
 __device__ __forceinline__ void pp_wait_vm(int q, int total) {  // K-half q+1 landed (see the header)
-  const int n = 2 * (2 * (min(total, q + NS - 1) - (q + 2) > 0 ? min(total, q + NS - 1) - (q + 2) : 0) +
-                     (q + NS - 1 < total ? 1 : 0));
-  if constexpr (NS == 5) {
-    if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int full = min(total, q + NS - 1) - (q + 2);
+  const int n = 2 * (2 * (full > 0 ? full : 0) + (q + NS - 1 < total ? 1 : 0));
+  switch (n) {
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
 // ABL (timing ablations only, wrong results): 1 no global staging, 2 also no LDS reads, 3 staging without the
-// in-loop vmcnt waits (races)
+// in-loop vmcnt waits (races), 4 every workgroup stages the operands of tile 0 (L2-resident), waits kept
 template <int EPI, int RH, int ABL = 0, int NS = 4>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
   using CF = C256;
@@ -717,11 +732,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int tm = (a.M + 255) / 256, tn = (a.N + 255) / 256, ntiles = tm * tn;
-  const int G = gridDim.x;
-  const int tile0 = xcd_remap(blockIdx.x, G);
-  if (tile0 >= ntiles) return;
+  const TileWalk walk = tile_walk(blockIdx.x, gridDim.x, ntiles, a.walk);
+  const int tile0 = walk.first, G = walk.stride;
+  if (tile0 >= walk.end) return;
   const int nkh = a.K / 32;
-  const int total = ((ntiles - 1 - tile0) / G + 1) * nkh;
+  const int total = ((walk.end - 1 - tile0) / G + 1) * nkh;
 
   const int srow = lane >> 2, schunk = (lane & 3) ^ ring_swz((lane >> 4) & 3);
   const char* sa = nullptr;
@@ -729,7 +744,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
   uint32_t oa[2], ob[2];
   auto set_stage_tile = [&](int t) {
     int m0, n0;
-    tile_origin(t, a.M, a.N, 256, 256, m0, n0);
+    tile_origin(ABL == 4 ? 0 : t, a.M, a.N, 256, 256, m0, n0);
     sa = (const char*)(a.A + (size_t)m0 * a.lda);
     sb = (const char*)(a.B + (size_t)n0 * a.ldb);
 #pragma unroll
@@ -746,11 +761,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
     char* slot = smem + (st_q % NS) * SLOT;
     const int kb = st_kh * 64;
     if (part == 0) {
-      if (ABL == 0 || ABL == 3)
+      if (ABL == 0 || ABL == 3 || ABL == 4)
 #pragma unroll
         for (int i = 0; i < 2; ++i) glds16(sa + kb + oa[i], slot + (2 * wave + i) * 1024);
     } else {
-      if (ABL == 0 || ABL == 3)
+      if (ABL == 0 || ABL == 3 || ABL == 4)
 #pragma unroll
         for (int i = 0; i < 2; ++i) glds16(sb + kb + ob[i], slot + BOFF + (2 * wave + i) * 1024);
       ++st_q;
@@ -838,7 +853,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
       for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(FA[i]));
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!ABL) pp_wait_vm<NS>(q, total);
+    if (ABL == 0 || ABL == 4) pp_wait_vm<NS>(q, total);
     __builtin_amdgcn_s_barrier();
     // ---- M_{2q+1}
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -855,7 +870,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
       zero_acc<8>(acc);
       kh = 0;
       tile += G;
-      if (tile < ntiles) tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
+      if (tile < walk.end) tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -863,6 +878,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 }
 
 static int g_tile_override = 0;  // 0 auto, 128 or 256 (tests / tuning)
+static int g_walk = 1;           // persistent tile walk (TileWalk): 1 chunked per XCD, 0 strided
 // 256x256 main loop: 0 = K-tile double buffer, compiler-waited fragment loads; 1 = same with hand-counted asm
 // reads; 2 = K-half ring (gemm_ring_kernel); 3 = ring with s_setprio around the MFMA clusters; 4 = ring with
 // wave-group ping-pong (gemm_pp_kernel)
@@ -923,7 +939,9 @@ static int launch_pp(const GemmArgs& a, hipStream_t st) {
 }
 
 template <int EPI, int RH = 0>
-static int launch(const GemmArgs& a, hipStream_t st) {
+static int launch(const GemmArgs& args, hipStream_t st) {
+  GemmArgs a = args;
+  a.walk = g_walk;
   // 256x256 persistent tiles when the shape can fill the chip with them (halves L2->LDS traffic per
   // FLOP), 128x128 otherwise (N not a multiple of 256, or too few 256-row panels).  The QKV/RoPE and
   // LSE epilogues stay on 128x128 (register budget; their N is never a multiple of 256 in practice).
@@ -946,6 +964,7 @@ static int launch(const GemmArgs& a, hipStream_t st) {
       case 6: return launch_pp<EPI, RH, 2>(a, st);
       case 7: return launch_pp<EPI, RH, 3>(a, st);
       case 8: return launch_pp<EPI, RH, 0, 5>(a, st);
+      case 9: return launch_pp<EPI, RH, 4>(a, st);
       default: return launch_cfg<EPI, RH, C256, true>(a, st);
     }
   }
@@ -953,6 +972,11 @@ static int launch(const GemmArgs& a, hipStream_t st) {
 
 EDGE_API int edge_gemm_set_tile(int t) {
   g_tile_override = t;
+  return 0;
+}
+
+EDGE_API int edge_gemm_set_walk(int w) {
+  g_walk = w;
   return 0;
 }
 

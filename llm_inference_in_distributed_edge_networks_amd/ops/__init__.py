@@ -90,7 +90,7 @@ def set_gemm_tile(tile: int) -> None:
     call("edge_gemm_set_tile", int(tile))
 
 
-GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8}  # s-a*: timing ablations
+GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8, "s-a4": 9}  # s-a*: timing ablations
 
 
 def set_gemm_variant(v: int) -> None:
@@ -98,6 +98,11 @@ def set_gemm_variant(v: int) -> None:
     1 the same with hand-counted asm reads, 2 the K-half ring, 3 the ring with s_setprio, 4 the ring with
     wave-group ping-pong."""
     call("edge_gemm_set_variant", int(v))
+
+
+def set_gemm_walk(chunked: bool) -> None:
+    """Persistent 256x256 GEMMs: XCD-contiguous tile chunks (default) or the grid-strided walk.  A/B only."""
+    call("edge_gemm_set_walk", int(bool(chunked)))
 
 
 def set_gemm_config(spec: str) -> None:

@@ -33,6 +33,7 @@ _SIGS = {
     "edge_row_rscale": [c_p, c_p, c_i, c_i, c_i, c_f, c_p],
     "edge_gemm_set_tile": [c_i],
     "edge_gemm_set_variant": [c_i],
+    "edge_gemm_set_walk": [c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p],
     "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],

@@ -60,9 +60,12 @@ def main():
         out = torch.empty(M, No, device=dev, dtype=torch.bfloat16)
         tiles = a.tiles.split(",")
 
-        def mk(spec):
+        def mk(spec):  # spec may end in "/w0" = strided persistent tile walk instead of XCD chunks
+            cfg, _, walk = spec.partition("/w")
+
             def f():
-                ops.set_gemm_config(spec)
+                ops.set_gemm_config(cfg)
+                ops.set_gemm_walk(walk != "0")
                 ops.linear(x, w, bias=b, residual=r, act=act, out=out)
             return f
         variants = {t: mk(t) for t in tiles}
@@ -80,6 +83,7 @@ def main():
             t_o.append(min(statistics.median(t_v[t]) for t in tiles))
             t_l.append(timeit(lib, a.iters) if not a.no_lib else 1.0)
         ops.set_gemm_config("0")
+        ops.set_gemm_walk(True)
         fl = 2.0 * M * N * K
         for t, v in t_v.items():
             print(f"   tile={t:>4s}: {statistics.median(v)*1e6:8.1f}us {fl/statistics.median(v)/1e12:7.1f} TF", flush=True)
