@@ -43,6 +43,7 @@ def build_comm(force: bool = False, verbose: bool = False) -> str:
     """The native RCCL transport (links librccl; kept out of the kernel library)."""
     if not force and os.path.exists(COMM_LIB) and os.path.getmtime(COMM_LIB) >= os.path.getmtime(COMM_SRC):
         return COMM_LIB
+    os.makedirs(os.path.dirname(COMM_LIB), exist_ok=True)
     tmp = COMM_LIB + ".tmp"
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-o", tmp, COMM_SRC,
