@@ -5,7 +5,9 @@ Reference dispatch:
 * Pythia ``main.py:23-32``: ``params["experiment"]`` in {"last_row", "initial"} else ``ValueError``;
 * Qwen2 ``main.py:108-119``: channel sweep if the first method names a channel quantizer, otherwise
   the 4-method importance sweep (the reference's ``str.contains`` / module-call bugs B2/B3 fixed);
-* Relevance ``main.py``: LRP head-relevance calibration (its params-path bug B13 fixed).
+* Relevance ``main.py``: LRP head-relevance calibration (its params-path bug B13 fixed);
+* ``experiment: "pipeline"`` / ``num_stages`` > 1 / ``split_layers`` (new): the real N-stage split
+  with a quantized boundary message per stage hand-off (``pipeline_experiment``).
 
 All drivers run single-process or data-parallel under ``torchrun`` (windows sharded by batch,
 sums all-reduced), write JSON results in the reference's nested-list layouts, checkpoint every
@@ -233,8 +235,95 @@ def _print_table(res: dict) -> None:
             log(f"{m:20s} {L:5d} | " + " ".join(f"{v:10.4f}" for v in res["avg_ppl_results"][mi][li]))
 
 
+def pipeline_experiment(p: Params, default_model: str) -> dict:
+    """Real N-stage split inference (BASELINE.json configs 1-5), one result per (method, ratio).
+
+    The reference only simulates the device boundary (``qwen_layer_wise.py:54-70``).  Here
+    ``num_stages`` > 1 (or ``split_layers``) partitions the layers; under ``torchrun`` with
+    ``world = num_stages * dp`` every rank runs one stage and the boundary message goes over
+    RCCL (gloo on CPU); a single process runs all stages locally with the same codec.  Every
+    boundary uses ``codec`` with importance ``method`` scored at that boundary layer.  Output
+    ``pipeline_results.json``: ``{method: {ratio: {ppl, wire_bytes_per_token, tokens_per_s}}}``.
+    """
+    from ..parallel import BoundaryConfig, DistributedPipeline, Grid, LocalPipeline, PipelinePlan
+    env = init_distributed(p.device)
+    device = str(env.device) if env.device.type == "cuda" else resolve_device(p)
+    dtype = resolve_dtype(p, device)
+    cfg = get_config(p.model or default_model)
+    max_len = p.max_length or cfg.max_position
+    pp = len(p.split_layers) + 1 if p.split_layers else p.num_stages
+    plan = PipelinePlan.from_split_layers(cfg.num_layers, p.split_layers) if p.split_layers \
+        else PipelinePlan.balanced(cfg, pp, max_len)
+    distributed = env.world_size > 1
+    if distributed:
+        if env.world_size % pp:
+            raise ValueError(f"world size {env.world_size} is not a multiple of num_stages {pp}")
+        grid = Grid(env.world_size, pp)
+        dp_idx, stage = grid.coords(env.rank)
+        model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed,
+                                  layers=plan.stage_layers(stage), with_embed=stage == 0, with_head=stage == pp - 1)
+    else:
+        model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed)
+    ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed)
+    wins = sliding_windows(ids.shape[1], max_len, p.stride)
+    if p.max_windows:
+        wins = wins[: p.max_windows]
+    methods = [canonical(m) for m in p.methods]
+    hw = None
+    if "weighted_importance" in methods:
+        path = p.head_weights or _default_head_weights()
+        if not (path and os.path.exists(path)):
+            raise FileNotFoundError("weighted_importance needs attention_head_weights.json "
+                                    "(run Experiments/Relevance/main.py or set params['head_weights'])")
+        hw = load_head_weights(path)
+    log(f"pipeline: model={cfg.name} weights={prov} data={data_prov} stages={plan.num_stages} "
+        f"boundaries={plan.boundary_layers()} world={env.world_size} codec={p.codec} windows={len(wins)}")
+    results: dict = {}
+    for m in methods:
+        for r in p.ratios:
+            bcfg = BoundaryConfig(p.codec, float(r), m, hw)
+            bl = list(batches(ids, wins, p.window_batch))
+            t0 = time.perf_counter()
+            if distributed:
+                runner = DistributedPipeline(model, plan, bcfg, grid, env.rank)
+                acc, info = runner.evaluate(bl)
+                wire = torch.tensor([info["wire_bytes_per_token"] if stage < pp - 1 else 0.0], dtype=torch.float64,
+                                    device=env.device if env.backend == "nccl" else "cpu")
+                all_reduce_sum(wire)
+                wire_pt = float(wire) / (grid.dp * max(1, pp - 1))
+            else:
+                runner = LocalPipeline(model, plan, bcfg)
+                acc = runner.evaluate(bl)
+                wb = runner.wire_bytes_per_token()
+                wire_pt = sum(wb) / len(wb) if wb else 0.0
+            if device.startswith("cuda"):
+                torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            toks = sum(w.end - w.begin for w in wins)
+            results.setdefault(m, {})[str(r)] = {"ppl": acc.ppl(), "total_nll": acc.total_nll,
+                                                 "n_tokens": acc.n_tokens, "wire_bytes_per_token": wire_pt,
+                                                 "tokens_per_s": toks / max(dt, 1e-9), "seconds": dt}
+            if env.is_main:
+                log(f"{m:20s} ratio={r:<5} ppl={acc.ppl():.4f} wire={wire_pt:.1f} B/token "
+                    f"({toks / max(dt, 1e-9):,.0f} tok/s)")
+    out = {"results": results, "stages": plan.num_stages, "boundaries": plan.boundary_layers(),
+           "stage_layers": [list(plan.stage_layers(s)) for s in range(plan.num_stages)], "codec": p.codec,
+           "world_size": env.world_size, "weights": prov, "data": data_prov, "device": device, "dtype": str(dtype),
+           "max_length": max_len, "params": p.to_dict()}
+    if env.is_main:
+        os.makedirs(p.output_dir, exist_ok=True)
+        dump_json(out, os.path.join(p.output_dir, "pipeline_results.json"))
+    return out
+
+
 # ------------------------------------------------------------------------------------------
+def wants_pipeline(p: Params) -> bool:
+    return p.experiment == "pipeline" or p.num_stages > 1 or bool(p.split_layers)
+
+
 def pythia_main(p: Params) -> dict:
+    if wants_pipeline(p):
+        return pipeline_experiment(p, "pythia-70m")
     if p.experiment == "last_row":
         return importance_sweep(p, "pythia-70m", "avg_ppl_results_pythia_70m")
     if p.experiment == "initial":
@@ -243,6 +332,8 @@ def pythia_main(p: Params) -> dict:
 
 
 def qwen2_main(p: Params) -> dict:
+    if wants_pipeline(p):
+        return pipeline_experiment(p, "qwen2-0.5b")
     if p.methods and "channel" in str(p.methods[0]):
         return channel_sweep(p, "qwen2-0.5b")
     return importance_sweep(p, "qwen2-0.5b", "avg_ppl_results")

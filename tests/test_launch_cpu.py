@@ -1,0 +1,97 @@
+"""The driver's multi-process launch paths on CPU (gloo): ``torch.distributed.run ... bench.py`` and the
+pipeline entry point (BASELINE configs 1-5) under torchrun, compared with their single-process runs."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env():
+    e = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    e.pop("RANK", None)
+    e.pop("WORLD_SIZE", None)
+    return e
+
+
+def _torchrun(n, args, cwd=ROOT, timeout=600):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    return subprocess.run(cmd, cwd=cwd, env=_env(), capture_output=True, text=True, timeout=timeout)
+
+
+BENCH = ["bench.py", "--model", "tiny-qwen2", "--batch", "2", "--microbatches", "2", "--steps", "2", "--warmup", "1",
+         "--max-length", "128", "--split", "1"]
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_bench_contract_cpu(n):
+    if n == 1:
+        r = subprocess.run([sys.executable] + BENCH + ["--gpus", "1"], cwd=ROOT, env=_env(), capture_output=True,
+                           text=True, timeout=600)
+    else:
+        r = _torchrun(n, BENCH + ["--gpus", str(n)])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    dp = max(1, n // 2)
+    assert d["config"]["parallelism"] == f"pp{2 if n > 1 else 1}xdp{dp}"
+    assert d["config"]["global_batch"] == 2 * 2 * dp
+    assert d["ppl_random_weights"] and d["ppl_random_weights"] > 1
+
+
+def test_pipeline_entry_distributed_equals_local(tmp_path):
+    cfg = {"model": "tiny-qwen2", "num_stages": 2, "codec": "mixed_int4_int8", "methods": ["last_row"],
+           "ratios": [0, 0.5], "max_length": 128, "stride": 32, "window_batch": 3, "dataset": "synthetic",
+           "synthetic_tokens": 1200, "device": "cpu", "resume": False}
+    res = {}
+    for n in (1, 2):
+        d = tmp_path / f"n{n}"
+        d.mkdir()
+        (d / "params.json").write_text(json.dumps(dict(cfg, output_dir=str(d))))
+        main = os.path.join(ROOT, "Experiments", "Pipeline", "main.py")
+        if n == 1:
+            r = subprocess.run([sys.executable, main], cwd=d, env=_env(), capture_output=True, text=True, timeout=600)
+        else:
+            r = _torchrun(2, [main], cwd=d)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[n] = json.loads((d / "pipeline_results.json").read_text())
+    for r in ("0", "0.5"):
+        a, b = res[1]["results"]["last_row"][r], res[2]["results"]["last_row"][r]
+        assert abs(a["ppl"] - b["ppl"]) / a["ppl"] < 1e-6
+        assert a["wire_bytes_per_token"] == pytest.approx(b["wire_bytes_per_token"], rel=1e-6)
+    assert res[1]["results"]["last_row"]["0.5"]["wire_bytes_per_token"] < \
+        res[1]["results"]["last_row"]["0"]["wire_bytes_per_token"]
+
+
+def test_baseline_config_files_load():
+    from llm_inference_in_distributed_edge_networks_amd.config import Params
+    from llm_inference_in_distributed_edge_networks_amd.codec import get_codec
+    d = os.path.join(ROOT, "Experiments", "Pipeline", "configs")
+    names = sorted(os.listdir(d))
+    assert len(names) == 5
+    for n in names:
+        p = Params.load(os.path.join(d, n))
+        get_codec(p.codec)
+        assert p.num_stages > 1 or p.split_layers
