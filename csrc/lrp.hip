@@ -1,0 +1,466 @@
+// AttnLRP relevance backward for the offline head-relevance calibration (reference C8,
+// Experiments/Relevance/main.py:84-103 with lxt's efficient AttnLRP rules).
+//
+// The relevance pass is "Input x modified Gradient": a backward pass through the frozen model in which
+//   * the two attention matmuls (Q K^T and A V) and the gate*up product use the uniform rule (each operand
+//     gets half of the plain gradient),
+//   * SiLU uses the identity rule (backward multiplies by silu(g)/g = sigmoid(g)),
+//   * the norms are linear in x with the normaliser detached,
+//   * the softmax uses its plain gradient.
+// Only input gradients are needed (weights are frozen), so the backward of every linear layer is one GEMM
+// with the transposed weight (csrc/gemm.hip) and the per-layer residual/row-scale epilogue.  This file holds
+// the non-GEMM parts:
+//
+//   lrp_attn_delta : D[b,h,i] = sum_j A_ij dA_ij = 0.5 dO_i . O_i (uniform rule on A V); per-(window, head)
+//                    relevance rel[b,h] = sum_i D[b,h,i] - the quantity the reference hook sums over S x S
+//                    (sum_{ij} A * dA).  No S x S tensor exists anywhere.
+//   lrp_attn_dkdv  : dK, dV for one (window, kv head, 64-key block), looping over the q heads of the GQA
+//                    group and the causal query tiles: P recomputed from Q K^T and the forward LSE,
+//                    dA = 0.5 dO V^T, dS = P (dA - D), dV = 0.5 P^T dO, dK = 0.5 dS^T Q.
+//   lrp_attn_dq    : dQ = 0.5 dS K for one (window, q head, 64-query block) over its causal key tiles.
+//                    dK/dV and dQ are separate sweeps: no atomics, deterministic.
+//   lrp_rope_pack  : inverse RoPE (transpose rotation) + q scaling, scatter dQ/dK/dV into the token-major
+//                    d[q|k|v] operand of the QKV input-gradient GEMM.
+//   swiglu_il / lrp_swiglu_bwd : forward SiLU(g)*u and its LRP backward on the interleaved gate|up layout
+//                    (IL_BLOCK = 16 columns of gate, then 16 of up).
+//   lrp_gelu_bwd / lrp_ln_bwd : GPT-NeoX rules (GELU identity rule; LayerNorm with detached variance).
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 everywhere.  Lane l holds A[row = l&15][k = 8(l>>4)..+7],
+// B[k = 8(l>>4)..+7][col = l&15] and C[row = 4(l>>4)+r][col = l&15].  Products whose K dimension is the
+// token axis reuse the lane-local probabilities of two 16-token sub-tiles as the A (or B) operand, with the
+// token order permuted as kappa(g, j) = 16(j>>2) + 4g + (j&3); the other operand is read from a transposed
+// LDS tile in the same order (the forward kernel's P.V trick).
+#include "common.h"
+
+namespace {
+constexpr int LD_ROW = 72;   // row-major 64-wide bf16 tile, padded row (144 B) -> conflict-light b128 reads
+constexpr int LD_T = 40;     // transposed [64][32] tile, padded row (80 B)
+
+__device__ __forceinline__ bf16x8_t ld_row_frag(const bf16_t* t, int row, int col) {
+  return *(const bf16x8_t*)(t + row * LD_ROW + col);
+}
+
+// B (or A) operand over the permuted token axis from a transposed [64][LD_T] tile: element j <-> token
+// kappa(g, j) of the 32-token tile, row `d`.
+__device__ __forceinline__ bf16x8_t ld_t_frag(const bf16_t* t, int d, int g) {
+  const u32x2_t lo = *(const u32x2_t*)(t + d * LD_T + 4 * g);
+  const u32x2_t hi = *(const u32x2_t*)(t + d * LD_T + 16 + 4 * g);
+  u32x4_t v = {lo[0], lo[1], hi[0], hi[1]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// Stage 32 rows x 64 bf16 (row stride `ld` elements, rows clamped to < nrows) into a row-major tile and,
+// if `tt` != nullptr, its transpose.  256 threads: one 16 B chunk each.
+__device__ __forceinline__ void stage32(const bf16_t* __restrict__ src, size_t ld, int row0, int nrows, bf16_t* tr,
+                                        bf16_t* tt) {
+  const int t = threadIdx.x, r = t >> 3, c = (t & 7) * 8;
+  int gr = row0 + r;
+  u32x4_t v = {0u, 0u, 0u, 0u};
+  if (gr < nrows) v = *(const u32x4_t*)(src + (size_t)gr * ld + c);
+  *(u32x4_t*)(tr + r * LD_ROW + c) = v;
+  if (tt) {
+    const bf16_t* e = (const bf16_t*)&v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tt[(c + i) * LD_T + r] = e[i];
+  }
+}
+
+__device__ __forceinline__ bf16x8_t pack8(const f32x4_t& a, const f32x4_t& b) {
+  bf16x8_t f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    f[r] = (__bf16)a[r];
+    f[4 + r] = (__bf16)b[r];
+  }
+  return f;
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// D and per-(window, head) relevance.  o, dO token-major [B*S, Hq*64]; D [B,Hq,S]; rel [B,Hq].
+__global__ __launch_bounds__(256) void lrp_attn_delta_kernel(const bf16_t* __restrict__ o,
+                                                             const bf16_t* __restrict__ dO, float* __restrict__ D,
+                                                             float* __restrict__ rel, int Hq, int S) {
+  __shared__ float red[4];
+  const int bh = blockIdx.x, b = bh / Hq, h = bh - b * Hq;
+  float tot = 0.f;
+  for (int i = threadIdx.x; i < S; i += 256) {
+    const size_t off = ((size_t)b * S + i) * (size_t)(Hq * 64) + h * 64;
+    const u32x4_t* po = (const u32x4_t*)(o + off);
+    const u32x4_t* pd = (const u32x4_t*)(dO + off);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const u32x4_t a = po[c], d = pd[c];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += bf_lo(a[e]) * bf_lo(d[e]) + bf_hi(a[e]) * bf_hi(d[e]);
+    }
+    s *= 0.5f;
+    D[(size_t)bh * S + i] = s;
+    tot += s;
+  }
+  tot = block_sum<256>(tot, red);
+  if (threadIdx.x == 0) rel[bh] = tot;
+}
+
+// ---------------------------------------------------------------------------------------------
+// dK, dV.  q [B,Hq,S,64] (pre-scaled), k, v [B,Hkv,S,64], dO token-major, lse/D [B,Hq,S] -> dk, dv fp32
+// [B,Hkv,S,64].  Workgroup = (b, hk, 64-key block); wave w owns keys kb*64 + 16w .. +15.
+__global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                            const bf16_t* __restrict__ v,
+                                                            const bf16_t* __restrict__ dO,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ D, float* __restrict__ dk,
+                                                            float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
+  __shared__ __attribute__((aligned(16))) bf16_t sQ[32 * LD_ROW];
+  __shared__ __attribute__((aligned(16))) bf16_t sO[32 * LD_ROW];
+  __shared__ __attribute__((aligned(16))) bf16_t tQ[64 * LD_T];
+  __shared__ __attribute__((aligned(16))) bf16_t tO[64 * LD_T];
+  __shared__ float sL[32], sD[32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int nkb = (S + 63) / 64;
+  const int kb = blockIdx.x % nkb;
+  const int bhk = blockIdx.x / nkb, b = bhk / Hkv, hk = bhk - b * Hkv;
+  const int G = Hq / Hkv;
+  const int key = kb * 64 + wave * 16 + cl;          // this lane's key (B-operand column / A-operand row)
+  const int keyc = key < S ? key : S - 1;
+  const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const bf16_t* vh = v + ((size_t)b * Hkv + hk) * S * 64;
+  bf16x8_t kB[2], vB[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    kB[ks] = *(const bf16x8_t*)(kh + (size_t)keyc * 64 + ks * 32 + g * 8);
+    vB[ks] = *(const bf16x8_t*)(vh + (size_t)keyc * 64 + ks * 32 + g * 8);
+  }
+  f32x4_t dka[4], dva[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int q_first = (kb * 64) & ~31;
+  for (int hh = 0; hh < G; ++hh) {
+    const int h = hk * G + hh;
+    const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
+    const bf16_t* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
+    const float* lh = lse + ((size_t)b * Hq + h) * S;
+    const float* dh = D + ((size_t)b * Hq + h) * S;
+    for (int q0 = q_first; q0 < S; q0 += 32) {
+      __syncthreads();
+      stage32(qh, 64, q0, S, sQ, tQ);
+      stage32(doh, (size_t)Hq * 64, q0, S, sO, tO);
+      if (tid < 32) {
+        const int qi = q0 + tid;
+        sL[tid] = qi < S ? lh[qi] : INFINITY;
+        sD[tid] = qi < S ? dh[qi] : 0.f;
+      }
+      __syncthreads();
+      f32x4_t p[2], ds[2];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        f32x4_t s = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(sQ, sub * 16 + cl, ks * 32 + g * 8), kB[ks], s,
+                                                       0, 0, 0);
+          da = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(sO, sub * 16 + cl, ks * 32 + g * 8), vB[ks], da,
+                                                        0, 0, 0);
+        }
+        // s[r] = score(query = q0 + sub*16 + 4g + r, key)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = sub * 16 + g * 4 + r;
+          const int qi = q0 + ql;
+          const bool ok = qi < S && key <= qi && key < S;
+          const float pr = ok ? __expf(s[r] - sL[ql]) : 0.f;
+          p[sub][r] = pr;
+          ds[sub][r] = pr * (0.5f * da[r] - sD[ql]);
+        }
+      }
+      const bf16x8_t pf = pack8(p[0], p[1]);
+      const bf16x8_t dsf = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dva[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, ld_t_frag(tO, dt * 16 + cl, g), dva[dt], 0, 0, 0);
+        dka[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsf, ld_t_frag(tQ, dt * 16 + cl, g), dka[dt], 0, 0, 0);
+      }
+    }
+  }
+  // C[row = key 4g + r of this wave][col = d 16dt + cl]
+  float* dkh = dk + ((size_t)b * Hkv + hk) * S * 64;
+  float* dvh = dv + ((size_t)b * Hkv + hk) * S * 64;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int kr = kb * 64 + wave * 16 + g * 4 + r;
+    if (kr < S) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dkh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dka[dt][r];
+        dvh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dva[dt][r];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dQ.  Workgroup = (b, h, 64-query block); wave w owns queries qb*64 + 16w .. +15 (lane column cl).
+// S^T = K Q^T and dA^T = V dO^T keep the query on the lane, so dQ^T = K^T dS^T takes dS^T lane-locally.
+__global__ __launch_bounds__(256) void lrp_attn_dq_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                          const bf16_t* __restrict__ v, const bf16_t* __restrict__ dO,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ D, float* __restrict__ dq,
+                                                          int B, int Hq, int Hkv, int S) {
+  __shared__ __attribute__((aligned(16))) bf16_t sK[32 * LD_ROW];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[32 * LD_ROW];
+  __shared__ __attribute__((aligned(16))) bf16_t tK[64 * LD_T];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int nqb = (S + 63) / 64;
+  const int qb = nqb - 1 - blockIdx.x / (B * Hq);          // heaviest query blocks first
+  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
+  const int qi = qb * 64 + wave * 16 + cl;
+  const int qic = qi < S ? qi : S - 1;
+  const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
+  const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const bf16_t* vh = v + ((size_t)b * Hkv + hk) * S * 64;
+  const bf16_t* dorow = dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64;
+  bf16x8_t qB[2], oB[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    qB[ks] = *(const bf16x8_t*)(qh + (size_t)qic * 64 + ks * 32 + g * 8);
+    oB[ks] = *(const bf16x8_t*)(dorow + ks * 32 + g * 8);
+  }
+  const float lq = lse[((size_t)b * Hq + h) * S + qic];
+  const float dq_ = D[((size_t)b * Hq + h) * S + qic];
+  f32x4_t acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int kend = min(S, qb * 64 + 64);
+  for (int k0 = 0; k0 < kend; k0 += 32) {
+    __syncthreads();
+    stage32(kh, 64, k0, S, sK, tK);
+    stage32(vh, 64, k0, S, sV, nullptr);
+    __syncthreads();
+    f32x4_t ds[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4_t s = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(sK, sub * 16 + cl, ks * 32 + g * 8), qB[ks], s, 0,
+                                                     0, 0);
+        da = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(sV, sub * 16 + cl, ks * 32 + g * 8), oB[ks], da, 0,
+                                                      0, 0);
+      }
+      // s[r] = score(key = k0 + sub*16 + 4g + r, query = qi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + sub * 16 + g * 4 + r;
+        const bool ok = qi < S && kj <= qi;
+        const float pr = ok ? __expf(s[r] - lq) : 0.f;
+        ds[sub][r] = pr * (0.5f * da[r] - dq_);
+      }
+    }
+    const bf16x8_t dsf = pack8(ds[0], ds[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_t_frag(tK, dt * 16 + cl, g), dsf, acc[dt], 0, 0, 0);
+  }
+  // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
+  if (qi < S) {
+    float* o = dq + (((size_t)b * Hq + h) * S + qi) * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = 0.5f * acc[dt];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Inverse RoPE + q scale + scatter into token-major d[q|k|v] (bf16 [B*S, (Hq+2Hkv)*64]).
+// Forward: r1 = x1 c - x2 s, r2 = x2 c + x1 s (first rot_dim dims).  Transpose: x1 = r1 c + r2 s,
+// x2 = r2 c - r1 s.  One thread per (token, head, d).
+__global__ __launch_bounds__(256) void lrp_rope_pack_kernel(const float* __restrict__ dq, const float* __restrict__ dk,
+                                                            const float* __restrict__ dv,
+                                                            const float* __restrict__ cosT,
+                                                            const float* __restrict__ sinT, bf16_t* __restrict__ out,
+                                                            int B, int S, int Hq, int Hkv, int rot_dim, float q_scale) {
+  const int Ht = Hq + 2 * Hkv;
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t total = (size_t)B * S * Ht * 64;
+  if (idx >= total) return;
+  const int d = idx & 63;
+  const size_t th = idx >> 6;
+  const int hh = th % Ht;
+  const size_t t = th / Ht;
+  const int b = t / S, s = t - (size_t)b * S;
+  const float* src;
+  float scale = 1.f;
+  bool rope = true;
+  if (hh < Hq) {
+    src = dq + (((size_t)b * Hq + hh) * S + s) * 64;
+    scale = q_scale;
+  } else if (hh < Hq + Hkv) {
+    src = dk + (((size_t)b * Hkv + (hh - Hq)) * S + s) * 64;
+  } else {
+    src = dv + (((size_t)b * Hkv + (hh - Hq - Hkv)) * S + s) * 64;
+    rope = false;
+  }
+  float val;
+  const int half = rot_dim >> 1;
+  if (!rope || d >= rot_dim) {
+    val = src[d];
+  } else if (d < half) {
+    const float c = cosT[(size_t)s * half + d], sn = sinT[(size_t)s * half + d];
+    val = src[d] * c + src[d + half] * sn;
+  } else {
+    const int j = d - half;
+    const float c = cosT[(size_t)s * half + j], sn = sinT[(size_t)s * half + j];
+    val = src[d] * c - src[j] * sn;
+  }
+  out[idx] = f2bf(val * scale);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Interleaved gate|up (blocks of 16 columns): a = silu(g) * u  and the LRP backward
+//   dg = 0.5 dm u sigmoid(g)  (uniform rule on g*u, identity rule on SiLU),  du = 0.5 dm silu(g).
+__global__ __launch_bounds__(256) void swiglu_il_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ a,
+                                                        size_t n, int I) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n) return;
+  const size_t t = idx / I;
+  const int c = idx - t * I, blk = c >> 4, e = c & 15;
+  const bf16_t* row = gu + t * (size_t)(2 * I) + blk * 32 + e;
+  const float g = bf2f(row[0]), u = bf2f(row[16]);
+  a[idx] = f2bf(g / (1.f + __expf(-g)) * u);
+}
+
+__global__ __launch_bounds__(256) void lrp_swiglu_bwd_kernel(const bf16_t* __restrict__ dm,
+                                                             const bf16_t* __restrict__ gu, bf16_t* __restrict__ dgu,
+                                                             size_t n, int I) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n) return;
+  const size_t t = idx / I;
+  const int c = idx - t * I, blk = c >> 4, e = c & 15;
+  const size_t off = t * (size_t)(2 * I) + blk * 32 + e;
+  const float g = bf2f(gu[off]), u = bf2f(gu[off + 16]), m = bf2f(dm[idx]);
+  const float sg = 1.f / (1.f + __expf(-g));
+  dgu[off] = f2bf(0.5f * m * u * sg);
+  dgu[off + 16] = f2bf(0.5f * m * g * sg);
+}
+
+// GELU identity rule: dx = dy * gelu(a)/a (0.5 at a = 0).  a = pre-activation (bf16), in place on dy.
+__global__ __launch_bounds__(256) void lrp_gelu_bwd_kernel(bf16_t* __restrict__ dy, const bf16_t* __restrict__ a,
+                                                           size_t n) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n) return;
+  const float x = bf2f(a[idx]);
+  const float gel = 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  const float ratio = fabsf(x) > 1e-6f ? gel / x : 0.5f;
+  dy[idx] = f2bf(bf2f(dy[idx]) * ratio);
+}
+
+// LayerNorm with detached variance (mean NOT detached): y = (x - mean x) * rstd * w + b.
+// dx = gc - mean(gc), gc = dy * rstd * w.  out = resid + dx1 (+ dx2 for the second norm of the dual).
+// One wave per row.  rstd [R] fp32.
+__global__ __launch_bounds__(256) void lrp_ln_bwd_kernel(const bf16_t* __restrict__ dy1, const float* __restrict__ rs1,
+                                                         const bf16_t* __restrict__ w1,
+                                                         const bf16_t* __restrict__ dy2, const float* __restrict__ rs2,
+                                                         const bf16_t* __restrict__ w2,
+                                                         const bf16_t* __restrict__ resid, bf16_t* __restrict__ out,
+                                                         int R, int H) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const size_t base = (size_t)row * H;
+  const float r1 = rs1[row], r2 = dy2 ? rs2[row] : 0.f;
+  float m1 = 0.f, m2 = 0.f;
+  for (int c = lane; c < H; c += 64) {
+    m1 += bf2f(dy1[base + c]) * r1 * bf2f(w1[c]);
+    if (dy2) m2 += bf2f(dy2[base + c]) * r2 * bf2f(w2[c]);
+  }
+  m1 = wave_sum(m1) / H;
+  m2 = wave_sum(m2) / H;
+  for (int c = lane; c < H; c += 64) {
+    float v = bf2f(resid[base + c]) + bf2f(dy1[base + c]) * r1 * bf2f(w1[c]) - m1;
+    if (dy2) v += bf2f(dy2[base + c]) * r2 * bf2f(w2[c]) - m2;
+    out[base + c] = f2bf(v);
+  }
+}
+
+// LayerNorm statistics (for the rules above): rstd of (x - mean) per row.
+__global__ __launch_bounds__(256) void ln_rstd_kernel(const bf16_t* __restrict__ x, float* __restrict__ rstd, int R,
+                                                      int H, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const size_t base = (size_t)row * H;
+  float s = 0.f;
+  for (int c = lane; c < H; c += 64) s += bf2f(x[base + c]);
+  const float mu = wave_sum(s) / H;
+  float v = 0.f;
+  for (int c = lane; c < H; c += 64) {
+    const float d = bf2f(x[base + c]) - mu;
+    v += d * d;
+  }
+  v = wave_sum(v) / H;
+  if (lane == 0) rstd[row] = rsqrtf(v + eps);
+}
+
+// ---------------------------------------------------------------------------------------------
+static inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
+
+EDGE_API int edge_lrp_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dO,
+                               const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, int B, int Hq,
+                               int Hkv, int S, hipStream_t st) {
+  if (B <= 0 || S <= 0) return 0;
+  if (Hq % Hkv) return (int)hipErrorInvalidValue;
+  const int nb = (S + 63) / 64;
+  lrp_attn_delta_kernel<<<B * Hq, 256, 0, st>>>((const bf16_t*)o, (const bf16_t*)dO, D, rel, Hq, S);
+  lrp_attn_dkdv_kernel<<<B * Hkv * nb, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                      (const bf16_t*)dO, lse, D, dk, dv, B, Hq, Hkv, S);
+  lrp_attn_dq_kernel<<<B * Hq * nb, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                                                   (const bf16_t*)dO, lse, D, dq, B, Hq, Hkv, S);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_lrp_rope_pack(const float* dq, const float* dk, const float* dv, const float* cosT,
+                                const float* sinT, void* out, int B, int S, int Hq, int Hkv, int rot_dim,
+                                float q_scale, hipStream_t st) {
+  const size_t n = (size_t)B * S * (Hq + 2 * Hkv) * 64;
+  if (!n) return 0;
+  if (rot_dim > 64 || rot_dim % 2) return (int)hipErrorInvalidValue;
+  lrp_rope_pack_kernel<<<nblk(n), 256, 0, st>>>(dq, dk, dv, cosT, sinT, (bf16_t*)out, B, S, Hq, Hkv, rot_dim,
+                                                 q_scale);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_swiglu_il(const void* gu, void* a, long long T, int I, hipStream_t st) {
+  const size_t n = (size_t)T * I;
+  if (!n) return 0;
+  if (I % 16) return (int)hipErrorInvalidValue;
+  swiglu_il_kernel<<<nblk(n), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)a, n, I);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_lrp_swiglu_bwd(const void* dm, const void* gu, void* dgu, long long T, int I, hipStream_t st) {
+  const size_t n = (size_t)T * I;
+  if (!n) return 0;
+  if (I % 16) return (int)hipErrorInvalidValue;
+  lrp_swiglu_bwd_kernel<<<nblk(n), 256, 0, st>>>((const bf16_t*)dm, (const bf16_t*)gu, (bf16_t*)dgu, n, I);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_lrp_gelu_bwd(void* dy, const void* a, long long n, hipStream_t st) {
+  if (n <= 0) return 0;
+  lrp_gelu_bwd_kernel<<<nblk(n), 256, 0, st>>>((bf16_t*)dy, (const bf16_t*)a, (size_t)n);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_lrp_ln_bwd(const void* dy1, const float* rs1, const void* w1, const void* dy2, const float* rs2,
+                             const void* w2, const void* resid, void* out, int R, int H, hipStream_t st) {
+  if (R <= 0) return 0;
+  lrp_ln_bwd_kernel<<<(R + 3) / 4, 256, 0, st>>>((const bf16_t*)dy1, rs1, (const bf16_t*)w1, (const bf16_t*)dy2,
+                                                 rs2, (const bf16_t*)w2, (const bf16_t*)resid, (bf16_t*)out, R, H);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_ln_rstd(const void* x, float* rstd, int R, int H, float eps, hipStream_t st) {
+  if (R <= 0) return 0;
+  ln_rstd_kernel<<<(R + 3) / 4, 256, 0, st>>>((const bf16_t*)x, rstd, R, H, eps);
+  return (int)hipGetLastError();
+}

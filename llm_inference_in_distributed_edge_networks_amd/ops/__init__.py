@@ -271,3 +271,102 @@ def head_nll(h, w, targets):
     call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
+
+
+# ---- AttnLRP relevance backward (csrc/lrp.hip) ---------------------------------------------------------
+def linear_rowscale(x: torch.Tensor, w: torch.Tensor, rscale: torch.Tensor, residual=None) -> torch.Tensor:
+    """``rscale[:, None] * (x @ w.T) + residual`` (rscale fp32 [M]): the input-gradient GEMM of a norm-folded
+    projection under the detached-normaliser rule."""
+    if not _gpu(x):
+        y = ref._f(x) @ ref._f(w).t() * rscale.float().view(-1, 1)
+        if residual is not None:
+            y = y + ref._f(residual)
+        return y.to(x.dtype)
+    _check_bf16(x, w, residual)
+    M, K = x.shape
+    N = w.shape[0]
+    out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    rs = rscale.to(torch.float32).contiguous()
+    call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), None,
+         ptr(residual), 0 if residual is None else residual.stride(0), 0, ptr(rs), None, stream())
+    return out
+
+
+def lrp_attn_bwd(q, k, v, o, dO, lse):
+    """-> (D [B,Hq,S], rel [B,Hq], dq [B,Hq,S,64], dk, dv [B,Hkv,S,64]) fp32; see ``reference.lrp_attn_bwd``."""
+    if not _gpu(q):
+        return ref.lrp_attn_bwd(q, k, v, o, dO, lse)
+    _check_bf16(q, k, v, o, dO)
+    B, Hq, S, D = q.shape
+    Hkv = k.shape[1]
+    assert D == 64 and k.shape == v.shape == (B, Hkv, S, D) and o.shape == dO.shape == (B * S, Hq * D)
+    assert lse.shape == (B, Hq, S) and lse.dtype == torch.float32 and lse.is_contiguous()
+    f32 = dict(dtype=torch.float32, device=q.device)
+    Dl, rel = torch.empty(B, Hq, S, **f32), torch.empty(B, Hq, **f32)
+    dq = torch.empty(B, Hq, S, D, **f32)
+    dk, dv = torch.empty(B, Hkv, S, D, **f32), torch.empty(B, Hkv, S, D, **f32)
+    call("edge_lrp_attn_bwd", ptr(q), ptr(k), ptr(v), ptr(o), ptr(dO), ptr(lse), ptr(Dl), ptr(rel), ptr(dq), ptr(dk),
+         ptr(dv), B, Hq, Hkv, S, stream())
+    return Dl, rel, dq, dk, dv
+
+
+def lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, dtype=torch.bfloat16):
+    if not _gpu(dq):
+        return ref.lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, dtype)
+    for t in (dq, dk, dv):
+        assert t.dtype == torch.float32 and t.is_contiguous()
+    out = torch.empty(B * S, (Hq + 2 * Hkv) * 64, dtype=torch.bfloat16, device=dq.device)
+    call("edge_lrp_rope_pack", ptr(dq), ptr(dk), ptr(dv), ptr(cos), ptr(sin), ptr(out), B, S, Hq, Hkv, rot_dim,
+         float(q_scale), stream())
+    return out
+
+
+def swiglu_il(gu: torch.Tensor) -> torch.Tensor:
+    if not _gpu(gu):
+        return ref.swiglu_il(gu)
+    _check_bf16(gu)
+    T, N2 = gu.shape
+    a = torch.empty(T, N2 // 2, dtype=gu.dtype, device=gu.device)
+    call("edge_swiglu_il", ptr(gu), ptr(a), T, N2 // 2, stream())
+    return a
+
+
+def lrp_swiglu_bwd(dm: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
+    if not _gpu(gu):
+        return ref.lrp_swiglu_bwd(dm, gu)
+    _check_bf16(dm, gu)
+    T, N2 = gu.shape
+    assert dm.shape == (T, N2 // 2)
+    dgu = torch.empty_like(gu)
+    call("edge_lrp_swiglu_bwd", ptr(dm), ptr(gu), ptr(dgu), T, N2 // 2, stream())
+    return dgu
+
+
+def lrp_gelu_bwd(dy: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+    if not _gpu(dy):
+        return ref.lrp_gelu_bwd(dy, a)
+    _check_bf16(dy, a)
+    out = dy.clone()
+    call("edge_lrp_gelu_bwd", ptr(out), ptr(a), out.numel(), stream())
+    return out
+
+
+def ln_rstd(x: torch.Tensor, eps: float) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.ln_rstd(x, eps)
+    _check_bf16(x)
+    R, H = x.shape
+    out = torch.empty(R, dtype=torch.float32, device=x.device)
+    call("edge_ln_rstd", ptr(x), ptr(out), R, H, float(eps), stream())
+    return out
+
+
+def lrp_ln_bwd(dy1, rs1, w1, dy2, rs2, w2, resid):
+    if not _gpu(resid):
+        return ref.lrp_ln_bwd(dy1, rs1, w1, dy2, rs2, w2, resid)
+    _check_bf16(dy1, w1, dy2, w2, resid)
+    R, H = resid.shape
+    out = torch.empty_like(resid)
+    call("edge_lrp_ln_bwd", ptr(dy1), ptr(rs1), ptr(w1), ptr(dy2), ptr(rs2), ptr(w2), ptr(resid), ptr(out), R, H,
+         stream())
+    return out

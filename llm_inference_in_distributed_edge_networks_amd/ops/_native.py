@@ -46,6 +46,13 @@ _SIGS = {
     "edge_channel_stats": [c_p, c_p, c_ll, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_rowmax": [c_p, c_p, c_i, c_i, c_p],
     "edge_pack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_lrp_attn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    "edge_lrp_rope_pack": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
+    "edge_swiglu_il": [c_p, c_p, c_ll, c_i, c_p],
+    "edge_lrp_swiglu_bwd": [c_p, c_p, c_p, c_ll, c_i, c_p],
+    "edge_lrp_gelu_bwd": [c_p, c_p, c_ll, c_p],
+    "edge_lrp_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p],
+    "edge_ln_rstd": [c_p, c_p, c_i, c_i, c_f, c_p],
     "edge_unpack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
 }
 

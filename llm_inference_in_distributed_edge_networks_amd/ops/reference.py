@@ -188,3 +188,81 @@ def rownorm_scale(ssq: torch.Tensor, K: int, eps: float) -> torch.Tensor:
 def fold_norm_weight(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
     """W' = W diag(norm_w): rmsnorm(x) @ W^T == (x @ W'^T) * rsqrt(mean(x^2) + eps) (up to rounding)."""
     return (_f(w) * _f(norm_w).view(1, -1)).to(w.dtype)
+
+
+# ---- AttnLRP relevance backward (csrc/lrp.hip) --------------------------------------------------------
+def lrp_attn_bwd(q, k, v, o, dO, lse):
+    """Uniform rule on Q K^T and A V, plain softmax gradient.  q [B,Hq,S,D] pre-scaled, k/v [B,Hkv,S,D],
+    o/dO token-major [B*S, Hq*D], lse [B,Hq,S].  Returns (D [B,Hq,S], rel [B,Hq], dq [B,Hq,S,D],
+    dk [B,Hkv,S,D], dv [B,Hkv,S,D]) in fp32 (dq w.r.t. the pre-scaled q)."""
+    B, Hq, S, D = q.shape
+    Hkv = k.shape[1]
+    G = Hq // Hkv
+    kk, vv = _f(k).repeat_interleave(G, 1), _f(v).repeat_interleave(G, 1)
+    oh = _f(o).view(B, S, Hq, D).permute(0, 2, 1, 3)
+    dOh = _f(dO).view(B, S, Hq, D).permute(0, 2, 1, 3)
+    Dl = 0.5 * (oh * dOh).sum(-1)
+    mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+    p = torch.exp(_f(q) @ kk.transpose(-1, -2) - lse[..., None]).masked_fill(mask, 0.0)
+    dA = 0.5 * dOh @ vv.transpose(-1, -2)
+    dS = p * (dA - Dl[..., None])
+    dq = 0.5 * dS @ kk
+    dkk = 0.5 * dS.transpose(-1, -2) @ _f(q)
+    dvv = 0.5 * p.transpose(-1, -2) @ dOh
+    dk = dkk.view(B, Hkv, G, S, D).sum(2)
+    dv = dvv.view(B, Hkv, G, S, D).sum(2)
+    return Dl, Dl.sum(-1), dq, dk, dv
+
+
+def rope_bwd(dx: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, rot_dim: int) -> torch.Tensor:
+    """Transpose of ``apply_rope``: x1 = r1 c + r2 s, x2 = r2 c - r1 s."""
+    half = rot_dim // 2
+    r1, r2 = dx[..., :half], dx[..., half:rot_dim]
+    return torch.cat([r1 * cos + r2 * sin, r2 * cos - r1 * sin, dx[..., rot_dim:]], -1)
+
+
+def lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, dtype=torch.float32):
+    """Inverse RoPE + q scale, scattered to token-major d[q|k|v] [B*S, (Hq+2Hkv)*D]."""
+    c, s_ = cos[:S], sin[:S]
+    dqp = rope_bwd(_f(dq) * q_scale, c, s_, rot_dim)
+    dkp = rope_bwd(_f(dk), c, s_, rot_dim)
+    y = torch.cat([dqp, dkp, _f(dv)], 1)                     # [B, Ht, S, D]
+    return y.permute(0, 2, 1, 3).reshape(B * S, -1).to(dtype)
+
+
+def swiglu_il(gu: torch.Tensor) -> torch.Tensor:
+    g, u = deinterleave_gate_up(_f(gu))
+    return (F.silu(g) * u).to(gu.dtype)
+
+
+def lrp_swiglu_bwd(dm: torch.Tensor, gu: torch.Tensor) -> torch.Tensor:
+    """dg = 0.5 dm u sigmoid(g), du = 0.5 dm silu(g), re-interleaved like ``gu``."""
+    g, u = deinterleave_gate_up(_f(gu))
+    sg = torch.sigmoid(g)
+    dg, du = 0.5 * _f(dm) * u * sg, 0.5 * _f(dm) * g * sg
+    T, I = dg.shape
+    out = torch.stack([dg.reshape(T, I // IL_BLOCK, IL_BLOCK), du.reshape(T, I // IL_BLOCK, IL_BLOCK)], 2)
+    return out.reshape(T, 2 * I).to(gu.dtype)
+
+
+def lrp_gelu_bwd(dy: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+    af = _f(a)
+    ratio = torch.where(af.abs() > 1e-6, gelu(af) / torch.where(af.abs() > 1e-6, af, torch.ones_like(af)),
+                        torch.full_like(af, 0.5))
+    return (_f(dy) * ratio).to(dy.dtype)
+
+
+def ln_rstd(x: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = _f(x)
+    return torch.rsqrt((xf - xf.mean(-1, keepdim=True)).pow(2).mean(-1) + eps)
+
+
+def lrp_ln_bwd(dy1, rs1, w1, dy2, rs2, w2, resid):
+    """resid + sum over the (one or two) LayerNorms of (gc - mean(gc)), gc = dy * rstd * w."""
+    def one(dy, rs, w):
+        gc = _f(dy) * rs.view(-1, 1) * _f(w).view(1, -1)
+        return gc - gc.mean(-1, keepdim=True)
+    out = _f(resid) + one(dy1, rs1, w1)
+    if dy2 is not None:
+        out = out + one(dy2, rs2, w2)
+    return out.to(resid.dtype)

@@ -20,7 +20,9 @@ framework's own model weights ("efficient" LRP = Input x modified-Gradient):
 
 The tests check per-rule conservation (Gradient x Input through each rule sums to the output relevance)
 and that the head relevance computed from the head outputs equals the literal S x S probability hook.
-This is an offline calibration pass; it runs on PyTorch ops (hipBLASLt on the GPU) in fp32.
+``head_relevance`` here is the autograd oracle (fp32, one window).  The production pass is
+``engine.RelevanceEngine``: the same rules as explicit backward kernels (``csrc/lrp.hip``), batched over
+windows, checked against this oracle by the tests.
 """
 from __future__ import annotations
 
@@ -199,14 +201,17 @@ def relevance_main(p) -> list:
     if p.max_windows:
         wins = wins[: p.max_windows]
     log(f"relevance: model={cfg.name} weights={prov} data={data_prov} windows={len(wins)}")
+    from ..eval.windows import batches
+    from .engine import RelevanceEngine
+    eng = RelevanceEngine(model)
     acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=device)
     pb = progress_bar(len(wins), env.is_main)
-    for wi, w in enumerate(wins):
-        if wi % env.world_size != env.rank:
+    for bi, b in enumerate(batches(ids, wins, max(1, p.window_batch))):
+        if bi % env.world_size != env.rank:
             continue
-        rel, _, _ = head_relevance(model, ids[:, w.begin:w.end].to(device))
-        acc += rel.double()
-        pb.update(env.world_size)
+        rel, _, _ = eng.head_relevance(b.ids)
+        acc += rel.double().sum(0)
+        pb.update(b.B * env.world_size)
     pb.close()
     all_reduce_sum(acc)
     weights = normalize_per_layer(acc).float().cpu().tolist()

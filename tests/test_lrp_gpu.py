@@ -1,0 +1,99 @@
+"""AttnLRP relevance kernels (csrc/lrp.hip) and the batched RelevanceEngine on gfx950 vs the fp32 oracle."""
+import pytest
+import torch
+
+from llm_inference_in_distributed_edge_networks_amd import ops
+from llm_inference_in_distributed_edge_networks_amd.models import TINY_NEOX, TINY_QWEN2, DecoderLM
+from llm_inference_in_distributed_edge_networks_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rnd(*shape, s=1.0, seed=0, dtype=torch.bfloat16):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * s).to(dtype)
+
+
+def rel_err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    assert torch.isfinite(a).all()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,S", [(2, 14, 2, 512), (1, 8, 8, 200), (3, 4, 2, 96), (1, 2, 1, 37)])
+def test_lrp_attn_bwd(B, Hq, Hkv, S):
+    q = rnd(B, Hq, S, 64, s=0.5, seed=1) * 0.125
+    k = rnd(B, Hkv, S, 64, s=0.5, seed=2)
+    v = rnd(B, Hkv, S, 64, seed=3)
+    dO = rnd(B * S, Hq * 64, seed=4)
+    vt = torch.zeros(B, Hkv, 64, R.s_pad(S), dtype=torch.bfloat16)
+    vt[..., :S] = v.transpose(-1, -2)
+    o, lse = R.attention(q, k, vt, S, need_lse=True)
+    ref = R.lrp_attn_bwd(q, k, v, o, dO, lse)
+    got = ops.lrp_attn_bwd(*(t.to(DEV) for t in (q, k, v, o, dO)), lse.float().contiguous().to(DEV))
+    names = ["D", "rel", "dq", "dk", "dv"]
+    for n, g_, r_ in zip(names, got, ref):
+        assert g_.shape == r_.shape, n
+        e = rel_err(g_, r_)
+        assert e < 2e-2, f"{n}: rel err {e:.3g}"
+
+
+def test_lrp_rope_pack():
+    B, S, Hq, Hkv = 2, 70, 4, 2
+    for rot in (64, 16):
+        cos, sin = R.rope_tables(128, rot, 1e4)
+        dq, dk, dv = rnd(B, Hq, S, 64, seed=5, dtype=torch.float32), rnd(B, Hkv, S, 64, seed=6, dtype=torch.float32), \
+            rnd(B, Hkv, S, 64, seed=7, dtype=torch.float32)
+        ref = R.lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot, 0.125)
+        got = ops.lrp_rope_pack(dq.to(DEV), dk.to(DEV), dv.to(DEV), cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv, rot, 0.125)
+        assert rel_err(got, ref) < 5e-3
+
+
+def test_swiglu_and_gelu_rules():
+    gu = rnd(300, 1024, seed=8)
+    dm = rnd(300, 512, seed=9)
+    assert rel_err(ops.swiglu_il(gu.to(DEV)), R.swiglu_il(gu)) < 1e-2
+    assert rel_err(ops.lrp_swiglu_bwd(dm.to(DEV), gu.to(DEV)), R.lrp_swiglu_bwd(dm, gu)) < 1e-2
+    a = rnd(300, 512, seed=10)
+    assert rel_err(ops.lrp_gelu_bwd(dm.to(DEV), a.to(DEV)), R.lrp_gelu_bwd(dm, a)) < 1e-2
+    x = rnd(300, 256, seed=11) * 2 + 0.5
+    rs = ops.ln_rstd(x.to(DEV), 1e-5)
+    assert rel_err(rs, R.ln_rstd(x, 1e-5)) < 1e-3
+    dy1, dy2, res = rnd(300, 256, seed=12), rnd(300, 256, seed=13), rnd(300, 256, seed=14)
+    w1, w2 = rnd(256, seed=15), rnd(256, seed=16)
+    r = R.lrp_ln_bwd(dy1, rs.cpu(), w1, dy2, rs.cpu(), w2, res)
+    got = ops.lrp_ln_bwd(*(t.to(DEV) for t in (dy1,)), rs, w1.to(DEV), dy2.to(DEV), rs, w2.to(DEV), res.to(DEV))
+    assert rel_err(got, r) < 1e-2
+
+
+def test_linear_rowscale():
+    x, w = rnd(512, 1024, seed=17), rnd(256, 1024, s=0.05, seed=18)
+    rs = torch.rand(512) + 0.5
+    res = rnd(512, 256, seed=19)
+    got = ops.linear_rowscale(x.to(DEV), w.to(DEV), rs.to(DEV), residual=res.to(DEV))
+    assert rel_err(got, R._f(x) @ R._f(w).t() * rs.view(-1, 1) + R._f(res)) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX], ids=lambda c: c.name)
+def test_relevance_engine_gpu_vs_cpu(cfg):
+    """bf16 HIP relevance pass vs the fp32 CPU engine (== autograd oracle) on the same weights."""
+    from llm_inference_in_distributed_edge_networks_amd.relevance.engine import RelevanceEngine
+    mg = DecoderLM.random_init(cfg, 3, device=DEV, dtype=torch.bfloat16, std=0.05)
+    mc = DecoderLM.random_init(cfg, 3, std=0.05)
+    # identical (bf16-rounded) weights on both sides
+    for Lg, Lc in zip(mg.layers, mc.layers):
+        for kk in Lc:
+            Lc[kk] = Lg[kk].float().cpu() if kk in Lg else Lc[kk]
+    for kk in ("embed", "head", "norm_w", "norm_b"):
+        if mc.w.get(kk) is not None:
+            mc.w[kk] = mg.w[kk].float().cpu()
+    mc.layers = mc.w["layers"]
+    ids = torch.randint(0, cfg.vocab_size, (4, 128), generator=torch.Generator().manual_seed(2))
+    rg, ing, mxg = RelevanceEngine(mg).head_relevance(ids.to(DEV))
+    rc, inc, mxc = RelevanceEngine(mc).head_relevance(ids)
+    assert rel_err(mxg, mxc) < 2e-2
+    assert rel_err(rg, rc) < 0.1, rel_err(rg, rc)
+    # the calibrated table (normalised per layer over all windows) is what weighted_importance consumes
+    wg, wc = rg.sum(0), rc.sum(0)
+    assert rel_err(wg / wg.sum(-1, keepdim=True), wc / wc.sum(-1, keepdim=True)) < 0.1

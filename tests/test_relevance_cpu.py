@@ -46,3 +46,45 @@ def test_output_identity_equals_probability_hook():
         r_probs, _, _ = head_relevance(m, ids, via_probs=True)
         r_out, _, _ = head_relevance(m, ids)
         assert torch.allclose(r_probs, r_out, rtol=1e-4, atol=1e-6)
+
+
+def test_engine_equals_autograd_oracle():
+    """Explicit-backward RelevanceEngine (the production pass, batched) == autograd AttnLRP, per window."""
+    from llm_inference_in_distributed_edge_networks_amd.relevance.engine import RelevanceEngine
+    for cfg in (TINY_QWEN2, TINY_NEOX):
+        m = DecoderLM.random_init(cfg, 3, std=0.05)
+        ids = torch.randint(0, cfg.vocab_size, (3, 56), generator=torch.Generator().manual_seed(1))
+        rel, in_rel, mx = RelevanceEngine(m).head_relevance(ids)
+        assert rel.shape == (3, cfg.num_layers, cfg.num_heads)
+        for b in range(3):
+            r0, in0, mx0 = head_relevance(m, ids[b:b + 1])
+            assert torch.allclose(rel[b], r0, rtol=1e-4, atol=1e-5)
+            assert abs(float(in_rel[b]) - float(in0)) < 1e-3 * max(1.0, abs(float(in0)))
+            assert abs(float(mx[b]) - float(mx0)) < 1e-4
+
+
+def test_lrp_reference_ops_match_autograd():
+    """The reference LRP attention backward == autograd through the uniform / softmax rules."""
+    from llm_inference_in_distributed_edge_networks_amd.ops import reference as R
+    from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import _Softmax
+    g = torch.Generator().manual_seed(0)
+    B, Hq, Hkv, S, D = 2, 4, 2, 40, 64
+    q = torch.randn(B, Hq, S, D, generator=g) * 0.3
+    k = torch.randn(B, Hkv, S, D, generator=g) * 0.3
+    v = torch.randn(B, Hkv, S, D, generator=g)
+    dO = torch.randn(B * S, Hq * D, generator=g)
+    qa, ka, va = (t.clone().requires_grad_(True) for t in (q, k, v))
+    kk, vv = ka.repeat_interleave(2, 1), va.repeat_interleave(2, 1)
+    sc = _UniformMatmul.apply(qa, kk.transpose(-1, -2)).masked_fill(torch.ones(S, S, dtype=torch.bool).triu(1),
+                                                                    float("-inf"))
+    A = _Softmax.apply(sc)
+    A.retain_grad()
+    oh = _UniformMatmul.apply(A, vv)
+    o = oh.permute(0, 2, 1, 3).reshape(B * S, Hq * D)
+    (o * dO).sum().backward()
+    lse = torch.logsumexp(sc.detach(), -1)
+    Dl, rel, dq, dk, dv = R.lrp_attn_bwd(q, k, v, o.detach(), dO, lse)
+    assert torch.allclose(rel, (A * A.grad).sum((2, 3)), rtol=1e-4, atol=1e-4)
+    assert torch.allclose(dq, qa.grad, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(dk, ka.grad, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(dv, va.grad, rtol=1e-4, atol=1e-5)
