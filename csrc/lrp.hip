@@ -14,9 +14,9 @@
 //   lrp_attn_delta : D[b,h,i] = sum_j A_ij dA_ij = 0.5 dO_i . O_i (uniform rule on A V); per-(window, head)
 //                    relevance rel[b,h] = sum_i D[b,h,i] - the quantity the reference hook sums over S x S
 //                    (sum_{ij} A * dA).  No S x S tensor exists anywhere.
-//   lrp_attn_dkdv  : dK, dV for one (window, kv head, 64-key block), looping over the q heads of the GQA
-//                    group and the causal query tiles: P recomputed from Q K^T and the forward LSE,
-//                    dA = 0.5 dO V^T, dS = P (dA - D), dV = 0.5 P^T dO, dK = 0.5 dS^T Q.
+//   lrp_attn_dkdv  : dK, dV partials for one (window, q head, 64-key block) over the causal query tiles:
+//                    P recomputed from Q K^T and the forward LSE, dA = 0.5 dO V^T, dS = P (dA - D),
+//                    dV = 0.5 P^T dO, dK = 0.5 dS^T Q.  The GQA group sum is fused into lrp_rope_pack.
 //   lrp_attn_dq    : dQ = 0.5 dS K for one (window, q head, 64-query block) over its causal key tiles.
 //                    dK/dV and dQ are separate sweeps: no atomics, deterministic.
 //   lrp_rope_pack  : inverse RoPE (transpose rotation) + q scaling, scatter dQ/dK/dV into the token-major
@@ -104,8 +104,9 @@ __global__ __launch_bounds__(256) void lrp_attn_delta_kernel(const bf16_t* __res
 }
 
 // ---------------------------------------------------------------------------------------------
-// dK, dV.  q [B,Hq,S,64] (pre-scaled), k, v [B,Hkv,S,64], dO token-major, lse/D [B,Hq,S] -> dk, dv fp32
-// [B,Hkv,S,64].  Workgroup = (b, hk, 64-key block); wave w owns keys kb*64 + 16w .. +15.
+// dK, dV partials per q head.  q [B,Hq,S,64] (pre-scaled), k, v [B,Hkv,S,64], dO token-major,
+// lse/D [B,Hq,S] -> dk, dv fp32 [B,Hq,S,64] (the GQA group sum happens in lrp_rope_pack).  Workgroup =
+// (b, q head, 64-key block): 7x the workgroups of a per-kv-head sweep; wave w owns keys kb*64+16w..+15.
 __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                             const bf16_t* __restrict__ v,
                                                             const bf16_t* __restrict__ dO,
@@ -119,9 +120,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __rest
   __shared__ float sL[32], sD[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int nkb = (S + 63) / 64;
-  const int kb = blockIdx.x % nkb;
-  const int bhk = blockIdx.x / nkb, b = bhk / Hkv, hk = bhk - b * Hkv;
-  const int G = Hq / Hkv;
+  const int kb = blockIdx.x / (B * Hq);                // lightest (last) key blocks last: kb ascending = heavy first
+  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
   const int key = kb * 64 + wave * 16 + cl;          // this lane's key (B-operand column / A-operand row)
   const int keyc = key < S ? key : S - 1;
   const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
@@ -135,10 +135,10 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __rest
   f32x4_t dka[4], dva[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  (void)nkb;
 
   const int q_first = (kb * 64) & ~31;
-  for (int hh = 0; hh < G; ++hh) {
-    const int h = hk * G + hh;
+  {
     const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
     const bf16_t* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
     const float* lh = lse + ((size_t)b * Hq + h) * S;
@@ -185,8 +185,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __rest
     }
   }
   // C[row = key 4g + r of this wave][col = d 16dt + cl]
-  float* dkh = dk + ((size_t)b * Hkv + hk) * S * 64;
-  float* dvh = dv + ((size_t)b * Hkv + hk) * S * 64;
+  float* dkh = dk + ((size_t)b * Hq + h) * S * 64;
+  float* dvh = dv + ((size_t)b * Hq + h) * S * 64;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int kr = kb * 64 + wave * 16 + g * 4 + r;
@@ -273,7 +273,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_kernel(const bf16_t* __restri
 }
 
 // ---------------------------------------------------------------------------------------------
-// Inverse RoPE + q scale + scatter into token-major d[q|k|v] (bf16 [B*S, (Hq+2Hkv)*64]).
+// Inverse RoPE + q scale + GQA group sum of the dK/dV partials ([B,Hq,S,64] each) + scatter into
+// token-major d[q|k|v] (bf16 [B*S, (Hq+2Hkv)*64]).
 // Forward: r1 = x1 c - x2 s, r2 = x2 c + x1 s (first rot_dim dims).  Transpose: x1 = r1 c + r2 s,
 // x2 = r2 c - r1 s.  One thread per (token, head, d).
 __global__ __launch_bounds__(256) void lrp_rope_pack_kernel(const float* __restrict__ dq, const float* __restrict__ dk,
@@ -293,26 +294,37 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_kernel(const float* __restr
   const float* src;
   float scale = 1.f;
   bool rope = true;
+  const int G = Hq / Hkv;
+  int ng = 1;
   if (hh < Hq) {
     src = dq + (((size_t)b * Hq + hh) * S + s) * 64;
     scale = q_scale;
   } else if (hh < Hq + Hkv) {
-    src = dk + (((size_t)b * Hkv + (hh - Hq)) * S + s) * 64;
+    src = dk + (((size_t)b * Hq + (hh - Hq) * G) * S + s) * 64;
+    ng = G;
   } else {
-    src = dv + (((size_t)b * Hkv + (hh - Hq - Hkv)) * S + s) * 64;
+    src = dv + (((size_t)b * Hq + (hh - Hq - Hkv) * G) * S + s) * 64;
+    ng = G;
     rope = false;
   }
-  float val;
+  // dk / dv: sum of the per-q-head partials of the GQA group (head stride S*64)
   const int half = rot_dim >> 1;
+  const int dp = (!rope || d >= rot_dim) ? d : (d < half ? d + half : d - half);
+  float x0 = 0.f, xp = 0.f;
+  for (int gi = 0; gi < ng; ++gi) {
+    x0 += src[(size_t)gi * S * 64 + d];
+    xp += src[(size_t)gi * S * 64 + dp];
+  }
+  float val;
   if (!rope || d >= rot_dim) {
-    val = src[d];
+    val = x0;
   } else if (d < half) {
     const float c = cosT[(size_t)s * half + d], sn = sinT[(size_t)s * half + d];
-    val = src[d] * c + src[d + half] * sn;
+    val = x0 * c + xp * sn;
   } else {
     const int j = d - half;
     const float c = cosT[(size_t)s * half + j], sn = sinT[(size_t)s * half + j];
-    val = src[d] * c - src[j] * sn;
+    val = x0 * c - xp * sn;
   }
   out[idx] = f2bf(val * scale);
 }
@@ -320,29 +332,47 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_kernel(const float* __restr
 // ---------------------------------------------------------------------------------------------
 // Interleaved gate|up (blocks of 16 columns): a = silu(g) * u  and the LRP backward
 //   dg = 0.5 dm u sigmoid(g)  (uniform rule on g*u, identity rule on SiLU),  du = 0.5 dm silu(g).
+// One thread per 8 consecutive columns of one 16-column block: 16-byte loads and stores.
 __global__ __launch_bounds__(256) void swiglu_il_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ a,
-                                                        size_t n, int I) {
+                                                        size_t n8, int I) {
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= n) return;
-  const size_t t = idx / I;
-  const int c = idx - t * I, blk = c >> 4, e = c & 15;
+  if (idx >= n8) return;
+  const int I8 = I >> 3;
+  const size_t t = idx / I8;
+  const int c = (int)(idx - t * I8) * 8, blk = c >> 4, e = c & 15;
   const bf16_t* row = gu + t * (size_t)(2 * I) + blk * 32 + e;
-  const float g = bf2f(row[0]), u = bf2f(row[16]);
-  a[idx] = f2bf(g / (1.f + __expf(-g)) * u);
+  const u32x4_t gv = *(const u32x4_t*)row, uv = *(const u32x4_t*)(row + 16);
+  u32x4_t o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float g0 = bf_lo(gv[i]), g1 = bf_hi(gv[i]);
+    o[i] = pack_bf2(g0 / (1.f + __expf(-g0)) * bf_lo(uv[i]), g1 / (1.f + __expf(-g1)) * bf_hi(uv[i]));
+  }
+  *(u32x4_t*)(a + t * (size_t)I + c) = o;
 }
 
 __global__ __launch_bounds__(256) void lrp_swiglu_bwd_kernel(const bf16_t* __restrict__ dm,
                                                              const bf16_t* __restrict__ gu, bf16_t* __restrict__ dgu,
-                                                             size_t n, int I) {
+                                                             size_t n8, int I) {
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= n) return;
-  const size_t t = idx / I;
-  const int c = idx - t * I, blk = c >> 4, e = c & 15;
+  if (idx >= n8) return;
+  const int I8 = I >> 3;
+  const size_t t = idx / I8;
+  const int c = (int)(idx - t * I8) * 8, blk = c >> 4, e = c & 15;
   const size_t off = t * (size_t)(2 * I) + blk * 32 + e;
-  const float g = bf2f(gu[off]), u = bf2f(gu[off + 16]), m = bf2f(dm[idx]);
-  const float sg = 1.f / (1.f + __expf(-g));
-  dgu[off] = f2bf(0.5f * m * u * sg);
-  dgu[off + 16] = f2bf(0.5f * m * g * sg);
+  const u32x4_t gv = *(const u32x4_t*)(gu + off), uv = *(const u32x4_t*)(gu + off + 16);
+  const u32x4_t mv = *(const u32x4_t*)(dm + t * (size_t)I + c);
+  u32x4_t og, ou;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float g0 = bf_lo(gv[i]), g1 = bf_hi(gv[i]);
+    const float s0 = 1.f / (1.f + __expf(-g0)), s1 = 1.f / (1.f + __expf(-g1));
+    const float m0 = 0.5f * bf_lo(mv[i]), m1 = 0.5f * bf_hi(mv[i]);
+    og[i] = pack_bf2(m0 * bf_lo(uv[i]) * s0, m1 * bf_hi(uv[i]) * s1);
+    ou[i] = pack_bf2(m0 * g0 * s0, m1 * g1 * s1);
+  }
+  *(u32x4_t*)(dgu + off) = og;
+  *(u32x4_t*)(dgu + off + 16) = ou;
 }
 
 // GELU identity rule: dx = dy * gelu(a)/a (0.5 at a = 0).  a = pre-activation (bf16), in place on dy.
@@ -411,7 +441,7 @@ EDGE_API int edge_lrp_attn_bwd(const void* q, const void* k, const void* v, cons
   if (Hq % Hkv) return (int)hipErrorInvalidValue;
   const int nb = (S + 63) / 64;
   lrp_attn_delta_kernel<<<B * Hq, 256, 0, st>>>((const bf16_t*)o, (const bf16_t*)dO, D, rel, Hq, S);
-  lrp_attn_dkdv_kernel<<<B * Hkv * nb, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+  lrp_attn_dkdv_kernel<<<B * Hq * nb, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                       (const bf16_t*)dO, lse, D, dk, dv, B, Hq, Hkv, S);
   lrp_attn_dq_kernel<<<B * Hq * nb, 256, 0, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                                                    (const bf16_t*)dO, lse, D, dq, B, Hq, Hkv, S);
@@ -430,18 +460,18 @@ EDGE_API int edge_lrp_rope_pack(const float* dq, const float* dk, const float* d
 }
 
 EDGE_API int edge_swiglu_il(const void* gu, void* a, long long T, int I, hipStream_t st) {
-  const size_t n = (size_t)T * I;
-  if (!n) return 0;
+  const size_t n8 = (size_t)T * I / 8;
+  if (!n8) return 0;
   if (I % 16) return (int)hipErrorInvalidValue;
-  swiglu_il_kernel<<<nblk(n), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)a, n, I);
+  swiglu_il_kernel<<<nblk(n8), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)a, n8, I);
   return (int)hipGetLastError();
 }
 
 EDGE_API int edge_lrp_swiglu_bwd(const void* dm, const void* gu, void* dgu, long long T, int I, hipStream_t st) {
-  const size_t n = (size_t)T * I;
-  if (!n) return 0;
+  const size_t n8 = (size_t)T * I / 8;
+  if (!n8) return 0;
   if (I % 16) return (int)hipErrorInvalidValue;
-  lrp_swiglu_bwd_kernel<<<nblk(n), 256, 0, st>>>((const bf16_t*)dm, (const bf16_t*)gu, (bf16_t*)dgu, n, I);
+  lrp_swiglu_bwd_kernel<<<nblk(n8), 256, 0, st>>>((const bf16_t*)dm, (const bf16_t*)gu, (bf16_t*)dgu, n8, I);
   return (int)hipGetLastError();
 }
 

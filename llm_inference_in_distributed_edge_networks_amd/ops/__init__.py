@@ -293,7 +293,8 @@ def linear_rowscale(x: torch.Tensor, w: torch.Tensor, rscale: torch.Tensor, resi
 
 
 def lrp_attn_bwd(q, k, v, o, dO, lse):
-    """-> (D [B,Hq,S], rel [B,Hq], dq [B,Hq,S,64], dk, dv [B,Hkv,S,64]) fp32; see ``reference.lrp_attn_bwd``."""
+    """-> (D [B,Hq,S], rel [B,Hq], dq, dk, dv [B,Hq,S,64]) fp32 (dk/dv per-q-head partials); see
+    ``reference.lrp_attn_bwd``."""
     if not _gpu(q):
         return ref.lrp_attn_bwd(q, k, v, o, dO, lse)
     _check_bf16(q, k, v, o, dO)
@@ -304,7 +305,7 @@ def lrp_attn_bwd(q, k, v, o, dO, lse):
     f32 = dict(dtype=torch.float32, device=q.device)
     Dl, rel = torch.empty(B, Hq, S, **f32), torch.empty(B, Hq, **f32)
     dq = torch.empty(B, Hq, S, D, **f32)
-    dk, dv = torch.empty(B, Hkv, S, D, **f32), torch.empty(B, Hkv, S, D, **f32)
+    dk, dv = torch.empty(B, Hq, S, D, **f32), torch.empty(B, Hq, S, D, **f32)
     call("edge_lrp_attn_bwd", ptr(q), ptr(k), ptr(v), ptr(o), ptr(dO), ptr(lse), ptr(Dl), ptr(rel), ptr(dq), ptr(dk),
          ptr(dv), B, Hq, Hkv, S, stream())
     return Dl, rel, dq, dk, dv

@@ -194,7 +194,8 @@ def fold_norm_weight(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
 def lrp_attn_bwd(q, k, v, o, dO, lse):
     """Uniform rule on Q K^T and A V, plain softmax gradient.  q [B,Hq,S,D] pre-scaled, k/v [B,Hkv,S,D],
     o/dO token-major [B*S, Hq*D], lse [B,Hq,S].  Returns (D [B,Hq,S], rel [B,Hq], dq [B,Hq,S,D],
-    dk [B,Hkv,S,D], dv [B,Hkv,S,D]) in fp32 (dq w.r.t. the pre-scaled q)."""
+    dk, dv [B,Hq,S,D]) in fp32: dq w.r.t. the pre-scaled q; dk/dv are per-q-head partials (the GQA group
+    sum is part of ``lrp_rope_pack``)."""
     B, Hq, S, D = q.shape
     Hkv = k.shape[1]
     G = Hq // Hkv
@@ -207,10 +208,8 @@ def lrp_attn_bwd(q, k, v, o, dO, lse):
     dA = 0.5 * dOh @ vv.transpose(-1, -2)
     dS = p * (dA - Dl[..., None])
     dq = 0.5 * dS @ kk
-    dkk = 0.5 * dS.transpose(-1, -2) @ _f(q)
-    dvv = 0.5 * p.transpose(-1, -2) @ dOh
-    dk = dkk.view(B, Hkv, G, S, D).sum(2)
-    dv = dvv.view(B, Hkv, G, S, D).sum(2)
+    dk = 0.5 * dS.transpose(-1, -2) @ _f(q)
+    dv = 0.5 * p.transpose(-1, -2) @ dOh
     return Dl, Dl.sum(-1), dq, dk, dv
 
 
@@ -222,8 +221,12 @@ def rope_bwd(dx: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, rot_dim: in
 
 
 def lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, dtype=torch.float32):
-    """Inverse RoPE + q scale, scattered to token-major d[q|k|v] [B*S, (Hq+2Hkv)*D]."""
+    """Inverse RoPE + q scale + GQA group sum of the dk/dv partials [B,Hq,S,D], scattered to token-major
+    d[q|k|v] [B*S, (Hq+2Hkv)*D]."""
     c, s_ = cos[:S], sin[:S]
+    G = Hq // Hkv
+    dk = _f(dk).view(B, Hkv, G, S, -1).sum(2)
+    dv = _f(dv).view(B, Hkv, G, S, -1).sum(2)
     dqp = rope_bwd(_f(dq) * q_scale, c, s_, rot_dim)
     dkp = rope_bwd(_f(dk), c, s_, rot_dim)
     y = torch.cat([dqp, dkp, _f(dv)], 1)                     # [B, Ht, S, D]

@@ -43,8 +43,7 @@ def test_lrp_rope_pack():
     B, S, Hq, Hkv = 2, 70, 4, 2
     for rot in (64, 16):
         cos, sin = R.rope_tables(128, rot, 1e4)
-        dq, dk, dv = rnd(B, Hq, S, 64, seed=5, dtype=torch.float32), rnd(B, Hkv, S, 64, seed=6, dtype=torch.float32), \
-            rnd(B, Hkv, S, 64, seed=7, dtype=torch.float32)
+        dq, dk, dv = (rnd(B, Hq, S, 64, seed=sd, dtype=torch.float32) for sd in (5, 6, 7))
         ref = R.lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot, 0.125)
         got = ops.lrp_rope_pack(dq.to(DEV), dk.to(DEV), dv.to(DEV), cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv, rot, 0.125)
         assert rel_err(got, ref) < 5e-3

@@ -86,5 +86,5 @@ def test_lrp_reference_ops_match_autograd():
     Dl, rel, dq, dk, dv = R.lrp_attn_bwd(q, k, v, o.detach(), dO, lse)
     assert torch.allclose(rel, (A * A.grad).sum((2, 3)), rtol=1e-4, atol=1e-4)
     assert torch.allclose(dq, qa.grad, rtol=1e-4, atol=1e-5)
-    assert torch.allclose(dk, ka.grad, rtol=1e-4, atol=1e-5)
-    assert torch.allclose(dv, va.grad, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(dk.view(B, Hkv, 2, S, D).sum(2), ka.grad, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(dv.view(B, Hkv, 2, S, D).sum(2), va.grad, rtol=1e-4, atol=1e-5)
