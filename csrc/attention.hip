@@ -2,7 +2,8 @@
 // reference:
 //
 //   flash_attn_fwd : O = softmax(Q K^T) V with online softmax, never materialising S x S; optional
-//                    per-row LSE output (input of the column-sum scorer).
+//                    per-row LSE output (input of the column-sum scorer).  v2 (default) below the v1
+//                    kernel: mask-free interior tiles, exp2 + lazy rescale, 3-stage ring, XCD-aware order.
 //   attn_lastrow   : P[S-1, :] per head  -> "last_row" importance (Qwen2-0.5B/main.py:80-86).
 //   attn_colsum    : sum_i P[i, j] per head, recomputed from Q, K and the LSE (FA-backward style sweep,
 //                    key block outer / query tiles inner) -> "regular_importance", "weighted_importance",
@@ -167,6 +168,168 @@ __global__ __launch_bounds__(256, 2) void flash_attn_fwd_kernel(const bf16_t* __
 }
 
 // ---------------------------------------------------------------------------------------------
+// v2 forward (default).  Same tile geometry and operand layouts as flash_attn_fwd_kernel; what changed is
+// what the profile of v1 showed (≈210 VALU per wave per 64-key tile against 16 MFMAs, and a 1-tile load
+// lead that left every tile waiting on L2/MALL):
+//   * masking only on the diagonal tile (kb == qb is the only tile with keys > query or keys >= S);
+//     interior tiles run a mask-free body;
+//   * exp2 domain: p = exp2(fma(s, log2e, -m2)) (one FMA + one v_exp per score);
+//   * lazy rescaling: the running max moves only when a row's tile max exceeds it by more than TAU = 8
+//     (log2 units, wave-uniform decision), so the alpha rescale of O and l is skipped on most tiles and
+//     p stays <= 2^8 (exact in fp32, representable in bf16);
+//   * a 3-stage K/V ring: tile kb+2 is issued while tile kb is computed (vmcnt(4) keeps tile kb+1 in
+//     flight across the barrier);
+//   * XCD-aware block order: the query blocks and heads of one (window, kv head) group run on one XCD,
+//     so its K/V tiles are fetched into that XCD's L2 once; heavy (late) query blocks are dispatched first.
+namespace {
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float TAU = 8.f;
+constexpr int NST = 3;
+
+// Key order: MFMA ni, row i reads key 32(ni>>1) + 8(i>>2) + 4(ni&1) + (i&3), so lane group g holds keys
+// 32ks + 8g .. +7 of P in pf[ks] (consecutive), and the V^T operand of P.V is ONE 16-byte row-chunk read.
+template <bool MASK>
+__device__ __forceinline__ void fa2_tile(const char* lk, const char* lv, const bf16x8_t (&qf)[2], f32x4_t (&oacc)[4],
+                                         float& m2, float& l_run, int kb, int qrow, int S, int g, int ql) {
+  f32x4_t st[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    st[ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int r = 32 * (ni >> 1) + 8 * (ql >> 2) + 4 * (ni & 1) + (ql & 3);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t kf = *(const bf16x8_t*)(lk + r * 128 + (((ks * 4 + g) ^ aswz(r)) << 4));
+      st[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], st[ni], 0, 0, 0);
+    }
+  }
+  if constexpr (MASK) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kb * KT + 32 * (ni >> 1) + 8 * g + 4 * (ni & 1) + r;
+        if (key > qrow || key >= S) st[ni][r] = -INFINITY;
+      }
+  }
+  float mloc = -INFINITY;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[ni][r]);
+  mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+  mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+  const float mc = mloc * LOG2E;
+  if (__builtin_amdgcn_ballot_w64(mc > m2 + TAU)) {      // wave-uniform: rescale every row exactly
+    const float mn = fmaxf(m2, mc);
+    const float alpha = __builtin_amdgcn_exp2f(m2 - mn);  // m2 = -inf on the first tile -> 0
+    m2 = mn;
+    l_run *= alpha;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) oacc[d] *= alpha;
+  }
+  bf16x8_t pf[2];
+  float ps = 0.f;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(st[ni][r], LOG2E, -m2));
+      ps += p;
+      pf[ni >> 1][(ni & 1) * 4 + r] = (__bf16)p;
+    }
+  l_run += ps;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int row = dt * 16 + ql;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t vf = *(const bf16x8_t*)(lv + row * 128 + (((ks * 4 + g) ^ aswz(row)) << 4));
+      oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[ks], oacc[dt], 0, 0, 0);
+    }
+  }
+}
+}  // namespace
+
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void flash_attn_fwd2_kernel(const bf16_t* __restrict__ q,
+                                                                 const bf16_t* __restrict__ k,
+                                                                 const bf16_t* __restrict__ vt,
+                                                                 bf16_t* __restrict__ o, float* __restrict__ lse,
+                                                                 int B, int Hq, int Hkv, int S, int s_pad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
+  const int nqb = (S + 63) / 64;
+  const int G = Hq / Hkv, NG = B * Hkv;
+  // blocks x, x+8, x+16, ... share an XCD (round-robin dispatch): XCD `xcd` owns groups xcd, xcd+8, ...
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int cnt = (NG - xcd + 7) >> 3;                 // groups owned by this XCD slot
+  const int per_qb = cnt * G;
+  if (j >= per_qb * nqb) return;
+  const int qb = nqb - 1 - j / per_qb;                  // heavy query blocks first
+  const int rem = j - (nqb - 1 - qb) * per_qb;
+  const int grp = xcd + 8 * (rem / G);
+  const int b = grp / Hkv, hk = grp - b * Hkv, h = hk * G + rem % G;
+
+  const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
+  const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const bf16_t* vh = vt + ((size_t)b * Hkv + hk) * 64 * (size_t)s_pad;
+
+  const int q0 = qb * 64 + wave * 16;
+  const int qrow = q0 + ql;
+  const int qld = qrow < S ? qrow : S - 1;
+  bf16x8_t qf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) qf[ks] = *(const bf16x8_t*)(qh + (size_t)qld * 64 + ks * 32 + g * 8);
+
+  f32x4_t oacc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m2 = -INFINITY, l_run = 0.f;
+
+  const int nkb = qb + 1;
+  stage64(kh, 64, 0, S, 0, smem, wave, lane);
+  stage64(vh, s_pad, 0, 64, 0, smem + TILE, wave, lane);
+  if (nkb > 1) {
+    stage64(kh, 64, KT, S, 0, smem + 2 * TILE, wave, lane);
+    stage64(vh, s_pad, 0, 64, KT, smem + 3 * TILE, wave, lane);
+  }
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 2 < nkb) {
+      char* nx = smem + ((kb + 2) % NST) * 2 * TILE;
+      stage64(kh, 64, (kb + 2) * KT, S, 0, nx, wave, lane);
+      stage64(vh, s_pad, 0, 64, (kb + 2) * KT, nx + TILE, wave, lane);
+    }
+    const char* cur = smem + (kb % NST) * 2 * TILE;
+    if (kb < qb) fa2_tile<false>(cur, cur + TILE, qf, oacc, m2, l_run, kb, qrow, S, g, ql);
+    else fa2_tile<true>(cur, cur + TILE, qf, oacc, m2, l_run, kb, qrow, S, g, ql);
+  }
+
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (qrow < S) {
+    const float inv = 1.f / l_run;
+    bf16_t* orow = o + ((size_t)b * S + qrow) * (size_t)(Hq * 64) + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      u32x2_t w;
+      w[0] = pack_bf2(oacc[dt][0] * inv, oacc[dt][1] * inv);
+      w[1] = pack_bf2(oacc[dt][2] * inv, oacc[dt][3] * inv);
+      *(u32x2_t*)(orow + dt * 16 + g * 4) = w;
+    }
+    if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = m2 * 0.6931471805599453f + logf(l_run);
+  }
+}
+
+static int g_attn_variant = 3;
+EDGE_API int edge_attn_set_variant(int v) {
+  g_attn_variant = (v >= 1 && v <= 3) ? v : 3;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Last-row probabilities: one workgroup per (b, h); P[S-1, j] = softmax_j(q_{S-1} . k_j).
 __global__ __launch_bounds__(256) void attn_lastrow_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                            float* __restrict__ out, int Hq, int Hkv, int S) {
@@ -286,6 +449,17 @@ EDGE_API int edge_flash_attn_fwd(const void* q, const void* k, const void* vt, v
   if (B <= 0 || S <= 0) return 0;
   if (Hq % Hkv || s_pad % 64 || s_pad < S) return (int)hipErrorInvalidValue;
   const int nqb = (S + 63) / 64;
+  if (g_attn_variant >= 2) {  // 2: v2 at 2 workgroups/CU, 3: v2 at 3 workgroups/CU
+    const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
+    const dim3 grid(8 * maxcnt * G * nqb);
+    if (g_attn_variant == 3)
+      hipLaunchKernelGGL(flash_attn_fwd2_kernel<3>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
+                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, B, Hq, Hkv, S, s_pad);
+    else
+      hipLaunchKernelGGL(flash_attn_fwd2_kernel<2>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
+                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, B, Hq, Hkv, S, s_pad);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(flash_attn_fwd_kernel, dim3(B * Hq * nqb), dim3(256), 4 * TILE, st, (const bf16_t*)q,
                      (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, B, Hq, Hkv, S, s_pad);
   return (int)hipGetLastError();

@@ -219,6 +219,12 @@ def attention(q, k, vt, S, need_lse=False):
     return o, lse
 
 
+def set_attn_variant(v: int) -> None:
+    """Flash-attention forward kernel: 3 (default: v2 at 3 workgroups/CU), 2 (v2 at 2/CU) or 1 (the first
+    version).  A/B and tests only."""
+    call("edge_attn_set_variant", int(v))
+
+
 def attn_lastrow(q, k, S):
     if not _gpu(q):
         return ref.attn_lastrow(q, k, S)

@@ -145,8 +145,16 @@ def _qkv(B, S, Hq, Hkv, seed):
     return q, k, vt
 
 
-@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (1, 100, 4, 2), (3, 64, 8, 8), (1, 1000, 2, 1)])
-def test_flash_attention(B, S, Hq, Hkv):
+@pytest.fixture(params=[2, 3, 1], ids=["fa2", "fa2occ3", "fa1"])
+def attn_variant(request):
+    ops.set_attn_variant(request.param)
+    yield request.param
+    ops.set_attn_variant(3)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (1, 100, 4, 2), (3, 64, 8, 8), (1, 1000, 2, 1),
+                                        (5, 200, 14, 2), (9, 128, 4, 2)])
+def test_flash_attention(B, S, Hq, Hkv, attn_variant):
     q, k, vt = _qkv(B, S, Hq, Hkv, 40)
     o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True)
     ro, rlse = R.attention(q, k, vt, S, need_lse=True)
@@ -154,11 +162,13 @@ def test_flash_attention(B, S, Hq, Hkv):
     close(lse, rlse, atol=2e-3, rtol=1e-3)
 
 
-def test_flash_attention_spike():
-    # force the online-softmax rescale: one key much larger for one query, late in the sequence
+@pytest.mark.parametrize("pos", [(200, 230), (3, 250), (70, 71)])
+def test_flash_attention_spike(pos, attn_variant):
+    # force the online-softmax rescale: one key much larger for one query (early, late, same tile)
     B, S, Hq, Hkv = 1, 256, 2, 1
     q, k, vt = _qkv(B, S, Hq, Hkv, 50)
-    k[0, 0, 200] = q[0, 0, 230] * 400
+    kj, qi = pos
+    k[0, 0, kj] = q[0, 0, qi] * 400
     o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True)
     ro, rlse = R.attention(q, k, vt, S, need_lse=True)
     close(o, ro, atol=3e-2, rtol=2e-2)
