@@ -255,6 +255,7 @@ __global__ __launch_bounds__(256, OCC) void flash_attn_fwd2_kernel(const bf16_t*
                                                                  const bf16_t* __restrict__ k,
                                                                  const bf16_t* __restrict__ vt,
                                                                  bf16_t* __restrict__ o, float* __restrict__ lse,
+                                                                 const float* __restrict__ n_rows,
                                                                  int B, int Hq, int Hkv, int S, int s_pad) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
@@ -269,6 +270,8 @@ __global__ __launch_bounds__(256, OCC) void flash_attn_fwd2_kernel(const bf16_t*
   const int rem = j - (nqb - 1 - qb) * per_qb;
   const int grp = xcd + 8 * (rem / G);
   const int b = grp / Hkv, hk = grp - b * Hkv, h = hk * G + rem % G;
+  // scored-rows mode (last layer of a model): window b only needs query rows >= S-1-n_rows[b]
+  if (n_rows && qb * 64 + 63 < S - 1 - (int)n_rows[b]) return;
 
   const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
   const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
@@ -444,8 +447,10 @@ __global__ __launch_bounds__(256) void head_combine_kernel(const float* __restri
   out[idx] = (beta != 0.f ? beta * out[idx] : 0.f) + scale * acc;
 }
 
-EDGE_API int edge_flash_attn_fwd(const void* q, const void* k, const void* vt, void* o, float* lse, int B, int Hq,
-                                 int Hkv, int S, int s_pad, hipStream_t st) {
+// n_rows (nullable, [B] fp32): per-window count of scored rows (the last n_rows[b]+1 positions); query
+// blocks entirely before them are skipped (their O rows are left unwritten).  v2 only; v1 computes all.
+EDGE_API int edge_flash_attn_fwd(const void* q, const void* k, const void* vt, void* o, float* lse, const float* n_rows,
+                                 int B, int Hq, int Hkv, int S, int s_pad, hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
   if (Hq % Hkv || s_pad % 64 || s_pad < S) return (int)hipErrorInvalidValue;
   const int nqb = (S + 63) / 64;
@@ -454,10 +459,10 @@ EDGE_API int edge_flash_attn_fwd(const void* q, const void* k, const void* vt, v
     const dim3 grid(8 * maxcnt * G * nqb);
     if (g_attn_variant == 3)
       hipLaunchKernelGGL(flash_attn_fwd2_kernel<3>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
-                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, B, Hq, Hkv, S, s_pad);
+                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
     else
       hipLaunchKernelGGL(flash_attn_fwd2_kernel<2>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
-                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, B, Hq, Hkv, S, s_pad);
+                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(flash_attn_fwd_kernel, dim3(B * Hq * nqb), dim3(256), 4 * TILE, st, (const bf16_t*)q,

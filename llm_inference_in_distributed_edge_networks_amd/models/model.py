@@ -245,6 +245,47 @@ class DecoderLM:
             y = ops.linear(f, L["wproj"], L["bproj"], residual=y, out=y)
         return y, st
 
+    def layer_rows(self, i: int, x: torch.Tensor, B: int, S: int, rows: torch.Tensor,
+                   n_rows: torch.Tensor | None = None) -> torch.Tensor:
+        """Decoder layer ``i`` evaluated only at the flat row indices ``rows`` -> hidden [len(rows), H].
+
+        For the LAST layer only the scored rows reach the LM head (``row_nll``), so everything after the
+        K/V projection - attention queries, O-proj, MLP - is needed at those rows only (1/16 of the rows
+        with the reference's 512/32 window/stride).  K and V still come from every row.  ``n_rows`` lets
+        the attention kernel skip query blocks below the first scored row of each window."""
+        cfg, L = self.cfg, self.layers[i]
+        if L is None:
+            raise RuntimeError(f"layer {i} is not resident on this stage")
+        Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
+        rows = rows.to(self.device)
+        h2 = None
+        if self.fuse_norm:
+            ssq = getattr(x, "_edge_ssq", None)
+            if ssq is None:
+                ssq = ops.row_ssq(x)
+            q, k, vt = ops.qkv_rope(x, L["wqkv_n"], L["bqkv"], self.cos, self.sin, B, S, Hq, Hkv, D,
+                                    cfg.rotary_dim, self.q_scale, norm=(ssq, cfg.norm_eps))
+        else:
+            if cfg.arch == "qwen2":
+                h = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps)
+            else:
+                h, h2 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps)
+            q, k, vt = ops.qkv_rope(h, L["wqkv"], L["bqkv"], self.cos, self.sin, B, S, Hq, Hkv, D,
+                                    cfg.rotary_dim, self.q_scale)
+        o, _ = ops.attention(q, k, vt, S, n_rows=n_rows)
+        og, xg = o.index_select(0, rows), x.index_select(0, rows)
+        if self.fuse_norm:
+            y = ops.linear(og, L["wo"], residual=xg, want_ssq=True)
+            a = ops.linear(y, L["wgu_n"], act="swiglu_il", norm=(y._edge_ssq, cfg.norm_eps))
+            return ops.linear(a, L["wd"], residual=y, out=y)
+        if cfg.arch == "qwen2":
+            y = ops.linear(og, L["wo"], residual=xg)
+            a = ops.linear(ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps), L["wgu"], act="swiglu_il")
+            return ops.linear(a, L["wd"], residual=y, out=y)
+        y = ops.linear(og, L["wo"], L["bo"], residual=xg)
+        f = ops.linear(h2.index_select(0, rows), L["wfc"], L["bfc"], act="gelu")
+        return ops.linear(f, L["wproj"], L["bproj"], residual=y, out=y)
+
     def final_norm(self, x: torch.Tensor, rows: torch.Tensor | None = None) -> torch.Tensor:
         if self.cfg.arch == "qwen2":
             return ops.rmsnorm(x, self.w["norm_w"], self.cfg.norm_eps, rows)

@@ -207,7 +207,12 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     return q, k, vt
 
 
-def attention(q, k, vt, S, need_lse=False):
+def attention(q, k, vt, S, need_lse=False, n_rows=None):
+    """Causal GQA flash attention -> (o [B*S, Hq*64], lse [B,Hq,S] or None).
+
+    ``n_rows`` ([B] fp32, scored rows per window as in ``WindowBatch.n_rows``): only query rows
+    >= S-1-n_rows[b] are needed (last layer of the model); other 64-row blocks may be skipped and their
+    output rows are then undefined."""
     if not _gpu(q):
         return ref.attention(q, k, vt, S, need_lse)
     _check_bf16(q, k, vt)
@@ -215,7 +220,12 @@ def attention(q, k, vt, S, need_lse=False):
     Hkv = k.shape[1]
     o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)
     lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device) if need_lse else None
-    call("edge_flash_attn_fwd", ptr(q), ptr(k), ptr(vt), ptr(o), ptr(lse), B, Hq, Hkv, S, vt.shape[-1], stream())
+    nr = None
+    if n_rows is not None:
+        nr = n_rows.to(device=q.device, dtype=torch.float32).contiguous()
+        assert nr.numel() == B
+    call("edge_flash_attn_fwd", ptr(q), ptr(k), ptr(vt), ptr(o), ptr(lse), ptr(nr), B, Hq, Hkv, S, vt.shape[-1],
+         stream())
     return o, lse
 
 

@@ -37,7 +37,7 @@ _SIGS = {
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p],
     "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
-    "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_set_variant": [c_i],
     "edge_attn_lastrow": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_colsum": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],

@@ -72,6 +72,8 @@ class StageRunner:
         self.last = stage == plan.num_stages - 1
         self.boundary = None if self.last else self.layers[-1]
         self.stats = StageStats()
+        self.scored_rows_only = os.environ.get("EDGE_LAST_LAYER_ALL_ROWS", "0") in ("", "0")
+        self.rows_only = False
 
     def _tracker(self, S: int):
         if self.boundary is None or not self.bcfg.needs_importance(S):
@@ -90,8 +92,14 @@ class StageRunner:
         tr = self._tracker(S)
         if tr is not None and carry is not None:
             tr.load_carry(carry, self.layers[0])
+        self.rows_only = False
         for i in self.layers:
             need = tr.stats_for(i) if tr is not None else None
+            if self.last and i == m.cfg.num_layers - 1 and need is None and self.scored_rows_only:
+                # the model's last layer feeds only the LM head: evaluate it at the scored rows only
+                x = m.layer_rows(i, x, B, S, batch.rows, batch.n_rows)
+                self.rows_only = True
+                continue
             x, st = m.layer(i, x, B, S, stats=need)
             if need is not None:
                 tr.observe(i, st, S)
@@ -135,7 +143,10 @@ class StageRunner:
 
     def finish(self, x, batch: WindowBatch) -> torch.Tensor:
         """Per-window mean NLL [B] (last stage)."""
-        nll = self.model.row_nll(x, batch.rows, batch.targets)
+        rows = batch.rows
+        if self.rows_only:           # x already holds just the scored rows, in batch.rows order
+            rows = torch.arange(x.shape[0], device=x.device)
+        nll = self.model.row_nll(x, rows, batch.targets)
         return window_nll(nll, batch)
 
 

@@ -54,3 +54,20 @@ def test_gpu_ppl_close_to_fp32_cpu(cfg):
     pc = LocalPipeline(mc, plan, BoundaryConfig()).evaluate(batches(TOK, WINS, 4)).ppl()
     pg = LocalPipeline(mg, plan, BoundaryConfig()).evaluate(batches(TOK, WINS, 4)).ppl()
     assert abs(pg - pc) / pc < 0.02
+
+
+@pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX])
+def test_last_layer_scored_rows_only(cfg, monkeypatch):
+    """The model's last layer evaluated at the scored rows only (attention query blocks skipped, O-proj and
+    MLP on the gathered rows) gives the same per-window NLL as the full last layer."""
+    m = DecoderLM.random_init(cfg, 5, device="cuda", dtype=torch.bfloat16, std=0.05)
+    plan = PipelinePlan.from_split_layers(cfg.num_layers, [1])
+    bl = [b.to("cuda") for b in batches(TOK, WINS, 4)]
+    fast = LocalPipeline(m, plan, BoundaryConfig("mixed_int4_int8", 0.5, "last_row"), use_graphs=False)
+    monkeypatch.setenv("EDGE_LAST_LAYER_ALL_ROWS", "1")
+    full = LocalPipeline(m, plan, BoundaryConfig("mixed_int4_int8", 0.5, "last_row"), use_graphs=False)
+    assert fast.stages[-1].scored_rows_only and not full.stages[-1].scored_rows_only
+    for b in bl:
+        a, c = fast.run_batch(b), full.run_batch(b)
+        assert fast.stages[-1].rows_only
+        assert torch.allclose(a, c, rtol=1e-5, atol=1e-5), (a - c).abs().max()
