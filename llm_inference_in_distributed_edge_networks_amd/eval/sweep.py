@@ -61,6 +61,8 @@ class SweepEngine:
         self.forward_tokens = 0
         self.wire_bytes = torch.zeros(shape, dtype=torch.float64)
         self.tokens_done = 0
+        # the model's last layer only at the scored rows (see DecoderLM.layer_rows)
+        self.rows_only = os.environ.get("EDGE_LAST_LAYER_ALL_ROWS", "0") in ("", "0")
 
     # -------------------------------------------------------------- one batch
     def _prefix(self, batch: WindowBatch):
@@ -70,19 +72,25 @@ class SweepEngine:
                     for meth in self.methods}
         x = m.embed(batch.ids)
         saved = {}
+        last = m.cfg.num_layers - 1
+        rows = batch.rows
         for i in range(m.cfg.num_layers):
             kinds = set()
             for tr in trackers.values():
                 k = tr.stats_for(i)
                 if k:
                     kinds.add(k)
+            if i == last and not kinds and i not in self.layers and self.rows_only:
+                x = m.layer_rows(i, x, B, S, batch.rows, batch.n_rows)    # only the scored rows reach the head
+                rows = torch.arange(x.shape[0], device=x.device)
+                continue
             x, st = m.layer(i, x, B, S, stats=tuple(sorted(kinds)) or None)
             for tr in trackers.values():
                 if tr.stats_for(i):
                     tr.observe(i, st, S)
             if i in self.layers:
                 saved[i] = x
-        base = window_nll(m.row_nll(x, batch.rows, batch.targets), batch)
+        base = window_nll(m.row_nll(x, rows, batch.targets), batch)
         self.forward_tokens += B * S
         imp = {(meth, L): trackers[meth].importance(L) for meth in self.methods for L in self.layers}
         return base, saved, imp
@@ -126,12 +134,16 @@ class SweepEngine:
                         self.wire_bytes[mi, li, ri] += nbytes
                 V = len(chunk)
                 x = torch.cat(xs, 0)
-                for i in range(L + 1, m.cfg.num_layers):
-                    x, _ = m.layer(i, x, V * B, S)
-                # layer-token work in units of full-model forward tokens
-                self.forward_tokens += V * B * S * (m.cfg.num_layers - L - 1) / m.cfg.num_layers
                 off = (torch.arange(V, device=batch.rows.device) * (B * S)).repeat_interleave(batch.rows.numel())
                 rows = batch.rows.repeat(V) + off
+                for i in range(L + 1, m.cfg.num_layers):
+                    if i == m.cfg.num_layers - 1 and self.rows_only:
+                        x = m.layer_rows(i, x, V * B, S, rows, batch.n_rows.repeat(V))
+                        rows = torch.arange(x.shape[0], device=x.device)
+                    else:
+                        x, _ = m.layer(i, x, V * B, S)
+                # layer-token work in units of full-model forward tokens
+                self.forward_tokens += V * B * S * (m.cfg.num_layers - L - 1) / m.cfg.num_layers
                 nll = m.row_nll(x, rows, batch.targets.repeat(V))
                 wn = segment_mean(nll, batch.n_rows.to(nll.device).repeat(V)).view(V, B)
                 for vi, key in enumerate(chunk):
