@@ -56,6 +56,17 @@ using C256 = Cfg<256, 256, 2, 4>;   // 8 waves, 128 KiB LDS, 1 block/CU
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
+// T21-style store widening for the swapped 16x16 MFMA layout: lane group g = lane>>4 holds 4 consecutive
+// columns g*4.. of a 16-column group.  v_permlane16_swap exchanges rows 1,3 of `lo` with rows 0,2 of `hi`,
+// so for two groups (lo, hi) lanes g=0/2 end with 8 consecutive columns of `lo` and lanes g=1/3 with 8 of `hi`:
+// one 16-byte store per lane at column offset (g&1)*16 + (g>>1)*8 of the 32-column pair (was two 8-byte stores).
+__device__ __forceinline__ u32x4_t pair_swap16(u32x2_t lo, u32x2_t hi) {
+  const auto r0 = __builtin_amdgcn_permlane16_swap(lo[0], hi[0], false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(lo[1], hi[1], false, false);
+  return u32x4_t{r0[0], r1[0], r0[1], r1[1]};
+}
+__device__ __forceinline__ int pair_col(int g) { return (g & 1) * 16 + (g >> 1) * 8; }
+
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
@@ -208,26 +219,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
           }
         }
       }
-      if (m >= a.M) continue;
-      if (head < a.Hq) {
-        bf16_t* dst = a.qout + (((size_t)b * a.Hq + head) * a.S + pos) * 64;
+      if (!is_v) {  // q / k rows: 16-byte stores after the pair swap (head is wave-uniform, m per row)
+        const float sc = head < a.Hq ? a.q_scale : 1.f;
+        bf16_t* dst = head < a.Hq ? a.qout + (((size_t)b * a.Hq + head) * a.S + pos) * 64
+                                  : a.kout + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          u32x2_t w;
-          w[0] = pack_bf2(v[j][0] * a.q_scale, v[j][1] * a.q_scale);
-          w[1] = pack_bf2(v[j][2] * a.q_scale, v[j][3] * a.q_scale);
-          *(u32x2_t*)(dst + j * 16 + g * 4) = w;
-        }
-      } else if (!is_v) {
-        bf16_t* dst = a.kout + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          u32x2_t w;
-          w[0] = pack_bf2(v[j][0], v[j][1]);
-          w[1] = pack_bf2(v[j][2], v[j][3]);
-          *(u32x2_t*)(dst + j * 16 + g * 4) = w;
+        for (int q2 = 0; q2 < 2; ++q2) {
+          u32x2_t w0, w1;
+          w0[0] = pack_bf2(v[2 * q2][0] * sc, v[2 * q2][1] * sc);
+          w0[1] = pack_bf2(v[2 * q2][2] * sc, v[2 * q2][3] * sc);
+          w1[0] = pack_bf2(v[2 * q2 + 1][0] * sc, v[2 * q2 + 1][1] * sc);
+          w1[1] = pack_bf2(v[2 * q2 + 1][2] * sc, v[2 * q2 + 1][3] * sc);
+          const u32x4_t w = pair_swap16(w0, w1);
+          if (m < a.M) *(u32x4_t*)(dst + q2 * 32 + pair_col(g)) = w;
         }
       } else {
+        if (m >= a.M) continue;
         bf16_t* dst = a.vtout + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -243,23 +250,26 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
     const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
     const bool ok = m < a.M;
     if constexpr (EPI == EPI_SWIGLU) {
-      if (!ok) continue;
+      u32x2_t w[2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
-        const int n = nw / 2 + p * 16 + g * 4;
-        u32x2_t w;
         float o[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = silu(acc[i][2 * p][r]) * acc[i][2 * p + 1][r];
-        w[0] = pack_bf2(o[0], o[1]);
-        w[1] = pack_bf2(o[2], o[3]);
-        *(u32x2_t*)(a.C + (size_t)m * a.ldc + n) = w;
+        w[p][0] = pack_bf2(o[0], o[1]);
+        w[p][1] = pack_bf2(o[2], o[3]);
       }
+      const u32x4_t wv = pair_swap16(w[0], w[1]);   // every lane swaps (partners share m)
+      if (ok) *(u32x4_t*)(a.C + (size_t)m * a.ldc + nw / 2 + pair_col(g)) = wv;
     } else {
       float ss = 0.f;
-      if (ok) {
+      const int mr = ok ? m : a.M - 1;   // clamped row for loads; every lane takes part in the swaps
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+      for (int q2 = 0; q2 < 2; ++q2) {
+        u32x2_t w[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * q2 + h;
           const int n = nw + j * 16 + g * 4;
           float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU) {
@@ -271,16 +281,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
             for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
           }
           if constexpr (EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
-            const u32x2_t rw = *(const u32x2_t*)(a.resid + (size_t)m * a.ldr + n);
+            const u32x2_t rw = *(const u32x2_t*)(a.resid + (size_t)mr * a.ldr + n);
             o[0] += bf_lo(rw[0]); o[1] += bf_hi(rw[0]); o[2] += bf_lo(rw[1]); o[3] += bf_hi(rw[1]);
           }
-          u32x2_t w;
-          w[0] = pack_bf2(o[0], o[1]);
-          w[1] = pack_bf2(o[2], o[3]);
-          *(u32x2_t*)(a.C + (size_t)m * a.ldc + n) = w;
-          const float q0 = bf_lo(w[0]), q1 = bf_hi(w[0]), q2 = bf_lo(w[1]), q3 = bf_hi(w[1]);
-          ss += q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;  // of the stored (rounded) values
+          w[h][0] = pack_bf2(o[0], o[1]);
+          w[h][1] = pack_bf2(o[2], o[3]);
+          const float v0 = bf_lo(w[h][0]), v1 = bf_hi(w[h][0]), v2 = bf_lo(w[h][1]), v3 = bf_hi(w[h][1]);
+          ss += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;  // of the stored (rounded) values
         }
+        const u32x4_t wv = pair_swap16(w[0], w[1]);
+        if (ok) *(u32x4_t*)(a.C + (size_t)m * a.ldc + nw + q2 * 32 + pair_col(g)) = wv;
       }
       if (a.ssq_out) {  // uniform branch: every lane takes part in the shuffles
         ss += __shfl_xor(ss, 16, 64);
@@ -1003,6 +1013,8 @@ EDGE_API int edge_gemm(const void* A, const void* B, void* C, int M, int N, int 
   a.bias = (const bf16_t*)bias; a.resid = (const bf16_t*)resid; a.ldr = ldr;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
+  // the epilogues store 16-byte vectors (pair-swapped columns): 16-B aligned output rows
+  if (ldc % 8 || ((uintptr_t)C & 15) || (resid && ldr % 4)) return (int)hipErrorInvalidValue;
   // act: 0 none, 1 gelu, 2 swiglu-interleaved
   if (act == 2) return bias || resid ? (int)hipErrorInvalidValue : launch<EPI_SWIGLU>(a, st);
   if (act == 1) return resid || !bias ? (int)hipErrorInvalidValue : launch<EPI_BIAS_GELU>(a, st);
