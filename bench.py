@@ -36,6 +36,7 @@ from llm_inference_in_distributed_edge_networks_amd.models import build_model, g
 from llm_inference_in_distributed_edge_networks_amd.parallel import (BoundaryConfig, DistributedPipeline,  # noqa: E402
                                                                       Grid, LocalPipeline, PipelinePlan,
                                                                       init_distributed)
+from llm_inference_in_distributed_edge_networks_amd.parallel.dist import all_reduce_max_  # noqa: E402
 
 # Reference throughput on its own hardware: the Qwen2 sweep ran 1 eager + 100 split
 # forwards of 512 tokens per window at 16.03-16.35 s/window on a T4 = ~3.2k forward tokens/s.
@@ -130,7 +131,7 @@ def main():
     dt = time.perf_counter() - t0
     if env.is_dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        all_reduce_max_(t)
         dt = float(t.item())
 
     tok_per_step = grid.dp * a.microbatches * a.batch * a.max_length
@@ -142,7 +143,7 @@ def main():
         float(nll_acc[1]) > 0 else None
     if env.is_dist:
         t = torch.tensor([ppl or 0.0], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        all_reduce_max_(t)
         ppl = float(t.item())
     out = {
         "metric": "Qwen2-0.5B 2-stage split sliding-window PPL eval throughput (window tokens/sec)",

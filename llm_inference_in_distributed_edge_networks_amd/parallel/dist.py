@@ -49,18 +49,23 @@ def init_distributed(device: str = "auto", timeout_s: float = 600.0) -> DistEnv:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
+    # EDGE_SHARED_GPU=1: every rank on cuda:0 with a gloo process group and host-staged p2p - a rehearsal of
+    # the multi-GPU code path (CUDA tensors, graphs, pipeline protocol) on a one-GPU machine.  RCCL refuses
+    # two ranks on one device, so this is never the production path.
+    shared = use_cuda and os.environ.get("EDGE_SHARED_GPU", "0") not in ("", "0")
     if use_cuda:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        local_dev = 0 if shared else local
+        torch.cuda.set_device(local_dev)
+        dev = torch.device("cuda", local_dev)
     else:
         dev = torch.device("cpu")
     backend = "none"
     if world > 1:
-        backend = "nccl" if use_cuda else "gloo"
+        backend = "nccl" if (use_cuda and not shared) else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
             kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-            if use_cuda:
+            if backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(**kw)
     _ENV = DistEnv(rank, world, local, backend, dev)
@@ -87,10 +92,23 @@ def barrier() -> None:
         dist.barrier()
 
 
-def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
+def _all_reduce(t: torch.Tensor, op, group=None) -> torch.Tensor:
     if dist.is_available() and dist.is_initialized():
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        if t.is_cuda and dist.get_backend(group) == "gloo":   # EDGE_SHARED_GPU rehearsal: host-staged
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op, group=group)
     return t
+
+
+def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
+    return _all_reduce(t, dist.ReduceOp.SUM, group)
+
+
+def all_reduce_max_(t: torch.Tensor, group=None) -> torch.Tensor:
+    return _all_reduce(t, dist.ReduceOp.MAX, group)
 
 
 def all_reduce_max(x: float) -> float:

@@ -116,15 +116,45 @@ class RcclComm:
             self.h = None
 
 
+class _HostSend:
+    def __init__(self, work, host):
+        self.work, self.host = work, host     # keeps the staging buffer alive until the send completes
+
+    def wait(self):
+        self.work.wait()
+
+
+class _HostRecv:
+    def __init__(self, work, host, dst):
+        self.work, self.host, self.dst = work, host, dst
+
+    def wait(self):
+        self.work.wait()
+        self.dst.copy_(self.host)
+
+
 class TorchP2P:
-    """The default transport: torch.distributed isend/irecv (RCCL via ProcessGroupNCCL, or gloo)."""
+    """The default transport: torch.distributed isend/irecv (RCCL via ProcessGroupNCCL, or gloo).
+
+    CUDA tensors over a gloo group (the EDGE_SHARED_GPU rehearsal) are staged through host memory."""
+
+    @staticmethod
+    def _host_staged(t) -> bool:
+        import torch.distributed as dist
+        return t.is_cuda and dist.get_backend() == "gloo"
 
     def send(self, t, peer):
         import torch.distributed as dist
+        if self._host_staged(t):
+            h = t.to("cpu")
+            return _HostSend(dist.isend(h, peer), h)
         return dist.isend(t, peer)
 
     def recv(self, t, peer):
         import torch.distributed as dist
+        if self._host_staged(t):
+            h = torch.empty(t.shape, dtype=t.dtype)
+            return _HostRecv(dist.irecv(h, peer), h, t)
         return dist.irecv(t, peer)
 
 
