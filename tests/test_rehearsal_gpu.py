@@ -1,0 +1,44 @@
+"""Multi-process pipeline on one GPU (EDGE_SHARED_GPU=1: ranks share cuda:0 over gloo with host-staged
+p2p): the CUDA code path of the driver's N-GPU bench (graphs, streams, pipeline protocol) gives the same
+PPL as the single-process run.  RCCL itself needs one GPU per rank and is covered by test_rccl_gpu.py."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["bench.py", "--model", "tiny-qwen2", "--batch", "4", "--microbatches", "2", "--steps", "3", "--warmup", "1",
+        "--max-length", "256", "--split", "1"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(n, extra=(), env_extra=None):
+    env = dict(os.environ, EDGE_SHARED_GPU="1", **(env_extra or {}))
+    if n == 1:
+        cmd = [sys.executable] + ARGS + list(extra)
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+               "127.0.0.1", "--master-port", str(_port())] + ARGS + ["--gpus", str(n)] + list(extra)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def test_two_ranks_one_gpu_equals_single_process():
+    one = _run(1)
+    two = _run(2)
+    assert two["config"]["parallelism"] == "pp2xdp1"
+    assert two["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
+    chk = _run(2, ["--no-graphs"], {"EDGE_P2P_CHECK": "1"})
+    assert chk["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
