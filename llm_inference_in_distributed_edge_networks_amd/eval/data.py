@@ -45,8 +45,34 @@ def load_wikitext_tokens(hf_id: str, split: str = "test") -> torch.Tensor | None
     return enc.input_ids.to(torch.int64)
 
 
+def local_text_bytes(split: str = "eval", root: str = "") -> torch.Tensor:
+    """Byte ids [1, N] of real local text: the Python standard-library sources of this image, sorted by path;
+    every 10th file is the held-out ``eval`` split, the rest ``train``.  Used with the byte-level model
+    (``byte-qwen2``) for quality experiments, since no pretrained checkpoint or WikiText copy is reachable."""
+    import glob
+    import sys
+    root = root or os.path.join(sys.base_prefix, "lib", f"python{sys.version_info.major}.{sys.version_info.minor}")
+    files = sorted(glob.glob(os.path.join(root, "**", "*.py"), recursive=True))
+    files = [f for f in files if "site-packages" not in f and "dist-packages" not in f]
+    if not files:
+        raise FileNotFoundError(f"no python sources under {root}")
+    pick = [f for i, f in enumerate(files) if (i % 10 == 0) == (split == "eval")]
+    buf = bytearray()
+    for f in pick:
+        with open(f, "rb") as fh:
+            buf += fh.read()
+        buf += b"\n\n"
+    return torch.frombuffer(buf, dtype=torch.uint8).to(torch.int64).view(1, -1)
+
+
 def token_stream(dataset: str, hf_id: str, vocab_size: int, synthetic_tokens: int = 0, seed: int = 0):
     """Returns (ids [1, N], provenance)."""
+    if dataset in ("pysrc", "pysrc-eval", "pysrc-train"):
+        split = "train" if dataset == "pysrc-train" else "eval"
+        ids = local_text_bytes(split)
+        if synthetic_tokens:
+            ids = ids[:, :synthetic_tokens]
+        return ids, f"python-stdlib-bytes/{split}(n={ids.shape[1]})"
     if dataset == "wikitext":
         ids = load_wikitext_tokens(hf_id)
         if ids is not None:

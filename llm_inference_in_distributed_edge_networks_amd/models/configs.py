@@ -94,7 +94,15 @@ TINY_NEOX = ModelConfig(
     parallel_residual=True,
 )
 
-PRESETS = {c.name: c for c in (QWEN2_0_5B, PYTHIA_70M, TINY_QWEN2, TINY_NEOX)}
+# Byte-level Qwen2-architecture model for the quality experiments (tools/train_tiny_lm.py trains it on local
+# text; no pretrained checkpoint is reachable here).  Vocab 512 = 256 byte ids padded to the GEMM tiling.
+BYTE_QWEN2 = ModelConfig(
+    name="byte-qwen2", arch="qwen2", vocab_size=512, hidden_size=512, num_layers=8,
+    num_heads=8, num_kv_heads=2, head_dim=64, intermediate_size=1536, norm_eps=1e-6,
+    rope_theta=1e4, rotary_dim=64, max_position=2048, tie_embeddings=True,
+)
+
+PRESETS = {c.name: c for c in (QWEN2_0_5B, PYTHIA_70M, TINY_QWEN2, TINY_NEOX, BYTE_QWEN2)}
 ALIASES = {
     "Qwen/Qwen2-0.5B": "qwen2-0.5b", "qwen2": "qwen2-0.5b", "Qwen2-0.5B": "qwen2-0.5b",
     "EleutherAI/pythia-70m": "pythia-70m", "pythia": "pythia-70m", "Pythia-70M": "pythia-70m",

@@ -194,6 +194,47 @@ class DecoderLM:
             sd = torch.load(binf, map_location="cpu", weights_only=True)
         return cls.from_state_dict(cfg, sd, device, dtype, layers)
 
+    # ------------------------------------------------------------------ native checkpoints
+    _LAYER_KEYS = ("ln1_w", "ln1_b", "ln2_w", "ln2_b", "wqkv", "bqkv", "wo", "bo", "wgu", "wd", "wfc", "bfc",
+                   "wproj", "bproj")
+
+    def save_native(self, path: str) -> None:
+        """Weights in this framework's layouts (fused qkv, interleaved gate|up) as one safetensors file."""
+        from safetensors.torch import save_file
+        sd = {}
+        for k in ("embed", "norm_w", "norm_b"):
+            if self.w.get(k) is not None:
+                sd[k] = self.w[k]
+        if not self.cfg.tie_embeddings and self.w.get("head") is not None:
+            sd["head"] = self.w["head"]
+        for i, L in enumerate(self.layers):
+            if L is not None:
+                for k in self._LAYER_KEYS:
+                    if k in L:
+                        sd[f"layers.{i}.{k}"] = L[k]
+        save_file({k: v.detach().contiguous().cpu() for k, v in sd.items()}, path,
+                  metadata={"model": self.cfg.name})
+
+    @classmethod
+    def load_native(cls, cfg: ModelConfig, path: str, device="cpu", dtype=torch.float32, layers=None):
+        """Inverse of ``save_native`` (safetensors: nothing in the file is executed)."""
+        from safetensors.torch import load_file
+        sd = load_file(path)
+        keep = set(range(cfg.num_layers)) if layers is None else set(layers)
+
+        def fin(t):
+            return t.to(device=device, dtype=dtype).contiguous()
+        w: dict = {"layers": []}
+        for k in ("embed", "norm_w", "norm_b"):
+            w[k] = fin(sd[k]) if k in sd else None
+        for i in range(cfg.num_layers):
+            if i not in keep:
+                w["layers"].append(None)
+                continue
+            w["layers"].append({k: fin(sd[f"layers.{i}.{k}"]) for k in cls._LAYER_KEYS if f"layers.{i}.{k}" in sd})
+        w["head"] = w["embed"] if cfg.tie_embeddings else fin(sd["head"])
+        return cls(cfg, w, device, dtype)
+
     # ------------------------------------------------------------------ execution
     def embed(self, ids: torch.Tensor) -> torch.Tensor:
         """ids [B, S] -> hidden [B*S, H]."""
@@ -344,6 +385,8 @@ def build_model(cfg: ModelConfig, device="cpu", dtype=torch.float32, weights: st
 
     Returns (model, provenance string)."""
     path = weights or find_hf_snapshot(cfg.hf_id)
+    if path and os.path.isfile(path) and path.endswith(".safetensors"):
+        return DecoderLM.load_native(cfg, path, device, dtype, layers), f"native:{path}"
     if path and os.path.isdir(path):
         return DecoderLM.from_pretrained_dir(cfg, path, device, dtype, layers), f"hf:{path}"
     return (DecoderLM.random_init(cfg, seed, device, dtype, layers=layers, with_embed=with_embed,

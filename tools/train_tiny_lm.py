@@ -1,0 +1,106 @@
+"""Train the byte-level Qwen2-architecture model (``byte-qwen2``) on local text, for quality experiments.
+
+No pretrained checkpoint or WikiText copy is reachable from this machine, so PPL-vs-compression curves on
+random weights would be meaningless.  This trains a small model of the same architecture family as
+Qwen2-0.5B (GQA, RoPE, RMSNorm, SwiGLU, tied head) on the Python standard-library sources (byte tokens,
+``eval.data.local_text_bytes('train')``), then saves it with ``DecoderLM.save_native``; the experiment
+drivers load it with ``weights=<file>.safetensors``.
+
+The training forward is plain PyTorch autograd (bf16 autocast, SDPA) over the framework's own weight
+layout (fused qkv, interleaved gate|up), so the checkpoint is exactly what the HIP inference path runs.
+"""
+import argparse
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from llm_inference_in_distributed_edge_networks_amd.eval.data import local_text_bytes  # noqa: E402
+from llm_inference_in_distributed_edge_networks_amd.models import DecoderLM, get_config  # noqa: E402
+from llm_inference_in_distributed_edge_networks_amd.ops import reference as R  # noqa: E402
+
+
+def forward(w, cfg, ids, cos, sin):
+    B, S = ids.shape
+    Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
+    x = w["embed"][ids]
+    c, s = cos[:S], sin[:S]
+    for L in w["layers"]:
+        h = F.rms_norm(x, (cfg.hidden_size,), L["ln1_w"], cfg.norm_eps)
+        y = (h @ L["wqkv"].t() + L["bqkv"]).view(B, S, Hq + 2 * Hkv, D).transpose(1, 2)
+        q, k, v = y[:, :Hq], y[:, Hq:Hq + Hkv], y[:, Hq + Hkv:]
+        q, k = R.apply_rope(q.float(), c, s, cfg.rotary_dim).to(x.dtype), R.apply_rope(k.float(), c, s,
+                                                                                      cfg.rotary_dim).to(x.dtype)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
+        x = x + o.transpose(1, 2).reshape(B, S, Hq * D) @ L["wo"].t()
+        h = F.rms_norm(x, (cfg.hidden_size,), L["ln2_w"], cfg.norm_eps)
+        g, u = R.deinterleave_gate_up((h @ L["wgu"].t()).view(B * S, -1))
+        x = x + (F.silu(g) * u).view(B, S, -1) @ L["wd"].t()
+    x = F.rms_norm(x, (cfg.hidden_size,), w["norm_w"], cfg.norm_eps)
+    return x @ w["embed"].t()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="byte-qwen2")
+    ap.add_argument("--out", default="gpurun_out/byte_qwen2.safetensors")
+    ap.add_argument("--minutes", type=float, default=4.0)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--lr", type=float, default=2e-3)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+    torch.manual_seed(a.seed)
+    dev = "cuda"
+    cfg = get_config(a.model)
+    m = DecoderLM.random_init(cfg, a.seed, device=dev, dtype=torch.float32)
+    params = [m.w["embed"], m.w["norm_w"]] + [t for L in m.layers for t in L.values()]
+    for p in params:
+        p.requires_grad_(True)
+    w = {"embed": m.w["embed"], "norm_w": m.w["norm_w"], "layers": m.layers}
+    data = local_text_bytes("train").view(-1).to(dev)
+    held = local_text_bytes("eval").view(-1)[: 64 * (a.seq + 1)].view(64, a.seq + 1).to(dev)
+    opt = torch.optim.AdamW(params, lr=a.lr, betas=(0.9, 0.95), weight_decay=0.1)
+    cos, sin = m.cos, m.sin
+    t0, step, budget = time.time(), 0, a.minutes * 60
+    g = torch.Generator(device=dev).manual_seed(a.seed)
+    last_print = 0.0
+    while True:
+        el = time.time() - t0
+        if el > budget:
+            break
+        frac = el / budget
+        lr = a.lr * min(1.0, (step + 1) / 200) * (0.1 + 0.9 * 0.5 * (1 + math.cos(math.pi * frac)))
+        for grp in opt.param_groups:
+            grp["lr"] = lr
+        idx = torch.randint(0, data.numel() - a.seq - 1, (a.batch,), device=dev, generator=g)
+        chunk = torch.stack([data[i:i + a.seq + 1] for i in idx.tolist()])
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = forward(w, cfg, chunk[:, :-1], cos, sin)
+        loss = F.cross_entropy(logits.float().view(-1, cfg.vocab_size), chunk[:, 1:].reshape(-1))
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        step += 1
+        if el - last_print > 20:
+            last_print = el
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+                hl = F.cross_entropy(forward(w, cfg, held[:, :-1], cos, sin).float().view(-1, cfg.vocab_size),
+                                     held[:, 1:].reshape(-1))
+            print(f"step {step} t={el:.0f}s lr={lr:.2e} train {loss.item():.3f} held-out {hl.item():.3f} nats/byte "
+                  f"({hl.item() / math.log(2):.3f} bits/byte)", flush=True)
+    for p in params:
+        p.requires_grad_(False)
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    DecoderLM(cfg, {"embed": m.w["embed"], "norm_w": m.w["norm_w"], "head": m.w["embed"], "layers": m.layers},
+              "cpu", torch.float32).save_native(a.out)
+    print(f"saved {a.out} after {step} steps", flush=True)
+
+
+if __name__ == "__main__":
+    main()
