@@ -66,6 +66,8 @@ def main():
     held = local_text_bytes("eval").view(-1)[: 64 * (a.seq + 1)].view(64, a.seq + 1).to(dev)
     opt = torch.optim.AdamW(params, lr=a.lr, betas=(0.9, 0.95), weight_decay=0.1)
     cos, sin = m.cos, m.sin
+    print(f"training {cfg.name}: {sum(p.numel() for p in params) / 1e6:.1f}M params, {data.numel() / 1e6:.1f}M train "
+          f"bytes, batch {a.batch}x{a.seq}, {a.minutes} min", flush=True)
     t0, step, budget = time.time(), 0, a.minutes * 60
     g = torch.Generator(device=dev).manual_seed(a.seed)
     last_print = 0.0
