@@ -50,7 +50,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--model", default="qwen2-0.5b")
     p.add_argument("--batch", type=int, default=64, help="windows per micro-batch")
-    p.add_argument("--microbatches", type=int, default=2, help="micro-batches per step per replica")
+    p.add_argument("--microbatches", type=int, default=0,
+                   help="micro-batches per step per replica (default 2 x pipeline depth: every GPU does the "
+                        "work of 2 full-model micro-batches per step at any N, i.e. weak scaling)")
     p.add_argument("--max-length", type=int, default=512)
     p.add_argument("--stride", type=int, default=32)
     p.add_argument("--split", type=int, default=11, help="last layer of stage 0 (reference layer_of_interest)")
@@ -73,6 +75,8 @@ def main():
     world = env.world_size
     pp = 2 if world >= 2 else 1
     grid = Grid(world, pp)
+    if a.microbatches <= 0:
+        a.microbatches = 2 * pp
     plan2 = PipelinePlan.from_split_layers(cfg.num_layers, [a.split])
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     if pp == 1:
