@@ -29,7 +29,7 @@ METHODS = ["regular_importance", "weighted_importance", "last_row", "aggregate_t
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="byte-qwen2")
-    ap.add_argument("--weights", default="gpurun_out/byte_qwen2.safetensors")
+    ap.add_argument("--weights", default="/tmp/byte_qwen2.safetensors")
     ap.add_argument("--windows", type=int, default=1024)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--layers", default="1,3,5,6")

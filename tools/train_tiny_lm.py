@@ -47,7 +47,7 @@ def forward(w, cfg, ids, cos, sin):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="byte-qwen2")
-    ap.add_argument("--out", default="gpurun_out/byte_qwen2.safetensors")
+    ap.add_argument("--out", default="/tmp/byte_qwen2.safetensors")
     ap.add_argument("--minutes", type=float, default=4.0)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--seq", type=int, default=512)
@@ -71,6 +71,7 @@ def main():
     t0, step, budget = time.time(), 0, a.minutes * 60
     g = torch.Generator(device=dev).manual_seed(a.seed)
     last_print = 0.0
+    best = (float("inf"), 0, None)  # held-out loss, step, CPU snapshot (early stopping: the corpus is small)
     while True:
         el = time.time() - t0
         if el > budget:
@@ -89,15 +90,21 @@ def main():
         torch.nn.utils.clip_grad_norm_(params, 1.0)
         opt.step()
         step += 1
-        if el - last_print > 20:
+        if el - last_print > 15:
             last_print = el
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
                 hl = F.cross_entropy(forward(w, cfg, held[:, :-1], cos, sin).float().view(-1, cfg.vocab_size),
                                      held[:, 1:].reshape(-1))
+            if hl.item() < best[0]:
+                best = (hl.item(), step, [p.detach().to("cpu", copy=True) for p in params])
             print(f"step {step} t={el:.0f}s lr={lr:.2e} train {loss.item():.3f} held-out {hl.item():.3f} nats/byte "
                   f"({hl.item() / math.log(2):.3f} bits/byte)", flush=True)
     for p in params:
         p.requires_grad_(False)
+    if best[2] is not None:
+        for p, b in zip(params, best[2]):
+            p.copy_(b.to(p.device))
+        print(f"keeping the best held-out checkpoint: step {best[1]}, {best[0]:.3f} nats/byte", flush=True)
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     DecoderLM(cfg, {"embed": m.w["embed"], "norm_w": m.w["norm_w"], "head": m.w["embed"], "layers": m.layers},
               "cpu", torch.float32).save_native(a.out)
