@@ -887,7 +887,229 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
   if (wm == 0) __builtin_amdgcn_s_barrier();  // group 0 matches group 1's extra barrier
 }
 
-static int g_tile_override = 0;  // 0 auto, 128 or 256 (tests / tuning)
+// ---- 256x224 persistent GEMM for N = 896 (Qwen2 hidden size: O-proj and MLP down, both residual epilogues) ----
+// 896 = 3.5 x 256: the 256x256 tile computes a half-empty last column tile (1/8 of all MFMAs wasted, its
+// waves' SIMDs idle), and no power-of-two tile both avoids that and gives a tile count that divides the 256
+// CUs.  896 = 4 x 224 does: 8 waves as 4 (M) x 2 (N), each a 64x112 slab of 4x7 16x16x32 MFMA accumulators,
+// 128 x 4 = 512 tiles for M = 32768 (exactly 2 per CU).  Per 32-wide K half a wave reads 4 A + 7 B fragments
+// (11 ds_read_b128) for 28 MFMAs (the 256x256 loop: 8 for 16).  Same LDS image as the 128/256 tiles (rows of
+// 128 B, chunk c of row r at c ^ ((r >> 1) & 7)); the B tile is 28 1-KiB glds blocks, so waves 0-3 issue
+// one more than waves 4-7.  K loop as the register-pipelined C256 path: two sub-steps per K-tile with
+// X/Y fragment sets, one barrier per K-tile, the next tile's first K-tile staged under the epilogue.
+// Row sum-of-squares partials (fused RMSNorm producer) are per 112-column wave slab: ssq_out[m, N / 112].
+namespace w7 {
+constexpr int BM = 256, BN = 224, NW = 8, NT = 512, MI = 4, NJ = 7;
+constexpr int A_BYTES = BM * BK * 2, STAGE = A_BYTES + BN * BK * 2, LDS = 2 * STAGE;  // 60 KiB stages
+constexpr int A_INSTR = BM / 8 / NW, B_BLOCKS = BN / 8, B_INSTR = (B_BLOCKS + NW - 1) / NW;
+}  // namespace w7
+
+template <int EPI>
+__device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7::MI][w7::NJ], int m0, int n0,
+                                            int lane, int wm, int wn) {
+  const int g = lane >> 4;
+  const int nw = n0 + wn * 112;
+  const int P = a.N / 112;
+#pragma unroll
+  for (int i = 0; i < w7::MI; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    const bool ok = m < a.M;
+    const int mr = ok ? m : a.M - 1;  // clamped row for loads; every lane takes part in the swaps
+    const float rs = a.rscale ? a.rscale[mr] : 1.f;
+    float ss = 0.f;
+    u32x2_t w[w7::NJ];
+#pragma unroll
+    for (int j = 0; j < w7::NJ; ++j) {
+      const int n = nw + j * 16 + g * 4;
+      float o[4] = {acc[i][j][0] * rs, acc[i][j][1] * rs, acc[i][j][2] * rs, acc[i][j][3] * rs};
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID) {
+        const u32x2_t bw = *(const u32x2_t*)(a.bias + n);
+        o[0] += bf_lo(bw[0]); o[1] += bf_hi(bw[0]); o[2] += bf_lo(bw[1]); o[3] += bf_hi(bw[1]);
+      }
+      if constexpr (EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
+        const u32x2_t rw = *(const u32x2_t*)(a.resid + (size_t)mr * a.ldr + n);
+        o[0] += bf_lo(rw[0]); o[1] += bf_hi(rw[0]); o[2] += bf_lo(rw[1]); o[3] += bf_hi(rw[1]);
+      }
+      w[j][0] = pack_bf2(o[0], o[1]);
+      w[j][1] = pack_bf2(o[2], o[3]);
+      const float v0 = bf_lo(w[j][0]), v1 = bf_hi(w[j][0]), v2 = bf_lo(w[j][1]), v3 = bf_hi(w[j][1]);
+      ss += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;  // of the stored (rounded) values
+    }
+    bf16_t* row = a.C + (size_t)mr * a.ldc + nw;
+#pragma unroll
+    for (int q2 = 0; q2 < 3; ++q2) {  // column groups (0,1) (2,3) (4,5): 16-byte stores after the pair swap
+      const u32x4_t wv = pair_swap16(w[2 * q2], w[2 * q2 + 1]);
+      if (ok) *(u32x4_t*)(row + q2 * 32 + pair_col(g)) = wv;
+    }
+    if (ok) *(u32x2_t*)(row + 96 + g * 4) = w[6];  // group 6: 8-byte store
+    if (a.ssq_out) {  // uniform branch: every lane takes part in the shuffles
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (ok && g == 0) a.ssq_out[(size_t)m * P + nw / 112] = ss;
+    }
+  }
+}
+
+// Staging offsets (elements, 32-bit: the operands are < 2^31 elements) of this wave's glds blocks; instruction
+// i writes LDS rows [8 (i NW + w), +8) of the tile, as stage_ptrs.
+template <int NI>
+__device__ __forceinline__ void w7_offsets(int ld, int row0, int row_max, int wave, int lane, uint32_t (&o)[NI]) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int r = (i * w7::NW + wave) * 8 + (lane >> 3);
+    int gr = row0 + r;
+    gr = gr < row_max ? gr : row_max - 1;
+    o[i] = (uint32_t)gr * (uint32_t)ld + (uint32_t)(((lane & 7) ^ swz(r)) * 8);
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
+  using namespace w7;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tm = (a.M + BM - 1) / BM, tn = a.N / BN;
+  const int ntiles = tm * tn;
+  const TileWalk walk = tile_walk(blockIdx.x, gridDim.x, ntiles, a.walk);
+  int tile = walk.first;
+  if (tile >= walk.end) return;
+
+  f32x4_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  uint32_t oa[A_INSTR], ob[B_INSTR];
+  const bool b_last = wave < B_BLOCKS - (B_INSTR - 1) * NW;  // wave-uniform: issues the B tile's last blocks
+  const int sw = ((lane & 15) >> 1) & 7;
+  int abase[2], bbase[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = ks * 4 + (lane >> 4);
+    abase[ks] = (wm * 64 + (lane & 15)) * 128 + ((c ^ sw) << 4);
+    bbase[ks] = A_BYTES + (wn * 112 + (lane & 15)) * 128 + ((c ^ sw) << 4);
+  }
+  // Four sub-steps per K-tile, s = (ks, h): A fragments of K half ks (4) x B column groups h = 0: 0-3 (16
+  // MFMAs), h = 1: 4-6 (12 MFMAs).  Register sets: AX (ks 0) / AY (ks 1), BX (groups 0-3) / BY (4-6): the reads
+  // of sub-step s + 1 are in flight under the MFMAs of s, with 64 fragment VGPRs (a full X/Y double buffer of
+  // 11 fragments would need 88 and spill at the 256-register budget of 2 waves per SIMD).
+  bf16x8_t AX[MI], AY[MI], BX[4], BY[4];
+  auto rdA = [&](bf16x8_t(&F)[MI], const char* buf, int ks) {
+    const uint32_t va = lds_addr(buf) + abase[ks];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) DS_READ_B128(F[i], va, i * 2048);
+  };
+  auto rdB = [&](bf16x8_t(&F)[4], const char* buf, int ks, int h) {
+    const uint32_t vb = lds_addr(buf) + bbase[ks];
+    if (h == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) DS_READ_B128(F[j], vb, j * 2048);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) DS_READ_B128(F[j], vb, (4 + j) * 2048);
+    }
+  };
+  auto mma = [&](const bf16x8_t(&FA)[MI], const bf16x8_t(&FB)[4], int h) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (h == 1 && j == 3) continue;
+        acc[i][h * 4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[i][h * 4 + j], 0, 0, 0);
+      }
+  };
+  auto stage = [&](int k0, char* buf) {
+    const bf16_t* A = a.A + k0;
+    const bf16_t* B = a.B + k0;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) glds16(A + oa[i], buf + (i * NW + wave) * 1024);
+#pragma unroll
+    for (int i = 0; i < B_INSTR - 1; ++i) glds16(B + ob[i], buf + A_BYTES + (i * NW + wave) * 1024);
+    if (b_last) glds16(B + ob[B_INSTR - 1], buf + A_BYTES + ((B_INSTR - 1) * NW + wave) * 1024);
+  };
+  const int nk = a.K / BK;  // >= 2 (checked by the launcher)
+
+  // The staging stream runs two K-tiles ahead through all of this workgroup's tiles: K-tile q + 2 is issued
+  // right after the barrier that ends K-tile q, into the buffer q just released, and waited (vmcnt(0)) at the
+  // barrier ending q + 1 - a whole K-tile of MFMAs for the DMA to land.
+  int m0, n0;
+  tile_origin(tile, a.M, a.N, BM, BN, m0, n0);
+  w7_offsets<A_INSTR>(a.lda, m0, a.M, wave, lane, oa);
+  w7_offsets<B_INSTR>(a.ldb, n0, a.N, wave, lane, ob);
+  stage(0, smem);
+  stage(BK, smem + STAGE);
+  wait_vmcnt0();
+  __syncthreads();
+  rdA(AX, smem, 0);
+  rdB(BX, smem, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int g = 0;  // K-tiles consumed by this workgroup (LDS buffer parity)
+  while (true) {
+    const int next = tile + walk.stride;
+    const bool has_next = next < walk.end;
+    int nm0 = 0, nn0 = 0;
+    if (has_next) tile_origin(next, a.M, a.N, BM, BN, nm0, nn0);
+    for (int t = 0; t < nk; ++t, ++g) {
+      char* cur = smem + (g & 1) * STAGE;
+      const char* nxt = smem + ((g + 1) & 1) * STAGE;
+      // s0 (ks 0, groups 0-3): AX, BX
+      rdB(BY, cur, 0, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(AX, BX, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      // s1 (ks 0, groups 4-6): AX, BY
+      rdA(AY, cur, 1);
+      rdB(BX, cur, 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(AX, BY, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      // s2 (ks 1, groups 0-3): AY, BX
+      rdB(BY, cur, 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(AY, BX, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      // s3 (ks 1, groups 4-6): AY, BY.  Barrier (K-tile q + 1 landed and visible; every wave's reads of q
+      // retired), read s0 of q + 1, stage q + 2 into q's buffer
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + 1 < nk || has_next) {
+        rdA(AX, nxt, 0);
+        rdB(BX, nxt, 0, 0);
+      }
+      if (t + 2 < nk) {
+        stage((t + 2) * BK, cur);
+      } else if (has_next) {
+        if (t + 2 == nk) {
+          w7_offsets<A_INSTR>(a.lda, nm0, a.M, wave, lane, oa);
+          w7_offsets<B_INSTR>(a.ldb, nn0, a.N, wave, lane, ob);
+        }
+        stage((t + 2 - nk) * BK, cur);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma(AY, BY, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    w7_epilogue<EPI>(a, acc, m0, n0, lane, wm, wn);
+    if (!has_next) break;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next tile's s0 sets (asm reads, counted by hand)
+    tile = next;
+    m0 = nm0;
+    n0 = nn0;
+  }
+}
+
+static int g_tile_override = 0;  // 0 auto, 128, 224 or 256 (tests / tuning)
 static int g_walk = 1;           // persistent tile walk (TileWalk): 1 chunked per XCD, 0 strided
 // 256x256 main loop: 0 = K-tile double buffer, compiler-waited fragment loads; 1 = same with hand-counted asm
 // reads; 2 = K-half ring (gemm_ring_kernel); 3 = ring with s_setprio around the MFMA clusters; 4 = ring with
@@ -948,10 +1170,37 @@ static int launch_pp(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+static int g_w7 = 1;  // 256x224 tiles for N % 224 == 0 shapes that 256 does not divide (N = 896)
+
+// The 256x224 kernel takes the plain / bias / residual epilogues of N % 224 == 0 shapes that 256 does not
+// divide, when 256-row tiles fill the chip; tests force it at small M with tile override 224.
+static bool use_w7(int M, int N, int K, int epi) {
+  if (!(epi == EPI_NONE || epi == EPI_BIAS || epi == EPI_RESID || epi == EPI_BIAS_RESID)) return false;
+  if (N % 224 || N % 256 == 0 || K < 2 * BK) return false;
+  if (g_tile_override) return g_tile_override == 224;
+  return g_w7 && (long long)((M + 255) / 256) * (N / 224) >= 256;
+}
+
+template <int EPI>
+static int launch_w7(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + w7::BM - 1) / w7::BM) * (a.N / w7::BN);
+  const int grid = std::min(tiles, num_cus());
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_w7_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, w7::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_w7_kernel<EPI>), dim3(grid), dim3(w7::NT), w7::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
 template <int EPI, int RH = 0>
 static int launch(const GemmArgs& args, hipStream_t st) {
   GemmArgs a = args;
   a.walk = g_walk;
+  if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
+    if (use_w7(a.M, a.N, a.K, EPI)) return launch_w7<EPI>(a, st);
+  }
   // 256x256 persistent tiles when the shape can fill the chip with them (halves L2->LDS traffic per
   // FLOP), 128x128 otherwise (N not a multiple of 256, or too few 256-row panels).  The QKV/RoPE and
   // LSE epilogues stay on 128x128 (register budget; their N is never a multiple of 256 in practice).
@@ -988,6 +1237,19 @@ EDGE_API int edge_gemm_set_tile(int t) {
 EDGE_API int edge_gemm_set_walk(int w) {
   g_walk = w;
   return 0;
+}
+
+EDGE_API int edge_gemm_set_w7(int on) {
+  g_w7 = on;
+  return 0;
+}
+
+// Number of row sum-of-squares partials edge_gemm writes for this shape (ssq_out is [M, parts]): one per
+// 64-column slab, or one per 112-column wave slab on the 256x224 kernel.  act/bias/resid as edge_gemm.
+EDGE_API int edge_gemm_ssq_parts(int M, int N, int K, int act, int has_bias, int has_resid) {
+  if (act) return N / 64;
+  const int epi = has_bias ? (has_resid ? EPI_BIAS_RESID : EPI_BIAS) : (has_resid ? EPI_RESID : EPI_NONE);
+  return use_w7(M, N, K, epi) ? N / 112 : N / 64;
 }
 
 EDGE_API int edge_gemm_set_variant(int v) {

@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 
 from . import reference as ref
-from ._native import call, ptr, stream
+from ._native import call, lib, ptr, stream
 
 IL_BLOCK = ref.IL_BLOCK
 s_pad = ref.s_pad
@@ -86,7 +86,8 @@ def layernorm_dual(x, w1, b1, w2, b2, eps):
 
 
 def set_gemm_tile(tile: int) -> None:
-    """Force the GEMM block tile (128 or 256; 0 = automatic by shape).  Tuning / tests only."""
+    """Force the GEMM block tile (128, 224 or 256; 0 = automatic by shape).  Tuning / tests only.  224 is the
+    256x224 kernel for N % 224 == 0 shapes that 256 does not divide (the Qwen2 hidden size 896)."""
     call("edge_gemm_set_tile", int(tile))
 
 
@@ -98,6 +99,17 @@ def set_gemm_variant(v: int) -> None:
     1 the same with hand-counted asm reads, 2 the K-half ring, 3 the ring with s_setprio, 4 the ring with
     wave-group ping-pong."""
     call("edge_gemm_set_variant", int(v))
+
+
+def set_gemm_w7(on: bool) -> None:
+    """Automatic use of the 256x224 tiles for N = 896-like shapes (default on; A/B only)."""
+    call("edge_gemm_set_w7", int(bool(on)))
+
+
+def gemm_ssq_parts(M: int, N: int, K: int, act=None, bias=False, residual=False) -> int:
+    """Row sum-of-squares partials ``linear(..., want_ssq=True)`` produces for this shape: N/64 (64-column
+    slabs), or N/112 (wave slabs) when the 256x224 kernel runs it."""
+    return int(lib().edge_gemm_ssq_parts(M, N, K, _ACT[act], int(bool(bias)), int(bool(residual))))
 
 
 def set_gemm_walk(chunked: bool) -> None:
@@ -146,7 +158,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None,
     """``act(rowscale * (x @ w.T) + bias) + residual`` on MFMA (``residual`` may alias ``out``).
 
     ``norm=(ssq, eps)``: fused RMSNorm of ``x`` - rows are scaled by rsqrt(sum(ssq)/K + eps) (``w`` must
-    carry the folded norm weight).  ``want_ssq``: the output's per-row 64-column sum-of-squares partials
+    carry the folded norm weight).  ``want_ssq``: the output's per-row sum-of-squares partials (64- or 112-column slabs)
     are produced in the epilogue and attached as ``out._edge_ssq`` (for the next fused norm)."""
     if not _gpu(x):
         y = ref.linear(x, w, None, None, None, out_dtype=torch.float32) if norm is not None else None
@@ -178,7 +190,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None,
     if out is None:
         out = torch.empty(M, No, dtype=x.dtype, device=x.device)
     rs = None if norm is None else _norm_scale(norm, K)
-    ssq_out = torch.empty(M, No // 64, dtype=torch.float32, device=x.device) if want_ssq else None
+    ssq_out = torch.empty(M, gemm_ssq_parts(M, N, K, act, bias is not None, residual is not None),
+                          dtype=torch.float32, device=x.device) if want_ssq else None
     call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), _ACT[act], ptr(rs), ptr(ssq_out), stream())
     if want_ssq:

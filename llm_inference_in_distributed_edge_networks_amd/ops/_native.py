@@ -34,6 +34,8 @@ _SIGS = {
     "edge_gemm_set_tile": [c_i],
     "edge_gemm_set_variant": [c_i],
     "edge_gemm_set_walk": [c_i],
+    "edge_gemm_set_w7": [c_i],
+    "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p],
     "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
@@ -83,6 +85,8 @@ def lib():
         v = os.environ.get("EDGE_GEMM_VARIANT")  # A/B of the 256x256 main loop (see ops.set_gemm_variant)
         if v:
             L.edge_gemm_set_variant(int(v))
+        if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # A/B: N = 896 GEMMs back on the 256x256 tiles
+            L.edge_gemm_set_w7(0)
     return _lib
 
 

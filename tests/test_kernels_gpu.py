@@ -84,6 +84,39 @@ def test_gemm_persistent_multi_tile(M, N, K, epi, tile):
         ops.set_gemm_config("0")
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 896, 896), (256 * 70 + 37, 896, 128), (1000, 896, 4864), (64, 896, 192),
+                                   (300, 2688, 256)])
+@pytest.mark.parametrize("epi", ["none", "bias", "resid", "bias_resid"])
+def test_gemm_w7(M, N, K, epi):
+    """256x224 tiles (N % 224 == 0, N % 256 != 0): partial last row tile, the shortest K loop (two K-tiles, the
+    staging stream crosses tile boundaries every K-tile), more tiles than CUs, several column tiles."""
+    ops.set_gemm_config("224")
+    try:
+        _gemm_case(M, N, K, epi)
+    finally:
+        ops.set_gemm_config("0")
+
+
+def test_gemm_w7_auto_selected_and_inplace():
+    """The production shape (M = 32768 rows, N = 896) picks the 256x224 kernel by itself (112-column ssq
+    partials), in place on the residual stream, with the fused-norm row scale."""
+    M, K, N = 32768, 896, 896
+    assert ops.gemm_ssq_parts(M, N, K, residual=True) == N // 112
+    assert ops.gemm_ssq_parts(M, 1024, K, residual=True) == 1024 // 64
+    x = rnd(M, K, seed=40)
+    nw = rnd(K, s=0.1, seed=41) + 1
+    w = rnd(N, K, s=1 / math.sqrt(K), seed=42)
+    r = rnd(M, N, seed=43)
+    ssq = R.row_ssq(x)
+    rd = r.to(DEV)
+    y = ops.linear(x.to(DEV), R.fold_norm_weight(w, nw).to(DEV), residual=rd, out=rd, norm=(ssq.to(DEV), 1e-6),
+                   want_ssq=True)
+    ref = R.linear(R.rmsnorm(x, nw, 1e-6), w, residual=r, out_dtype=torch.float32)
+    close(y, ref, atol=5e-2, rtol=3e-2)
+    assert y._edge_ssq.shape == (M, N // 112)
+    close(y._edge_ssq.sum(1), R.row_ssq(y.cpu()).sum(1), atol=1e-2, rtol=1e-4)
+
+
 def _gemm_case(M, N, K, epi):
     x = rnd(M, K, seed=10)
     w = rnd(N, K, s=1 / math.sqrt(K), seed=11)
@@ -243,7 +276,7 @@ def test_row_ssq(H):
     close(s, R.row_ssq(x), atol=1e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("tile", ["128", "256", "256r", "256s", "256s5"])
+@pytest.mark.parametrize("tile", ["128", "224", "256", "256r", "256s", "256s5"])
 @pytest.mark.parametrize("act", [None, "swiglu_il"])
 def test_gemm_fused_norm_and_ssq_out(tile, act):
     M, K, N = 700, 896, 1024
@@ -262,8 +295,14 @@ def test_gemm_fused_norm_and_ssq_out(tile, act):
         ops.set_gemm_config("0")
     ref = R.linear(R.rmsnorm(x, nw, 1e-6), w, act=act, out_dtype=torch.float32)
     close(y, ref, atol=4e-2, rtol=3e-2)
-    # producer side: residual GEMM emits the ssq partials of its stored output
-    close(y2._edge_ssq, R.row_ssq(y2.cpu()), atol=1e-2, rtol=1e-4)
+    # producer side: residual GEMM emits the ssq partials of its stored output (64- or 112-column slabs)
+    ref_ssq = R.row_ssq(y2.cpu())
+    if y2._edge_ssq.shape == ref_ssq.shape:
+        close(y2._edge_ssq, ref_ssq, atol=1e-2, rtol=1e-4)
+    else:
+        assert tile == "224" and y2._edge_ssq.shape == (M, 896 // 112)
+        ref_ssq = y2.cpu().float().pow(2).reshape(M, 8, 112).sum(-1)
+        close(y2._edge_ssq, ref_ssq, atol=1e-2, rtol=1e-4)
 
 
 def test_qkv_rope_fused_norm():
