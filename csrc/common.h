@@ -23,6 +23,14 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// silu(x) = x / (1 + e^-x) on the hardware transcendentals (v_exp_f32, v_rcp_f32, ~1 ulp): a plain '/' compiles
+// to the IEEE division sequence (2 v_div_scale + v_div_fmas + v_div_fixup + v_rcp + FMAs), which made the
+// SwiGLU epilogue of the gate/up GEMM cost ~20 VALU per output.  Saturates correctly: e^-x = inf -> 0.
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float fast_silu(float x) { return x * fast_sigmoid(x); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -68,7 +68,7 @@ __device__ __forceinline__ u32x4_t pair_swap16(u32x2_t lo, u32x2_t hi) {
 __device__ __forceinline__ int pair_col(int g) { return (g & 1) * 16 + (g >> 1) * 8; }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float silu(float x) { return fast_silu(x); }
 
 // Per-lane source pointers of this wave's staging instructions (hoisted out of the K loop): instruction
 // i of wave w writes LDS rows [8*(i*NW+w), +8) of the tile, lane l -> row +l/8, physical 16-B chunk l%8,

@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void swiglu_il_kernel(const bf16_t* __restrict
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float g0 = bf_lo(gv[i]), g1 = bf_hi(gv[i]);
-    o[i] = pack_bf2(g0 / (1.f + __expf(-g0)) * bf_lo(uv[i]), g1 / (1.f + __expf(-g1)) * bf_hi(uv[i]));
+    o[i] = pack_bf2(fast_silu(g0) * bf_lo(uv[i]), fast_silu(g1) * bf_hi(uv[i]));
   }
   *(u32x4_t*)(a + t * (size_t)I + c) = o;
 }
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(256) void lrp_swiglu_bwd_kernel(const bf16_t* __res
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float g0 = bf_lo(gv[i]), g1 = bf_hi(gv[i]);
-    const float s0 = 1.f / (1.f + __expf(-g0)), s1 = 1.f / (1.f + __expf(-g1));
+    const float s0 = fast_sigmoid(g0), s1 = fast_sigmoid(g1);
     const float m0 = 0.5f * bf_lo(mv[i]), m1 = 0.5f * bf_hi(mv[i]);
     og[i] = pack_bf2(m0 * bf_lo(uv[i]) * s0, m1 * bf_hi(uv[i]) * s1);
     ou[i] = pack_bf2(m0 * g0 * s0, m1 * g1 * s1);
