@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 from llm_inference_in_distributed_edge_networks_amd.config import Params  # noqa: E402
 from llm_inference_in_distributed_edge_networks_amd.eval.experiments import qwen2_main  # noqa: E402
+from llm_inference_in_distributed_edge_networks_amd.parallel.dist import shutdown  # noqa: E402
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
@@ -28,3 +29,4 @@ if __name__ == "__main__":
     if p.max_length is None:
         p.max_length = 512
     qwen2_main(p)
+    shutdown()  # all ranks done: barrier + destroy the process group before interpreter exit

@@ -12,6 +12,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 from llm_inference_in_distributed_edge_networks_amd.config import Params  # noqa: E402
 from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import relevance_main  # noqa: E402
+from llm_inference_in_distributed_edge_networks_amd.parallel.dist import shutdown  # noqa: E402
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
@@ -22,3 +23,4 @@ if __name__ == "__main__":
     p = Params.load(a.params, device=a.device, max_windows=a.max_windows)
     p.model = p.model or "qwen2-0.5b"
     relevance_main(p)
+    shutdown()  # all ranks done: barrier + destroy the process group before interpreter exit
