@@ -326,9 +326,174 @@ __global__ __launch_bounds__(256, OCC) void flash_attn_fwd2_kernel(const bf16_t*
   }
 }
 
-static int g_attn_variant = 3;
+// ---------------------------------------------------------------------------------------------
+// v3 forward: v2's tile body with TWO 16-row query tiles per wave (128 query rows per workgroup).
+// v2 reads 16 ds_read_b128 (8 K + 8 V^T fragments) per 16 MFMAs per wave and tile: at 3 waves per SIMD that
+// alone asks ~250 B/clk/CU of the LDS array (peak 256).  Here every K and V^T fragment feeds both row tiles,
+// so the reads per MFMA halve.  Each wave runs the key tiles up to its own last row (wave-uniform skip of
+// the tile past the diagonal) and masks exactly one tile; softmax state is per row tile.
+namespace {
+template <bool MASK>
+__device__ __forceinline__ void fa3_tile(const char* lk, const char* lv, const bf16x8_t (&qf)[2][2],
+                                         f32x4_t (&oacc)[2][4], float (&m2)[2], float (&l_run)[2], int kb, int q0,
+                                         int S, int g, int ql) {
+  f32x4_t st[2][4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    st[0][ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    st[1][ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int r = 32 * (ni >> 1) + 8 * (ql >> 2) + 4 * (ni & 1) + (ql & 3);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t kf = *(const bf16x8_t*)(lk + r * 128 + (((ks * 4 + g) ^ aswz(r)) << 4));
+      st[0][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ks], st[0][ni], 0, 0, 0);
+      st[1][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ks], st[1][ni], 0, 0, 0);
+    }
+  }
+  bf16x8_t pf[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if constexpr (MASK) {
+      const int qrow = q0 + t * 16 + ql;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * KT + 32 * (ni >> 1) + 8 * g + 4 * (ni & 1) + r;
+          if (key > qrow || key >= S) st[t][ni][r] = -INFINITY;
+        }
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[t][ni][r]);
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float mc = mloc * LOG2E;
+    if (__builtin_amdgcn_ballot_w64(mc > m2[t] + TAU)) {   // wave-uniform: rescale every row of tile t exactly
+      const float mn = fmaxf(m2[t], mc);
+      const float alpha = __builtin_amdgcn_exp2f(m2[t] - mn);
+      m2[t] = mn;
+      l_run[t] *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) oacc[t][d] *= alpha;
+    }
+    float ps = 0.f;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(st[t][ni][r], LOG2E, -m2[t]));
+        ps += p;
+        pf[t][ni >> 1][(ni & 1) * 4 + r] = (__bf16)p;
+      }
+    l_run[t] += ps;
+  }
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int row = dt * 16 + ql;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t vf = *(const bf16x8_t*)(lv + row * 128 + (((ks * 4 + g) ^ aswz(row)) << 4));
+      oacc[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0][ks], oacc[0][dt], 0, 0, 0);
+      oacc[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1][ks], oacc[1][dt], 0, 0, 0);
+    }
+  }
+}
+}  // namespace
+
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void flash_attn_fwd3_kernel(const bf16_t* __restrict__ q,
+                                                                 const bf16_t* __restrict__ k,
+                                                                 const bf16_t* __restrict__ vt,
+                                                                 bf16_t* __restrict__ o, float* __restrict__ lse,
+                                                                 const float* __restrict__ n_rows,
+                                                                 int B, int Hq, int Hkv, int S, int s_pad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
+  const int nqb = (S + 127) / 128;
+  const int G = Hq / Hkv, NG = B * Hkv;
+  // XCD-aware order as v2: XCD `xcd` owns (window, kv head) groups xcd, xcd+8, ...; heavy query blocks first
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int cnt = (NG - xcd + 7) >> 3;
+  const int per_qb = cnt * G;
+  if (j >= per_qb * nqb) return;
+  const int qb = nqb - 1 - j / per_qb;
+  const int rem = j - (nqb - 1 - qb) * per_qb;
+  const int grp = xcd + 8 * (rem / G);
+  const int b = grp / Hkv, hk = grp - b * Hkv, h = hk * G + rem % G;
+  if (n_rows && qb * 128 + 127 < S - 1 - (int)n_rows[b]) return;  // scored-rows mode (last layer)
+
+  const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
+  const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const bf16_t* vh = vt + ((size_t)b * Hkv + hk) * 64 * (size_t)s_pad;
+
+  const int q0 = qb * 128 + wave * 32;  // this wave's rows: q0 + 16 t + ql
+  bf16x8_t qf[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int qrow = q0 + t * 16 + ql;
+    const int qld = qrow < S ? qrow : S - 1;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[t][ks] = *(const bf16x8_t*)(qh + (size_t)qld * 64 + ks * 32 + g * 8);
+  }
+  f32x4_t oacc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) oacc[t][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m2[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+
+  const int nkb = min(2 * qb + 2, (S + KT - 1) / KT);
+  const int kmax = (q0 + 31) / KT;  // last key tile this wave needs (wave-uniform)
+  stage64(kh, 64, 0, S, 0, smem, wave, lane);
+  stage64(vh, s_pad, 0, 64, 0, smem + TILE, wave, lane);
+  if (nkb > 1) {
+    stage64(kh, 64, KT, S, 0, smem + 2 * TILE, wave, lane);
+    stage64(vh, s_pad, 0, 64, KT, smem + 3 * TILE, wave, lane);
+  }
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 2 < nkb) {
+      char* nx = smem + ((kb + 2) % NST) * 2 * TILE;
+      stage64(kh, 64, (kb + 2) * KT, S, 0, nx, wave, lane);
+      stage64(vh, s_pad, 0, 64, (kb + 2) * KT, nx + TILE, wave, lane);
+    }
+    if (kb > kmax) continue;  // every key of this tile is past this wave's rows
+    const char* cur = smem + (kb % NST) * 2 * TILE;
+    if (kb * KT + KT - 1 <= q0 && kb * KT + KT - 1 < S)
+      fa3_tile<false>(cur, cur + TILE, qf, oacc, m2, l_run, kb, q0, S, g, ql);
+    else
+      fa3_tile<true>(cur, cur + TILE, qf, oacc, m2, l_run, kb, q0, S, g, ql);
+  }
+
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float l = l_run[t];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const int qrow = q0 + t * 16 + ql;
+    if (qrow < S) {
+      const float inv = __builtin_amdgcn_rcpf(l);
+      bf16_t* orow = o + ((size_t)b * S + qrow) * (size_t)(Hq * 64) + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        u32x2_t w;
+        w[0] = pack_bf2(oacc[t][dt][0] * inv, oacc[t][dt][1] * inv);
+        w[1] = pack_bf2(oacc[t][dt][2] * inv, oacc[t][dt][3] * inv);
+        *(u32x2_t*)(orow + dt * 16 + g * 4) = w;
+      }
+      if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = m2[t] * 0.6931471805599453f + logf(l);
+    }
+  }
+}
+
+static int g_attn_variant = 4;  // v3 at 3 workgroups/CU (58.5 us vs v2's 70.5 at the bench shape)
 EDGE_API int edge_attn_set_variant(int v) {
-  g_attn_variant = (v >= 1 && v <= 3) ? v : 3;
+  g_attn_variant = (v >= 1 && v <= 5) ? v : 4;
   return 0;
 }
 
@@ -454,6 +619,17 @@ EDGE_API int edge_flash_attn_fwd(const void* q, const void* k, const void* vt, v
   if (B <= 0 || S <= 0) return 0;
   if (Hq % Hkv || s_pad % 64 || s_pad < S) return (int)hipErrorInvalidValue;
   const int nqb = (S + 63) / 64;
+  if (g_attn_variant >= 4) {  // 4: v3 at 3 workgroups/CU, 5: v3 at 2 workgroups/CU
+    const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
+    const dim3 grid(8 * maxcnt * G * ((S + 127) / 128));
+    if (g_attn_variant == 4)
+      hipLaunchKernelGGL(flash_attn_fwd3_kernel<3>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
+                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
+    else
+      hipLaunchKernelGGL(flash_attn_fwd3_kernel<2>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
+                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
+    return (int)hipGetLastError();
+  }
   if (g_attn_variant >= 2) {  // 2: v2 at 2 workgroups/CU, 3: v2 at 3 workgroups/CU
     const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
     const dim3 grid(8 * maxcnt * G * nqb);

@@ -243,8 +243,8 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None):
 
 
 def set_attn_variant(v: int) -> None:
-    """Flash-attention forward kernel: 3 (default: v2 at 3 workgroups/CU), 2 (v2 at 2/CU) or 1 (the first
-    version).  A/B and tests only."""
+    """Flash-attention forward kernel: 4 (default: v3, two 16-row query tiles per wave, 3 workgroups/CU), 5 (v3 at
+    2/CU), 3 / 2 (v2 at 3 / 2 workgroups/CU), 1 (the first version).  A/B and tests only."""
     call("edge_attn_set_variant", int(v))
 
 

@@ -85,6 +85,9 @@ def lib():
         v = os.environ.get("EDGE_GEMM_VARIANT")  # A/B of the 256x256 main loop (see ops.set_gemm_variant)
         if v:
             L.edge_gemm_set_variant(int(v))
+        av = os.environ.get("EDGE_ATTN_VARIANT")  # A/B of the flash-attention forward (see ops.set_attn_variant)
+        if av:
+            L.edge_attn_set_variant(int(av))
         if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # A/B: N = 896 GEMMs back on the 256x256 tiles
             L.edge_gemm_set_w7(0)
     return _lib

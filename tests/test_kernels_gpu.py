@@ -178,11 +178,11 @@ def _qkv(B, S, Hq, Hkv, seed):
     return q, k, vt
 
 
-@pytest.fixture(params=[2, 3, 1], ids=["fa2", "fa2occ3", "fa1"])
+@pytest.fixture(params=[2, 3, 1, 4, 5], ids=["fa2", "fa2occ3", "fa1", "fa3occ3", "fa3"])
 def attn_variant(request):
     ops.set_attn_variant(request.param)
     yield request.param
-    ops.set_attn_variant(3)
+    ops.set_attn_variant(4)
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (1, 100, 4, 2), (3, 64, 8, 8), (1, 1000, 2, 1),
@@ -206,6 +206,20 @@ def test_flash_attention_spike(pos, attn_variant):
     ro, rlse = R.attention(q, k, vt, S, need_lse=True)
     close(o, ro, atol=3e-2, rtol=2e-2)
     close(lse, rlse, atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("S", [512, 200, 130])
+def test_flash_attention_scored_rows(S, attn_variant):
+    """n_rows mode (last layer): the rows >= S-1-n_rows[b] of every window are exact; others may be skipped."""
+    B, Hq, Hkv = 3, 14, 2
+    q, k, vt = _qkv(B, S, Hq, Hkv, 41)
+    n_rows = torch.tensor([32.0, 7.0, float(S - 1)])
+    o, _ = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, n_rows=n_rows.to(DEV))
+    ro, _ = R.attention(q, k, vt, S)
+    o, ro = o.view(B, S, -1), ro.view(B, S, -1)
+    for b in range(B):
+        lo = S - 1 - int(n_rows[b])
+        close(o[b, lo:], ro[b, lo:], atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (1, 100, 4, 2), (2, 2048, 8, 8)])

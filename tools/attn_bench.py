@@ -1,4 +1,4 @@
-"""Flash-attention forward: v1 vs v2 kernel at the bench shape (B windows x 512, 14 q / 2 kv heads, d=64)."""
+"""Flash-attention forward: v1 / v2 / v3 kernels at the bench shape (B windows x 512, 14 q / 2 kv heads, d=64)."""
 import argparse
 import json
 import os
@@ -27,7 +27,7 @@ def main():
     flop = 4.0 * B * Hq * 64 * sum(i + 1 for i in range(S))   # causal QK^T + PV
     res = {}
     for r in range(a.rounds):
-        for v in (1, 2, 3):
+        for v in (1, 2, 3, 4, 5):
             ops.set_attn_variant(v)
             for lse in (False, True):
                 ops.attention(q, k, vt, S, need_lse=lse)
@@ -40,7 +40,7 @@ def main():
                 us = st.elapsed_time(en) / a.iters * 1e3
                 key = f"v{v}{'_lse' if lse else ''}"
                 res.setdefault(key, []).append(us)
-    ops.set_attn_variant(3)
+    ops.set_attn_variant(4)
     out = {k_: {"us": round(min(v), 2), "TFLOPs": round(flop / min(v) * 1e-6, 1)} for k_, v in res.items()}
     print(json.dumps({"shape": [B, S, Hq, Hkv], **out}))
 
