@@ -33,6 +33,7 @@ struct GemmArgs {
   // partial per 64-column slab: ssq_out[m, n/64])
   const float* rscale; float* ssq_out;
   int walk;  // persistent tile walk: 1 = XCD-contiguous chunks (default), 0 = strided by the grid size
+  int skip_epi;  // timing ablation only (wrong results): the GEMM without its epilogue (gemm_bf16 / w7 kernels)
 };
 
 constexpr int BK = 64;
@@ -438,7 +439,8 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
       wait_vmcnt0();
       __syncthreads();
     }
-    gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
+    if (!a.skip_epi) gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
+    else if (acc[0][0][0] == 1234.5f && acc[MI - 1][3][3] == -1.f) a.C[0] = 0;  // keep the accumulators live
   } else {
     // Persistent (one workgroup per CU walks tiles v, v+G, v+2G, ... with v the XCD-grouped id of this
     // workgroup, so the 32 CUs of an XCD work on 32 consecutive grouped-M tiles).  Sub-steps
@@ -505,11 +507,13 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      {
+      if (!a.skip_epi) {
         // row scales loaded here, not across the K loop: this config runs at the 256-VGPR budget
         float rs[MI];
         load_rscale<MI, CF::WTM>(a, m0, wm, lane, rs);
         gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
+      } else if (acc[0][0][0] == 1234.5f && acc[MI - 1][3][3] == -1.f) {  // keep the accumulators live
+        a.C[0] = 0;
       }
       if (!has_next) break;
       zero_acc<MI>(acc);
@@ -903,18 +907,40 @@ constexpr int A_BYTES = BM * BK * 2, STAGE = A_BYTES + BN * BK * 2, LDS = 2 * ST
 constexpr int A_INSTR = BM / 8 / NW, B_BLOCKS = BN / 8, B_INSTR = (B_BLOCKS + NW - 1) / NW;
 }  // namespace w7
 
-template <int EPI>
+// MODE (A/B of the epilogue's memory traffic): bit 0 = non-temporal output stores, bit 1 = non-temporal
+// residual loads.
+template <int EPI, int MODE>
 __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7::MI][w7::NJ], int m0, int n0,
                                             int lane, int wm, int wn) {
   const int g = lane >> 4;
   const int nw = n0 + wn * 112;
   const int P = a.N / 112;
+  constexpr bool RES = EPI == EPI_RESID || EPI == EPI_BIAS_RESID;
+  // every residual load of the slab is issued up front (4 x 7 x 8 B per lane): one global round trip instead of
+  // one per 16-row group (the per-group load -> wait -> use chain cost ~30 % of the O-proj GEMM's time)
+  // (vmcnt also counts stores on gfx9: a load waited between the stores of two groups drains those stores too,
+  // so the row scales are fetched up front as well)
+  u32x2_t rv[w7::MI][w7::NJ];
+  float rsv[w7::MI];
+#pragma unroll
+  for (int i = 0; i < w7::MI; ++i) {
+    int mr = m0 + wm * 64 + i * 16 + (lane & 15);
+    mr = mr < a.M ? mr : a.M - 1;
+    rsv[i] = a.rscale ? a.rscale[mr] : 1.f;
+    if constexpr (RES) {
+      const bf16_t* rrow = a.resid + (size_t)mr * a.ldr + nw + g * 4;
+#pragma unroll
+      for (int j = 0; j < w7::NJ; ++j) {
+        if constexpr (MODE & 2) rv[i][j] = __builtin_nontemporal_load((const u32x2_t*)(rrow + j * 16));
+        else rv[i][j] = *(const u32x2_t*)(rrow + j * 16);
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < w7::MI; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
     const bool ok = m < a.M;
-    const int mr = ok ? m : a.M - 1;  // clamped row for loads; every lane takes part in the swaps
-    const float rs = a.rscale ? a.rscale[mr] : 1.f;
+    const float rs = rsv[i];
     float ss = 0.f;
     u32x2_t w[w7::NJ];
 #pragma unroll
@@ -925,8 +951,8 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
         const u32x2_t bw = *(const u32x2_t*)(a.bias + n);
         o[0] += bf_lo(bw[0]); o[1] += bf_hi(bw[0]); o[2] += bf_lo(bw[1]); o[3] += bf_hi(bw[1]);
       }
-      if constexpr (EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
-        const u32x2_t rw = *(const u32x2_t*)(a.resid + (size_t)mr * a.ldr + n);
+      if constexpr (RES) {
+        const u32x2_t rw = rv[i][j];
         o[0] += bf_lo(rw[0]); o[1] += bf_hi(rw[0]); o[2] += bf_lo(rw[1]); o[3] += bf_hi(rw[1]);
       }
       w[j][0] = pack_bf2(o[0], o[1]);
@@ -934,13 +960,19 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
       const float v0 = bf_lo(w[j][0]), v1 = bf_hi(w[j][0]), v2 = bf_lo(w[j][1]), v3 = bf_hi(w[j][1]);
       ss += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;  // of the stored (rounded) values
     }
-    bf16_t* row = a.C + (size_t)mr * a.ldc + nw;
+    bf16_t* row = a.C + (size_t)(ok ? m : a.M - 1) * a.ldc + nw;
 #pragma unroll
     for (int q2 = 0; q2 < 3; ++q2) {  // column groups (0,1) (2,3) (4,5): 16-byte stores after the pair swap
       const u32x4_t wv = pair_swap16(w[2 * q2], w[2 * q2 + 1]);
-      if (ok) *(u32x4_t*)(row + q2 * 32 + pair_col(g)) = wv;
+      if (ok) {
+        if constexpr (MODE & 1) __builtin_nontemporal_store(wv, (u32x4_t*)(row + q2 * 32 + pair_col(g)));
+        else *(u32x4_t*)(row + q2 * 32 + pair_col(g)) = wv;
+      }
     }
-    if (ok) *(u32x2_t*)(row + 96 + g * 4) = w[6];  // group 6: 8-byte store
+    if (ok) {  // group 6: 8-byte store
+      if constexpr (MODE & 1) __builtin_nontemporal_store(w[6], (u32x2_t*)(row + 96 + g * 4));
+      else *(u32x2_t*)(row + 96 + g * 4) = w[6];
+    }
     if (a.ssq_out) {  // uniform branch: every lane takes part in the shuffles
       ss += __shfl_xor(ss, 16, 64);
       ss += __shfl_xor(ss, 32, 64);
@@ -962,7 +994,7 @@ __device__ __forceinline__ void w7_offsets(int ld, int row0, int row_max, int wa
   }
 }
 
-template <int EPI>
+template <int EPI, int MODE>
 __global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
   using namespace w7;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1096,7 +1128,8 @@ __global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
       mma(AY, BY, 1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    w7_epilogue<EPI>(a, acc, m0, n0, lane, wm, wn);
+    if (!a.skip_epi) w7_epilogue<EPI, MODE>(a, acc, m0, n0, lane, wm, wn);
+    else if (acc[0][0][0] == 1234.5f && acc[MI - 1][NJ - 1][3] == -1.f) a.C[0] = 0;  // keep the accumulators live
     if (!has_next) break;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -1110,6 +1143,7 @@ __global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
 }
 
 static int g_tile_override = 0;  // 0 auto, 128, 224 or 256 (tests / tuning)
+static int g_skip_epi = 0;       // timing ablation (wrong results)
 static int g_walk = 1;           // persistent tile walk (TileWalk): 1 chunked per XCD, 0 strided
 // 256x256 main loop: 0 = K-tile double buffer, compiler-waited fragment loads; 1 = same with hand-counted asm
 // reads; 2 = K-half ring (gemm_ring_kernel); 3 = ring with s_setprio around the MFMA clusters; 4 = ring with
@@ -1181,23 +1215,37 @@ static bool use_w7(int M, int N, int K, int epi) {
   return g_w7 && (long long)((M + 255) / 256) * (N / 224) >= 256;
 }
 
-template <int EPI>
-static int launch_w7(const GemmArgs& a, hipStream_t st) {
+static int g_w7_mode = 0;  // W7 epilogue memory-traffic variant (A/B): bit 0 nt stores, bit 1 nt residual loads
+
+template <int EPI, int MODE>
+static int launch_w7m(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + w7::BM - 1) / w7::BM) * (a.N / w7::BN);
   const int grid = std::min(tiles, num_cus());
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_w7_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, w7::LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_w7_kernel<EPI, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              w7::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_w7_kernel<EPI>), dim3(grid), dim3(w7::NT), w7::LDS, st, a);
+  hipLaunchKernelGGL((gemm_w7_kernel<EPI, MODE>), dim3(grid), dim3(w7::NT), w7::LDS, st, a);
   return (int)hipGetLastError();
+}
+
+template <int EPI>
+static int launch_w7(const GemmArgs& a, hipStream_t st) {
+  switch (g_w7_mode) {
+    case 1: return launch_w7m<EPI, 1>(a, st);
+    case 2: return launch_w7m<EPI, 2>(a, st);
+    case 3: return launch_w7m<EPI, 3>(a, st);
+    default: return launch_w7m<EPI, 0>(a, st);
+  }
 }
 
 template <int EPI, int RH = 0>
 static int launch(const GemmArgs& args, hipStream_t st) {
   GemmArgs a = args;
   a.walk = g_walk;
+  a.skip_epi = g_skip_epi;
   if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
     if (use_w7(a.M, a.N, a.K, EPI)) return launch_w7<EPI>(a, st);
   }
@@ -1239,8 +1287,18 @@ EDGE_API int edge_gemm_set_walk(int w) {
   return 0;
 }
 
+EDGE_API int edge_gemm_set_skip_epi(int on) {
+  g_skip_epi = on;
+  return 0;
+}
+
 EDGE_API int edge_gemm_set_w7(int on) {
   g_w7 = on;
+  return 0;
+}
+
+EDGE_API int edge_gemm_set_w7_mode(int m) {
+  g_w7_mode = m & 3;
   return 0;
 }
 

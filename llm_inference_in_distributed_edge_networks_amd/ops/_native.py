@@ -35,6 +35,8 @@ _SIGS = {
     "edge_gemm_set_variant": [c_i],
     "edge_gemm_set_walk": [c_i],
     "edge_gemm_set_w7": [c_i],
+    "edge_gemm_set_skip_epi": [c_i],
+    "edge_gemm_set_w7_mode": [c_i],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p],
     "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],

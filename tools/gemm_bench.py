@@ -22,6 +22,7 @@ SHAPES = {  # name: (M, N, K, act, bias, resid)
     "o_proj_b64": (32768, 896, 896, None, False, True),
     "gate_up_b64": (32768, 9728, 896, "swiglu_il", False, False),
     "big": (8192, 8192, 8192, None, False, False),
+    "qkv_rope_b64": (32768, 1152, 896, "qkv_rope", True, False),   # fused QKV + bias + RoPE + scatter epilogue
 }
 
 
@@ -60,14 +61,28 @@ def main():
         out = torch.empty(M, No, device=dev, dtype=torch.bfloat16)
         tiles = a.tiles.split(",")
 
-        def mk(spec):  # spec may end in "/w0" = strided persistent tile walk instead of XCD chunks
-            cfg, _, walk = spec.partition("/w")
+        def mk(spec):  # spec may end in "/w0" = strided persistent tile walk instead of XCD chunks, or "/noepi" =
+            # timing ablation of the persistent 256x256 loop without its epilogue (wrong results)
+            # "/m<k>": W7 epilogue memory mode k (bit 0 nt stores, bit 1 nt residual loads)
+            noepi = spec.endswith("/noepi")
+            spec = spec.removesuffix("/noepi")
+            mode = int(spec.partition("/m")[2] or 0)
+            cfg, _, walk = spec.partition("/m")[0].partition("/w")
 
             def f():
                 ops.set_gemm_config(cfg)
                 ops.set_gemm_walk(walk != "0")
-                ops.linear(x, w, bias=b, residual=r, act=act, out=out)
+                ops._native.lib().edge_gemm_set_skip_epi(int(noepi))
+                ops._native.lib().edge_gemm_set_w7_mode(mode)
+                if act == "qkv_rope":
+                    ops.qkv_rope(x, w, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
+                else:
+                    ops.linear(x, w, bias=b, residual=r, act=act, out=out)
+                ops._native.lib().edge_gemm_set_skip_epi(0)
+                ops._native.lib().edge_gemm_set_w7_mode(0)
             return f
+        if act == "qkv_rope":
+            cos, sin = (t.to(dev) for t in ops.rope_tables(512, 64, 1e6))
         variants = {t: mk(t) for t in tiles}
         ours = variants[tiles[0]]
         lib = lambda: torch.matmul(x, w.t())  # noqa: E731
