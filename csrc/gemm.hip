@@ -100,7 +100,8 @@ __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
 // ---- epilogue: lane owns rows m0 + wm*WTM + i*16 + (lane&15), columns n0 + wn*64 + j*16 + 4*(lane>>4) + r
 template <int EPI, int RH, class CF>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[CF::MI][4], int m0, int n0,
-                                              int lane, int wm, int wn, const float (&rs)[CF::MI]) {
+                                              int lane, int wm, int wn, const float (&rs)[CF::MI],
+                                              char* lds = nullptr) {
   constexpr int MI = CF::MI;
   const int g = lane >> 4;
   const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
@@ -156,34 +157,54 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
   if constexpr (EPI == EPI_QKV_ROPE) {
     const int head = nw / 64;  // global head slot in [q heads | k heads | v heads]
     const bool is_v = head >= a.Hq + a.Hkv;
+    // Every global load of the epilogue (bias, RoPE tables of all row groups) is issued before the first store:
+    // vmcnt counts stores too, so a load waited between the stores of two row groups would drain them.
+    u32x2_t bw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bw[j] = *(const u32x2_t*)(a.bias + nw + j * 16 + g * 4);
+    constexpr int NJ = RH >= 16 ? RH / 16 : 1;  // register groups in the rotated low half
+    f32x4_t cs[MI][NJ], sn[MI][NJ];
+    int bi[MI], pi[MI];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
       const int mm = m < a.M ? m : a.M - 1;
-      const int b = mm / a.S, pos = mm - b * a.S;
+      bi[i] = mm / a.S;
+      pi[i] = mm - bi[i] * a.S;
+      if constexpr (RH >= 16) {
+        if (!is_v) {
+          // cos/sin of the 4 consecutive frequencies this lane needs per 16-column group: one float4 each
+          // (the frequency index of column d is d mod RH, shared by the pair (d, d+RH))
+#pragma unroll
+          for (int jf = 0; jf < NJ; ++jf) {
+            cs[i][jf] = *(const f32x4_t*)(a.cosT + pi[i] * RH + jf * 16 + g * 4);
+            sn[i][jf] = *(const f32x4_t*)(a.sinT + pi[i] * RH + jf * 16 + g * 4);
+          }
+        }
+      }
+    }
+    // V heads: transpose the wave's 64-row x 64-d slab through LDS ([d][row], row stride 72 elements) and store
+    // V^T rows as 16-byte chunks of 8 positions, instead of 16 scattered 2-byte stores per lane and row group.
+    // Needs the slab's 64 rows inside one window and < M (S % 64 == 0), and the LDS (free after the K loop).
+    const int row0 = m0 + wm * CF::WTM;
+    const bool v_lds = is_v && lds && CF::WTM == 64 && a.S % 64 == 0 && row0 + 63 < a.M;
+    bf16_t* tl = v_lds ? (bf16_t*)(lds + (wm * CF::NWN + wn) * (64 * 72 * 2)) : nullptr;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
+      const int b = bi[i], pos = pi[i];
       float v[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int n = nw + j * 16 + g * 4;
-        const u32x2_t bw = *(const u32x2_t*)(a.bias + n);
-        v[j][0] = acc[i][j][0] + bf_lo(bw[0]);
-        v[j][1] = acc[i][j][1] + bf_hi(bw[0]);
-        v[j][2] = acc[i][j][2] + bf_lo(bw[1]);
-        v[j][3] = acc[i][j][3] + bf_hi(bw[1]);
+        v[j][0] = acc[i][j][0] + bf_lo(bw[j][0]);
+        v[j][1] = acc[i][j][1] + bf_hi(bw[j][0]);
+        v[j][2] = acc[i][j][2] + bf_lo(bw[j][1]);
+        v[j][3] = acc[i][j][3] + bf_hi(bw[j][1]);
       }
       if constexpr (RH >= 16) {
         // rotate_half partner of column d is d +- RH: register j +- RH/16, same lane.
         constexpr int DJ = RH / 16;
         if (!is_v) {
-          // cos/sin of the 4 consecutive frequencies this lane needs per 16-column group: one float4
-          // load each (the frequency index of column d is d mod RH, shared by the pair (d, d+RH))
-          constexpr int NJ = RH / 16;  // register groups in the low half
-          f32x4_t cs[NJ], sn[NJ];
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            cs[j] = *(const f32x4_t*)(a.cosT + pos * RH + j * 16 + g * 4);
-            sn[j] = *(const f32x4_t*)(a.sinT + pos * RH + j * 16 + g * 4);
-          }
           float o[4][4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -192,7 +213,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
               if (j * 16 >= 2 * RH) { o[j][r] = v[j][r]; continue; }
               const bool lo = j * 16 < RH;
               const int jf = lo ? j : j - DJ;
-              const float c = cs[jf][r], sv = sn[jf][r];
+              const float c = cs[i][jf][r], sv = sn[i][jf][r];
               const float y = lo ? v[(j + DJ) & 3][r] : v[(j - DJ) & 3][r];
               o[j][r] = lo ? (v[j][r] * c - y * sv) : (v[j][r] * c + y * sv);
             }
@@ -234,6 +255,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
           const u32x4_t w = pair_swap16(w0, w1);
           if (m < a.M) *(u32x4_t*)(dst + q2 * 32 + pair_col(g)) = w;
         }
+      } else if (v_lds) {
+        const int rl = i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tl[(j * 16 + g * 4 + r) * 72 + rl] = f2bf(v[j][r]);
       } else {
         if (m >= a.M) continue;
         bf16_t* dst = a.vtout + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
@@ -241,6 +268,17 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) dst[(size_t)(j * 16 + g * 4 + r) * a.s_pad] = f2bf(v[j][r]);
+      }
+    }
+    if (v_lds) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done before it reads them back
+      const int b = bi[0], pos0 = pi[0] - (lane & 15);  // slab's first row (64-aligned, one window)
+      bf16_t* vbase = a.vtout + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = k * 64 + lane, d = c >> 3, pc = c & 7;
+        const u32x4_t w = *(const u32x4_t*)(tl + d * 72 + pc * 8);
+        *(u32x4_t*)(vbase + (size_t)d * a.s_pad + pc * 8) = w;
       }
     }
     return;
@@ -439,7 +477,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
       wait_vmcnt0();
       __syncthreads();
     }
-    if (!a.skip_epi) gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
+    if (!a.skip_epi) gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs, smem);  // LDS free: K loop done
     else if (acc[0][0][0] == 1234.5f && acc[MI - 1][3][3] == -1.f) a.C[0] = 0;  // keep the accumulators live
   } else {
     // Persistent (one workgroup per CU walks tiles v, v+G, v+2G, ... with v the XCD-grouped id of this
