@@ -63,12 +63,14 @@ class SweepEngine:
         self.tokens_done = 0
         # the model's last layer only at the scored rows (see DecoderLM.layer_rows)
         self.rows_only = os.environ.get("EDGE_LAST_LAYER_ALL_ROWS", "0") in ("", "0")
+        hw = sc.head_weights  # LRP head table on the model's device once
+        self.head_weights = None if hw is None else torch.as_tensor(hw).to(self.m.device, torch.float32).contiguous()
 
     # -------------------------------------------------------------- one batch
     def _prefix(self, batch: WindowBatch):
         """Unquantized forward: base per-window NLL, h_L per boundary layer, importance per (method, L)."""
         m, B, S = self.m, batch.B, batch.S
-        trackers = {meth: ImportanceTracker(meth, self.layers, m.cfg.num_heads, self.sc.head_weights)
+        trackers = {meth: ImportanceTracker(meth, self.layers, m.cfg.num_heads, self.head_weights)
                     for meth in self.methods}
         x = m.embed(batch.ids)
         saved = {}

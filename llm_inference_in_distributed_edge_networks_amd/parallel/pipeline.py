@@ -74,12 +74,14 @@ class StageRunner:
         self.stats = StageStats()
         self.scored_rows_only = os.environ.get("EDGE_LAST_LAYER_ALL_ROWS", "0") in ("", "0")
         self.rows_only = False
+        # LRP head table resident on the stage's device once (no host->device copy inside a captured graph)
+        hw = bcfg.head_weights
+        self.head_weights = None if hw is None else torch.as_tensor(hw).to(model.device, torch.float32).contiguous()
 
     def _tracker(self, S: int):
         if self.boundary is None or not self.bcfg.needs_importance(S):
             return None
-        return ImportanceTracker(self.bcfg.method, [self.boundary], self.model.cfg.num_heads,
-                                 self.bcfg.head_weights)
+        return ImportanceTracker(self.bcfg.method, [self.boundary], self.model.cfg.num_heads, self.head_weights)
 
     def carries_state(self) -> bool:
         return canonical(self.bcfg.method) in ("aggregate_till", "maximum_aggregation")

@@ -186,7 +186,7 @@ def relevance_main(p) -> list:
     """Entry point of Experiments/Relevance/main.py: writes attention_head_weights.json."""
     import json
 
-    from ..config import dump_json
+    from ..config import dump_json, resolve_dtype
     from ..eval.data import token_stream
     from ..eval.windows import sliding_windows
     from ..models import build_model, get_config
@@ -195,7 +195,8 @@ def relevance_main(p) -> list:
     env = init_distributed(p.device)
     device = str(env.device)
     cfg = get_config(p.model or "qwen2-0.5b")
-    model, prov = build_model(cfg, device, torch.float32, weights=p.weights, seed=p.seed)
+    # bf16 on the GPU (the HIP kernels' storage type), fp32 on the CPU oracle path
+    model, prov = build_model(cfg, device, resolve_dtype(p, device), weights=p.weights, seed=p.seed)
     ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed)
     wins = sliding_windows(ids.shape[1], p.max_length or 512, p.stride)
     if p.max_windows:
