@@ -51,8 +51,8 @@ def parse():
     p.add_argument("--model", default="qwen2-0.5b")
     p.add_argument("--batch", type=int, default=64, help="windows per micro-batch")
     p.add_argument("--microbatches", type=int, default=0,
-                   help="micro-batches per step per replica (default 2 x pipeline depth: every GPU does the "
-                        "work of 2 full-model micro-batches per step at any N, i.e. weak scaling)")
+                   help="micro-batches per step per replica (default 4 x pipeline depth: every GPU does the "
+                        "work of 4 full-model micro-batches per step at any N, i.e. weak scaling)")
     p.add_argument("--max-length", type=int, default=512)
     p.add_argument("--stride", type=int, default=32)
     p.add_argument("--split", type=int, default=11, help="last layer of stage 0 (reference layer_of_interest)")
@@ -76,7 +76,7 @@ def main():
     pp = 2 if world >= 2 else 1
     grid = Grid(world, pp)
     if a.microbatches <= 0:
-        a.microbatches = 2 * pp
+        a.microbatches = 4 * pp
     plan2 = PipelinePlan.from_split_layers(cfg.num_layers, [a.split])
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     if pp == 1:
@@ -96,6 +96,7 @@ def main():
     need = a.batch * a.microbatches * grid.dp
     pool = list(batches(tokens, wins[: need * 4], a.batch))
     pool = [b.to(dev) for b in pool]
+    pool_w = [b.weights.to(dev) for b in pool]   # per-window loss weights, resident (no H2D copy per step)
     nll_acc = torch.zeros(2, dtype=torch.float64, device=dev)
 
     per_step = a.microbatches * grid.dp
@@ -103,16 +104,19 @@ def main():
     def mbs_for(first_step: int, nsteps: int):
         return [pool[(first_step * per_step + i) % len(pool)] for i in range(nsteps * per_step)]
 
+    def wts_for(first_step: int, nsteps: int):
+        return [pool_w[(first_step * per_step + i) % len(pool)] for i in range(nsteps * per_step)]
+
     def run_steps(first_step: int, nsteps: int):
         """nsteps consecutive steps.  pp=1: micro-batch by micro-batch on the local 2-stage pipeline.
         pp>1: one continuous pipeline over all nsteps*microbatches (stages stay busy across step
         boundaries; the only fill/drain is at the ends of the timed region)."""
         mbs = mbs_for(first_step, nsteps)
         if pp == 1:
-            for b in mbs:
+            for b, w in zip(mbs, wts_for(first_step, nsteps)):
                 wn = runner.run_batch(b)
-                nll_acc[0] += (wn.double() * b.weights.to(dev)).sum()
-                nll_acc[1] += float(b.weights.sum())
+                nll_acc[0] += (wn.double() * w).sum()   # device-side accumulation: no host sync per micro-batch
+                nll_acc[1] += w.sum()
         else:
             acc, _ = runner.evaluate(mbs)
             nll_acc[0] += acc.total_nll
