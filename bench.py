@@ -165,6 +165,7 @@ def main():
                    "transport": a.transport if pp > 1 else "local", "hip_graphs": not a.no_graphs},
         "scored_tokens_per_s": round(scored_per_step * a.steps / dt, 1),
         "wire_bytes_per_token": round(wire, 2),
+        "wire_bits_per_element": round(8 * wire / cfg.hidden_size, 3),
         "wire_compression_vs_bf16": round(2 * cfg.hidden_size / wire, 3),
         "wire_compression_vs_fp32_reference": round(4 * cfg.hidden_size / wire, 3),
         "ppl_random_weights": ppl, "weights": prov,
