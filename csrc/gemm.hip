@@ -33,7 +33,8 @@ struct GemmArgs {
   // partial per 64-column slab: ssq_out[m, n/64])
   const float* rscale; float* ssq_out;
   int walk;  // persistent tile walk: 1 = XCD-contiguous chunks (default), 0 = strided by the grid size
-  int skip_epi;  // timing ablation only (wrong results): the GEMM without its epilogue (gemm_bf16 / w7 kernels)
+  int skip_epi;  // timing ablation only (wrong results): 1 = no epilogue (gemm_bf16 / w7 kernels); 2 = persistent
+                 // 256x256 SwiGLU epilogue computed but not stored
 };
 
 constexpr int BK = 64;
@@ -299,7 +300,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
         w[p][1] = pack_bf2(o[2], o[3]);
       }
       const u32x4_t wv = pair_swap16(w[0], w[1]);   // every lane swaps (partners share m)
-      if (ok) *(u32x4_t*)(a.C + (size_t)m * a.ldc + nw / 2 + pair_col(g)) = wv;
+      if (ok && a.skip_epi != 2) *(u32x4_t*)(a.C + (size_t)m * a.ldc + nw / 2 + pair_col(g)) = wv;
     } else {
       float ss = 0.f;
       const int mr = ok ? m : a.M - 1;   // clamped row for loads; every lane takes part in the swaps
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      if (!a.skip_epi) {
+      if (a.skip_epi != 1) {
         // row scales loaded here, not across the K loop: this config runs at the 256-VGPR budget
         float rs[MI];
         load_rscale<MI, CF::WTM>(a, m0, wm, lane, rs);

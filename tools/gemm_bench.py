@@ -64,8 +64,8 @@ def main():
         def mk(spec):  # spec may end in "/w0" = strided persistent tile walk instead of XCD chunks, or "/noepi" =
             # timing ablation of the persistent 256x256 loop without its epilogue (wrong results)
             # "/m<k>": W7 epilogue memory mode k (bit 0 nt stores, bit 1 nt residual loads)
-            noepi = spec.endswith("/noepi")
-            spec = spec.removesuffix("/noepi")
+            noepi = 1 if spec.endswith("/noepi") else (2 if spec.endswith("/nostore") else 0)
+            spec = spec.removesuffix("/noepi").removesuffix("/nostore")
             mode = int(spec.partition("/m")[2] or 0)
             cfg, _, walk = spec.partition("/m")[0].partition("/w")
 
