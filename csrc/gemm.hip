@@ -33,6 +33,7 @@ struct GemmArgs {
   // partial per 64-column slab: ssq_out[m, n/64])
   const float* rscale; float* ssq_out;
   int walk;  // persistent tile walk: 1 = XCD-contiguous chunks (default), 0 = strided by the grid size
+  int rs_lds;    // persistent 256x256: row scales DMA'd to LDS in the last K-tile (default 1; 0 = A/B baseline)
   int skip_epi;  // timing ablation only (wrong results): 1 = no epilogue (gemm_bf16 / w7 kernels); 2 = persistent
                  // 256x256 SwiGLU epilogue computed but not stored
 };
@@ -50,8 +51,10 @@ struct Cfg {
   static_assert(BN / NWN == 64, "wave column slab must be 64");
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   static constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW;  // 1-KiB glds per wave per K-tile
-  static constexpr int LDS = 2 * STAGE;
   static constexpr bool PIPE = MI >= 8;  // register-pipelined fragments (1 block/CU configs)
+  // PIPE: + BM floats after the two stages, the tile's RMSNorm row scales (DMA'd during its last K-tile)
+  static constexpr int RS_OFF = 2 * STAGE;
+  static constexpr int LDS = 2 * STAGE + (PIPE ? BM * 4 : 0);
 };
 using C128 = Cfg<128, 128, 2, 2>;   // 4 waves, 64 KiB LDS, 2 blocks/CU
 using C256 = Cfg<256, 256, 2, 4>;   // 8 waves, 128 KiB LDS, 1 block/CU
@@ -507,6 +510,9 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
       const bool has_next = next < walk.end;
       int nm0 = 0, nn0 = 0;
       if (has_next) tile_origin(next, a.M, a.N, BM, BN, nm0, nn0);
+      // full row tile (the 16-B DMA chunks of 4 rows stay inside the array) and >= 2 K-tiles (the previous
+      // epilogue's LDS reads are behind a barrier before the DMA overwrites them)
+      const bool rs_lds = a.rs_lds && a.rscale && m0 + BM <= a.M && nk >= 2;
       for (int t = 0; t < nk; ++t, ++g) {
         const char* cur = smem + (g & 1) * CF::STAGE;
         char* nxt = smem + ((g + 1) & 1) * CF::STAGE;
@@ -515,6 +521,9 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           if (s == 0) {
+            // the row scales of this tile's epilogue: one glds by wave 0 in its last K-tile (landed and visible
+            // at that K-tile's barrier) instead of a global round trip at the start of the epilogue
+            if (rs_lds && t == nk - 1 && wave == 0) glds16(a.rscale + m0 + lane * 4, smem + CF::RS_OFF);
             if (more) {
               stage((t + 1) * BK, nxt);
             } else if (has_next) {
@@ -549,7 +558,13 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
       if (a.skip_epi != 1) {
         // row scales loaded here, not across the K loop: this config runs at the 256-VGPR budget
         float rs[MI];
-        load_rscale<MI, CF::WTM>(a, m0, wm, lane, rs);
+        if (rs_lds) {
+          const float* rsl = (const float*)(smem + CF::RS_OFF) + wm * CF::WTM + (lane & 15);
+#pragma unroll
+          for (int i = 0; i < MI; ++i) rs[i] = rsl[i * 16];
+        } else {
+          load_rscale<MI, CF::WTM>(a, m0, wm, lane, rs);
+        }
         gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
       } else if (acc[0][0][0] == 1234.5f && acc[MI - 1][3][3] == -1.f) {  // keep the accumulators live
         a.C[0] = 0;
@@ -1183,6 +1198,7 @@ __global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
 
 static int g_tile_override = 0;  // 0 auto, 128, 224 or 256 (tests / tuning)
 static int g_skip_epi = 0;       // timing ablation (wrong results)
+static int g_rs_lds = 1;         // row scales through LDS in the persistent 256x256 kernel (A/B switch)
 static int g_walk = 1;           // persistent tile walk (TileWalk): 1 chunked per XCD, 0 strided
 // 256x256 main loop: 0 = K-tile double buffer, compiler-waited fragment loads; 1 = same with hand-counted asm
 // reads; 2 = K-half ring (gemm_ring_kernel); 3 = ring with s_setprio around the MFMA clusters; 4 = ring with
@@ -1285,6 +1301,7 @@ static int launch(const GemmArgs& args, hipStream_t st) {
   GemmArgs a = args;
   a.walk = g_walk;
   a.skip_epi = g_skip_epi;
+  a.rs_lds = g_rs_lds;
   if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
     if (use_w7(a.M, a.N, a.K, EPI)) return launch_w7<EPI>(a, st);
   }
@@ -1323,6 +1340,11 @@ EDGE_API int edge_gemm_set_tile(int t) {
 
 EDGE_API int edge_gemm_set_walk(int w) {
   g_walk = w;
+  return 0;
+}
+
+EDGE_API int edge_gemm_set_rs_lds(int on) {
+  g_rs_lds = on;
   return 0;
 }
 
