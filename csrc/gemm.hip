@@ -1199,6 +1199,7 @@ __global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
 static int g_tile_override = 0;  // 0 auto, 128, 224 or 256 (tests / tuning)
 static int g_skip_epi = 0;       // timing ablation (wrong results)
 static int g_rs_lds = 1;         // row scales through LDS in the persistent 256x256 kernel (A/B switch)
+static int g_lse256 = 1;         // LM-head LSE GEMM on the persistent 256x256 tiles (A/B switch)
 static int g_walk = 1;           // persistent tile walk (TileWalk): 1 chunked per XCD, 0 strided
 // 256x256 main loop: 0 = K-tile double buffer, compiler-waited fragment loads; 1 = same with hand-counted asm
 // reads; 2 = K-half ring (gemm_ring_kernel); 3 = ring with s_setprio around the MFMA clusters; 4 = ring with
@@ -1308,7 +1309,13 @@ static int launch(const GemmArgs& args, hipStream_t st) {
   // 256x256 persistent tiles when the shape can fill the chip with them (halves L2->LDS traffic per
   // FLOP), 128x128 otherwise (N not a multiple of 256, or too few 256-row panels).  The QKV/RoPE and
   // LSE epilogues stay on 128x128 (register budget; their N is never a multiple of 256 in practice).
-  if constexpr (EPI == EPI_QKV_ROPE || EPI == EPI_LSE) {
+  if constexpr (EPI == EPI_QKV_ROPE) {
+    return launch_cfg<EPI, RH, C128>(a, st);
+  } else if constexpr (EPI == EPI_LSE) {
+    // LM head on the scored rows (M = 2048 at the bench batch, N = vocab): 256x256 persistent tiles when they
+    // fill the chip (A/B: g_lse256), else 128x128
+    const bool big = g_lse256 && a.N % 128 == 0 && (long long)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 256;
+    if (big && g_tile_override != 128) return launch_cfg<EPI, RH, C256, true>(a, st);
     return launch_cfg<EPI, RH, C128>(a, st);
   } else {
     // a partial last column tile (N % 256 == 128) wastes at most 1/(2*tn) of the MFMA work
@@ -1340,6 +1347,11 @@ EDGE_API int edge_gemm_set_tile(int t) {
 
 EDGE_API int edge_gemm_set_walk(int w) {
   g_walk = w;
+  return 0;
+}
+
+EDGE_API int edge_gemm_set_lse256(int on) {
+  g_lse256 = on;
   return 0;
 }
 

@@ -37,6 +37,7 @@ _SIGS = {
     "edge_gemm_set_w7": [c_i],
     "edge_gemm_set_skip_epi": [c_i],
     "edge_gemm_set_rs_lds": [c_i],
+    "edge_gemm_set_lse256": [c_i],
     "edge_gemm_set_w7_mode": [c_i],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p],
@@ -91,6 +92,8 @@ def lib():
         av = os.environ.get("EDGE_ATTN_VARIANT")  # A/B of the flash-attention forward (see ops.set_attn_variant)
         if av:
             L.edge_attn_set_variant(int(av))
+        if os.environ.get("EDGE_GEMM_LSE256", "1") == "0":  # A/B: LM-head LSE GEMM on 128x128 tiles
+            L.edge_gemm_set_lse256(0)
         if os.environ.get("EDGE_GEMM_RS_LDS", "1") == "0":  # A/B: row scales by global loads in the epilogue
             L.edge_gemm_set_rs_lds(0)
         if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # A/B: N = 896 GEMMs back on the 256x256 tiles

@@ -246,6 +246,26 @@ def test_head_nll(R_, V, K):
     close(nll, R.head_nll(h, w, t), atol=2e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("R_", [2048, 300])
+def test_head_nll_vocab_size_tiles(R_):
+    """Qwen2 vocabulary (N = 151936 = 593.5 x 256: partial last column tile) on the persistent 256x256 LSE GEMM
+    (full and partial row tiles), against the 128x128 kernel and the fp32 oracle."""
+    V, K = 151936, 896
+    h = rnd(R_, K, seed=72)
+    w = rnd(V, K, s=2 / math.sqrt(K), seed=73)
+    t = torch.randint(0, V, (R_,), generator=torch.Generator().manual_seed(74))
+    t[:4] = torch.tensor([0, V - 1, V - 64, V - 129])   # targets in the first / last (partial) column tiles
+    hd, wd, td = h.to(DEV), w.to(DEV), t.to(DEV)
+    nll = ops.head_nll(hd, wd, td)
+    ops._native.lib().edge_gemm_set_lse256(0)
+    try:
+        nll128 = ops.head_nll(hd, wd, td)
+    finally:
+        ops._native.lib().edge_gemm_set_lse256(1)
+    close(nll, nll128, atol=2e-3, rtol=1e-3)
+    close(nll[:64], R.head_nll(h[:64], w, t[:64]), atol=2e-2, rtol=1e-2)
+
+
 @pytest.mark.parametrize("name", sorted(C.CODECS))
 @pytest.mark.parametrize("B,S,H,ratio", [(2, 512, 896, 0.5), (1, 100, 256, 0.25), (3, 64, 512, 1.0)])
 def test_codec_bytes_match_cpu(name, B, S, H, ratio):
