@@ -13,6 +13,14 @@ of the HIP kernels so that the two are interchangeable op by op:
 * gate/up weights of SwiGLU MLPs are interleaved in blocks of 16 rows
   (``[g0..g15, u0..u15, g16..]``) so one GEMM tile holds matching gate and up
   columns and the SiLU*up product is an epilogue.
+
+Reference sites of the ops (SURVEY §2.4 K-ids; paths relative to the reference repo):
+embedding K1 (``Experiments/Qwen2-0.5B/qwen_layer_wise.py:46``), RoPE K2 (``qwen_layer_wise.py:47-48``,
+partial rotary ``Experiments/Pythia-70M/pythia_model.py:158-161``), RMSNorm / LayerNorm K3
+(``qwen_layer_wise.py:75``, ``pythia_model.py:193``), causal SDPA attention K5 (``qwen_layer_wise.py:17``),
+eager attention probabilities K6 (``Experiments/Qwen2-0.5B/main.py:159``; here ``attention_probs``, test-only),
+LM head + shifted CE K9/K10 (``qwen_layer_wise.py:28-40``), importance reductions K11
+(``Experiments/Qwen2-0.5B/main.py:46-92``), AttnLRP backward K17 (``Experiments/Relevance/main.py:84-103``).
 """
 from __future__ import annotations
 
