@@ -32,6 +32,9 @@ struct GemmArgs {
   // pre-folded into B) and producer side (per-row sum of squares of the stored bf16 outputs, one
   // partial per 64-column slab: ssq_out[m, n/64])
   const float* rscale; float* ssq_out;
+  // consumer side without a row_rscale launch (QKV): rscale[m] computed at tile start from the producer's
+  // partials, rsqrt(sum_p ssq_in[m, p] * norm_inv_k + norm_eps); takes precedence over rscale
+  const float* ssq_in; int ssq_parts; float norm_inv_k, norm_eps;
   int walk;  // persistent tile walk: 1 = XCD-contiguous chunks (default), 0 = strided by the grid size
   int rs_lds;    // persistent 256x256: row scales DMA'd to LDS in the last K-tile (default 1; 0 = A/B baseline)
   int skip_epi;  // timing ablation only (wrong results): 1 = no epilogue (gemm_bf16 / w7 kernels); 2 = persistent
@@ -111,7 +114,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
   const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
   if (nw >= a.N) return;        // slab beyond N in a partial last column tile (wave-uniform)
 
-  if (a.rscale) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
+  if (a.rscale || a.ssq_in) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -344,8 +347,46 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
   }
 }
 
+// Row sums of NP sum-of-squares partials with every load issued before the first add (one round trip)
+template <int MI, int WTM, int NP>
+__device__ __forceinline__ void rscale_from_partials(const GemmArgs& a, int m0, int wm, int lane, float (&rs)[MI]) {
+  float v[MI][NP];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    int m = m0 + wm * WTM + i * 16 + (lane & 15);
+    m = m < a.M ? m : a.M - 1;
+    const float* p = a.ssq_in + (size_t)m * NP;
+    if constexpr (NP % 4 == 0) {
+#pragma unroll
+      for (int j = 0; j < NP; j += 4) *(f32x4_t*)&v[i][j] = *(const f32x4_t*)(p + j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NP; j += 2) {
+        const u32x2_t w = *(const u32x2_t*)(p + j);
+        v[i][j] = __uint_as_float(w[0]);
+        v[i][j + 1] = __uint_as_float(w[1]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) ss += v[i][j];
+    rs[i] = rsqrtf(ss * a.norm_inv_k + a.norm_eps);
+  }
+}
+
 template <int MI, int WTM>
 __device__ __forceinline__ void load_rscale(const GemmArgs& a, int m0, int wm, int lane, float (&rs)[MI]) {
+  // partial counts of the producers: 8 (256x224 GEMMs' 112-column slabs), 14 (64-column slabs of H=896).  Only
+  // compiled into the 128x128 tiles (the QKV GEMM): the 256-VGPR 256x256 loops spill with the extra registers.
+  if constexpr (MI <= 4) {
+    if (a.ssq_in) {
+      if (a.ssq_parts == 8) return rscale_from_partials<MI, WTM, 8>(a, m0, wm, lane, rs);
+      return rscale_from_partials<MI, WTM, 14>(a, m0, wm, lane, rs);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     int m = m0 + wm * WTM + i * 16 + (lane & 15);
@@ -1419,9 +1460,13 @@ EDGE_API int edge_gemm(const void* A, const void* B, void* C, int M, int N, int 
 
 EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, void* q, void* k, void* vt,
                                 const float* cosT, const float* sinT, int M, int K, int S, int Hq, int Hkv,
-                                int rot_dim, int s_pad, float q_scale, const float* rscale, hipStream_t st) {
+                                int rot_dim, int s_pad, float q_scale, const float* rscale, const float* ssq_in,
+                                int ssq_parts, float norm_eps, hipStream_t st) {
   GemmArgs a{};
   a.rscale = rscale;
+  a.ssq_in = ssq_in; a.ssq_parts = ssq_parts; a.norm_inv_k = 1.f / (float)K; a.norm_eps = norm_eps;
+  if (ssq_in && ssq_parts != 8 && ssq_parts != 14) return (int)hipErrorInvalidValue;
+  if (ssq_in && ((uintptr_t)ssq_in & 15)) return (int)hipErrorInvalidValue;
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
   a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = K; a.lda = K; a.ldb = K;
   a.bias = (const bf16_t*)bias;

@@ -9,6 +9,8 @@ Every op has exactly two implementations with identical layouts and semantics:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import reference as ref
@@ -21,6 +23,7 @@ interleave_gate_up = ref.interleave_gate_up
 deinterleave_gate_up = ref.deinterleave_gate_up
 
 _ACT = {None: 0, "gelu": 1, "swiglu_il": 2}
+_QKV_ROW_RSCALE = os.environ.get("EDGE_QKV_ROW_RSCALE", "0") not in ("", "0")
 
 
 def _gpu(t: torch.Tensor) -> bool:
@@ -214,9 +217,16 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     k = torch.empty(B, Hkv, S, D, dtype=x.dtype, device=x.device)
     vt = torch.zeros(B, Hkv, D, sp, dtype=x.dtype, device=x.device) if sp != S else \
         torch.empty(B, Hkv, D, sp, dtype=x.dtype, device=x.device)
-    rs = None if norm is None else _norm_scale(norm, K)
+    # fused RMSNorm: with 8 or 14 sum-of-squares partials per row the kernel forms the row scale itself at tile
+    # start (no row_rscale launch; EDGE_QKV_ROW_RSCALE=1 restores it for A/B)
+    ssq, eps = norm if norm is not None else (None, 0.0)
+    rs = None
+    if ssq is not None:
+        if _QKV_ROW_RSCALE or ssq.shape[1] not in (8, 14) or not ssq.is_contiguous() or ssq.data_ptr() % 16:
+            rs, ssq = _norm_scale(norm, K), None
     call("edge_gemm_qkv_rope", ptr(x), ptr(wqkv), ptr(bqkv), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, K, S,
-         Hq, Hkv, rot_dim, sp, float(q_scale), ptr(rs), stream())
+         Hq, Hkv, rot_dim, sp, float(q_scale), ptr(rs), ptr(ssq), 0 if ssq is None else ssq.shape[1], float(eps),
+         stream())
     return q, k, vt
 
 
