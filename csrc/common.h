@@ -12,6 +12,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;      // 16x16 MFMA ac
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;    // 32x32 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;     // packed-f32 VALU operands (v_pk_mul/add/fma_f32)
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 

@@ -299,11 +299,19 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
       u32x2_t w[2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
-        float o[4];
+        // silu(g) * u on float pairs: the multiplies and the add issue as v_pk_* (two lanes' worth per VALU
+        // slot), leaving the two transcendentals per output (v_exp_f32, v_rcp_f32) as the epilogue's cost
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = silu(acc[i][2 * p][r]) * acc[i][2 * p + 1][r];
-        w[p][0] = pack_bf2(o[0], o[1]);
-        w[p][1] = pack_bf2(o[2], o[3]);
+        for (int h = 0; h < 2; ++h) {
+          const f32x2_t gg = {acc[i][2 * p][2 * h], acc[i][2 * p][2 * h + 1]};
+          const f32x2_t uu = {acc[i][2 * p + 1][2 * h], acc[i][2 * p + 1][2 * h + 1]};
+          const f32x2_t t = gg * f32x2_t{-1.4426950408889634f, -1.4426950408889634f};
+          f32x2_t e = {__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+          e = e + f32x2_t{1.f, 1.f};
+          const f32x2_t r = {__builtin_amdgcn_rcpf(e[0]), __builtin_amdgcn_rcpf(e[1])};
+          const f32x2_t o = (gg * uu) * r;
+          w[p][h] = pack_bf2(o[0], o[1]);
+        }
       }
       const u32x4_t wv = pair_swap16(w[0], w[1]);   // every lane swaps (partners share m)
       if (ok && a.skip_epi != 2) *(u32x4_t*)(a.C + (size_t)m * a.ldc + nw / 2 + pair_col(g)) = wv;

@@ -15,7 +15,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "_native", "libedge_kernels.so")
+# EDGE_KERNEL_LIB: load another build of the library (A/B of two kernel builds in one GPU session)
+LIB_PATH = os.environ.get("EDGE_KERNEL_LIB") or os.path.join(os.path.dirname(_HERE), "_native", "libedge_kernels.so")
 
 _lib = None
 
