@@ -40,6 +40,8 @@ _SIGS = {
     "edge_gemm_set_rs_lds": [c_i],
     "edge_gemm_set_lse256": [c_i],
     "edge_gemm_set_w7_mode": [c_i],
+    "edge_gemm_set_w7_rscale": [c_i],
+    "edge_gemm_rs": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_p, c_p, c_p, c_i, c_f, c_p],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],
@@ -84,6 +86,8 @@ def lib():
                 "(python -c 'import __graft_entry__ as g; g.build()')")
         L = ctypes.CDLL(LIB_PATH)
         for name, argt in _SIGS.items():
+            if os.environ.get("EDGE_KERNEL_LIB") and not hasattr(L, name):
+                continue  # an older build under A/B: entry points it predates stay unbound
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = c_i
