@@ -40,8 +40,6 @@ _SIGS = {
     "edge_gemm_set_rs_lds": [c_i],
     "edge_gemm_set_lse256": [c_i],
     "edge_gemm_set_w7_mode": [c_i],
-    "edge_gemm_set_w7_rscale": [c_i],
-    "edge_gemm_rs": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_p, c_p, c_p, c_i, c_f, c_p],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],

@@ -59,3 +59,16 @@ def test_head_combine_cpu():
     x = torch.rand(2, 3, 10)
     w = torch.tensor([1.0, -2.0, 0.5])
     assert torch.allclose(ops.head_combine(x, w, 0.1), 0.1 * (x * w.view(1, 3, 1)).sum(1))
+
+
+def test_native_library_exports_every_bound_entry_point():
+    """Every ctypes signature in ops/_native.py names a symbol of the in-tree library build (a stale entry fails
+    every GPU op at load time)."""
+    import ctypes
+    import os
+
+    from llm_inference_in_distributed_edge_networks_amd.ops import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("kernel library not built")
+    L = ctypes.CDLL(_native.LIB_PATH)
+    assert [n for n in _native._SIGS if not hasattr(L, n)] == []
