@@ -1,4 +1,5 @@
 """fp32 reference ops: layouts and identities the HIP kernels rely on."""
+import pytest
 import math
 
 import torch
