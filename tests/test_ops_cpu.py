@@ -1,7 +1,7 @@
 """fp32 reference ops: layouts and identities the HIP kernels rely on."""
-import pytest
 import math
 
+import pytest
 import torch
 
 from llm_inference_in_distributed_edge_networks_amd import ops
