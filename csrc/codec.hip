@@ -9,21 +9,23 @@
 // nibble), 3 int2 (ternary, 4 per byte).  Scale modes: 0 per token (fp32 [B*S]), 1 per window for the
 // lo class (fp32 [B], reference Q1 "one global max-abs" int4), 2 per channel (fp32 [B*H]; reference
 // channel_8/4/1_max store max|x_c|, channel_1_mean stores mean_c + 1e-8), 3 none (pass-through).
+// Activations are bf16 or fp32 (the fp32 execution mode); row format 4 keeps a row in fp32 (the reference leaves
+// its un-selected tokens in fp32, Experiments/Qwen2-0.5B/qwen_layer_wise.py:54-70).
 #include "common.h"
 
-enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3 };
+enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3, FMT_F32 = 4 };
 enum { SC_TOKEN = 0, SC_WINDOW = 1, SC_CHANNEL = 2, SC_NONE = 3 };
 enum { CH_MAXABS = 0, CH_MEAN = 1 };
 
 struct CodecArgs {
-  bf16_t* x; uint8_t* msg;
+  void* x; uint8_t* msg;
   long long off_mask, off_scale, off_hi, off_lo;
   int B, S, H, k, mw;           // mw: mask words per window
   int hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo, ch_kind;
 };
 
 __device__ __forceinline__ int fmt_row_bytes(int fmt, int H) {
-  return fmt == FMT_BF16 ? 2 * H : fmt == FMT_INT8 ? H : fmt == FMT_INT4 ? H / 2 : H / 4;
+  return fmt == FMT_F32 ? 4 * H : fmt == FMT_BF16 ? 2 * H : fmt == FMT_INT8 ? H : fmt == FMT_INT4 ? H / 2 : H / 4;
 }
 
 __device__ __forceinline__ int wave_isum(int v) {
@@ -78,7 +80,11 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ i
 
 // Per-(window, channel) statistics over the window's rows (optionally only lo-class rows).
 // mode 0: max|x|, mode 1: mean(x) + 1e-8.   grid (B, ceil(H/64)), 256 threads = 4 row groups x 64 ch.
-__global__ __launch_bounds__(256) void channel_stats_kernel(const bf16_t* __restrict__ x,
+__device__ __forceinline__ float ldx(const bf16_t* p, size_t i) { return bf2f(p[i]); }
+__device__ __forceinline__ float ldx(const float* p, size_t i) { return p[i]; }
+
+template <class T>
+__global__ __launch_bounds__(256) void channel_stats_kernel(const T* __restrict__ x,
                                                             const uint32_t* __restrict__ mask, int mask_stride,
                                                             float* __restrict__ out, int S, int H, int mode,
                                                             int only_lo) {
@@ -89,7 +95,7 @@ __global__ __launch_bounds__(256) void channel_stats_kernel(const bf16_t* __rest
   if (c < H) {
     for (int j = rg; j < S; j += 4) {
       if (only_lo && !((mb[j >> 5] >> (j & 31)) & 1u)) continue;
-      const float xv = bf2f(x[((size_t)b * S + j) * H + c]);
+      const float xv = ldx(x, ((size_t)b * S + j) * H + c);
       acc = mode == 0 ? fmaxf(acc, fabsf(xv)) : acc + xv;
     }
   }
@@ -114,6 +120,22 @@ __global__ __launch_bounds__(256) void rowmax_kernel(const float* __restrict__ i
 
 // ---------------------------------------------------------------------------------------------
 template <int NCH>
+__device__ __forceinline__ void load_row8(const float* __restrict__ src, int H, float (&v)[NCH][8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < H) {
+      const f32x4_t a = *(const f32x4_t*)(src + col), b = *(const f32x4_t*)(src + col + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[c][e] = a[e]; v[c][4 + e] = b[e]; }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
+    }
+  }
+}
+template <int NCH>
 __device__ __forceinline__ void load_row8(const bf16_t* __restrict__ src, int H, float (&v)[NCH][8]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -132,7 +154,7 @@ __device__ __forceinline__ void load_row8(const bf16_t* __restrict__ src, int H,
 
 __device__ __forceinline__ float qround(float t, float qmax, float qmin) { return fminf(fmaxf(rintf(t), qmin), qmax); }
 
-template <int NCH>
+template <int NCH, class T>
 __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.B * a.S) return;
@@ -147,13 +169,14 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
   uint8_t* dst = is_lo ? a.msg + a.off_lo + ((size_t)b * a.k + slot_lo) * rb
                        : a.msg + a.off_hi + ((size_t)b * (a.S - a.k) + (j - slot_lo)) * rb;
   float v[NCH][8];
-  load_row8<NCH>(a.x + (size_t)row * a.H, a.H, v);
+  load_row8<NCH>((const T*)a.x + (size_t)row * a.H, a.H, v);
   float* scales = (float*)(a.msg + a.off_scale);
 
   // scale / quantiser for this row
   float inv = 0.f, mul = 0.f;  // code = round(x * inv) for token & channel; window mode uses ref formula
-  if (fmt == FMT_BF16 && a.scale_mode == SC_TOKEN && lane == 0) scales[row] = 0.f;
-  if (fmt != FMT_BF16) {
+  const bool raw = fmt == FMT_BF16 || fmt == FMT_F32;
+  if (raw && a.scale_mode == SC_TOKEN && lane == 0) scales[row] = 0.f;
+  if (!raw) {
     if (a.scale_mode == SC_TOKEN) {
       float am = 0.f;
 #pragma unroll
@@ -175,6 +198,11 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
     const int col = (c * 64 + lane) * 8;
     if (col >= a.H) continue;
     int q[8];
+    if (fmt == FMT_F32) {
+      *(f32x4_t*)(dst + col * 4) = f32x4_t{v[c][0], v[c][1], v[c][2], v[c][3]};
+      *(f32x4_t*)(dst + col * 4 + 16) = f32x4_t{v[c][4], v[c][5], v[c][6], v[c][7]};
+      continue;
+    }
     if (fmt == FMT_BF16) {
       u32x4_t w;
 #pragma unroll
@@ -220,7 +248,18 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
   }
 }
 
-template <int NCH>
+__device__ __forceinline__ void store8(bf16_t* dst, const float (&o)[8]) {
+  u32x4_t w;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) w[e] = pack_bf2(o[2 * e], o[2 * e + 1]);
+  *(u32x4_t*)dst = w;
+}
+__device__ __forceinline__ void store8(float* dst, const float (&o)[8]) {
+  *(f32x4_t*)dst = f32x4_t{o[0], o[1], o[2], o[3]};
+  *(f32x4_t*)(dst + 4) = f32x4_t{o[4], o[5], o[6], o[7]};
+}
+
+template <int NCH, class T>
 __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.B * a.S) return;
@@ -236,17 +275,27 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
                              : a.msg + a.off_hi + ((size_t)b * (a.S - a.k) + (j - slot_lo)) * rb;
   const float* scales = (const float*)(a.msg + a.off_scale);
   float s = 0.f;
-  if (fmt != FMT_BF16) {
+  if (fmt != FMT_BF16 && fmt != FMT_F32) {
     if (a.scale_mode == SC_TOKEN) s = scales[row];
     else if (a.scale_mode == SC_WINDOW) s = scales[b];
   }
-  bf16_t* out = a.x + (size_t)row * a.H;
+  T* out = (T*)a.x + (size_t)row * a.H;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (c * 64 + lane) * 8;
     if (col >= a.H) continue;
-    if (fmt == FMT_BF16) {
-      *(u32x4_t*)(out + col) = *(const u32x4_t*)(src + col * 2);
+    if (fmt == FMT_BF16 || fmt == FMT_F32) {
+      float o[8];
+      if (fmt == FMT_F32) {
+        const f32x4_t x0 = *(const f32x4_t*)(src + col * 4), x1 = *(const f32x4_t*)(src + col * 4 + 16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[e] = x0[e]; o[4 + e] = x1[e]; }
+      } else {
+        const u32x4_t w = *(const u32x4_t*)(src + col * 2);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[2 * e] = bf_lo(w[e]); o[2 * e + 1] = bf_hi(w[e]); }
+      }
+      store8(out + col, o);
       continue;
     }
     int q[8];
@@ -277,10 +326,7 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
         o[e] = (a.ch_kind == CH_MEAN || qmax == 1) ? qf * sc : qf * sc / (float)qmax;
       }
     }
-    u32x4_t w;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) w[e] = pack_bf2(o[2 * e], o[2 * e + 1]);
-    *(u32x4_t*)(out + col) = w;
+    store8(out + col, o);
   }
 }
 
@@ -298,7 +344,7 @@ static CodecArgs make_args(void* x, void* msg, long long om, long long os, long 
                            int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo,
                            int ch_kind) {
   CodecArgs a;
-  a.x = (bf16_t*)x; a.msg = (uint8_t*)msg;
+  a.x = x; a.msg = (uint8_t*)msg;
   a.off_mask = om; a.off_scale = os; a.off_hi = oh; a.off_lo = ol;
   a.B = B; a.S = S; a.H = H; a.k = k; a.mw = ((S + 63) / 64) * 2;
   a.hi_fmt = hi_fmt; a.lo_fmt = lo_fmt; a.scale_mode = scale_mode; a.qmax_hi = qmax_hi; a.qmax_lo = qmax_lo;
@@ -322,11 +368,16 @@ EDGE_API int edge_set_mask(void* msg, long long off_mask, int B, int S, int all_
 
 // channel_stats: mode 0 max|x|, 1 mean+1e-8; only_lo restricts to lo-class rows.  out: [B, H] fp32
 EDGE_API int edge_channel_stats(const void* x, const void* msg, long long off_mask, float* out, int B, int S, int H,
-                                int mode, int only_lo, hipStream_t st) {
+                                int mode, int only_lo, int x_f32, hipStream_t st) {
   if (B <= 0) return 0;
   const int mw = ((S + 63) / 64) * 2;
-  hipLaunchKernelGGL(channel_stats_kernel, dim3(B, (H + 63) / 64), dim3(256), 0, st, (const bf16_t*)x,
-                     (const uint32_t*)((const uint8_t*)msg + off_mask), mw, out, S, H, mode, only_lo);
+  const uint32_t* mask = (const uint32_t*)((const uint8_t*)msg + off_mask);
+  if (x_f32)
+    hipLaunchKernelGGL(channel_stats_kernel<float>, dim3(B, (H + 63) / 64), dim3(256), 0, st, (const float*)x, mask,
+                       mw, out, S, H, mode, only_lo);
+  else
+    hipLaunchKernelGGL(channel_stats_kernel<bf16_t>, dim3(B, (H + 63) / 64), dim3(256), 0, st, (const bf16_t*)x, mask,
+                       mw, out, S, H, mode, only_lo);
   return (int)hipGetLastError();
 }
 
@@ -338,24 +389,26 @@ EDGE_API int edge_rowmax(const float* in, float* out, int R, int H, hipStream_t 
 
 EDGE_API int edge_pack(const void* x, void* msg, long long om, long long os, long long oh, long long ol, int B, int S,
                        int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo, int ch_kind,
-                       hipStream_t st) {
+                       int x_f32, hipStream_t st) {
   if (H % 32) return (int)hipErrorInvalidValue;
   CodecArgs a = make_args((void*)x, msg, om, os, oh, ol, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
                           ch_kind);
   const int rows = B * S;
   if (rows <= 0) return 0;
-  DISPATCH_NCH(H, hipLaunchKernelGGL(pack_kernel<NCH>, dim3((rows + 3) / 4), dim3(256), 0, st, a));
+  if (x_f32) DISPATCH_NCH(H, hipLaunchKernelGGL((pack_kernel<NCH, float>), dim3((rows + 3) / 4), dim3(256), 0, st, a));
+  else DISPATCH_NCH(H, hipLaunchKernelGGL((pack_kernel<NCH, bf16_t>), dim3((rows + 3) / 4), dim3(256), 0, st, a));
   return (int)hipGetLastError();
 }
 
 EDGE_API int edge_unpack(void* x, const void* msg, long long om, long long os, long long oh, long long ol, int B,
                          int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo,
-                         int ch_kind, hipStream_t st) {
+                         int ch_kind, int x_f32, hipStream_t st) {
   if (H % 32) return (int)hipErrorInvalidValue;
   CodecArgs a = make_args(x, (void*)msg, om, os, oh, ol, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
                           ch_kind);
   const int rows = B * S;
   if (rows <= 0) return 0;
-  DISPATCH_NCH(H, hipLaunchKernelGGL(unpack_kernel<NCH>, dim3((rows + 3) / 4), dim3(256), 0, st, a));
+  if (x_f32) DISPATCH_NCH(H, hipLaunchKernelGGL((unpack_kernel<NCH, float>), dim3((rows + 3) / 4), dim3(256), 0, st, a));
+  else DISPATCH_NCH(H, hipLaunchKernelGGL((unpack_kernel<NCH, bf16_t>), dim3((rows + 3) / 4), dim3(256), 0, st, a));
   return (int)hipGetLastError();
 }

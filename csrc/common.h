@@ -24,6 +24,58 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// ---- fp32 execution by split-bf16 MFMA ("x6") -------------------------------------------------------------
+// x = x0 + x1 + x2 exactly, each a bf16 (8 significant bits; the residual after two round-to-nearest steps has at
+// most 8 significant bits left).  A product x*y is then sum_{i+j<=2} xi*yj up to terms of relative size 2^-27,
+// below fp32's own rounding (2^-24), and every bf16 x bf16 product is exact in the fp32 MFMA accumulator.
+// The six terms are laid out as a K-concatenation, so an ordinary bf16 MFMA GEMM over K' = 6K computes the
+// fp32-accurate product:  A' row = [a2 | a0 | a1 | a1 | a0 | a0],  B' row = [b0 | b2 | b1 | b0 | b1 | b0]
+// (the small terms first: they are accumulated before the large ones).  X6_APLANE / X6_BPLANE give the plane
+// of each K-block.  Activations that feed a GEMM are stored in this "X6" layout [rows, 6K] by their producer.
+constexpr int X6_TERMS = 6;
+__device__ __forceinline__ void split3(float x, float& p0, float& p1, float& p2) {
+  p0 = (float)(__bf16)x;
+  const float r = x - p0;
+  p1 = (float)(__bf16)r;
+  p2 = (float)(__bf16)(r - p1);
+}
+// Store 4 consecutive values v[0..3] at column `col` of an X6 row (block width K): six 8-byte stores.
+__device__ __forceinline__ void store_x6_4(bf16_t* __restrict__ row, int K, int col, const float (&v)[4]) {
+  float p[3][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) split3(v[e], p[0][e], p[1][e], p[2][e]);
+  u32x2_t w[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    w[i][0] = pack_bf2(p[i][0], p[i][1]);
+    w[i][1] = pack_bf2(p[i][2], p[i][3]);
+  }
+  // A-side plane order of the six K-blocks: 2 0 1 1 0 0
+  *(u32x2_t*)(row + 0 * (size_t)K + col) = w[2];
+  *(u32x2_t*)(row + 1 * (size_t)K + col) = w[0];
+  *(u32x2_t*)(row + 2 * (size_t)K + col) = w[1];
+  *(u32x2_t*)(row + 3 * (size_t)K + col) = w[1];
+  *(u32x2_t*)(row + 4 * (size_t)K + col) = w[0];
+  *(u32x2_t*)(row + 5 * (size_t)K + col) = w[0];
+}
+// 8 consecutive values: six 16-byte stores.
+__device__ __forceinline__ void store_x6_8(bf16_t* __restrict__ row, int K, int col, const float (&v)[8]) {
+  float p[3][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) split3(v[e], p[0][e], p[1][e], p[2][e]);
+  u32x4_t w[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[i][e] = pack_bf2(p[i][2 * e], p[i][2 * e + 1]);
+  *(u32x4_t*)(row + 0 * (size_t)K + col) = w[2];
+  *(u32x4_t*)(row + 1 * (size_t)K + col) = w[0];
+  *(u32x4_t*)(row + 2 * (size_t)K + col) = w[1];
+  *(u32x4_t*)(row + 3 * (size_t)K + col) = w[1];
+  *(u32x4_t*)(row + 4 * (size_t)K + col) = w[0];
+  *(u32x4_t*)(row + 5 * (size_t)K + col) = w[0];
+}
+
 // silu(x) = x / (1 + e^-x) on the hardware transcendentals (v_exp_f32, v_rcp_f32, ~1 ulp): a plain '/' compiles
 // to the IEEE division sequence (2 v_div_scale + v_div_fmas + v_div_fixup + v_rcp + FMAs), which made the
 // SwiGLU epilogue of the gate/up GEMM cost ~20 VALU per output.  Saturates correctly: e^-x = inf -> 0.

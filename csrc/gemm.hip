@@ -16,12 +16,24 @@
 #include <algorithm>
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_GELU = 4, EPI_SWIGLU = 5,
-       EPI_QKV_ROPE = 6, EPI_LSE = 7 };
+       EPI_QKV_ROPE = 6, EPI_LSE = 7,
+       // fp32 execution (operands in the X6 split-bf16 layout, common.h; K is the concatenated 6K): fp32 outputs,
+       // fp32 bias / residual, or X6-layout outputs for epilogues whose result feeds the next GEMM
+       EPI_F32 = 8, EPI_F32_BIAS = 9, EPI_F32_RESID = 10, EPI_F32_BIAS_RESID = 11, EPI_X6_BIAS_GELU = 12,
+       EPI_X6_SWIGLU = 13, EPI_F32_QKV_ROPE = 14 };
+constexpr bool epi_f32(int e) { return e >= EPI_F32; }
+constexpr bool epi_plain(int e) {  // none / bias / residual epilogues (the 256x224 kernel's set)
+  return e == EPI_NONE || e == EPI_BIAS || e == EPI_RESID || e == EPI_BIAS_RESID || e == EPI_F32 ||
+         e == EPI_F32_BIAS || e == EPI_F32_RESID || e == EPI_F32_BIAS_RESID;
+}
 
 struct GemmArgs {
   const bf16_t* A; const bf16_t* B; bf16_t* C;
   int M, N, K, lda, ldb, ldc;
   const bf16_t* bias; const bf16_t* resid; int ldr;
+  // fp32 epilogues: fp32 output / bias / residual (C may alias resid), X6 outputs go to C with ldc = 6 * width
+  float* Cf; const float* biasf; const float* residf;
+  float* qf; float* kf; float* vtf;
   // QKV_ROPE
   bf16_t* qout; bf16_t* kout; bf16_t* vtout;
   const float* cosT; const float* sinT;
@@ -104,6 +116,131 @@ __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
   return *(const bf16x8_t*)(lds + r * 128 + ((c ^ swz(r)) << 4));
 }
 
+// ---- fp32-execution epilogues (EPI >= EPI_F32).  Same ownership as gemm_epilogue below: lane owns rows
+// m0 + wm*WTM + i*16 + (lane&15) and columns nw + j*16 + 4*(lane>>4) + r of the wave's 64-column slab, so every
+// output is 4 consecutive fp32 values (one 16-byte store) or 4 consecutive values of each of the six X6 blocks.
+template <int EPI, int RH, class CF>
+__device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&acc)[CF::MI][4], int m0, int nw,
+                                                  int lane, int wm) {
+  constexpr int MI = CF::MI;
+  const int g = lane >> 4;
+  if constexpr (EPI == EPI_F32_QKV_ROPE) {
+    const int head = nw / 64;  // global head slot in [q heads | k heads | v heads]
+    const bool is_v = head >= a.Hq + a.Hkv;
+    f32x4_t bw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bw[j] = *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
+      const int mm = m < a.M ? m : a.M - 1;
+      const int b = mm / a.S, pos = mm - b * a.S;
+      float v[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[j][r] = acc[i][j][r] + bw[j][r];
+      if constexpr (RH >= 16) {
+        constexpr int DJ = RH / 16;
+        if (!is_v) {
+          float o[4][4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if (j * 16 >= 2 * RH) { o[j][r] = v[j][r]; continue; }
+              const bool lo = j * 16 < RH;
+              const int fi = (lo ? j : j - DJ) * 16 + g * 4 + r;
+              const float c = a.cosT[pos * RH + fi], sv = a.sinT[pos * RH + fi];
+              const float y = lo ? v[(j + DJ) & 3][r] : v[(j - DJ) & 3][r];
+              o[j][r] = lo ? (v[j][r] * c - y * sv) : (v[j][r] * c + y * sv);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][r] = o[j][r];
+        }
+      } else if constexpr (RH > 0) {
+        float p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[r] = __shfl_xor(v[0][r], 4 * RH, 64);
+        if (!is_v) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int d = g * 4 + r;
+            if (d < 2 * RH) {
+              const bool lo = d < RH;
+              const int fi = lo ? d : d - RH;
+              const float c = a.cosT[pos * RH + fi], s = a.sinT[pos * RH + fi];
+              v[0][r] = lo ? (v[0][r] * c - p[r] * s) : (v[0][r] * c + p[r] * s);
+            }
+          }
+        }
+      }
+      if (m >= a.M) continue;
+      if (!is_v) {
+        const float sc = head < a.Hq ? a.q_scale : 1.f;
+        float* dst = head < a.Hq ? a.qf + (((size_t)b * a.Hq + head) * a.S + pos) * 64
+                                 : a.kf + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *(f32x4_t*)(dst + j * 16 + g * 4) = f32x4_t{v[j][0] * sc, v[j][1] * sc, v[j][2] * sc, v[j][3] * sc};
+      } else {
+        float* dst = a.vtf + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dst[(size_t)(j * 16 + g * 4 + r) * a.s_pad] = v[j][r];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
+    if (m >= a.M) continue;
+    if constexpr (EPI == EPI_X6_SWIGLU) {
+      // gate/up interleaved in 16-column blocks: acc[i][2p] gate, acc[i][2p+1] up of output columns
+      // nw/2 + 16p + 4g + r; silu in full precision (the fast reciprocal/exp path is for bf16 outputs)
+      bf16_t* row = a.C + (size_t)m * a.ldc;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gg = acc[i][2 * p][r], uu = acc[i][2 * p + 1][r];
+          o[r] = gg / (1.f + expf(-gg)) * uu;
+        }
+        store_x6_4(row, a.N / 2, nw / 2 + p * 16 + g * 4, o);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nw + j * 16 + g * 4;
+        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID || EPI == EPI_X6_BIAS_GELU) {
+          const f32x4_t bw = *(const f32x4_t*)(a.biasf + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] += bw[r];
+        }
+        if constexpr (EPI == EPI_X6_BIAS_GELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
+          store_x6_4(a.C + (size_t)m * a.ldc, a.N, n, o);
+        } else {
+          if constexpr (EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID) {
+            const f32x4_t rw = *(const f32x4_t*)(a.residf + (size_t)m * a.ldr + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] += rw[r];
+          }
+          *(f32x4_t*)(a.Cf + (size_t)m * a.ldc + n) = f32x4_t{o[0], o[1], o[2], o[3]};
+        }
+      }
+    }
+  }
+}
+
 // ---- epilogue: lane owns rows m0 + wm*WTM + i*16 + (lane&15), columns n0 + wn*64 + j*16 + 4*(lane>>4) + r
 template <int EPI, int RH, class CF>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[CF::MI][4], int m0, int n0,
@@ -113,6 +250,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
   const int g = lane >> 4;
   const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
   if (nw >= a.N) return;        // slab beyond N in a partial last column tile (wave-uniform)
+  if constexpr (epi_f32(EPI)) {
+    return gemm_epilogue_f32<EPI, RH, CF>(a, acc, m0, nw, lane, wm);
+  }
 
   if (a.rscale || a.ssq_in) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
 #pragma unroll
@@ -1018,6 +1158,40 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
   const int g = lane >> 4;
   const int nw = n0 + wn * 112;
   const int P = a.N / 112;
+  if constexpr (epi_f32(EPI)) {
+    // fp32 execution: fp32 bias / residual / output.  Residuals are loaded two row groups at a time (all four
+    // would be 112 VGPRs and spill at this kernel's 256-register budget), each pair before that pair's stores.
+    constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID;
+#pragma unroll
+    for (int ih = 0; ih < w7::MI; ih += 2) {
+      f32x4_t rv[2][w7::NJ];
+      if constexpr (RESF) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          int mr = m0 + wm * 64 + (ih + i) * 16 + (lane & 15);
+          mr = mr < a.M ? mr : a.M - 1;
+          const float* rrow = a.residf + (size_t)mr * a.ldr + nw + g * 4;
+#pragma unroll
+          for (int j = 0; j < w7::NJ; ++j) rv[i][j] = *(const f32x4_t*)(rrow + j * 16);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int m = m0 + wm * 64 + (ih + i) * 16 + (lane & 15);
+        if (m >= a.M) continue;
+        float* row = a.Cf + (size_t)m * a.ldc + nw + g * 4;
+#pragma unroll
+        for (int j = 0; j < w7::NJ; ++j) {
+          f32x4_t o = acc[ih + i][j];
+          if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID)
+            o += *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
+          if constexpr (RESF) o += rv[i][j];
+          *(f32x4_t*)(row + j * 16) = o;
+        }
+      }
+    }
+    return;
+  }
   constexpr bool RES = EPI == EPI_RESID || EPI == EPI_BIAS_RESID;
   // every residual load of the slab is issued up front (4 x 7 x 8 B per lane): one global round trip instead of
   // one per 16-row group (the per-group load -> wait -> use chain cost ~30 % of the O-proj GEMM's time)
@@ -1245,8 +1419,13 @@ __global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
   }
 }
 
+// Timing ablations that produce wrong results (skipped epilogues, pp-kernel variants 5-9) are compiled only into a
+// tuning build (-DEDGE_TUNING_BUILD=1, tools/gemm_bench.py); the production library cannot reach them.
+#ifndef EDGE_TUNING_BUILD
+#define EDGE_TUNING_BUILD 0
+#endif
 static int g_tile_override = 0;  // 0 auto, 128, 224 or 256 (tests / tuning)
-static int g_skip_epi = 0;       // timing ablation (wrong results)
+static int g_skip_epi = 0;       // timing ablation (wrong results; tuning build only)
 static int g_rs_lds = 1;         // row scales through LDS in the persistent 256x256 kernel (A/B switch)
 static int g_lse256 = 1;         // LM-head LSE GEMM on the persistent 256x256 tiles (A/B switch)
 static int g_walk = 1;           // persistent tile walk (TileWalk): 1 chunked per XCD, 0 strided
@@ -1314,7 +1493,7 @@ static int g_w7 = 1;  // 256x224 tiles for N % 224 == 0 shapes that 256 does not
 // The 256x224 kernel takes the plain / bias / residual epilogues of N % 224 == 0 shapes that 256 does not
 // divide, when 256-row tiles fill the chip; tests force it at small M with tile override 224.
 static bool use_w7(int M, int N, int K, int epi) {
-  if (!(epi == EPI_NONE || epi == EPI_BIAS || epi == EPI_RESID || epi == EPI_BIAS_RESID)) return false;
+  if (!epi_plain(epi)) return false;
   if (N % 224 || N % 256 == 0 || K < 2 * BK) return false;
   if (g_tile_override) return g_tile_override == 224;
   return g_w7 && (long long)((M + 255) / 256) * (N / 224) >= 256;
@@ -1338,6 +1517,7 @@ static int launch_w7m(const GemmArgs& a, hipStream_t st) {
 
 template <int EPI>
 static int launch_w7(const GemmArgs& a, hipStream_t st) {
+  if constexpr (epi_f32(EPI)) return launch_w7m<EPI, 0>(a, st);  // the modes A/B the bf16 epilogue's traffic
   switch (g_w7_mode) {
     case 1: return launch_w7m<EPI, 1>(a, st);
     case 2: return launch_w7m<EPI, 2>(a, st);
@@ -1350,15 +1530,15 @@ template <int EPI, int RH = 0>
 static int launch(const GemmArgs& args, hipStream_t st) {
   GemmArgs a = args;
   a.walk = g_walk;
-  a.skip_epi = g_skip_epi;
+  a.skip_epi = EDGE_TUNING_BUILD ? g_skip_epi : 0;
   a.rs_lds = g_rs_lds;
-  if constexpr (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_RESID || EPI == EPI_BIAS_RESID) {
+  if constexpr (epi_plain(EPI)) {
     if (use_w7(a.M, a.N, a.K, EPI)) return launch_w7<EPI>(a, st);
   }
   // 256x256 persistent tiles when the shape can fill the chip with them (halves L2->LDS traffic per
   // FLOP), 128x128 otherwise (N not a multiple of 256, or too few 256-row panels).  The QKV/RoPE and
   // LSE epilogues stay on 128x128 (register budget; their N is never a multiple of 256 in practice).
-  if constexpr (EPI == EPI_QKV_ROPE) {
+  if constexpr (EPI == EPI_QKV_ROPE || EPI == EPI_F32_QKV_ROPE) {
     return launch_cfg<EPI, RH, C128>(a, st);
   } else if constexpr (EPI == EPI_LSE) {
     // LM head on the scored rows (M = 2048 at the bench batch, N = vocab): 256x256 persistent tiles when they
@@ -1369,22 +1549,28 @@ static int launch(const GemmArgs& args, hipStream_t st) {
   } else {
     // a partial last column tile (N % 256 == 128) wastes at most 1/(2*tn) of the MFMA work
     const int tn = (a.N + 255) / 256;
-    const bool fits = a.N % 256 == 0 || (a.N % 128 == 0 && tn >= 4 && EPI != EPI_SWIGLU);
+    const bool fits = a.N % 256 == 0 || (a.N % 128 == 0 && tn >= 4 && EPI != EPI_SWIGLU && EPI != EPI_X6_SWIGLU);
     const bool big = fits && ((long long)((a.M + 255) / 256) * tn >= 256);
     const bool use256 = g_tile_override ? g_tile_override == 256 && fits : big;
     if (!use256) return launch_cfg<EPI, RH, C128>(a, st);
     const int variant = g_c256_variant >= 0 ? g_c256_variant : (a.K >= 2048 ? 4 : 1);
-    switch (variant) {
-      case 0: return launch_cfg<EPI, RH, C256, false>(a, st);
-      case 2: return launch_ring<EPI, RH, false>(a, st);
-      case 3: return launch_ring<EPI, RH, true>(a, st);
-      case 4: return launch_pp<EPI, RH>(a, st);
-      case 5: return launch_pp<EPI, RH, 1>(a, st);  // timing ablations (wrong results)
-      case 6: return launch_pp<EPI, RH, 2>(a, st);
-      case 7: return launch_pp<EPI, RH, 3>(a, st);
-      case 8: return launch_pp<EPI, RH, 0, 5>(a, st);
-      case 9: return launch_pp<EPI, RH, 4>(a, st);
-      default: return launch_cfg<EPI, RH, C256, true>(a, st);
+    if constexpr (epi_f32(EPI)) {  // fp32 execution: K is always >= 6 x 64; the two production main loops only
+      return variant == 4 ? launch_pp<EPI, RH>(a, st) : launch_cfg<EPI, RH, C256, true>(a, st);
+    } else {
+      switch (variant) {
+        case 0: return launch_cfg<EPI, RH, C256, false>(a, st);
+        case 2: return launch_ring<EPI, RH, false>(a, st);
+        case 3: return launch_ring<EPI, RH, true>(a, st);
+        case 4: return launch_pp<EPI, RH>(a, st);
+        case 8: return launch_pp<EPI, RH, 0, 5>(a, st);  // 5-slot ring
+#if EDGE_TUNING_BUILD
+        case 5: return launch_pp<EPI, RH, 1>(a, st);  // timing ablations (wrong results)
+        case 6: return launch_pp<EPI, RH, 2>(a, st);
+        case 7: return launch_pp<EPI, RH, 3>(a, st);
+        case 9: return launch_pp<EPI, RH, 4>(a, st);
+#endif
+        default: return launch_cfg<EPI, RH, C256, true>(a, st);
+      }
     }
   }
 }
@@ -1410,6 +1596,7 @@ EDGE_API int edge_gemm_set_rs_lds(int on) {
 }
 
 EDGE_API int edge_gemm_set_skip_epi(int on) {
+  if (!EDGE_TUNING_BUILD && on) return (int)hipErrorNotSupported;
   g_skip_epi = on;
   return 0;
 }
@@ -1433,6 +1620,7 @@ EDGE_API int edge_gemm_ssq_parts(int M, int N, int K, int act, int has_bias, int
 }
 
 EDGE_API int edge_gemm_set_variant(int v) {
+  if (!EDGE_TUNING_BUILD && (v == 5 || v == 6 || v == 7 || v == 9)) return (int)hipErrorNotSupported;
   g_c256_variant = v;
   return 0;
 }
@@ -1490,6 +1678,62 @@ EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, 
     case 16: return launch<EPI_QKV_ROPE, 8>(a, st);
     case 32: return launch<EPI_QKV_ROPE, 16>(a, st);
     case 64: return launch<EPI_QKV_ROPE, 32>(a, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// fp32 execution (X6 operands, common.h): A [M, 6K], B [N, 6K] split-bf16 K-concatenations, so the K of the GEMM
+// is Kx = 6K.  act 0 none -> fp32 C [M, ldc] (+ fp32 bias, + fp32 residual, which may alias C); act 1 bias + GELU
+// -> X6 output [M, 6N] in C (bf16, ldc = 6N); act 2 interleaved SwiGLU -> X6 output [M, 6N/2] (ldc = 3N).
+EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, int Kx, int lda, int ldb, int ldc,
+                           const float* bias, const float* resid, int ldr, int act, hipStream_t st) {
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B;
+  a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.biasf = bias; a.residf = resid; a.ldr = ldr;
+  if (Kx % (X6_TERMS * BK)) return (int)hipErrorInvalidValue;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  if (((uintptr_t)C & 15) || ldc % 4 || (resid && (ldr % 4 || ((uintptr_t)resid & 15))) ||
+      (bias && ((uintptr_t)bias & 15)))
+    return (int)hipErrorInvalidValue;
+  if (act == 2) {
+    if (bias || resid || ldc != 3 * N) return (int)hipErrorInvalidValue;
+    a.C = (bf16_t*)C;
+    return launch<EPI_X6_SWIGLU>(a, st);
+  }
+  if (act == 1) {
+    if (resid || !bias || ldc != 6 * N) return (int)hipErrorInvalidValue;
+    a.C = (bf16_t*)C;
+    return launch<EPI_X6_BIAS_GELU>(a, st);
+  }
+  a.Cf = (float*)C;
+  if (bias && resid) return launch<EPI_F32_BIAS_RESID>(a, st);
+  if (bias) return launch<EPI_F32_BIAS>(a, st);
+  if (resid) return launch<EPI_F32_RESID>(a, st);
+  return launch<EPI_F32>(a, st);
+}
+
+// fp32 QKV projection + bias + RoPE + head-major scatter: X [M, 6K] (X6), W [(Hq+2Hkv)*64, 6K] (X6), fp32 bias,
+// fp32 outputs q [B,Hq,S,64] (x q_scale), k [B,Hkv,S,64], vt [B,Hkv,64,s_pad].
+EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* bias, float* q, float* k, float* vt,
+                                    const float* cosT, const float* sinT, int M, int Kx, int S, int Hq, int Hkv,
+                                    int rot_dim, int s_pad, float q_scale, hipStream_t st) {
+  GemmArgs a{};
+  a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
+  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = Kx; a.ldb = Kx;
+  a.biasf = bias; a.qf = q; a.kf = k; a.vtf = vt;
+  a.cosT = cosT; a.sinT = sinT; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.s_pad = s_pad;
+  a.q_scale = q_scale;
+  if (!bias || M % S || Kx % (X6_TERMS * BK) || ((uintptr_t)bias & 15)) return (int)hipErrorInvalidValue;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  switch (rot_dim) {
+    case 0: return launch<EPI_F32_QKV_ROPE, 0>(a, st);
+    case 8: return launch<EPI_F32_QKV_ROPE, 4>(a, st);
+    case 16: return launch<EPI_F32_QKV_ROPE, 8>(a, st);
+    case 32: return launch<EPI_F32_QKV_ROPE, 16>(a, st);
+    case 64: return launch<EPI_F32_QKV_ROPE, 32>(a, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

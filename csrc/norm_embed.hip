@@ -216,3 +216,179 @@ EDGE_API int edge_row_rscale(const float* ssq, float* rs, int R, int P, int H, f
   row_rscale_kernel<<<(R + 255) / 256, 256, 0, st>>>(ssq, rs, R, P, H, eps);
   return (int)hipGetLastError();
 }
+
+// =============================================================================================
+// fp32 execution mode: fp32 activations in, fp32 statistics, and GEMM-input outputs written in the X6 split-bf16
+// layout [R, 6H] (common.h) that the fp32-mode GEMMs consume (out_x6 = 0: plain fp32 [R, H] instead).
+template <int NCH>
+__device__ __forceinline__ void load_row_f32(const float* __restrict__ src, int H, float (&v)[NCH][8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < H) {
+      const f32x4_t a = *(const f32x4_t*)(src + col), b = *(const f32x4_t*)(src + col + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[c][j] = a[j]; v[c][4 + j] = b[j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+}
+
+template <int NCH>
+__device__ __forceinline__ void store_row_f32_or_x6(void* __restrict__ dst, int H, const float (&v)[NCH][8],
+                                                    bool x6) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col >= H) continue;
+    if (x6) {
+      store_x6_8((bf16_t*)dst, H, col, v[c]);
+    } else {
+      float* d = (float*)dst + col;
+      *(f32x4_t*)d = f32x4_t{v[c][0], v[c][1], v[c][2], v[c][3]};
+      *(f32x4_t*)(d + 4) = f32x4_t{v[c][4], v[c][5], v[c][6], v[c][7]};
+    }
+  }
+}
+
+__device__ __forceinline__ size_t out_row_elems(int H, bool x6) { return x6 ? (size_t)X6_TERMS * H : (size_t)H; }
+__device__ __forceinline__ void* out_row(void* y, size_t r, int H, bool x6) {
+  return x6 ? (void*)((bf16_t*)y + r * out_row_elems(H, true)) : (void*)((float*)y + r * (size_t)H);
+}
+
+// HF Qwen2RMSNorm in fp32: y = w * (x * rsqrt(mean(x^2) + eps)).
+template <int NCH>
+__global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          void* __restrict__ y, const int* __restrict__ rows, int R,
+                                                          int H, float eps, int x6) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int src_row = rows ? rows[r] : r;
+  float v[NCH][8], g[NCH][8];
+  load_row_f32<NCH>(x + (size_t)src_row * H, H, v);
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss = fmaf(v[c][j], v[c][j], ss);
+  ss = wave_sum(ss);
+  const float rs = 1.f / sqrtf(ss / (float)H + eps);
+  load_row_f32<NCH>(w, H, g);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[c][j] = g[c][j] * (v[c][j] * rs);
+  store_row_f32_or_x6<NCH>(out_row(y, r, H, x6), H, v, x6);
+}
+
+template <int NCH, bool DUAL>
+__global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* __restrict__ x, const float* __restrict__ w1,
+                                                            const float* __restrict__ b1, const float* __restrict__ w2,
+                                                            const float* __restrict__ b2, void* __restrict__ y1,
+                                                            void* __restrict__ y2, const int* __restrict__ rows, int R,
+                                                            int H, float eps, int x6) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int src_row = rows ? rows[r] : r;
+  const int lane = threadIdx.x & 63;
+  float v[NCH][8], g[NCH][8], b[NCH][8], o[NCH][8];
+  load_row_f32<NCH>(x + (size_t)src_row * H, H, v);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[c][j];
+  const float mean = wave_sum(s) / (float)H;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const bool ok = (c * 64 + lane) * 8 < H;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = v[c][j] - mean;
+      v[c][j] = d;
+      ss += ok ? d * d : 0.f;
+    }
+  }
+  const float rs = 1.f / sqrtf(wave_sum(ss) / (float)H + eps);
+  load_row_f32<NCH>(w1, H, g);
+  load_row_f32<NCH>(b1, H, b);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[c][j] = fmaf(v[c][j] * rs, g[c][j], b[c][j]);
+  store_row_f32_or_x6<NCH>(out_row(y1, r, H, x6), H, o, x6);
+  if (DUAL) {
+    load_row_f32<NCH>(w2, H, g);
+    load_row_f32<NCH>(b2, H, b);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[c][j] = fmaf(v[c][j] * rs, g[c][j], b[c][j]);
+    store_row_f32_or_x6<NCH>(out_row(y2, r, H, x6), H, o, x6);
+  }
+}
+
+// fp32 [R, H] (rows optionally gathered) -> X6 [R, 6H]
+template <int NCH>
+__global__ __launch_bounds__(256) void split6_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                     const int* __restrict__ rows, int R, int H) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  float v[NCH][8];
+  load_row_f32<NCH>(x + (size_t)(rows ? rows[r] : r) * H, H, v);
+  store_row_f32_or_x6<NCH>(y + (size_t)r * X6_TERMS * H, H, v, true);
+}
+
+__global__ __launch_bounds__(256) void embedding_f32_kernel(const int64_t* __restrict__ ids,
+                                                            const float* __restrict__ table, float* __restrict__ out,
+                                                            int T, int H, int V) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= T) return;
+  int64_t id = ids[r];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+  const f32x4_t* src = (const f32x4_t*)(table + (size_t)id * H);
+  f32x4_t* dst = (f32x4_t*)(out + (size_t)r * H);
+  for (int c = threadIdx.x & 63; c < H / 4; c += 64) dst[c] = src[c];
+}
+
+EDGE_API int edge_rmsnorm_f32(const float* x, const float* w, void* y, const int* rows, int R, int H, float eps,
+                              int out_x6, hipStream_t st) {
+  if (H % 8 || R <= 0) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+  dim3 grid((R + 3) / 4);
+  DISPATCH_NCH(H, rmsnorm_f32_kernel<NCH><<<grid, 256, 0, st>>>(x, w, y, rows, R, H, eps, out_x6));
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_layernorm_f32(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                                void* y1, void* y2, const int* rows, int R, int H, float eps, int out_x6,
+                                hipStream_t st) {
+  if (H % 8 || R <= 0) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+  dim3 grid((R + 3) / 4);
+  if (y2) {
+    DISPATCH_NCH(H, (layernorm_f32_kernel<NCH, true><<<grid, 256, 0, st>>>(x, w1, b1, w2, b2, y1, y2, rows, R, H, eps,
+                                                                           out_x6)));
+  } else {
+    DISPATCH_NCH(H, (layernorm_f32_kernel<NCH, false><<<grid, 256, 0, st>>>(x, w1, b1, nullptr, nullptr, y1, nullptr,
+                                                                            rows, R, H, eps, out_x6)));
+  }
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_split6(const float* x, void* y, const int* rows, int R, int H, hipStream_t st) {
+  if (H % 8 || R <= 0) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+  DISPATCH_NCH(H, split6_kernel<NCH><<<(R + 3) / 4, 256, 0, st>>>(x, (bf16_t*)y, rows, R, H));
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_embedding_f32(const int64_t* ids, const float* table, float* out, int T, int H, int V,
+                                hipStream_t st) {
+  if (H % 4) return (int)hipErrorInvalidValue;
+  if (T <= 0) return 0;
+  embedding_f32_kernel<<<(T + 3) / 4, 256, 0, st>>>(ids, table, out, T, H, V);
+  return (int)hipGetLastError();
+}

@@ -342,8 +342,9 @@ def _args(spec, L):
 
 
 def _encode_gpu(x, spec, L, imp, msg):
-    if x.dtype != torch.bfloat16:
-        raise TypeError("GPU boundary codec expects bf16 activations")
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("GPU boundary codec expects bf16 or fp32 activations")
+    xf32 = int(x.dtype == torch.float32)
     st = stream()
     msg[:32].copy_(_gpu_header(spec, L, x.device))
     if 0 < L.k < L.S:
@@ -354,17 +355,19 @@ def _encode_gpu(x, spec, L, imp, msg):
         call("edge_set_mask", ptr(msg), L.off_mask, L.B, L.S, 1 if L.k >= L.S else 0, st)
     if spec.scale_mode == SC_WINDOW:
         tmp = torch.empty(L.B, L.H, dtype=torch.float32, device=x.device)
-        call("edge_channel_stats", ptr(x), ptr(msg), L.off_mask, ptr(tmp), L.B, L.S, L.H, CH_MAXABS, 1, st)
+        call("edge_channel_stats", ptr(x), ptr(msg), L.off_mask, ptr(tmp), L.B, L.S, L.H, CH_MAXABS, 1, xf32, st)
         call("edge_rowmax", ptr(tmp), msg.data_ptr() + L.off_scale, L.B, L.H, st)
     elif spec.scale_mode == SC_CHANNEL:
         call("edge_channel_stats", ptr(x), ptr(msg), L.off_mask, msg.data_ptr() + L.off_scale, L.B, L.S, L.H,
-             spec.ch_kind, 0, st)
-    call("edge_pack", ptr(x), ptr(msg), *_args(spec, L), st)
+             spec.ch_kind, 0, xf32, st)
+    call("edge_pack", ptr(x), ptr(msg), *_args(spec, L), xf32, st)
     return msg
 
 
 def _decode_gpu(msg, spec, L, out):
-    call("edge_unpack", ptr(out), ptr(msg), *_args(spec, L), stream())
+    if out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous():
+        raise TypeError("GPU boundary codec decodes into contiguous bf16 or fp32 activations")
+    call("edge_unpack", ptr(out), ptr(msg), *_args(spec, L), int(out.dtype == torch.float32), stream())
     return out
 
 

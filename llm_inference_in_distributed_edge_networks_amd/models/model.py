@@ -22,6 +22,15 @@ At a boundary layer the attention can additionally emit the statistics the
 importance scorers need (last-row probabilities, or row LSE + column sums), so
 the S x S attention map of the reference's second "eager" model copy
 (``Qwen2-0.5B/main.py:132-134``) is never materialised.
+
+Precision.  The reference evaluates fp32 models (``qwen_layer_wise.py:17`` and
+``pythia_model.py:25`` load without ``torch_dtype``).  On the GPU a model built with
+``dtype=torch.float32`` runs the fp32 execution mode: the residual stream, norms,
+attention, softmax statistics and the boundary codec are fp32, and every GEMM takes its
+operands in the X6 split-bf16 layout (``ops.reference.x6_act`` / ``x6_weight``: six bf16
+MFMA products per fp32 product, exact to 2^-27 relative).  Producers of GEMM inputs (norms,
+attention, the SwiGLU / GELU epilogues) write X6 directly; weights are expanded once at
+load.  ``dtype=torch.bfloat16`` is the faster bf16 mode.
 """
 from __future__ import annotations
 
@@ -44,13 +53,28 @@ class AttnStats:
     colsum: torch.Tensor | None = None    # [B, Hq, S] sum_i P[i, j]
 
 
+_X6_KEYS = ("wqkv", "wo", "wgu", "wd", "wfc", "wproj")
+
+
 class DecoderLM:
-    def __init__(self, cfg: ModelConfig, weights: dict, device="cpu", dtype=torch.float32):
+    def __init__(self, cfg: ModelConfig, weights: dict, device="cpu", dtype=torch.float32, x6: bool | None = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
         self.w = weights
         self.layers = weights["layers"]
+        # fp32 execution on the GPU: X6 operands (x6=True also runs the same op sequence on CPU, for tests)
+        self.x6 = (self.device.type == "cuda" and dtype == torch.float32) if x6 is None else bool(x6)
+        if self.x6:
+            if dtype != torch.float32:
+                raise ValueError("the X6 (fp32) execution mode needs fp32 weights")
+            for L in self.layers:
+                if L is not None:
+                    for k in _X6_KEYS:
+                        if k in L:
+                            L[k + "6"] = ops.reference.x6_weight(L[k])
+            if weights.get("head") is not None:
+                weights["head6"] = ops.reference.x6_weight(weights["head"])
         cos, sin = ops.rope_tables(cfg.max_position, cfg.rotary_dim, cfg.rope_theta)
         self.cos = cos.to(self.device).contiguous()
         self.sin = sin.to(self.device).contiguous()
@@ -68,7 +92,8 @@ class DecoderLM:
     # ------------------------------------------------------------------ construction
     @classmethod
     def random_init(cls, cfg: ModelConfig, seed: int = 0, device="cpu", dtype=torch.float32, std: float = 0.02,
-                    layers: range | None = None, with_embed: bool = True, with_head: bool = True):
+                    layers: range | None = None, with_embed: bool = True, with_head: bool = True,
+                    x6: bool | None = None):
         """Seeded random weights of the given architecture (HF ``_init_weights`` style: N(0, 0.02)).
 
         ``layers`` restricts allocation to a layer range (a pipeline stage only holds its own layers);
@@ -118,7 +143,7 @@ class DecoderLM:
             w["head"] = fin(hd) if with_head else None
         if not with_embed and not cfg.tie_embeddings:
             w["embed"] = None
-        return cls(cfg, w, device, dtype)
+        return cls(cfg, w, device, dtype, x6=x6)
 
     @classmethod
     def from_state_dict(cls, cfg: ModelConfig, sd: dict, device="cpu", dtype=torch.float32,
@@ -248,6 +273,8 @@ class DecoderLM:
         cfg, L = self.cfg, self.layers[i]
         if L is None:
             raise RuntimeError(f"layer {i} is not resident on this stage")
+        if self.x6:
+            return self._layer_x6(i, x, B, S, stats)
         Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
         if self.fuse_norm:
             ssq = getattr(x, "_edge_ssq", None)
@@ -286,6 +313,46 @@ class DecoderLM:
             y = ops.linear(f, L["wproj"], L["bproj"], residual=y, out=y)
         return y, st
 
+    @staticmethod
+    def _stat_kinds(stats):
+        kinds = () if stats is None else ((stats,) if isinstance(stats, str) else tuple(stats))
+        for kd in kinds:
+            if kd not in ("lastrow", "colsum"):
+                raise ValueError(kd)
+        return kinds
+
+    def _attn_x6(self, i, x, B, S, need_lse=False, n_rows=None):
+        """fp32 mode: norm(s) -> X6 QKV GEMM (+bias+RoPE) -> fp32 attention with X6 output."""
+        cfg, L = self.cfg, self.layers[i]
+        h26 = None
+        if cfg.arch == "qwen2":
+            h6 = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps, x6=True)
+        else:
+            h6, h26 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps, x6=True)
+        q, k, vt = ops.qkv_rope_x6(h6, L["wqkv6"], L["bqkv"], self.cos, self.sin, B, S, cfg.num_heads,
+                                   cfg.num_kv_heads, cfg.head_dim, cfg.rotary_dim, self.q_scale)
+        o6, lse = ops.attention(q, k, vt, S, need_lse=need_lse, n_rows=n_rows, x6=True)
+        return q, k, o6, lse, h26
+
+    def _mlp_x6(self, i, o6, x, h26):
+        cfg, L = self.cfg, self.layers[i]
+        if cfg.arch == "qwen2":
+            y = ops.linear_x6(o6, L["wo6"], residual=x)
+            a6 = ops.linear_x6(ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps, x6=True), L["wgu6"], act="swiglu_il")
+            return ops.linear_x6(a6, L["wd6"], residual=y, out=y)
+        y = ops.linear_x6(o6, L["wo6"], L["bo"], residual=x)
+        f6 = ops.linear_x6(h26, L["wfc6"], L["bfc"], act="gelu")
+        return ops.linear_x6(f6, L["wproj6"], L["bproj"], residual=y, out=y)
+
+    def _layer_x6(self, i, x, B, S, stats):
+        kinds = self._stat_kinds(stats)
+        q, k, o6, lse, h26 = self._attn_x6(i, x, B, S, need_lse="colsum" in kinds)
+        st = None
+        if kinds:
+            st = AttnStats(lastrow=ops.attn_lastrow(q, k, S) if "lastrow" in kinds else None,
+                           colsum=ops.attn_colsum(q, k, lse, S) if "colsum" in kinds else None)
+        return self._mlp_x6(i, o6, x, h26), st
+
     def layer_rows(self, i: int, x: torch.Tensor, B: int, S: int, rows: torch.Tensor,
                    n_rows: torch.Tensor | None = None) -> torch.Tensor:
         """Decoder layer ``i`` evaluated only at the flat row indices ``rows`` -> hidden [len(rows), H].
@@ -299,6 +366,10 @@ class DecoderLM:
             raise RuntimeError(f"layer {i} is not resident on this stage")
         Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
         rows = rows.to(self.device)
+        if self.x6:
+            _, _, o6, _, h26 = self._attn_x6(i, x, B, S, n_rows=n_rows)
+            return self._mlp_x6(i, o6.index_select(0, rows), x.index_select(0, rows),
+                                None if h26 is None else h26.index_select(0, rows))
         h2 = None
         if self.fuse_norm:
             ssq = getattr(x, "_edge_ssq", None)
@@ -334,6 +405,13 @@ class DecoderLM:
 
     def row_nll(self, x: torch.Tensor, rows: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         """Per-row NLL of the scored rows only (final norm + LM head + CE fused)."""
+        if self.x6:
+            rows = rows.to(self.device)
+            if self.cfg.arch == "qwen2":
+                h6 = ops.rmsnorm(x, self.w["norm_w"], self.cfg.norm_eps, rows, x6=True)
+            else:
+                h6 = ops.layernorm(x, self.w["norm_w"], self.w["norm_b"], self.cfg.norm_eps, rows, x6=True)
+            return ops.head_nll_x6(h6, self.w["head6"], targets.to(self.device))
         h = self.final_norm(x, rows.to(self.device))
         return ops.head_nll(h, self.w["head"], targets.to(self.device))
 

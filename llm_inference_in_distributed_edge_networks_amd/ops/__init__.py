@@ -3,7 +3,10 @@
 Every op has exactly two implementations with identical layouts and semantics:
 
 * CUDA/HIP tensors -> the hand-written gfx950 kernel from ``csrc/`` (``_native``);
-  a missing library is an error, never a silent fallback;
+  a missing library is an error, never a silent fallback.  Two GPU precisions:
+  bf16 activations (bf16 MFMA), and fp32 activations - the reference's precision - where
+  GEMM operands travel in the X6 split-bf16 layout (``reference.x6_act`` / ``x6_weight``,
+  csrc/common.h) and attention runs on the f32 matrix cores (csrc/attention_f32.hip);
 * CPU tensors -> the fp32 PyTorch oracle in ``reference.py`` (used for the
   CPU WikiText-2 configuration and as the test oracle).
 """
@@ -23,11 +26,27 @@ interleave_gate_up = ref.interleave_gate_up
 deinterleave_gate_up = ref.deinterleave_gate_up
 
 _ACT = {None: 0, "gelu": 1, "swiglu_il": 2}
-_QKV_ROW_RSCALE = os.environ.get("EDGE_QKV_ROW_RSCALE", "0") not in ("", "0")
+from ._native import tuning as _tuning  # noqa: E402
+
+_QKV_ROW_RSCALE = _tuning() and os.environ.get("EDGE_QKV_ROW_RSCALE", "0") not in ("", "0")
 
 
 def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
+
+
+def _check_f32(*ts):
+    for t in ts:
+        if t is not None and t.dtype != torch.float32:
+            raise TypeError(f"fp32-mode HIP kernels take fp32 tensors, got {t.dtype}")
+        if t is not None and not t.is_contiguous():
+            raise ValueError("HIP kernels take contiguous tensors")
+
+
+def _check_x6(*ts):
+    for t in ts:
+        if t is not None and (t.dtype != torch.bfloat16 or t.shape[-1] % 6 or not t.is_contiguous()):
+            raise TypeError("X6 operands are contiguous bf16 [rows, 6K] tensors (reference.x6_act / x6_weight)")
 
 
 def _check_bf16(*ts):
@@ -42,43 +61,74 @@ def _check_bf16(*ts):
 def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
     if not _gpu(table):
         return ref.embedding(ids, table)
-    _check_bf16(table)
     ids = ids.reshape(-1).to(torch.int64).contiguous()
     T, (V, H) = ids.numel(), table.shape
     out = torch.empty(T, H, dtype=table.dtype, device=table.device)
+    if table.dtype == torch.float32:
+        _check_f32(table)
+        call("edge_embedding_f32", ptr(ids), ptr(table), ptr(out), T, H, V, stream())
+        return out
+    _check_bf16(table)
     call("edge_embedding", ptr(ids), ptr(table), ptr(out), T, H, V, stream())
     return out
 
 
-def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, rows: torch.Tensor | None = None) -> torch.Tensor:
-    """RMSNorm of ``x[rows]`` (all rows if ``rows`` is None)."""
+def _out_f32_or_x6(R: int, H: int, x6: bool, device) -> torch.Tensor:
+    return torch.empty(R, 6 * H, dtype=torch.bfloat16, device=device) if x6 else \
+        torch.empty(R, H, dtype=torch.float32, device=device)
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, rows: torch.Tensor | None = None,
+            x6: bool = False) -> torch.Tensor:
+    """RMSNorm of ``x[rows]`` (all rows if ``rows`` is None).  fp32 ``x`` with ``x6``: output in the X6 layout."""
     if not _gpu(x):
-        return ref.rmsnorm(x if rows is None else x.index_select(0, rows.long()), w, eps)
-    _check_bf16(x, w)
+        y = ref.rmsnorm(x if rows is None else x.index_select(0, rows.long()), w, eps)
+        return ref.x6_act(y) if x6 else y
     R = x.shape[0] if rows is None else rows.numel()
     H = x.shape[1]
     rows32 = None if rows is None else rows.to(torch.int32).contiguous()
+    if x.dtype == torch.float32:
+        _check_f32(x, w)
+        y = _out_f32_or_x6(R, H, x6, x.device)
+        call("edge_rmsnorm_f32", ptr(x), ptr(w), ptr(y), ptr(rows32), R, H, float(eps), int(x6), stream())
+        return y
+    _check_bf16(x, w)
     y = torch.empty(R, H, dtype=x.dtype, device=x.device)
     call("edge_rmsnorm", ptr(x), ptr(w), ptr(y), ptr(rows32), R, H, float(eps), stream())
     return y
 
 
-def layernorm(x, w, b, eps, rows=None):
+def layernorm(x, w, b, eps, rows=None, x6: bool = False):
     if not _gpu(x):
-        return ref.layernorm(x if rows is None else x.index_select(0, rows.long()), w, b, eps)
-    _check_bf16(x, w, b)
+        y = ref.layernorm(x if rows is None else x.index_select(0, rows.long()), w, b, eps)
+        return ref.x6_act(y) if x6 else y
     R = x.shape[0] if rows is None else rows.numel()
     H = x.shape[1]
     rows32 = None if rows is None else rows.to(torch.int32).contiguous()
+    if x.dtype == torch.float32:
+        _check_f32(x, w, b)
+        y = _out_f32_or_x6(R, H, x6, x.device)
+        call("edge_layernorm_f32", ptr(x), ptr(w), ptr(b), None, None, ptr(y), None, ptr(rows32), R, H, float(eps),
+             int(x6), stream())
+        return y
+    _check_bf16(x, w, b)
     y = torch.empty(R, H, dtype=x.dtype, device=x.device)
     call("edge_layernorm", ptr(x), ptr(w), ptr(b), None, None, ptr(y), None, ptr(rows32), R, H, float(eps), stream())
     return y
 
 
-def layernorm_dual(x, w1, b1, w2, b2, eps):
+def layernorm_dual(x, w1, b1, w2, b2, eps, x6: bool = False):
     """Two LayerNorms of the same input (GPT-NeoX parallel residual reads ln1(x) and ln2(x))."""
     if not _gpu(x):
-        return ref.layernorm_dual(x, w1, b1, w2, b2, eps)
+        y1, y2 = ref.layernorm_dual(x, w1, b1, w2, b2, eps)
+        return (ref.x6_act(y1), ref.x6_act(y2)) if x6 else (y1, y2)
+    if x.dtype == torch.float32:
+        _check_f32(x, w1, b1, w2, b2)
+        R, H = x.shape
+        y1, y2 = _out_f32_or_x6(R, H, x6, x.device), _out_f32_or_x6(R, H, x6, x.device)
+        call("edge_layernorm_f32", ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(y1), ptr(y2), None, R, H,
+             float(eps), int(x6), stream())
+        return y1, y2
     _check_bf16(x, w1, b1, w2, b2)
     R, H = x.shape
     y1 = torch.empty_like(x)
@@ -94,7 +144,8 @@ def set_gemm_tile(tile: int) -> None:
     call("edge_gemm_set_tile", int(tile))
 
 
-GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8, "s-a4": 9}  # s-a*: timing ablations
+# s-a*: timing ablations with wrong results, only in a tuning build of the library (-DEDGE_TUNING_BUILD=1)
+GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8, "s-a4": 9}
 
 
 def set_gemm_variant(v: int) -> None:
@@ -230,23 +281,32 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     return q, k, vt
 
 
-def attention(q, k, vt, S, need_lse=False, n_rows=None):
+def attention(q, k, vt, S, need_lse=False, n_rows=None, x6: bool = False):
     """Causal GQA flash attention -> (o [B*S, Hq*64], lse [B,Hq,S] or None).
 
     ``n_rows`` ([B] fp32, scored rows per window as in ``WindowBatch.n_rows``): only query rows
     >= S-1-n_rows[b] are needed (last layer of the model); other 64-row blocks may be skipped and their
-    output rows are then undefined."""
+    output rows are then undefined.  fp32 q/k/vt run the f32 matrix-core kernel; ``x6`` then writes o in
+    the X6 layout [B*S, 6*Hq*64] the O-projection consumes."""
     if not _gpu(q):
-        return ref.attention(q, k, vt, S, need_lse)
-    _check_bf16(q, k, vt)
+        o, lse = ref.attention(q, k, vt, S, need_lse)
+        return (ref.x6_act(o) if x6 else o), lse
     B, Hq, _, D = q.shape
     Hkv = k.shape[1]
-    o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)
     lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device) if need_lse else None
     nr = None
     if n_rows is not None:
         nr = n_rows.to(device=q.device, dtype=torch.float32).contiguous()
         assert nr.numel() == B
+    if q.dtype == torch.float32:
+        _check_f32(q, k, vt)
+        assert D == 64 and vt.shape[-1] % 64 == 0 and vt.shape[-1] >= S
+        o = _out_f32_or_x6(B * S, Hq * D, x6, q.device)
+        call("edge_flash_attn_fwd_f32", ptr(q), ptr(k), ptr(vt), ptr(o), ptr(lse), ptr(nr), B, Hq, Hkv, S,
+             vt.shape[-1], int(x6), stream())
+        return o, lse
+    _check_bf16(q, k, vt)
+    o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)
     call("edge_flash_attn_fwd", ptr(q), ptr(k), ptr(vt), ptr(o), ptr(lse), ptr(nr), B, Hq, Hkv, S, vt.shape[-1],
          stream())
     return o, lse
@@ -263,7 +323,8 @@ def attn_lastrow(q, k, S):
         return ref.attn_lastrow(q, k, S)
     B, Hq = q.shape[:2]
     out = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
-    call("edge_attn_lastrow", ptr(q), ptr(k), ptr(out), B, Hq, k.shape[1], S, stream())
+    fn = "edge_attn_lastrow_f32" if q.dtype == torch.float32 else "edge_attn_lastrow"
+    call(fn, ptr(q), ptr(k), ptr(out), B, Hq, k.shape[1], S, stream())
     return out
 
 
@@ -272,7 +333,8 @@ def attn_colsum(q, k, lse, S):
         return ref.attn_colsum(q, k, lse, S)
     B, Hq = q.shape[:2]
     out = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
-    call("edge_attn_colsum", ptr(q), ptr(k), ptr(lse.contiguous()), ptr(out), B, Hq, k.shape[1], S, stream())
+    fn = "edge_attn_colsum_f32" if q.dtype == torch.float32 else "edge_attn_colsum"
+    call(fn, ptr(q), ptr(k), ptr(lse.contiguous()), ptr(out), B, Hq, k.shape[1], S, stream())
     return out
 
 
@@ -308,6 +370,95 @@ def head_nll(h, w, targets):
     nll = torch.empty(R, dtype=torch.float32, device=h.device)
     t64 = targets.to(torch.int64).contiguous()
     call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, stream())
+    call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
+    return nll
+
+
+# ---- fp32 execution mode: X6 GEMMs (csrc/gemm.hip EPI_F32*, EPI_X6_*) ---------------------------------------
+def split6(x: torch.Tensor, rows: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 [R, K] (optionally rows gathered) -> X6 [R, 6K]."""
+    if not _gpu(x):
+        return ref.x6_act(x if rows is None else x.index_select(0, rows.long()))
+    _check_f32(x)
+    R = x.shape[0] if rows is None else rows.numel()
+    rows32 = None if rows is None else rows.to(torch.int32).contiguous()
+    y = torch.empty(R, 6 * x.shape[1], dtype=torch.bfloat16, device=x.device)
+    call("edge_split6", ptr(x), ptr(y), ptr(rows32), R, x.shape[1], stream())
+    return y
+
+
+def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=None, out=None) -> torch.Tensor:
+    """fp32-accurate ``act(x @ w.T + bias) + residual`` from X6 operands (x6 [M, 6K], w6 [N, 6K]).
+
+    act None -> fp32 [M, N] (``residual`` fp32, may alias ``out``); act "gelu" / "swiglu_il" -> the activation in
+    the X6 layout ([M, 6N] / [M, 3N]) for the next GEMM."""
+    M, Kx = x6.shape
+    N = w6.shape[0]
+    if not _gpu(x6):
+        y = ref.x6_to_f32(x6) @ ref.x6_to_f32(w6).t()
+        if bias is not None:
+            y = y + bias.float()
+        if act == "gelu":
+            return ref.x6_act(ref.gelu(y))
+        if act == "swiglu_il":
+            g, u = ref.deinterleave_gate_up(y)
+            return ref.x6_act(torch.nn.functional.silu(g) * u)
+        if residual is not None:
+            y = y + residual.float()
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _check_x6(x6, w6)
+    _check_f32(bias, residual)
+    assert w6.shape[1] == Kx
+    if act is None:
+        if out is None:
+            out = torch.empty(M, N, dtype=torch.float32, device=x6.device)
+        ldc = out.stride(0)
+        code = 0
+    else:
+        No = N // 2 if act == "swiglu_il" else N
+        out = torch.empty(M, 6 * No, dtype=torch.bfloat16, device=x6.device)
+        ldc = 6 * No
+        code = _ACT[act]
+    call("edge_gemm_f32", ptr(x6), ptr(w6), ptr(out), M, N, Kx, x6.stride(0), w6.stride(0), ldc, ptr(bias),
+         ptr(residual), 0 if residual is None else residual.stride(0), code, stream())
+    return out
+
+
+def qkv_rope_x6(x6, w6, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
+    """fp32 fused QKV projection + bias + RoPE + head-major scatter from X6 operands -> fp32 (q, k, vt)."""
+    if not _gpu(x6):
+        return ref.qkv_rope(ref.x6_to_f32(x6), ref.x6_to_f32(w6), bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim,
+                            q_scale)
+    _check_x6(x6, w6)
+    _check_f32(bias)
+    assert D == 64, "HIP attention path is specialised for head_dim 64"
+    M, Kx = x6.shape
+    sp = s_pad(S)
+    f32 = dict(dtype=torch.float32, device=x6.device)
+    q = torch.empty(B, Hq, S, D, **f32)
+    k = torch.empty(B, Hkv, S, D, **f32)
+    vt = torch.zeros(B, Hkv, D, sp, **f32) if sp != S else torch.empty(B, Hkv, D, sp, **f32)
+    call("edge_gemm_qkv_rope_f32", ptr(x6), ptr(w6), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, S,
+         Hq, Hkv, rot_dim, sp, float(q_scale), stream())
+    return q, k, vt
+
+
+def head_nll_x6(h6: torch.Tensor, w6: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    """fp32 fused LM head + cross entropy on the scored rows from X6 operands: per-row NLL."""
+    if not _gpu(h6):
+        return ref.head_nll(ref.x6_to_f32(h6), ref.x6_to_f32(w6), targets)
+    _check_x6(h6, w6)
+    R, Kx = h6.shape
+    V = w6.shape[0]
+    nparts = V // 64
+    f32 = dict(dtype=torch.float32, device=h6.device)
+    pmax, psum = torch.empty(R, nparts, **f32), torch.empty(R, nparts, **f32)
+    tgt, nll = torch.empty(R, **f32), torch.empty(R, **f32)
+    t64 = targets.to(torch.int64).contiguous()
+    call("edge_gemm_lse", ptr(h6), ptr(w6), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
 

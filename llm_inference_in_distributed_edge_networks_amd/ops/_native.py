@@ -52,9 +52,9 @@ _SIGS = {
     "edge_head_combine": [c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p],
     "edge_select": [c_p, c_i, c_i, c_i, c_p, c_ll, c_p, c_p],
     "edge_set_mask": [c_p, c_ll, c_i, c_i, c_i, c_p],
-    "edge_channel_stats": [c_p, c_p, c_ll, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_channel_stats": [c_p, c_p, c_ll, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_rowmax": [c_p, c_p, c_i, c_i, c_p],
-    "edge_pack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_pack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_lrp_attn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_lrp_rope_pack": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_swiglu_il": [c_p, c_p, c_ll, c_i, c_p],
@@ -62,12 +62,43 @@ _SIGS = {
     "edge_lrp_gelu_bwd": [c_p, c_p, c_ll, c_p],
     "edge_lrp_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_ln_rstd": [c_p, c_p, c_i, c_i, c_f, c_p],
-    "edge_unpack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_unpack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    # fp32 execution mode (X6 split-bf16 GEMM operands, fp32 attention / norms / codec)
+    "edge_gemm_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p],
+    "edge_gemm_qkv_rope_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
+    "edge_flash_attn_fwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_attn_lastrow_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    "edge_attn_colsum_f32": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    "edge_rmsnorm_f32": [c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_i, c_p],
+    "edge_layernorm_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_i, c_p],
+    "edge_split6": [c_p, c_p, c_p, c_i, c_i, c_p],
+    "edge_embedding_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_p],
 }
 
 
 class NativeLibraryMissing(RuntimeError):
     pass
+
+
+def tuning() -> bool:
+    """Kernel A/B switches (EDGE_GEMM_VARIANT, EDGE_ATTN_VARIANT, ...) are honoured only with EDGE_TUNING=1, so a
+    stray environment variable can never change the production kernel selection."""
+    return os.environ.get("EDGE_TUNING", "0") not in ("", "0")
+
+
+def _apply_tuning_env(L) -> None:
+    v = os.environ.get("EDGE_GEMM_VARIANT")  # A/B of the 256x256 main loop (see ops.set_gemm_variant)
+    if v:
+        L.edge_gemm_set_variant(int(v))
+    av = os.environ.get("EDGE_ATTN_VARIANT")  # A/B of the flash-attention forward (see ops.set_attn_variant)
+    if av:
+        L.edge_attn_set_variant(int(av))
+    if os.environ.get("EDGE_GEMM_LSE256", "1") == "0":  # LM-head LSE GEMM on 128x128 tiles
+        L.edge_gemm_set_lse256(0)
+    if os.environ.get("EDGE_GEMM_RS_LDS", "1") == "0":  # row scales by global loads in the epilogue
+        L.edge_gemm_set_rs_lds(0)
+    if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # N = 896 GEMMs back on the 256x256 tiles
+        L.edge_gemm_set_w7(0)
 
 
 def available() -> bool:
@@ -90,18 +121,8 @@ def lib():
             fn.argtypes = argt
             fn.restype = c_i
         _lib = L
-        v = os.environ.get("EDGE_GEMM_VARIANT")  # A/B of the 256x256 main loop (see ops.set_gemm_variant)
-        if v:
-            L.edge_gemm_set_variant(int(v))
-        av = os.environ.get("EDGE_ATTN_VARIANT")  # A/B of the flash-attention forward (see ops.set_attn_variant)
-        if av:
-            L.edge_attn_set_variant(int(av))
-        if os.environ.get("EDGE_GEMM_LSE256", "1") == "0":  # A/B: LM-head LSE GEMM on 128x128 tiles
-            L.edge_gemm_set_lse256(0)
-        if os.environ.get("EDGE_GEMM_RS_LDS", "1") == "0":  # A/B: row scales by global loads in the epilogue
-            L.edge_gemm_set_rs_lds(0)
-        if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # A/B: N = 896 GEMMs back on the 256x256 tiles
-            L.edge_gemm_set_w7(0)
+        if tuning():
+            _apply_tuning_env(L)
     return _lib
 
 

@@ -182,6 +182,41 @@ def head_nll(h, w, targets):
     return torch.logsumexp(logits, -1) - logits.gather(1, targets.long().view(-1, 1)).squeeze(1)
 
 
+# ---- fp32 execution by split-bf16 MFMA ("X6", csrc/common.h) -------------------------------------------------
+# x = x0 + x1 + x2 exactly (three bf16 planes); a GEMM over the K-concatenations
+#   A' = [a2 | a0 | a1 | a1 | a0 | a0],  B' = [b0 | b2 | b1 | b0 | b1 | b0]
+# sums the six products a_i b_j with i + j <= 2, i.e. the fp32 product up to terms of relative size 2^-27.
+X6_APLANES = (2, 0, 1, 1, 0, 0)
+X6_BPLANES = (0, 2, 1, 0, 1, 0)
+
+
+def split3(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    xf = _f(x)
+    p0 = xf.to(torch.bfloat16)
+    r = xf - p0.float()
+    p1 = r.to(torch.bfloat16)
+    p2 = (r - p1.float()).to(torch.bfloat16)
+    return p0, p1, p2
+
+
+def x6_act(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [R, K] -> X6 activation layout [R, 6K] bf16 (what the fp32-mode kernels emit for GEMM inputs)."""
+    p = split3(x)
+    return torch.cat([p[i] for i in X6_APLANES], -1).contiguous()
+
+
+def x6_weight(w: torch.Tensor) -> torch.Tensor:
+    """fp32 [N, K] nn.Linear weight -> X6 weight layout [N, 6K] bf16."""
+    p = split3(w)
+    return torch.cat([p[i] for i in X6_BPLANES], -1).contiguous()
+
+
+def x6_to_f32(x6: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``x6_act``: the fp32 value is the sum of the three distinct planes (blocks 1, 2, 0)."""
+    K = x6.shape[-1] // 6
+    return x6[..., K:2 * K].float() + x6[..., 2 * K:3 * K].float() + x6[..., :K].float()
+
+
 # ---- fused RMSNorm (GPU fast path) semantics -------------------------------------------------------
 def row_ssq(x: torch.Tensor) -> torch.Tensor:
     """Per-row sum of squares in 64-column slabs: [T, H/64] fp32."""

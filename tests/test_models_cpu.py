@@ -69,3 +69,24 @@ def test_presets():
     p = get_config("pythia")
     assert p is PYTHIA_70M and p.rotary_dim == 16 and p.parallel_residual
     assert 69e6 < p.num_params() < 72e6
+
+
+@pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX])
+def test_x6_execution_path_matches_fp32(cfg):
+    """The fp32 GPU mode's op sequence (X6 split-bf16 GEMM operands, ops.*_x6) run on CPU equals plain fp32."""
+    ref_m = DecoderLM.random_init(cfg, 5)
+    x6_m = DecoderLM.random_init(cfg, 5, x6=True)
+    ids = torch.randint(0, cfg.vocab_size, (2, 48), generator=torch.Generator().manual_seed(3))
+    B, S = ids.shape
+    xr, xx = ref_m.embed(ids), x6_m.embed(ids)
+    for i in range(cfg.num_layers):
+        xr, sr = ref_m.layer(i, xr, B, S, stats=("lastrow", "colsum"))
+        xx, sx = x6_m.layer(i, xx, B, S, stats=("lastrow", "colsum"))
+        assert torch.allclose(sx.lastrow, sr.lastrow, atol=1e-6) and torch.allclose(sx.colsum, sr.colsum, atol=1e-5)
+    assert (xx - xr).abs().max() < 1e-4
+    rows = torch.arange(S - 8, S).repeat(B) + torch.arange(B).repeat_interleave(8) * S
+    tg = torch.randint(0, cfg.vocab_size, (rows.numel(),))
+    assert torch.allclose(x6_m.row_nll(xx, rows, tg), ref_m.row_nll(xr, rows, tg), atol=1e-4)
+    # last-layer scored-rows shortcut
+    xl = x6_m.layer_rows(cfg.num_layers - 1, x6_m.forward_hidden(ids, 0, cfg.num_layers - 1), B, S, rows)
+    assert torch.allclose(xl, xr.index_select(0, rows), atol=1e-4)
