@@ -244,21 +244,38 @@ class DistributedPipeline:
             reqs.append(self.tr.recv(carry, self.prev))
         return msg, carry, reqs
 
-    def evaluate(self, batches) -> tuple[PPLAccumulator, dict]:
+    def evaluate(self, batches, timing: bool = False) -> tuple[PPLAccumulator, dict]:
         """Run this rank's share of ``batches`` as one continuous pipeline (no flush between batches).
 
-        Returns the globally reduced accumulator (valid on every rank)."""
+        Returns the globally reduced accumulator (valid on every rank) and this rank's stage report.  With
+        ``timing`` the report carries a GPU-event breakdown of the stage's stream: ``compute_ms`` (stage
+        graphs), ``recv_wait_ms`` (stream stalled on the incoming boundary message), ``send_post_ms`` (host
+        time posting sends) and ``bubble_frac`` = 1 - compute / wall."""
         mine = [b.to(self.device) for b in self.my_batches(batches)]
         acc_local = torch.zeros(2, dtype=torch.float64, device=self.device)
         wd = watchdog_from_env(f"stage{self.stage}")
         tag = f"stage{self.stage}"
-        pending_sends = []
+        cuda = self.device.type == "cuda"
+        timing = timing and cuda
+        evs = []
+        send_post = 0.0
+        # two graph slots: the boundary message of micro-batch i lives in slot i % 2's static buffer, so the
+        # send of i overlaps the compute of i + 1; before slot i % 2 is replayed again (i + 2) the stream waits
+        # for the send that still reads it (GPU-side wait, no host sync, no copy of the message)
+        in_flight: list = [None, None]
         recv_next = self._post_recv(mine[0]) if (self.prev is not None and mine) else None
         t0 = time.perf_counter()
+        if timing:
+            ev_begin = torch.cuda.Event(enable_timing=True)
+            ev_begin.record()
         for i, b in enumerate(mine):
             msg_in = carry_in = None
+            slot = i & 1
             if wd:
                 wd.beat()
+            if timing:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             if self.prev is not None:
                 msg_in, carry_in, reqs = recv_next
                 with trace.range(f"{tag}/recv_wait"):
@@ -266,32 +283,62 @@ class DistributedPipeline:
                         r.wait()
                 if i + 1 < len(mine):
                     recv_next = self._post_recv(mine[i + 1])  # prefetch: overlap next transfer with compute
+            if in_flight[slot] is not None:
+                for r in in_flight[slot]:
+                    r.wait()
+                in_flight[slot] = None
+            if timing:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
             self.runner.account(b)
             with trace.range(f"{tag}/compute"):
                 out = self.graphs(b.ids, b.rows, b.targets, b.row_window, b.n_rows,
-                                  *(() if self.prev is None else (msg_in, carry_in)))
+                                  *(() if self.prev is None else (msg_in, carry_in)), slot=slot)
+            if timing:
+                e2 = torch.cuda.Event(enable_timing=True)
+                e2.record()
+                evs.append((e0, e1, e2))
             if self.next is not None:
                 msg, c = out
-                if self.graphs.enabled:      # graph outputs are static buffers: hand NCCL private copies
-                    msg, c = msg.clone(), c.clone()
                 trace.counter(f"{tag}/wire_bytes", msg.numel() + 4 * c.numel())
+                ts = time.perf_counter()
                 with trace.range(f"{tag}/send_post"):
                     reqs = [self.tr.send(msg, self.next)] + ([self.tr.send(c, self.next)] if c.numel() else [])
-                pending_sends.append((msg, c, reqs))
-                while len(pending_sends) > 2:   # bound in-flight sends (memory) without stalling compute
-                    for r in pending_sends.pop(0)[2]:
-                        r.wait()
+                send_post += time.perf_counter() - ts
+                if self.graphs.enabled:
+                    in_flight[slot] = reqs
+                else:
+                    in_flight[slot] = None
+                    self._eager_sends = getattr(self, "_eager_sends", [])
+                    self._eager_sends.append(reqs)
+                    while len(self._eager_sends) > 2:
+                        for r in self._eager_sends.pop(0):
+                            r.wait()
             else:
                 w = b.weights.to(self.device)
                 acc_local[0] += (out.double() * w).sum()
                 acc_local[1] += w.sum()
-        for _, _, reqs in pending_sends:
-            for r in reqs:
+        for reqs in in_flight + getattr(self, "_eager_sends", []):
+            for r in reqs or ():
                 r.wait()
+        self._eager_sends = []
+        report = {"stage": self.stage, "dp": self.dp_idx, "layers": [self.runner.layers.start,
+                                                                     self.runner.layers.stop - 1]}
+        if timing:
+            ev_end = torch.cuda.Event(enable_timing=True)
+            ev_end.record()
+            torch.cuda.synchronize()
+            comp = sum(e1.elapsed_time(e2) for _, e1, e2 in evs)
+            wait = sum(e0.elapsed_time(e1) for e0, e1, _ in evs)
+            wall = ev_begin.elapsed_time(ev_end)
+            report.update(compute_ms=round(comp, 3), recv_wait_ms=round(wait, 3), send_post_ms=round(1e3 * send_post, 3),
+                          wall_ms=round(wall, 3), bubble_frac=round(max(0.0, 1.0 - comp / wall), 4) if wall else None,
+                          microbatches=len(evs))
         if wd:
             wd.stop()
         self.runner.stats.compute_s += time.perf_counter() - t0
         all_reduce_sum(acc_local)
         acc = PPLAccumulator()
         acc.total_nll, acc.n_tokens = float(acc_local[0]), float(acc_local[1])
-        return acc, {"stage": self.stage, "dp": self.dp_idx, "wire_bytes_per_token": self.runner.stats.bytes_per_token}
+        report["wire_bytes_per_token"] = self.runner.stats.bytes_per_token
+        return acc, report

@@ -50,8 +50,9 @@ class _Handle:
         self.comm, self.is_recv = comm, is_recv
 
     def wait(self):
-        if self.is_recv:   # compute stream waits for the receive (GPU-side)
-            _ok(lib().edge_rccl_signal_to(self.comm.h, torch.cuda.current_stream().cuda_stream), "signal_to")
+        # the current stream waits (GPU-side) for the comm stream's work so far: a receive's data is visible, or
+        # a send has finished reading its buffer (the pipeline reuses graph output buffers after this)
+        _ok(lib().edge_rccl_signal_to(self.comm.h, torch.cuda.current_stream().cuda_stream), "signal_to")
 
 
 class RcclComm:

@@ -7,6 +7,11 @@ buffers and replays it: one launch instead of hundreds, no Python or ctypes over
 Kernels launched through the ctypes library go to the current (capturing) stream, so they are
 captured like any torch op.  Batches with a new signature (first / last window of a corpus) run
 eagerly the first time they are seen and are captured on the second sighting.
+
+Outputs of a replay are the graph's STATIC buffers: the next replay of the same graph overwrites them.  A caller
+that hands an output to asynchronous work (an RCCL send of the boundary message) uses ``slot``: each slot is an
+independent capture with its own buffers, so with two slots replay i+1 writes other memory than the send of
+replay i reads; before replaying a slot again the caller makes the stream wait for that slot's send.
 """
 from __future__ import annotations
 
@@ -28,10 +33,10 @@ class GraphCache:
     def _sig(args):
         return tuple((tuple(a.shape), a.dtype, a.device) for a in args)
 
-    def __call__(self, *args):
+    def __call__(self, *args, slot: int = 0):
         if not self.enabled or not all(torch.is_tensor(a) and a.is_cuda for a in args):
             return self.fn(*args)
-        key = self._sig(args)
+        key = (self._sig(args), slot)
         g = self.graphs.get(key)
         if g is None:
             n = self.seen.get(key, 0)
