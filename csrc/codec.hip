@@ -2,7 +2,11 @@
 // quantize/pack / unpack/dequantize of the hidden state that crosses a pipeline-stage boundary.
 //
 // Wire message (offsets computed on the host, codec/wire.py, every section 16-byte aligned):
-//   [header 32 B][class bitmask B x MW u32][scales][hi-class rows][lo-class rows]
+//   fixed k     : [header 32 B][class bitmask B x MW u32][scales][hi-class rows][lo-class rows]
+//   variable k  : [header 32 B][class bitmask][k per window, B x i32][scales][lo-class rows][hi-class rows]
+// (variable k = top-rho selection: each window quantizes the tokens outside its smallest importance mass
+// reaching a threshold; window b's rows follow the sum of the k (or S - k) of the windows before it, and the hi
+// section starts right after the Sum k lo rows, so the message is compact; the buffer has capacity for any k).
 // A token whose bit is set belongs to the low-precision ("lo") class.  Rows of each class are stored in
 // token order; a row's slot is the popcount of the mask bits before it, so the receiver needs nothing
 // but the mask.  Row formats: 0 bf16, 1 int8, 2 int4 (two's-complement nibbles, even element in the low
@@ -20,6 +24,7 @@ enum { CH_MAXABS = 0, CH_MEAN = 1 };
 struct CodecArgs {
   void* x; uint8_t* msg;
   long long off_mask, off_scale, off_hi, off_lo;
+  long long off_kvec;           // >= 0: variable-k layout (k per window at msg + off_kvec), else fixed k
   int B, S, H, k, mw;           // mw: mask words per window
   int hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo, ch_kind;
 };
@@ -47,35 +52,96 @@ __device__ __forceinline__ int lo_prefix(const uint32_t* __restrict__ mask, int 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Rank tokens by importance (ascending, ties by index) and mark the k least important as lo.
-__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ imp, int S, int k, int mw,
-                                                     uint32_t* __restrict__ mask_out, int mask_stride,
-                                                     int* __restrict__ rank_out) {
-  extern __shared__ float v[];
-  const int b = blockIdx.x;
+// Token selection: one workgroup per window sorts the window's (importance, position) pairs
+// ascending with an LDS bitonic sort of 64-bit keys (order-preserving float bits << 32 | position: ties by
+// position, NaN ranked above +inf, -0 == +0 - the order of a stable torch.sort) and marks the first k positions
+// as the lo class.
+//   mode 0 (ratio)  : k given (reference int(ratio * S), qwen_layer_wise.py:57).
+//   mode 1 (top-rho): in descending order, keep the shortest prefix whose mass reaches thr = 1 - 0.1 ratio and
+//                     quantize the rest: keep = first i with sum_{j<i} desc_j >= thr (thr <= 0 -> 0, none -> S),
+//                     k = S - keep (the intended semantics of pythia_model.py:92-112, its token-id indexing bug
+//                     B21 fixed); the exclusive prefix sums are an LDS block scan.  k is written to kvec[b].
+__device__ __forceinline__ uint32_t ord_key(float f) {
+  if (f != f) return 0xFFFFFFFFu;                  // NaN last
+  uint32_t u = __float_as_uint(f == 0.f ? 0.f : f);  // -0 -> +0
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_val(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+constexpr int SEL_T = 512;
+__global__ __launch_bounds__(SEL_T) void select_sort_kernel(const float* __restrict__ imp, int S, int P, int mode,
+                                                            int k_fixed, float thr, uint32_t* __restrict__ mask_out,
+                                                            int mw, int* __restrict__ kvec) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];  // P keys, then mw mask words
+  uint32_t* mwords = (uint32_t*)(keys + P);
+  __shared__ float part[SEL_T];
+  __shared__ int cut;
+  const int b = blockIdx.x, tid = threadIdx.x;
   const float* ib = imp + (size_t)b * S;
-  for (int j = threadIdx.x; j < S; j += 256) v[j] = ib[j];
+  for (int i = tid; i < P; i += SEL_T)
+    keys[i] = i < S ? (((unsigned long long)ord_key(ib[i]) << 32) | (unsigned)i) : ~0ull;
+  for (int w = tid; w < mw; w += SEL_T) mwords[w] = 0u;
+  if (tid == 0) cut = S;
   __syncthreads();
-  uint32_t* mb = mask_out + (size_t)b * mask_stride;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int base = 0; base < mw * 32; base += 256) {
-    const int j = base + threadIdx.x;
-    bool lo = false;
-    if (j < S) {
-      const float vj = v[j];
-      int r = 0;
-      for (int i = 0; i < S; ++i) {
-        const float vi = v[i];
-        r += (vi < vj) || (vi == vj && i < j);
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += SEL_T) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = keys[i], c = keys[ixj];
+          if (((i & k) == 0) == (a > c)) { keys[i] = c; keys[ixj] = a; }
+        }
       }
-      if (rank_out) rank_out[(size_t)b * S + j] = r;
-      lo = r < k;
+      __syncthreads();
     }
-    const unsigned long long bal = __ballot(lo);
-    const int w0 = (base + wave * 64) >> 5;
-    if (lane == 0 && w0 < mw) mb[w0] = (uint32_t)bal;
-    if (lane == 1 && w0 + 1 < mw) mb[w0 + 1] = (uint32_t)(bal >> 32);
   }
+  int kk = k_fixed;
+  if (mode == 1) {
+    // descending value i = keys[S-1-i]; thread t owns the contiguous run [t*C, t*C + C) of descending positions
+    const int C = (S + SEL_T - 1) / SEL_T;
+    const int i0 = tid * C;
+    float run = 0.f;
+    for (int e = 0; e < C && i0 + e < S; ++e) run += key_val((uint32_t)(keys[S - 1 - (i0 + e)] >> 32));
+    part[tid] = run;
+    __syncthreads();
+    for (int off = 1; off < SEL_T; off <<= 1) {  // Hillis-Steele inclusive scan of the run sums
+      const float v = tid >= off ? part[tid - off] : 0.f;
+      __syncthreads();
+      part[tid] += v;
+      __syncthreads();
+    }
+    float excl = tid ? part[tid - 1] : 0.f;
+    for (int e = 0; e < C && i0 + e < S; ++e) {
+      if (excl >= thr) { atomicMin(&cut, i0 + e); break; }
+      excl += key_val((uint32_t)(keys[S - 1 - (i0 + e)] >> 32));
+    }
+    __syncthreads();
+    kk = S - cut;
+  }
+  for (int p = tid; p < kk; p += SEL_T) {
+    const int idx = (int)(keys[p] & 0xFFFFFFFFu);
+    atomicOr(&mwords[idx >> 5], 1u << (idx & 31));
+  }
+  __syncthreads();
+  uint32_t* mb = mask_out + (size_t)b * mw;
+  for (int w = tid; w < mw; w += SEL_T) mb[w] = mwords[w];
+  if (kvec && tid == 0) kvec[b] = kk;
+}
+
+// Variable-k layout: lo rows of the windows before b (Kb) and in total (Kt), by one wave.
+__device__ __forceinline__ void kvar_prefix(const CodecArgs& a, int b, int& Kb, int& Kt) {
+  const int lane = threadIdx.x & 63;
+  const int* kv = (const int*)(a.msg + a.off_kvec);
+  int before = 0, all = 0;
+  for (int w = lane; w < a.B; w += 64) {
+    const int v = kv[w];
+    all += v;
+    before += w < b ? v : 0;
+  }
+  Kb = wave_isum(before);
+  Kt = wave_isum(all);
 }
 
 // Per-(window, channel) statistics over the window's rows (optionally only lo-class rows).
@@ -166,8 +232,17 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
   const int fmt = is_lo ? a.lo_fmt : a.hi_fmt;
   const int qmax = is_lo ? a.qmax_lo : a.qmax_hi;
   const int rb = fmt_row_bytes(fmt, a.H);
-  uint8_t* dst = is_lo ? a.msg + a.off_lo + ((size_t)b * a.k + slot_lo) * rb
-                       : a.msg + a.off_hi + ((size_t)b * (a.S - a.k) + (j - slot_lo)) * rb;
+  uint8_t* dst;
+  if (a.off_kvec >= 0) {
+    int Kb, Kt;
+    kvar_prefix(a, b, Kb, Kt);
+    const long long off_hi = a.off_lo + (((long long)Kt * fmt_row_bytes(a.lo_fmt, a.H) + 15) & ~15ll);
+    dst = is_lo ? a.msg + a.off_lo + ((size_t)Kb + slot_lo) * rb
+                : a.msg + off_hi + ((size_t)b * a.S - Kb + (j - slot_lo)) * rb;
+  } else {
+    dst = is_lo ? a.msg + a.off_lo + ((size_t)b * a.k + slot_lo) * rb
+                : a.msg + a.off_hi + ((size_t)b * (a.S - a.k) + (j - slot_lo)) * rb;
+  }
   float v[NCH][8];
   load_row8<NCH>((const T*)a.x + (size_t)row * a.H, a.H, v);
   float* scales = (float*)(a.msg + a.off_scale);
@@ -271,8 +346,17 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
   const int fmt = is_lo ? a.lo_fmt : a.hi_fmt;
   const int qmax = is_lo ? a.qmax_lo : a.qmax_hi;
   const int rb = fmt_row_bytes(fmt, a.H);
-  const uint8_t* src = is_lo ? a.msg + a.off_lo + ((size_t)b * a.k + slot_lo) * rb
-                             : a.msg + a.off_hi + ((size_t)b * (a.S - a.k) + (j - slot_lo)) * rb;
+  const uint8_t* src;
+  if (a.off_kvec >= 0) {
+    int Kb, Kt;
+    kvar_prefix(a, b, Kb, Kt);
+    const long long off_hi = a.off_lo + (((long long)Kt * fmt_row_bytes(a.lo_fmt, a.H) + 15) & ~15ll);
+    src = is_lo ? a.msg + a.off_lo + ((size_t)Kb + slot_lo) * rb
+                : a.msg + off_hi + ((size_t)b * a.S - Kb + (j - slot_lo)) * rb;
+  } else {
+    src = is_lo ? a.msg + a.off_lo + ((size_t)b * a.k + slot_lo) * rb
+                : a.msg + a.off_hi + ((size_t)b * (a.S - a.k) + (j - slot_lo)) * rb;
+  }
   const float* scales = (const float*)(a.msg + a.off_scale);
   float s = 0.f;
   if (fmt != FMT_BF16 && fmt != FMT_F32) {
@@ -340,24 +424,31 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
     else return (int)hipErrorInvalidValue;                            \
   } while (0)
 
-static CodecArgs make_args(void* x, void* msg, long long om, long long os, long long oh, long long ol, int B, int S,
-                           int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo,
-                           int ch_kind) {
+static CodecArgs make_args(void* x, void* msg, long long om, long long os, long long oh, long long ol, long long okv,
+                           int B, int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi,
+                           int qmax_lo, int ch_kind) {
   CodecArgs a;
   a.x = x; a.msg = (uint8_t*)msg;
-  a.off_mask = om; a.off_scale = os; a.off_hi = oh; a.off_lo = ol;
+  a.off_mask = om; a.off_scale = os; a.off_hi = oh; a.off_lo = ol; a.off_kvec = okv;
   a.B = B; a.S = S; a.H = H; a.k = k; a.mw = ((S + 63) / 64) * 2;
   a.hi_fmt = hi_fmt; a.lo_fmt = lo_fmt; a.scale_mode = scale_mode; a.qmax_hi = qmax_hi; a.qmax_lo = qmax_lo;
   a.ch_kind = ch_kind;
   return a;
 }
 
-EDGE_API int edge_select(const float* imp, int B, int S, int k, void* msg, long long off_mask, int* rank_out,
-                         hipStream_t st) {
+// mode 0: k least important per window; mode 1: top-rho cut at mass thr, k per window -> msg + off_kvec (int32).
+EDGE_API int edge_select(const float* imp, int B, int S, int k, void* msg, long long off_mask, int mode, float thr,
+                         long long off_kvec, hipStream_t st) {
   if (B <= 0) return 0;
+  if (S <= 0 || S > 8192 || (mode == 1 && off_kvec < 0)) return (int)hipErrorInvalidValue;
+  int P = 1;
+  while (P < S) P <<= 1;
   const int mw = ((S + 63) / 64) * 2;
-  hipLaunchKernelGGL(select_kernel, dim3(B), dim3(256), S * sizeof(float), st, imp, S, k, mw,
-                     (uint32_t*)((uint8_t*)msg + off_mask), mw, rank_out);
+  const size_t lds = (size_t)P * 8 + (size_t)mw * 4;
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)select_sort_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(select_sort_kernel, dim3(B), dim3(SEL_T), lds, st, imp, S, P, mode, k, thr,
+                     (uint32_t*)((uint8_t*)msg + off_mask), mw, off_kvec >= 0 ? (int*)((uint8_t*)msg + off_kvec) : nullptr);
   return (int)hipGetLastError();
 }
 
@@ -387,11 +478,11 @@ EDGE_API int edge_rowmax(const float* in, float* out, int R, int H, hipStream_t 
   return (int)hipGetLastError();
 }
 
-EDGE_API int edge_pack(const void* x, void* msg, long long om, long long os, long long oh, long long ol, int B, int S,
-                       int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo, int ch_kind,
-                       int x_f32, hipStream_t st) {
+EDGE_API int edge_pack(const void* x, void* msg, long long om, long long os, long long oh, long long ol, long long okv,
+                       int B, int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo,
+                       int ch_kind, int x_f32, hipStream_t st) {
   if (H % 32) return (int)hipErrorInvalidValue;
-  CodecArgs a = make_args((void*)x, msg, om, os, oh, ol, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
+  CodecArgs a = make_args((void*)x, msg, om, os, oh, ol, okv, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
                           ch_kind);
   const int rows = B * S;
   if (rows <= 0) return 0;
@@ -400,11 +491,11 @@ EDGE_API int edge_pack(const void* x, void* msg, long long om, long long os, lon
   return (int)hipGetLastError();
 }
 
-EDGE_API int edge_unpack(void* x, const void* msg, long long om, long long os, long long oh, long long ol, int B,
-                         int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo,
-                         int ch_kind, int x_f32, hipStream_t st) {
+EDGE_API int edge_unpack(void* x, const void* msg, long long om, long long os, long long oh, long long ol,
+                         long long okv, int B, int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi,
+                         int qmax_lo, int ch_kind, int x_f32, hipStream_t st) {
   if (H % 32) return (int)hipErrorInvalidValue;
-  CodecArgs a = make_args(x, (void*)msg, om, os, oh, ol, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
+  CodecArgs a = make_args(x, (void*)msg, om, os, oh, ol, okv, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
                           ch_kind);
   const int rows = B * S;
   if (rows <= 0) return 0;

@@ -250,15 +250,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
   const int g = lane >> 4;
   const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
   if (nw >= a.N) return;        // slab beyond N in a partial last column tile (wave-uniform)
-  if constexpr (epi_f32(EPI)) {
-    return gemm_epilogue_f32<EPI, RH, CF>(a, acc, m0, nw, lane, wm);
-  }
 
   if (a.rscale || a.ssq_in) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] *= rs[i];
+  }
+  if constexpr (epi_f32(EPI)) {
+    return gemm_epilogue_f32<EPI, RH, CF>(a, acc, m0, nw, lane, wm);
   }
 
   if constexpr (EPI == EPI_LSE) {
@@ -1180,9 +1180,10 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
         const int m = m0 + wm * 64 + (ih + i) * 16 + (lane & 15);
         if (m >= a.M) continue;
         float* row = a.Cf + (size_t)m * a.ldc + nw + g * 4;
+        const float rsm = a.rscale ? a.rscale[m] : 1.f;
 #pragma unroll
         for (int j = 0; j < w7::NJ; ++j) {
-          f32x4_t o = acc[ih + i][j];
+          f32x4_t o = acc[ih + i][j] * rsm;
           if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID)
             o += *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
           if constexpr (RESF) o += rv[i][j];
@@ -1686,8 +1687,10 @@ EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, 
 // is Kx = 6K.  act 0 none -> fp32 C [M, ldc] (+ fp32 bias, + fp32 residual, which may alias C); act 1 bias + GELU
 // -> X6 output [M, 6N] in C (bf16, ldc = 6N); act 2 interleaved SwiGLU -> X6 output [M, 6N/2] (ldc = 3N).
 EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, int Kx, int lda, int ldb, int ldc,
-                           const float* bias, const float* resid, int ldr, int act, hipStream_t st) {
+                           const float* bias, const float* resid, int ldr, int act, const float* rscale,
+                           hipStream_t st) {
   GemmArgs a{};
+  a.rscale = rscale;  // optional per-row scale of the product (before bias / activation / residual)
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B;
   a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.biasf = bias; a.residf = resid; a.ldr = ldr;

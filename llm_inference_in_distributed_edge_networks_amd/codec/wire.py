@@ -3,7 +3,7 @@
 Message for a micro-batch of ``B`` windows of ``S`` tokens, hidden size ``H``,
 ``k`` lo-class tokens per window (all sections 16-byte aligned)::
 
-    header   32 B   int32[8] = magic 'EDGB', version, codec id, B, S, H, k, hi-row format
+    header   32 B   int32[8] = magic 'EDGB', version, codec id, B, S, H, k (-1: variable), hi-row format
     mask     B * MW uint32        bit j of window b set <=> token j is in the lo class (MW = 2*ceil(S/64))
     scales   fp32                 per token [B*S] | per window [B] | per channel [B*H]
     hi rows  B*(S-k) rows         token order within each window
@@ -12,6 +12,14 @@ Message for a micro-batch of ``B`` windows of ``S`` tokens, hidden size ``H``,
 The size depends only on (codec, B, S, H, k, native dtype), so sender and
 receiver agree on it without a handshake and the receiver can post its
 ``irecv`` before the sender has produced anything.
+
+Selection.  ``"ratio"`` (the reference): the ``k = int(ratio*S)`` least important tokens of
+every window.  ``"top_rho"`` (Pythia ``'upto ratio'``, ``pythia_model.py:92-112``): each
+window keeps the shortest prefix of its tokens by descending importance whose mass reaches
+``1 - ratio`` and quantizes the rest, so k varies per window.  That message carries
+``k`` per window after the mask and stores the lo rows first and the hi rows right after
+the ``sum k`` lo rows (compact); its buffer (``Layout.total``) has capacity for any k and
+``payload_bytes(sum_k)`` is what a link would carry.
 
 ``encode``/``decode`` run the gfx950 kernels of ``csrc/codec.hip`` for CUDA
 tensors and a bit-identical PyTorch implementation for CPU tensors.
@@ -81,19 +89,31 @@ class Layout:
     B: int
     S: int
     H: int
-    k: int
+    k: int            # lo tokens per window (-1: variable, see kvar)
     mw: int
     hi_fmt: int
     lo_fmt: int
     off_mask: int
     off_scale: int
-    off_hi: int
+    off_hi: int       # -1 when kvar (the hi section follows the sum-k lo rows)
     off_lo: int
-    total: int
+    total: int        # bytes of the message buffer (the capacity when kvar)
+    kvar: bool = False
+    off_kvec: int = -1
 
     @property
     def payload_bytes_per_token(self) -> float:
         return self.total / (self.B * self.S)
+
+    def payload_bytes(self, k_total: int | None = None) -> int:
+        """Bytes of the message proper: ``total`` for fixed k; for variable k with ``k_total`` lo rows in all."""
+        if not self.kvar:
+            return self.total
+        return self.off_lo + _a16(k_total * _row_bytes(self.lo_fmt, self.H)) + \
+            (self.B * self.S - k_total) * _row_bytes(self.hi_fmt, self.H)
+
+    def hi_offset(self, k_total: int) -> int:
+        return self.off_hi if not self.kvar else self.off_lo + _a16(k_total * _row_bytes(self.lo_fmt, self.H))
 
 
 def native_fmt(dtype: torch.dtype) -> int:
@@ -112,7 +132,8 @@ def num_lo(spec: CodecSpec, ratio: float, S: int) -> int:
 
 
 @lru_cache(maxsize=256)
-def layout(spec: CodecSpec, B: int, S: int, H: int, k: int, dtype: torch.dtype = torch.bfloat16) -> Layout:
+def layout(spec: CodecSpec, B: int, S: int, H: int, k: int, dtype: torch.dtype = torch.bfloat16,
+           kvar: bool = False) -> Layout:
     if H % 32:
         raise ValueError("hidden size must be a multiple of 32 for the packed formats")
     nf = native_fmt(dtype)
@@ -121,6 +142,12 @@ def layout(spec: CodecSpec, B: int, S: int, H: int, k: int, dtype: torch.dtype =
     mw = 2 * ((S + 63) // 64)
     off_mask = 32
     n_scale = {SC_TOKEN: B * S, SC_WINDOW: B, SC_CHANNEL: B * H, SC_NONE: 0}[spec.scale_mode]
+    if kvar:
+        off_kvec = off_mask + _a16(B * mw * 4)
+        off_scale = off_kvec + _a16(B * 4)
+        off_lo = off_scale + _a16(n_scale * 4)
+        total = off_lo + _a16(B * S * max(_row_bytes(hi, H), _row_bytes(lo, H))) + 16
+        return Layout(B, S, H, -1, mw, hi, lo, off_mask, off_scale, -1, off_lo, total, True, off_kvec)
     off_scale = off_mask + _a16(B * mw * 4)
     off_hi = off_scale + _a16(n_scale * 4)
     off_lo = off_hi + _a16(B * (S - k) * _row_bytes(hi, H))
@@ -150,17 +177,35 @@ def _words_to_mask(words: torch.Tensor, S: int) -> torch.Tensor:
     return bits.reshape(words.shape[0], -1)[:, :S].bool()
 
 
-def select_mask(imp: torch.Tensor, k: int) -> torch.Tensor:
-    """bool [B, S]: the k least important tokens (ascending, ties by position) of each window."""
+def _canon(imp: torch.Tensor) -> torch.Tensor:
+    v = imp.float()
+    return torch.where(v == 0, torch.zeros_like(v), v)   # -0 == +0 (the kernel's key canonicalisation)
+
+
+def select_mask(imp: torch.Tensor, k) -> torch.Tensor:
+    """bool [B, S]: the k least important tokens (ascending, ties by position, NaN last) of each window; ``k`` an
+    int or a per-window sequence."""
     B, S = imp.shape
-    lo = torch.zeros(B, S, dtype=torch.bool, device=imp.device)
-    if k <= 0:
-        return lo
-    if k >= S:
-        return ~lo
-    order = torch.sort(imp.float(), dim=1, stable=True).indices[:, :k]
-    lo.scatter_(1, order, True)
-    return lo
+    ks = torch.as_tensor(k, dtype=torch.int64).reshape(-1).expand(B) if not isinstance(k, int) else \
+        torch.full((B,), k, dtype=torch.int64)
+    order = torch.sort(_canon(imp).cpu(), dim=1, stable=True).indices
+    pos = torch.arange(S).view(1, S).expand(B, S)
+    lo = torch.zeros(B, S, dtype=torch.bool)
+    lo.scatter_(1, order, pos < ks.view(B, 1).clamp(0, S))
+    return lo.to(imp.device)
+
+
+def top_rho_k(imp: torch.Tensor, mass: float) -> torch.Tensor:
+    """Per-window lo count of top-rho selection: keep the shortest descending-importance prefix whose mass reaches
+    ``mass`` (keep = first i with sum_{j<i} desc_j >= mass; mass <= 0 keeps nothing), quantize the rest.  [B] int64.
+    Descending order = the ascending stable order reversed (as csrc/codec.hip)."""
+    B, S = imp.shape
+    asc = torch.sort(_canon(imp).cpu(), dim=1, stable=True).values
+    desc = asc.flip(1).double()
+    excl = torch.cumsum(desc, 1) - desc
+    ge = excl >= mass
+    keep = torch.where(ge.any(1), ge.to(torch.int64).argmax(1), torch.full((B,), S, dtype=torch.int64))
+    return S - keep
 
 
 def _qcodes(x: torch.Tensor, spec: CodecSpec, is_lo: bool, scale_row, ch_scale) -> torch.Tensor:
@@ -227,7 +272,7 @@ def _dequant(q: torch.Tensor, spec: CodecSpec, is_lo: bool, scale_row, ch_scale)
 
 
 def _header(spec: CodecSpec, L: Layout) -> torch.Tensor:
-    return torch.tensor([MAGIC, VERSION, spec.cid, L.B, L.S, L.H, L.k, L.hi_fmt], dtype=torch.int32)
+    return torch.tensor([MAGIC, VERSION, spec.cid, L.B, L.S, L.H, -1 if L.kvar else L.k, L.hi_fmt], dtype=torch.int32)
 
 
 def _encode_cpu(x, spec, L, lo_mask):
@@ -236,6 +281,10 @@ def _encode_cpu(x, spec, L, lo_mask):
     msg[:32] = _header(spec, L).view(torch.uint8)
     mw_bytes = _mask_words(lo_mask, L.mw).view(torch.uint8).reshape(-1)
     msg[L.off_mask:L.off_mask + mw_bytes.numel()] = mw_bytes
+    kt = int(lo_mask.sum())
+    if L.kvar:
+        kv = lo_mask.sum(1).to(torch.int32).contiguous().view(torch.uint8)
+        msg[L.off_kvec:L.off_kvec + kv.numel()] = kv
     xf = x.float().reshape(B, S, H)
     # statistics
     scales = None
@@ -259,12 +308,11 @@ def _encode_cpu(x, spec, L, lo_mask):
     # rows
     for is_lo in (False, True):
         fmt = L.lo_fmt if is_lo else L.hi_fmt
-        n_per = k if is_lo else S - k
-        if n_per == 0:
-            continue
         sel = lo_mask if is_lo else ~lo_mask
-        rows = xf[sel]                                      # [B*n_per, H] in window/token order
-        off = L.off_lo if is_lo else L.off_hi
+        if not bool(sel.any()):
+            continue
+        rows = xf[sel]                                      # [n, H] in window/token order
+        off = L.off_lo if is_lo else L.hi_offset(kt)
         if fmt == FMT_F32:
             data = rows.contiguous().view(torch.uint8).reshape(-1)
         elif fmt == FMT_BF16:
@@ -297,13 +345,14 @@ def _decode_cpu(msg, spec, L, dtype):
         scales = msg[L.off_scale:L.off_scale + B * 4].view(torch.float32)
     elif spec.scale_mode == SC_CHANNEL:
         ch = msg[L.off_scale:L.off_scale + B * H * 4].view(torch.float32).reshape(B, H)
+    kt = int(lo_mask.sum())
     for is_lo in (False, True):
         fmt = L.lo_fmt if is_lo else L.hi_fmt
-        n = B * (k if is_lo else S - k)
+        sel = lo_mask if is_lo else ~lo_mask
+        n = int(sel.sum())
         if n == 0:
             continue
-        sel = lo_mask if is_lo else ~lo_mask
-        off = L.off_lo if is_lo else L.off_hi
+        off = L.off_lo if is_lo else L.hi_offset(kt)
         nb = n * _row_bytes(fmt, H)
         raw = msg[off:off + nb]
         if fmt == FMT_F32:
@@ -337,20 +386,25 @@ def _gpu_header(spec, L, device):
 
 
 def _args(spec, L):
-    return (L.off_mask, L.off_scale, L.off_hi, L.off_lo, L.B, L.S, L.H, L.k, L.hi_fmt, L.lo_fmt, spec.scale_mode,
-            spec.qmax_hi, spec.qmax_lo, spec.ch_kind)
+    return (L.off_mask, L.off_scale, L.off_hi, L.off_lo, L.off_kvec, L.B, L.S, L.H, max(L.k, 0), L.hi_fmt, L.lo_fmt,
+            spec.scale_mode, spec.qmax_hi, spec.qmax_lo, spec.ch_kind)
 
 
-def _encode_gpu(x, spec, L, imp, msg):
+def _encode_gpu(x, spec, L, imp, msg, mass=0.0):
     if x.dtype not in (torch.bfloat16, torch.float32):
         raise TypeError("GPU boundary codec expects bf16 or fp32 activations")
     xf32 = int(x.dtype == torch.float32)
     st = stream()
     msg[:32].copy_(_gpu_header(spec, L, x.device))
-    if 0 < L.k < L.S:
+    if L.kvar:
+        if imp is None:
+            raise ValueError("top-rho selection needs token importance")
+        call("edge_select", ptr(imp.float().contiguous()), L.B, L.S, 0, ptr(msg), L.off_mask, 1, float(mass),
+             L.off_kvec, st)
+    elif 0 < L.k < L.S:
         if imp is None:
             raise ValueError(f"codec {spec.name} with 0 < k < S needs token importance")
-        call("edge_select", ptr(imp.float().contiguous()), L.B, L.S, L.k, ptr(msg), L.off_mask, None, st)
+        call("edge_select", ptr(imp.float().contiguous()), L.B, L.S, L.k, ptr(msg), L.off_mask, 0, 0.0, -1, st)
     else:
         call("edge_set_mask", ptr(msg), L.off_mask, L.B, L.S, 1 if L.k >= L.S else 0, st)
     if spec.scale_mode == SC_WINDOW:
@@ -372,12 +426,39 @@ def _decode_gpu(msg, spec, L, out):
 
 
 # --------------------------------------------------------------------------------------------
+SELECTIONS = ("ratio", "top_rho")
+
+
+def uses_kvar(spec: CodecSpec, selection: str) -> bool:
+    if selection not in SELECTIONS:
+        raise ValueError(f"unknown selection {selection!r}; known: {SELECTIONS}")
+    return selection == "top_rho" and spec.uses_ratio
+
+
 def encode(x: torch.Tensor, spec: CodecSpec, B: int, S: int, ratio: float = 0.0, importance=None,
-           out: torch.Tensor | None = None, k: int | None = None) -> tuple[torch.Tensor, Layout]:
+           out: torch.Tensor | None = None, k: int | None = None,
+           selection: str = "ratio") -> tuple[torch.Tensor, Layout]:
     """Quantize and pack ``x`` ([B*S, H]) into one boundary message (uint8 tensor).
 
-    The lo class is the ``k = int(ratio*S)`` least important tokens (``k`` may be given directly)."""
+    ``selection="ratio"``: the lo class is the ``k = int(ratio*S)`` least important tokens (``k`` may be given
+    directly).  ``"top_rho"``: every window keeps its shortest descending-importance prefix reaching mass
+    ``1 - ratio`` and quantizes the rest (per-window k, variable-k message)."""
     H = x.shape[-1]
+    if uses_kvar(spec, selection):
+        if importance is None:
+            raise ValueError("top-rho selection needs token importance")
+        L = layout(spec, B, S, H, -1, x.dtype, kvar=True)
+        mass = 1.0 - float(ratio)
+        if x.is_cuda:
+            if out is None:
+                out = torch.zeros(L.total, dtype=torch.uint8, device=x.device)
+            return _encode_gpu(x.contiguous(), spec, L, importance, out, mass), L
+        lo = select_mask(importance, top_rho_k(importance, mass))
+        msg = _encode_cpu(x, spec, L, lo)
+        if out is not None:
+            out.copy_(msg)
+            return out, L
+        return msg, L
     k = num_lo(spec, ratio, S) if k is None else (k if spec.uses_ratio else 0)
     L = layout(spec, B, S, H, k, x.dtype)
     if x.is_cuda:
@@ -407,7 +488,19 @@ def decode(msg: torch.Tensor, spec: CodecSpec, L: Layout, dtype=torch.bfloat16, 
 
 
 def fake_quant(x: torch.Tensor, spec: CodecSpec, B: int, S: int, ratio: float = 0.0, importance=None,
-               k: int | None = None):
+               k: int | None = None, selection: str = "ratio"):
     """decode(encode(x)): what the receiving stage sees.  Returns (x_hat, message bytes)."""
-    msg, L = encode(x, spec, B, S, ratio, importance, k=k)
-    return decode(msg, spec, L, x.dtype), L.total
+    msg, L = encode(x, spec, B, S, ratio, importance, k=k, selection=selection)
+    return decode(msg, spec, L, x.dtype), message_payload(msg, L)
+
+
+def message_k(msg: torch.Tensor, L: Layout) -> torch.Tensor:
+    """Per-window lo counts of a message [B] (reads the k vector of a variable-k message)."""
+    if not L.kvar:
+        return torch.full((L.B,), L.k, dtype=torch.int64)
+    return msg[L.off_kvec:L.off_kvec + 4 * L.B].view(torch.int32).to(torch.int64)
+
+
+def message_payload(msg: torch.Tensor, L: Layout) -> int:
+    """Bytes a link carries for this message (host sync for a variable-k message)."""
+    return L.total if not L.kvar else L.payload_bytes(int(message_k(msg, L).sum()))

@@ -30,11 +30,12 @@ class Params:
     # ---- new keys (defaults reproduce the reference) -------------------------
     model: str = ""                          # preset name, filled by the entry point
     weights: str = ""                        # path to an HF safetensors dir; "" -> HF cache if present, else random
-    dataset: str = "wikitext"                # "wikitext" | "synthetic"
+    dataset: str = "wikitext"                # "wikitext" | "synthetic" | "pysrc*"
+    strict_data: bool = False                # wikitext requested but not cached locally: error instead of a warning
     synthetic_tokens: int = 0                # length of the synthetic stream (0 -> 299,078, the WikiText-2 test size)
     max_windows: int = 0                     # 0 = whole corpus
     window_batch: int = 8                    # windows per forward batch
-    dtype: str = "auto"                      # "auto" (fp32 on CPU, bf16 on GPU) | "fp32" | "bf16"
+    dtype: str = "auto"                      # "auto" = "fp32" (the reference's precision, CPU and GPU) | "bf16"
     device: str = "auto"                     # "auto" | "cpu" | "cuda"
     codec: str = "ref_int4_global"           # boundary codec used for the ratio sweep (see codec/)
     num_stages: int = 1                      # pipeline stages for the distributed runner
@@ -99,8 +100,12 @@ def resolve_dtype(p: Params, device: str):
     if p.dtype == "fp32":
         return torch.float32
     if p.dtype == "bf16":
+        if not device.startswith("cuda"):
+            raise ValueError("dtype bf16 is a GPU execution mode; the CPU path is the fp32 oracle")
         return torch.bfloat16
-    return torch.bfloat16 if device.startswith("cuda") else torch.float32
+    if p.dtype != "auto":
+        raise ValueError(f"unknown dtype {p.dtype!r} (auto | fp32 | bf16)")
+    return torch.float32   # the reference evaluates fp32 models (qwen_layer_wise.py:17: no torch_dtype)
 
 
 def env_flag(name: str, default: bool = False) -> bool:

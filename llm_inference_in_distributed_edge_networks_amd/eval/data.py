@@ -65,8 +65,14 @@ def local_text_bytes(split: str = "eval", root: str = "") -> torch.Tensor:
     return torch.frombuffer(buf, dtype=torch.uint8).to(torch.int64).view(1, -1)
 
 
-def token_stream(dataset: str, hf_id: str, vocab_size: int, synthetic_tokens: int = 0, seed: int = 0):
-    """Returns (ids [1, N], provenance)."""
+class DatasetUnavailable(FileNotFoundError):
+    pass
+
+
+def token_stream(dataset: str, hf_id: str, vocab_size: int, synthetic_tokens: int = 0, seed: int = 0,
+                 strict: bool = False):
+    """Returns (ids [1, N], provenance).  ``dataset="wikitext"`` without a local cache falls back to the synthetic
+    stream with a loud warning (``strict``: raises instead); ``dataset="synthetic"`` asks for it explicitly."""
     if dataset in ("pysrc", "pysrc-eval", "pysrc-train"):
         split = "train" if dataset == "pysrc-train" else "eval"
         ids = local_text_bytes(split)
@@ -77,5 +83,14 @@ def token_stream(dataset: str, hf_id: str, vocab_size: int, synthetic_tokens: in
         ids = load_wikitext_tokens(hf_id)
         if ids is not None:
             return ids, "wikitext-2-raw-v1/test"
+        msg = (f"WikiText-2 (or the {hf_id} tokenizer) is not available locally: the PPL below is on a SYNTHETIC "
+               "token stream, not WikiText-2 (set dataset='synthetic' to ask for it, strict_data=true to fail)")
+        if strict:
+            raise DatasetUnavailable(msg)
+        import warnings
+        warnings.warn(msg, RuntimeWarning, stacklevel=2)
+        print(f"WARNING: {msg}", flush=True)
+    elif dataset != "synthetic":
+        raise ValueError(f"unknown dataset {dataset!r} (wikitext | synthetic | pysrc | pysrc-eval | pysrc-train)")
     n = synthetic_tokens or WIKITEXT2_TEST_TOKENS
     return synthetic_stream(n, vocab_size, seed), f"synthetic(n={n},seed={seed})"

@@ -29,7 +29,7 @@ from ..parallel.dist import all_reduce_sum, get_env, init_distributed
 from ..utils.checkpoint import SweepState
 from ..utils.logging import log, progress_bar
 from .data import token_stream
-from .sweep import SweepConfig, SweepEngine, run_sweep
+from .sweep import SweepConfig, SweepEngine, SweepMethod, run_sweep
 from .windows import batches, sliding_windows
 
 CHANNEL_METHODS = ("channel_8", "channel_4", "channel_1_mean", "channel_1_max")
@@ -41,7 +41,8 @@ def _setup(p: Params, default_model: str):
     dtype = resolve_dtype(p, device)
     cfg = get_config(p.model or default_model)
     model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed)
-    ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed)
+    ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed,
+                                  strict=p.strict_data)
     max_len = p.max_length or cfg.max_position
     wins = sliding_windows(ids.shape[1], max_len, p.stride)
     if p.max_windows:
@@ -63,7 +64,7 @@ def _reduce(engine: SweepEngine):
     if not env.is_dist:
         return
     dev = env.device if env.backend == "nccl" else torch.device("cpu")
-    t = torch.cat([engine.total_nll.reshape(-1), engine.wire_bytes.reshape(-1),
+    t = torch.cat([engine.total_nll.reshape(-1), engine.wire_bytes.reshape(-1), engine.sum_window_nll.reshape(-1),
                    torch.tensor([engine.n_tokens, engine.windows_done, engine.tokens_done, engine.forward_tokens],
                                 dtype=torch.float64)]).to(dev)
     all_reduce_sum(t)
@@ -71,8 +72,9 @@ def _reduce(engine: SweepEngine):
     n = engine.total_nll.numel()
     engine.total_nll = t[:n].reshape(engine.total_nll.shape)
     engine.wire_bytes = t[n:2 * n].reshape(engine.wire_bytes.shape)
+    engine.sum_window_nll = t[2 * n:3 * n].reshape(engine.sum_window_nll.shape)
     engine.n_tokens, engine.windows_done, engine.tokens_done, engine.forward_tokens = \
-        float(t[2 * n]), int(t[2 * n + 1]), int(t[2 * n + 2]), int(t[2 * n + 3])
+        float(t[3 * n]), int(t[3 * n + 1]), int(t[3 * n + 2]), int(t[3 * n + 3])
 
 
 def importance_sweep(p: Params, default_model: str, out_name: str) -> dict:
@@ -87,8 +89,7 @@ def importance_sweep(p: Params, default_model: str, out_name: str) -> dict:
                                     "(run Experiments/Relevance/main.py or set params['head_weights'])")
     sc = SweepConfig(methods, p.layers_of_interest, p.ratios, p.codec, hw)
     eng = SweepEngine(model, sc)
-    state = SweepState(os.path.join(p.output_dir, f"{out_name}.rank{env.rank}.ckpt.json"), p.config_hash(),
-                       enabled=p.resume)
+    state = _state(p, env, out_name)
     pb = progress_bar(len(wins), env.is_main)
     res = run_sweep(eng, _shard(batches(ids, wins, p.window_batch), env), state, p.checkpoint_every,
                     progress=pb.update, reduce_fn=_reduce)
@@ -103,116 +104,88 @@ def importance_sweep(p: Params, default_model: str, out_name: str) -> dict:
     return res
 
 
+def _state(p: Params, env, name: str) -> SweepState:
+    return SweepState(os.path.join(p.output_dir, f"{name}.rank{env.rank}.ckpt.json"), p.config_hash(),
+                      enabled=p.resume, shard=(env.rank, env.world_size, f"batch-mod/{p.window_batch}"))
+
+
 def channel_sweep(p: Params, default_model: str) -> dict:
-    """Reference ``channel_wise.py``: per-channel quantization of the whole boundary tensor."""
+    """Reference ``channel_wise.py``: per-channel quantization of the whole boundary tensor.
+
+    One unquantized prefix forward per window batch; the 4 channel codecs (and every boundary layer) fork
+    from it in one stacked suffix forward (the reference re-runs the whole model per (method, layer))."""
     env, cfg, model, ids, wins, meta = _setup(p, default_model)
-    out = {"layers_of_interest": p.layers_of_interest, "methods": list(p.methods), "avg_ppl_results": []}
-    engines = {}
     for meth in p.methods:
         if meth not in CHANNEL_METHODS:
             raise ValueError(f"channel sweep got non-channel method {meth!r}")
-        engines[meth] = SweepEngine(model, SweepConfig(["regular_importance"], p.layers_of_interest, [1], meth))
-    t0 = time.perf_counter()
-    for b in _shard(batches(ids, wins, p.window_batch), env):
-        b = b.to(model.device)
-        for e in engines.values():
-            e.run_batch(b)
-    for e in engines.values():
-        _reduce(e)
-    res_l = []
-    for li, L in enumerate(p.layers_of_interest):
-        res_l.append([float(engines[m].ppl()[0, li, 0]) for m in p.methods])
-    out["avg_ppl_results"] = res_l           # [layer][method] (reference layout)
-    out["wire_bytes_per_token"] = [[float(engines[m].wire_bytes[0, li, 0]) / max(1, engines[m].tokens_done)
-                                    for m in p.methods] for li in range(len(p.layers_of_interest))]
-    out["seconds"] = time.perf_counter() - t0
+    rows = [SweepMethod(m, None, codec=m) for m in p.methods]
+    eng = SweepEngine(model, SweepConfig(rows, p.layers_of_interest, [1], p.methods[0]))
+    pb = progress_bar(len(wins), env.is_main)
+    res = run_sweep(eng, _shard(batches(ids, wins, p.window_batch), env), _state(p, env, "channel"),
+                    p.checkpoint_every, progress=pb.update, reduce_fn=_reduce)
+    pb.close()
+    ppl = eng.ppl()
+    out = {"layers_of_interest": p.layers_of_interest, "methods": list(p.methods)}
+    out["avg_ppl_results"] = [[float(ppl[mi, li, 0]) for mi in range(len(p.methods))]
+                              for li in range(len(p.layers_of_interest))]          # [layer][method] (reference)
+    out["wire_bytes_per_token"] = [[float(eng.wire_bytes[mi, li, 0]) / max(1, eng.tokens_done)
+                                    for mi in range(len(p.methods))] for li in range(len(p.layers_of_interest))]
+    out["seconds"] = res["seconds"]
+    out["windows"] = res["windows"]
+    out["windows_per_s"] = res["windows"] / max(res["seconds"], 1e-9)
     out.update(meta)
     if env.is_main:
         os.makedirs(p.output_dir, exist_ok=True)
         dump_json(out, os.path.join(p.output_dir, "avg_ppl_results_channel.json"))
         for li, L in enumerate(p.layers_of_interest):
-            log(f"layer {L}: " + "  ".join(f"{m}={v:.4f}" for m, v in zip(p.methods, res_l[li])))
+            log(f"layer {L}: " + "  ".join(f"{m}={v:.4f}" for m, v in zip(p.methods, out["avg_ppl_results"][li])))
     return out
+
+
+INITIAL_QUANT_LAYER = 2   # initial_exp.py:118/:122
+
+
+def initial_rows(layers_of_interest) -> list:
+    """Pythia ``initial`` orderings (``initial_exp.py:27-72``) as sweep rows at the fixed boundary layer 2."""
+    rows = []
+    for l in layers_of_interest:
+        if l == "aggregate upto 2":
+            rows.append(SweepMethod(str(l), "aggregate_till"))
+        elif l == "maximum aggregation":
+            rows.append(SweepMethod(str(l), "maximum_aggregation"))
+        elif l == "upto ratio":
+            rows.append(SweepMethod(str(l), "regular_importance", selection="top_rho"))
+        else:
+            rows.append(SweepMethod(str(l), "regular_importance", source_layer=int(l)))
+    return rows
 
 
 def initial_experiment(p: Params) -> dict:
     """Pythia ``initial_exp.py``: quantize at layer 2 with orderings from special 'layers'.
 
     ``layers_of_interest`` entries: int l (order by layer-l column mean), 'aggregate upto 2',
-    'maximum aggregation', 'upto ratio' (top-rho on the layer-2 distribution).  Ratios are ints
-    0..10 meaning 0.1*ratio of the tokens (Q4, ``pythia_model.py:142``).  Quantizer: per-token int8
-    on the selected tokens (intended semantics of Q2, B9-B11 fixed).  Output ``exp_1.json`` =
-    ``{layer: {ratio: mean_nll}}`` (unweighted mean over windows, ``initial_exp.py:130-134``).
+    'maximum aggregation', 'upto ratio' (top-rho on the layer-2 distribution, k per window).  Ratios are
+    ints 0..10 meaning 0.1*ratio of the tokens (Q4, ``pythia_model.py:142``; top-rho mass 1 - 0.1*ratio).
+    Quantizer: per-token int8 on the selected tokens (intended semantics of Q2, B9-B11 fixed).  Like the
+    reference (``initial_exp.py:113-122``: one batch row per ratio) every (ordering, ratio) variant of a window
+    batch runs in ONE stacked suffix forward after a single shared prefix; no host sync per window.  Output
+    ``exp_1.json`` = ``{layer: {ratio: mean_nll}}`` (unweighted mean over windows, ``initial_exp.py:130-134``).
     """
-    from .. import codec as C
-    from ..importance import ImportanceTracker
-    from .windows import window_nll
     env, cfg, model, ids, wins, meta = _setup(p, "pythia-70m")
-    QL = 2
-    spec = C.get_codec("int8_token_keep")
-    sums: dict = {}
-    counts = 0
-    for b in _shard(batches(ids, wins, p.window_batch), env):
-        b = b.to(model.device)
-        B, S = b.B, b.S
-        tr = ImportanceTracker("aggregate_till", [0, 1, 2], cfg.num_heads)
-        trm = ImportanceTracker("maximum_aggregation", [2], cfg.num_heads)
-        x = model.embed(b.ids)
-        regs = {}
-        h2 = None
-        for i in range(cfg.num_layers):
-            need = "colsum" if i <= max(2, max([l for l in p.layers_of_interest if isinstance(l, int)] or [0])) \
-                else None
-            x, st = model.layer(i, x, B, S, stats=need)
-            if need:
-                tr.observe(i, st, S) if i <= 2 else None
-                trm.observe(i, st, S) if i <= 2 else None
-                from .. import ops
-                regs[i] = ops.head_combine(st.colsum, None, 1.0 / (cfg.num_heads * S))
-            if i == QL:
-                h2 = x
-        for l in p.layers_of_interest:
-            if l == "aggregate upto 2":
-                imp = tr.importance(2)
-            elif l == "maximum aggregation":
-                imp = trm.importance(2)
-            elif l == "upto ratio":
-                imp = regs[2]
-            else:
-                imp = regs[int(l)]
-            for r in p.ratios:
-                if l == "upto ratio":
-                    # top-rho: keep the smallest prefix (by descending importance) reaching 1 - 0.1*r mass
-                    srt = torch.sort(imp.float(), dim=1, descending=True).values
-                    cum = srt.cumsum(1)
-                    keep = (cum < (1 - 0.1 * float(r))).sum(1) + 1
-                    ks = (S - keep.clamp(max=S)).tolist()
-                else:
-                    ks = [int(0.1 * float(r) * S)] * B
-                wn = []
-                for bi in range(B):
-                    xb = h2.view(B, S, -1)[bi].contiguous()
-                    xq, _ = C.fake_quant(xb, spec, 1, S, importance=imp[bi:bi + 1], k=ks[bi])
-                    xs = xq
-                    for i in range(QL + 1, cfg.num_layers):
-                        xs, _ = model.layer(i, xs, 1, S)
-                    sel = b.row_window == bi
-                    rows = b.rows[sel] - bi * S
-                    nll = model.row_nll(xs, rows, b.targets[sel])
-                    wn.append(float(nll.mean()))
-                key = (str(l), r)
-                sums[key] = sums.get(key, 0.0) + sum(wn)
-        counts += B
-    if env.is_dist:
-        keys = sorted(sums, key=str)
-        t = torch.tensor([sums[k] for k in keys] + [counts], dtype=torch.float64)
-        all_reduce_sum(t)
-        sums = dict(zip(keys, t[:-1].tolist()))
-        counts = int(t[-1])
-    res = {}
-    for (l, r), s in sums.items():
-        res.setdefault(l, {})[str(r)] = s / counts
-    out = {"exp_1": res, "ppl": {l: {r: math.exp(v) for r, v in d.items()} for l, d in res.items()}, **meta}
+    sc = SweepConfig(initial_rows(p.layers_of_interest), [INITIAL_QUANT_LAYER], p.ratios, codec="int8_token_keep",
+                     ratio_scale=0.1)
+    eng = SweepEngine(model, sc)
+    pb = progress_bar(len(wins), env.is_main)
+    res = run_sweep(eng, _shard(batches(ids, wins, p.window_batch), env), _state(p, env, "exp_1"),
+                    p.checkpoint_every, progress=pb.update, reduce_fn=_reduce)
+    pb.close()
+    mw = res["mean_window_nll"]
+    exp1 = {name: {str(r): mw[mi][0][ri] for ri, r in enumerate(p.ratios)} for mi, name in enumerate(eng.methods)}
+    out = {"exp_1": exp1, "ppl": {l: {r: math.exp(v) for r, v in d.items()} for l, d in exp1.items()},
+           "wire_bytes_per_token": {name: {str(r): res["wire_bytes_per_token"][mi][0][ri]
+                                           for ri, r in enumerate(p.ratios)} for mi, name in enumerate(eng.methods)},
+           "windows": res["windows"], "seconds": res["seconds"],
+           "windows_per_s": res["windows"] / max(res["seconds"], 1e-9), **meta}
     if env.is_main:
         os.makedirs(p.output_dir, exist_ok=True)
         dump_json(out, os.path.join(p.output_dir, "exp_1.json"))
@@ -264,7 +237,8 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
                                   layers=plan.stage_layers(stage), with_embed=stage == 0, with_head=stage == pp - 1)
     else:
         model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed)
-    ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed)
+    ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed,
+                                  strict=p.strict_data)
     wins = sliding_windows(ids.shape[1], max_len, p.stride)
     if p.max_windows:
         wins = wins[: p.max_windows]

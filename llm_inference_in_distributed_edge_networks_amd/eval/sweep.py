@@ -8,15 +8,24 @@ forward per (method, layer, ratio) - 101 forwards of 512 tokens per Qwen2 window
 Here, per window batch:
 
 1. ONE unquantized forward: it yields the ratio-0 NLL, the hidden state after every boundary layer
-   of interest (kept on device) and every method's importance at those layers (fused attention
-   statistics, no S x S maps);
+   of interest (kept on device) and every method's importance at the layers it is needed (fused
+   attention statistics, no S x S maps);
 2. per boundary layer L, the (method, ratio) variants are de-duplicated (ratio 0 and "all tokens
    quantized" do not depend on the method), their fake-quantized copies of h_L are stacked along the
    batch dimension and ONLY layers L+1.. are run, once, on the stacked batch (shared-prefix fork).
 
+A sweep row is a ``SweepMethod``: an importance method (or none, for importance-free codecs), the
+layer its importance is read at (default: the boundary layer), the selection rule ("ratio" or
+"top_rho") and the codec.  That covers all three reference drivers with one engine:
+``Experiments/Qwen2-0.5B/main.py`` (4 methods x layers x ratios), the Pythia ``initial`` sweep
+(``initial_exp.py:113-122``: orderings from other layers, top-rho, boundary fixed at layer 2, all
+ratios of a window in ONE stacked suffix forward) and the channel sweep (``channel_wise.py:35-68``:
+4 importance-free codecs forked from one prefix).
+
 Results keep the reference layouts: ``total_nll[method][layer][ratio]`` and
 ``avg_ppl_results[method][layer][ratio]`` (ordered as in params.json), channel sweeps
-``[layer][method]``.  Progress is checkpointed every ``checkpoint_every`` windows and resumed.
+``[layer][method]``, plus the unweighted mean per-window NLL of the ``initial`` experiment.
+Progress is checkpointed every ``checkpoint_every`` windows and resumed.
 """
 from __future__ import annotations
 
@@ -36,9 +45,19 @@ from ..utils.checkpoint import SweepState
 from .windows import WindowBatch, segment_mean, window_nll
 
 
+@dataclass(frozen=True)
+class SweepMethod:
+    """One row of a sweep."""
+    name: str                          # result key
+    method: str | None                 # importance method, None for importance-free codecs
+    codec: str | None = None           # None -> SweepConfig.codec
+    source_layer: int | None = None    # importance read at this layer instead of the boundary layer
+    selection: str = "ratio"           # "ratio" | "top_rho" (codec.wire)
+
+
 @dataclass
 class SweepConfig:
-    methods: list
+    methods: list                      # method names (str) or SweepMethod
     layers: list
     ratios: list
     codec: str = "ref_int4_global"
@@ -46,16 +65,24 @@ class SweepConfig:
     max_fork_tokens: int = 1 << 17     # cap on tokens per stacked suffix forward
     ratio_scale: float = 1.0           # Pythia 'initial' uses ratio in 0..10 meaning 0.1*ratio
 
+    def rows(self) -> list:
+        out = []
+        for m in self.methods:
+            out.append(m if isinstance(m, SweepMethod) else SweepMethod(str(m), canonical(m)))
+        return out
+
 
 class SweepEngine:
     def __init__(self, model: DecoderLM, sc: SweepConfig):
         self.m, self.sc = model, sc
         self.spec = C.get_codec(sc.codec)
-        self.methods = list(sc.methods)
+        self.rows = sc.rows()
+        self.methods = [r.name for r in self.rows]
         self.layers = [int(l) for l in sc.layers]
         self.ratios = list(sc.ratios)
         shape = (len(self.methods), len(self.layers), len(self.ratios))
         self.total_nll = torch.zeros(shape, dtype=torch.float64)
+        self.sum_window_nll = torch.zeros(shape, dtype=torch.float64)   # unweighted (initial experiment)
         self.n_tokens = 0.0
         self.windows_done = 0
         self.forward_tokens = 0
@@ -67,11 +94,25 @@ class SweepEngine:
         self.head_weights = None if hw is None else torch.as_tensor(hw).to(self.m.device, torch.float32).contiguous()
 
     # -------------------------------------------------------------- one batch
+    def _needed(self) -> dict:
+        """importance method -> layers its importance is read at."""
+        need: dict = {}
+        for r in self.rows:
+            if r.method is None:
+                continue
+            src = [r.source_layer] if r.source_layer is not None else self.layers
+            need.setdefault(canonical(r.method), set()).update(int(x) for x in src)
+        return need
+
+    def _imp_key(self, r: SweepMethod, L: int):
+        return (canonical(r.method), r.source_layer if r.source_layer is not None else L)
+
     def _prefix(self, batch: WindowBatch):
-        """Unquantized forward: base per-window NLL, h_L per boundary layer, importance per (method, L)."""
+        """Unquantized forward: base per-window NLL, h_L per boundary layer, importance per (method, layer)."""
         m, B, S = self.m, batch.B, batch.S
-        trackers = {meth: ImportanceTracker(meth, self.layers, m.cfg.num_heads, self.head_weights)
-                    for meth in self.methods}
+        need = self._needed()
+        trackers = {meth: ImportanceTracker(meth, sorted(ls), m.cfg.num_heads, self.head_weights)
+                    for meth, ls in need.items()}
         x = m.embed(batch.ids)
         saved = {}
         last = m.cfg.num_layers - 1
@@ -94,11 +135,11 @@ class SweepEngine:
                 saved[i] = x
         base = window_nll(m.row_nll(x, rows, batch.targets), batch)
         self.forward_tokens += B * S
-        imp = {(meth, L): trackers[meth].importance(L) for meth in self.methods for L in self.layers}
+        imp = {(meth, L): trackers[meth].importance(L) for meth, ls in need.items() for L in ls}
         return base, saved, imp
 
-    def _k(self, ratio, S):
-        return C.wire.num_lo(self.spec, float(ratio) * self.sc.ratio_scale, S)
+    def _k(self, ratio, S, spec=None):
+        return C.wire.num_lo(spec or self.spec, float(ratio) * self.sc.ratio_scale, S)
 
     def run_batch(self, batch: WindowBatch) -> torch.Tensor:
         """Returns per-window NLL [M, Lc, R, B] for this batch (also accumulated)."""
@@ -110,17 +151,23 @@ class SweepEngine:
         for li, L in enumerate(self.layers):
             # de-duplicate variants: key -> list of (mi, ri)
             variants: dict = {}
-            for mi, meth in enumerate(self.methods):
+            for mi, row in enumerate(self.rows):
+                spec = C.get_codec(row.codec) if row.codec else self.spec
                 for ri, r in enumerate(self.ratios):
-                    k = self._k(r, S)
+                    reff = float(r) * self.sc.ratio_scale
+                    if C.wire.uses_kvar(spec, row.selection):
+                        key = (self._imp_key(row, L), "top_rho", reff, spec.name)
+                        variants.setdefault(key, []).append((mi, ri))
+                        continue
+                    k = self._k(r, S, spec)
                     # no lo tokens and an exact hi class (reference Q1 "ratio 0"): the unquantized base
-                    if k == 0 and self.spec.uses_ratio and self.spec.hi_fmt == C.wire.NATIVE:
+                    if k == 0 and spec.uses_ratio and spec.hi_fmt == C.wire.NATIVE:
                         out[mi, li, ri] = base
                         self.wire_bytes[mi, li, ri] += C.message_bytes(C.get_codec("passthrough"), B, S,
                                                                        m.cfg.hidden_size, 0.0, m.dtype)
                         continue
-                    method_free = k >= S or k == 0 or not self.spec.needs_importance
-                    key = ("all", k) if method_free else (meth, k)
+                    method_free = k >= S or k == 0 or not spec.needs_importance or row.method is None
+                    key = ("all", k, spec.name) if method_free else (self._imp_key(row, L), k, spec.name)
                     variants.setdefault(key, []).append((mi, ri))
             keys = list(variants)
             per_fork = max(1, self.sc.max_fork_tokens // (B * S))
@@ -128,9 +175,13 @@ class SweepEngine:
                 chunk = keys[c0:c0 + per_fork]
                 xs = []
                 for key in chunk:
-                    meth, k = key
-                    im = None if meth == "all" else imp[(meth, L)]
-                    xq, nbytes = C.fake_quant(saved[L], self.spec, B, S, importance=im, k=k)
+                    src, kk, cname = key[0], key[1], key[-1]
+                    spec = C.get_codec(cname)
+                    im = None if src == "all" else imp[src]
+                    if kk == "top_rho":
+                        xq, nbytes = C.fake_quant(saved[L], spec, B, S, key[2], importance=im, selection="top_rho")
+                    else:
+                        xq, nbytes = C.fake_quant(saved[L], spec, B, S, importance=im, k=kk)
                     xs.append(xq)
                     for (mi, ri) in variants[key]:
                         self.wire_bytes[mi, li, ri] += nbytes
@@ -152,7 +203,9 @@ class SweepEngine:
                     for (mi, ri) in variants[key]:
                         out[mi, li, ri] = wn[vi]
         w = batch.weights.to(out.device)
-        self.total_nll += (out.double() * w).sum(-1).cpu()
+        od = out.double()
+        self.total_nll += (od * w).sum(-1).cpu()
+        self.sum_window_nll += od.sum(-1).cpu()
         self.n_tokens += float(batch.weights.sum())
         self.windows_done += B
         self.tokens_done += B * S
@@ -170,14 +223,17 @@ class SweepEngine:
                                  for li in range(len(self.layers))] for mi in range(len(self.methods))],
             "total_nll": self.total_nll.tolist(), "n_tokens": self.n_tokens, "windows": self.windows_done,
             "wire_bytes_per_token": (self.wire_bytes / max(1, self.tokens_done)).tolist(),
+            "mean_window_nll": (self.sum_window_nll / max(1, self.windows_done)).tolist(),
         }
 
     def state(self) -> dict:
         return {"total_nll": self.total_nll.tolist(), "n_tokens": self.n_tokens, "windows_done": self.windows_done,
-                "wire_bytes": self.wire_bytes.tolist(), "tokens_done": self.tokens_done}
+                "wire_bytes": self.wire_bytes.tolist(), "tokens_done": self.tokens_done,
+                "sum_window_nll": self.sum_window_nll.tolist()}
 
     def load_state(self, st: dict) -> None:
         self.total_nll = torch.tensor(st["total_nll"], dtype=torch.float64)
+        self.sum_window_nll = torch.tensor(st["sum_window_nll"], dtype=torch.float64)
         self.n_tokens = float(st["n_tokens"])
         self.windows_done = int(st["windows_done"])
         self.wire_bytes = torch.tensor(st["wire_bytes"], dtype=torch.float64)

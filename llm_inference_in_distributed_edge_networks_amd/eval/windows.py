@@ -37,8 +37,10 @@ class Window:
 
     @property
     def weight(self) -> int:
-        # num_loss_tokens = num_valid_tokens - batch_size (batch_size = 1 in the reference)
-        return self.trg_len - 1
+        # num_loss_tokens = num_valid_tokens - batch_size (batch_size = 1 in the reference).  With stride >
+        # max_length, trg_len exceeds the window and the reference's target[:, :-trg_len] = -100 masks nothing:
+        # all length tokens are valid.
+        return min(self.trg_len, self.length) - 1
 
     @property
     def first_scored(self) -> int:

@@ -387,8 +387,9 @@ def split6(x: torch.Tensor, rows: torch.Tensor | None = None) -> torch.Tensor:
     return y
 
 
-def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=None, out=None) -> torch.Tensor:
-    """fp32-accurate ``act(x @ w.T + bias) + residual`` from X6 operands (x6 [M, 6K], w6 [N, 6K]).
+def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=None, out=None,
+              rscale=None) -> torch.Tensor:
+    """fp32-accurate ``act(rscale * (x @ w.T) + bias) + residual`` from X6 operands (x6 [M, 6K], w6 [N, 6K]).
 
     act None -> fp32 [M, N] (``residual`` fp32, may alias ``out``); act "gelu" / "swiglu_il" -> the activation in
     the X6 layout ([M, 6N] / [M, 3N]) for the next GEMM."""
@@ -396,6 +397,8 @@ def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=
     N = w6.shape[0]
     if not _gpu(x6):
         y = ref.x6_to_f32(x6) @ ref.x6_to_f32(w6).t()
+        if rscale is not None:
+            y = y * rscale.float().view(-1, 1)
         if bias is not None:
             y = y + bias.float()
         if act == "gelu":
@@ -410,7 +413,7 @@ def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=
             return out
         return y
     _check_x6(x6, w6)
-    _check_f32(bias, residual)
+    _check_f32(bias, residual, rscale)
     assert w6.shape[1] == Kx
     if act is None:
         if out is None:
@@ -423,7 +426,7 @@ def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=
         ldc = 6 * No
         code = _ACT[act]
     call("edge_gemm_f32", ptr(x6), ptr(w6), ptr(out), M, N, Kx, x6.stride(0), w6.stride(0), ldc, ptr(bias),
-         ptr(residual), 0 if residual is None else residual.stride(0), code, stream())
+         ptr(residual), 0 if residual is None else residual.stride(0), code, ptr(rscale), stream())
     return out
 
 

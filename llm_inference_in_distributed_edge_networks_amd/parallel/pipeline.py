@@ -29,7 +29,7 @@ from ..eval.windows import PPLAccumulator, WindowBatch, window_nll
 from ..importance import ImportanceTracker, canonical
 from ..models.model import DecoderLM
 from ..utils import trace
-from ..utils.graphs import GraphCache
+from ..utils.graphs import GraphCache, prerun_active
 from ..utils.watchdog import from_env as watchdog_from_env
 from .dist import Grid, all_reduce_sum
 from .plan import PipelinePlan
@@ -41,12 +41,19 @@ class BoundaryConfig:
     ratio: float = 0.0
     method: str = "last_row"
     head_weights: torch.Tensor | None = None
+    selection: str = "ratio"      # "ratio": int(ratio*S) least important; "top_rho": keep mass 1 - ratio
 
     @property
     def spec(self) -> C.CodecSpec:
         return C.get_codec(self.codec)
 
+    @property
+    def kvar(self) -> bool:
+        return C.wire.uses_kvar(self.spec, self.selection)
+
     def needs_importance(self, S: int) -> bool:
+        if self.kvar:
+            return self.spec.needs_importance and self.ratio < 1.0
         k = C.wire.num_lo(self.spec, self.ratio, S)
         return self.spec.needs_importance and 0 < k < S
 
@@ -58,10 +65,12 @@ class StageStats:
     wire_bytes: int = 0          # bytes this stage sent across its outgoing boundary
     wire_tokens: int = 0
     compute_s: float = 0.0
+    kvar_bytes: torch.Tensor | None = None   # variable-k messages: payload bytes summed on the device
 
     @property
     def bytes_per_token(self) -> float:
-        return self.wire_bytes / self.wire_tokens if self.wire_tokens else 0.0
+        b = self.wire_bytes + (float(self.kvar_bytes) if self.kvar_bytes is not None else 0.0)
+        return b / self.wire_tokens if self.wire_tokens else 0.0
 
 
 class StageRunner:
@@ -109,13 +118,23 @@ class StageRunner:
         return x, imp, (tr.carry() if tr is not None else None)
 
     def encode(self, x, batch: WindowBatch, imp, out=None):
-        msg, L = C.encode(x, self.bcfg.spec, batch.B, batch.S, self.bcfg.ratio, imp, out=out)
+        msg, L = C.encode(x, self.bcfg.spec, batch.B, batch.S, self.bcfg.ratio, imp, out=out,
+                          selection=self.bcfg.selection)
+        if L.kvar and not prerun_active():   # compact message payload, summed on the device (capturable, no sync)
+            kt = msg[L.off_kvec:L.off_kvec + 4 * L.B].view(torch.int32).sum().to(torch.float64)
+            rl, rh = C.wire._row_bytes(L.lo_fmt, L.H), C.wire._row_bytes(L.hi_fmt, L.H)
+            pay = L.off_lo + torch.ceil(kt * rl / 16) * 16 + (L.B * L.S - kt) * rh
+            if self.stats.kvar_bytes is None or self.stats.kvar_bytes.device != msg.device:
+                self.stats.kvar_bytes = torch.zeros((), dtype=torch.float64, device=msg.device)
+            self.stats.kvar_bytes += pay
         return msg, L
 
     def account(self, batch: WindowBatch) -> None:
         """Wire-byte accounting of the outgoing boundary (outside any captured graph)."""
         if not self.last:
-            self.stats.wire_bytes += self.layout(batch).total
+            L = self.layout(batch)
+            if not L.kvar:
+                self.stats.wire_bytes += L.total
             self.stats.wire_tokens += batch.B * batch.S
         self.stats.windows += batch.B
         self.stats.tokens += batch.tokens
@@ -140,6 +159,8 @@ class StageRunner:
 
     def layout(self, batch: WindowBatch) -> C.Layout:
         spec = self.bcfg.spec
+        if self.bcfg.kvar:
+            return C.layout(spec, batch.B, batch.S, self.model.cfg.hidden_size, -1, self.model.dtype, kvar=True)
         k = C.wire.num_lo(spec, self.bcfg.ratio, batch.S)
         return C.layout(spec, batch.B, batch.S, self.model.cfg.hidden_size, k, self.model.dtype)
 

@@ -179,7 +179,10 @@ def head_relevance(model, ids: torch.Tensor, dtype=torch.float32, via_probs: boo
 
 
 def normalize_per_layer(rel: torch.Tensor) -> torch.Tensor:
-    return rel / rel.sum(-1, keepdim=True)
+    """Each layer's heads divided by the layer sum (signed); a zero sum divides by 1e-9 as the reference does
+    (``Experiments/Relevance/main.py:111-118``) instead of producing NaN head weights."""
+    s = rel.sum(-1, keepdim=True)
+    return rel / torch.where(s != 0, s, torch.full_like(s, 1e-9))
 
 
 def relevance_main(p) -> list:
@@ -195,9 +198,14 @@ def relevance_main(p) -> list:
     env = init_distributed(p.device)
     device = str(env.device)
     cfg = get_config(p.model or "qwen2-0.5b")
-    # bf16 on the GPU (the HIP kernels' storage type), fp32 on the CPU oracle path
-    model, prov = build_model(cfg, device, resolve_dtype(p, device), weights=p.weights, seed=p.seed)
-    ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed)
+    # the explicit LRP engine's GPU kernels (csrc/lrp.hip) are bf16: dtype "auto" picks bf16 on the GPU for this
+    # offline calibration, fp32 on the CPU oracle path
+    dtype = torch.bfloat16 if (device.startswith("cuda") and p.dtype == "auto") else resolve_dtype(p, device)
+    if device.startswith("cuda") and dtype == torch.float32:
+        raise NotImplementedError("the GPU LRP engine runs bf16 (dtype: bf16 or auto); fp32 relevance runs on CPU")
+    model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed)
+    ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed,
+                                  strict=p.strict_data)
     wins = sliding_windows(ids.shape[1], p.max_length or 512, p.stride)
     if p.max_windows:
         wins = wins[: p.max_windows]

@@ -11,9 +11,16 @@ import json
 import os
 
 
+class ShardMismatch(RuntimeError):
+    """A checkpoint of this configuration was written under another data-parallel sharding."""
+
+
 class SweepState:
-    def __init__(self, path: str, config_hash: str, enabled: bool = True):
+    def __init__(self, path: str, config_hash: str, enabled: bool = True, shard: tuple | None = None):
+        """``shard`` = (rank, world_size, scheme): which windows this rank processes.  Resuming under a different
+        sharding would skip windows this rank never saw and count others twice, so it is refused."""
         self.path, self.hash, self.enabled = path, config_hash, enabled
+        self.shard = list(shard) if shard is not None else None
 
     def load(self):
         if not self.enabled or not os.path.exists(self.path):
@@ -25,12 +32,16 @@ class SweepState:
             return None
         if st.get("config_hash") != self.hash:
             return None
+        if self.shard is not None and st.get("shard") != self.shard:
+            raise ShardMismatch(f"{self.path} was written with sharding (rank, world, scheme) = {st.get('shard')}, "
+                                f"this run is {self.shard}: resume with the same world size, or delete the "
+                                "checkpoints / set resume=false to start over")
         return st
 
     def save(self, st: dict) -> None:
         if not self.enabled:
             return
-        st = dict(st, config_hash=self.hash)
+        st = dict(st, config_hash=self.hash, shard=self.shard)
         os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
         tmp = self.path + ".tmp"
         with open(tmp, "w") as f:

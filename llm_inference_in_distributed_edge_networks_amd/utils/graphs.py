@@ -20,6 +20,15 @@ from typing import Callable
 import torch
 
 
+_PRERUN = False
+
+
+def prerun_active() -> bool:
+    """True during the extra eager run that precedes a capture: side-effect counters (e.g. wire-byte accumulators)
+    skip it so every micro-batch is counted once."""
+    return _PRERUN
+
+
 class GraphCache:
     def __init__(self, fn: Callable, enabled: bool = True, warmup: int = 1):
         """``fn(*tensors) -> tensor or tuple of tensors``; every input must be a tensor."""
@@ -57,8 +66,13 @@ class GraphCache:
         graph = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+        global _PRERUN
         with torch.cuda.stream(s):
-            self.fn(*static_in)  # one more eager run on the capture stream
+            _PRERUN = True
+            try:
+                self.fn(*static_in)  # one more eager run on the capture stream
+            finally:
+                _PRERUN = False
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         with torch.cuda.graph(graph):

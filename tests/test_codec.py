@@ -143,3 +143,42 @@ def test_compression_ordering():
     assert bpt["passthrough"] > bpt["ref_int4_global"] > bpt["int8_token"] > bpt["mixed_int4_int8"] > \
         bpt["mixed_int2_int8"]
     assert abs(bpt["passthrough"] - 2 * H) < 2
+
+
+def test_select_mask_nan_and_ties():
+    """Selection order = stable ascending sort with NaN last and -0 == +0 (what the GPU bitonic kernel does)."""
+    imp = torch.tensor([[0.5, float("nan"), -0.0, 0.0, 0.5, -1.0, float("inf")]])
+    lo = C.wire.select_mask(imp, 4)
+    assert lo.tolist() == [[True, False, True, True, False, True, False]]
+    assert C.wire.select_mask(imp, [6]).sum() == 6 and not C.wire.select_mask(imp, [6])[0, 1]
+
+
+@pytest.mark.parametrize("mass,exp", [(1.0, 0), (0.0, 6), (-0.5, 6), (0.5, 5), (0.55, 4), (0.9, 2)])
+def test_top_rho_k(mass, exp):
+    """keep = first i with sum_{j<i} desc_j >= mass (pythia_model.py:92-112, B21 fixed): mass <= 0 keeps none."""
+    imp = torch.tensor([[0.05, 0.5, 0.1, 0.2, 0.1, 0.05]])   # desc 0.5 0.2 0.1 0.1 0.05 0.05
+    assert int(C.wire.top_rho_k(imp, mass)) == exp
+
+
+@pytest.mark.parametrize("codec", ["ref_int4_global", "mixed_int4_int8", "int8_token_keep"])
+def test_top_rho_message_roundtrip(codec):
+    B, S, H = 3, 64, 128
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B * S, H, generator=g)
+    imp = torch.softmax(torch.randn(B, S, generator=g) * 2, -1)
+    spec = C.get_codec(codec)
+    msg, L = C.encode(x, spec, B, S, 0.4, imp, selection="top_rho")
+    ks = C.wire.top_rho_k(imp, 0.6)
+    assert L.kvar and C.wire.message_k(msg, L).tolist() == ks.tolist()
+    y = C.decode(msg, spec, L, torch.float32)
+    lo = C.wire.select_mask(imp, ks)
+    # hi tokens exact (fp32 rows) unless the hi class is int8; lo tokens changed
+    if spec.hi_fmt == C.wire.NATIVE:
+        assert torch.equal(y.view(B, S, H)[~lo], x.view(B, S, H)[~lo])
+    # same result as the fixed-k codec applied window by window with that window's k
+    for b in range(B):
+        yb, _ = C.fake_quant(x.view(B, S, H)[b], spec, 1, S, importance=imp[b:b + 1], k=int(ks[b]))
+        if codec != "ref_int4_global":
+            assert torch.equal(yb, y.view(B, S, H)[b])
+    kt = int(ks.sum())
+    assert C.wire.message_payload(msg, L) == L.payload_bytes(kt) <= L.total

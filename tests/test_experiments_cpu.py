@@ -40,7 +40,10 @@ def test_pythia_initial(tmp_path):
                  tmp_path)
     res = json.loads((d / "exp_1.json").read_text())["exp_1"]
     assert set(res) == {"1", "aggregate upto 2", "maximum aggregation", "upto ratio"}
-    assert len({round(v["0"], 9) for v in res.values()}) == 1   # ratio 0 is method independent
+    # ratio 0 is method independent for the ratio orderings; top-rho at mass 1 may still cut the tail tokens
+    # whose mass lies beyond the rounded sum (as the reference's fp32 running total does)
+    assert len({round(v["0"], 9) for k, v in res.items() if k != "upto ratio"}) == 1
+    assert abs(res["upto ratio"]["0"] - res["1"]["0"]) < 1e-5
 
 
 def test_pythia_unknown_experiment(tmp_path):

@@ -56,9 +56,25 @@ def test_bench_contract_cpu(n):
         assert k in d, k
     assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
     dp = max(1, n // 2)
-    assert d["config"]["parallelism"] == f"pp{2 if n > 1 else 1}xdp{dp}"
+    assert d["config"]["parallelism"] == (f"pp2xdp{dp}" if n > 1 else "local-pp2")
     assert d["config"]["global_batch"] == 2 * 2 * dp
     assert d["ppl_random_weights"] and d["ppl_random_weights"] > 1
+    assert d["dtype"] == "fp32" and d["metric"].startswith("WikiText-2 PPL + inter-stage bytes/token")
+    if n > 1:   # per-stage GPU-time breakdown rows, one per rank
+        assert len(d["stages"]) == n and {s["stage"] for s in d["stages"]} == {0, 1}
+
+
+@pytest.mark.parametrize("pp", [4, 8])
+def test_bench_deep_pipeline_cpu(pp):
+    """BASELINE configs 4-5 as real pp-stage pipelines (--pp), gloo ranks on CPU."""
+    r = _torchrun(pp, BENCH[:-2] + ["--gpus", str(pp), "--pp", str(pp), "--model", "tiny-qwen2"]
+                  if pp <= 4 else ["bench.py", "--model", "byte-qwen2", "--batch", "1", "--microbatches", "2",
+                                   "--steps", "1", "--warmup", "1", "--max-length", "64", "--gpus", "8", "--pp", "8"],
+                  timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["config"]["parallelism"] == f"pp{pp}xdp1" and len(d["config"]["stage_layers"]) == pp
+    assert len(d["wire_bytes_per_token"]) == pp - 1 and len(d["stages"]) == pp
 
 
 def test_pipeline_entry_distributed_equals_local(tmp_path):

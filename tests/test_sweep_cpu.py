@@ -50,3 +50,36 @@ def test_resume(tmp_path):
     assert res["windows"] == full["windows"]
     # different config hash -> not resumed
     assert SweepState(str(tmp_path / "ck.json"), "other").load() is None
+
+
+def test_sweep_top_rho_equals_split_runner():
+    """Top-rho rows of the sweep engine == the pipeline runtime with selection='top_rho'."""
+    from llm_inference_in_distributed_edge_networks_amd.eval.sweep import SweepMethod
+    rows = [SweepMethod("rho", "regular_importance", selection="top_rho"),
+            SweepMethod("rho_last", "last_row", selection="top_rho")]
+    sc = SweepConfig(rows, [1], [0.25, 0.75], codec="mixed_int4_int8")
+    res = run_sweep(SweepEngine(M, sc), batches(TOK, WINS, 4))
+    for mi, meth in enumerate(["regular_importance", "last_row"]):
+        for ri, r in enumerate([0.25, 0.75]):
+            pipe = LocalPipeline(M, PipelinePlan.from_split_layers(4, [1]),
+                                 BoundaryConfig("mixed_int4_int8", r, meth, selection="top_rho"))
+            ppl = pipe.evaluate(batches(TOK, WINS, 4)).ppl()
+            assert abs(ppl - res["avg_ppl_results"][mi][0][ri]) / ppl < 1e-6
+            assert abs(pipe.wire_bytes_per_token()[0] - res["wire_bytes_per_token"][mi][0][ri]) < 1e-6
+
+
+def test_initial_rows_batched_equals_per_window():
+    """The batched Pythia 'initial' (one stacked suffix per batch) == each window / ordering / ratio on its own."""
+    from llm_inference_in_distributed_edge_networks_amd.eval.experiments import initial_rows
+    from llm_inference_in_distributed_edge_networks_amd.eval.sweep import SweepMethod
+    from llm_inference_in_distributed_edge_networks_amd.models import TINY_NEOX
+    mn = DecoderLM.random_init(TINY_NEOX, 1, std=0.06)
+    rows = initial_rows([3, "aggregate upto 2", "maximum aggregation", "upto ratio"])
+    sc = SweepConfig(rows, [2], [0, 3, 7, 10], codec="int8_token_keep", ratio_scale=0.1)
+    res = run_sweep(SweepEngine(mn, sc), batches(TOK, WINS, 4))
+    ref = run_sweep(SweepEngine(mn, SweepConfig(rows, [2], [0, 3, 7, 10], codec="int8_token_keep", ratio_scale=0.1,
+                                                max_fork_tokens=128)), batches(TOK, WINS, 1))
+    a, b = torch.tensor(res["mean_window_nll"]), torch.tensor(ref["mean_window_nll"])
+    assert torch.allclose(a, b, atol=2e-5), (a - b).abs().max()
+    # ratio 10 with top-rho: mass 0 -> every token quantized == the ratio-form ratio 10
+    assert abs(a[3, 0, 3] - a[0, 0, 3]) < 1e-6

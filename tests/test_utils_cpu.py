@@ -61,3 +61,43 @@ def test_graph_cache_cpu_passthrough():
     for _ in range(3):
         assert torch.equal(g(torch.ones(3)), torch.full((3,), 2.0))
     assert len(calls) == 3 and not g.graphs
+
+
+def test_checkpoint_refuses_other_sharding(tmp_path):
+    """A data-parallel checkpoint written at world=2 cannot be resumed at world=1 or 4."""
+    import pytest
+    from llm_inference_in_distributed_edge_networks_amd.utils.checkpoint import ShardMismatch, SweepState
+    p = str(tmp_path / "ck.json")
+    SweepState(p, "h", shard=(0, 2, "batch-mod/8")).save({"windows_done": 16})
+    assert SweepState(p, "h", shard=(0, 2, "batch-mod/8")).load()["windows_done"] == 16
+    for other in ((0, 1, "batch-mod/8"), (0, 4, "batch-mod/8"), (0, 2, "batch-mod/4")):
+        with pytest.raises(ShardMismatch):
+            SweepState(p, "h", shard=other).load()
+    assert SweepState(p, "other-config", shard=(0, 1, "x")).load() is None
+
+
+def test_window_weight_stride_longer_than_window():
+    """stride > max_length: the reference masks nothing (target[:, :-trg_len] with trg_len > S), weight S - 1."""
+    from llm_inference_in_distributed_edge_networks_amd.eval.windows import sliding_windows
+    ws = sliding_windows(1000, 64, 100)
+    assert ws[1].trg_len > ws[1].length and ws[1].weight == ws[1].length - 1
+    assert ws[0].weight == 63
+
+
+def test_normalize_per_layer_zero_sum():
+    import torch
+    from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import normalize_per_layer
+    r = normalize_per_layer(torch.tensor([[1.0, -1.0], [1.0, 3.0]]))
+    assert torch.isfinite(r).all() and torch.allclose(r[1], torch.tensor([0.25, 0.75]))
+
+
+def test_wikitext_fallback_is_loud(capsys):
+    import pytest
+    from llm_inference_in_distributed_edge_networks_amd.eval.data import DatasetUnavailable, token_stream
+    with pytest.warns(RuntimeWarning):
+        ids, prov = token_stream("wikitext", "no/such-model", 512, 1000)
+    assert prov.startswith("synthetic") and "WARNING" in capsys.readouterr().out
+    with pytest.raises(DatasetUnavailable):
+        token_stream("wikitext", "no/such-model", 512, 1000, strict=True)
+    with pytest.raises(ValueError):
+        token_stream("wikitxt", "x", 512)
