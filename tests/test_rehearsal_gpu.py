@@ -42,3 +42,20 @@ def test_two_ranks_one_gpu_equals_single_process():
     assert two["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
     chk = _run(2, ["--no-graphs"], {"EDGE_P2P_CHECK": "1"})
     assert chk["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
+
+
+def test_four_stage_pipeline_one_gpu_equals_local():
+    """BASELINE config 4 shape (--pp 4): 4 ranks sharing cuda:0 == the 4 stages in one process (fp32 mode)."""
+    one = _run(1, ["--pp", "4"])
+    four = _run(4, ["--pp", "4"])
+    assert four["config"]["parallelism"] == "pp4xdp1" and one["config"]["parallelism"] == "local-pp4"
+    assert four["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
+    assert len(four["stages"]) == 4 and all("compute_ms" in s for s in four["stages"])
+
+
+def test_serialized_kernel_mode_same_result():
+    """SURVEY §5.2 race check: with every kernel serialised (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1) the
+    2-rank pipeline gives bit-identical PPL to the normal asynchronous run - no result depends on stream overlap."""
+    fast = _run(2, ["--no-bf16"])
+    ser = _run(2, ["--no-bf16", "--no-graphs"], {"AMD_SERIALIZE_KERNEL": "3", "HIP_LAUNCH_BLOCKING": "1"})
+    assert ser["ppl_random_weights"] == fast["ppl_random_weights"]

@@ -55,10 +55,11 @@ def test_top_rho_equals_cpu(S, ratio):
     excl = torch.cumsum(desc, 1) - desc
     for b in range(imp.shape[0]):
         if int(ks[b]) != int(ref_k[b]):
-            # parallel fp32 scan vs fp64 sequential: only a cut sitting on the threshold may move by one
-            keep = S - int(ref_k[b])
-            near = (excl[b] - (1.0 - ratio)).abs().min()
-            assert abs(int(ks[b]) - int(ref_k[b])) == 1 and near < 1e-5, (b, int(ks[b]), int(ref_k[b]))
+            # parallel fp32 scan vs fp64 sequential sums: the cut may only move inside the run of positions whose
+            # exclusive mass is within fp32 rounding of the threshold (a tail of ~1e-8 probabilities at mass 1)
+            lo_keep, hi_keep = sorted((S - int(ks[b]), S - int(ref_k[b])))
+            gap = (excl[b, lo_keep:hi_keep + 1] - (1.0 - ratio)).abs().max()
+            assert gap < 1e-5, (b, int(ks[b]), int(ref_k[b]), float(gap))
             continue
         assert torch.equal(m[b], C.wire.select_mask(imp[b:b + 1], [int(ks[b])])[0])
 
