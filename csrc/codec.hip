@@ -17,7 +17,11 @@
 // its un-selected tokens in fp32, Experiments/Qwen2-0.5B/qwen_layer_wise.py:54-70).
 #include "common.h"
 
-enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3, FMT_F32 = 4 };
+enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3, FMT_F32 = 4, FMT_MXFP4 = 5, FMT_MXFP8 = 6 };
+// OCP microscaling rows (FMT_MXFP4: E2M1 codes, FMT_MXFP8: E4M3 codes): blocks of 32 consecutive channels share one
+// E8M0 scale 2^(floor(log2 max|x|) - emax) (emax 2 / 8), stored after the row's codes: [codes][H/32 scale bytes].
+// Quantize / dequantize with gfx950's scaled converts (v_cvt_scalef32_pk_fp4_f32 / _fp8_f32 and the inverses:
+// round-to-nearest-even of x / scale, saturating).
 enum { SC_TOKEN = 0, SC_WINDOW = 1, SC_CHANNEL = 2, SC_NONE = 3 };
 enum { CH_MAXABS = 0, CH_MEAN = 1 };
 
@@ -30,7 +34,8 @@ struct CodecArgs {
 };
 
 __device__ __forceinline__ int fmt_row_bytes(int fmt, int H) {
-  return fmt == FMT_F32 ? 4 * H : fmt == FMT_BF16 ? 2 * H : fmt == FMT_INT8 ? H : fmt == FMT_INT4 ? H / 2 : H / 4;
+  return fmt == FMT_F32 ? 4 * H : fmt == FMT_BF16 ? 2 * H : fmt == FMT_INT8 ? H : fmt == FMT_INT4 ? H / 2 :
+         fmt == FMT_MXFP4 ? H / 2 + H / 32 : fmt == FMT_MXFP8 ? H + H / 32 : H / 4;
 }
 
 __device__ __forceinline__ int wave_isum(int v) {
@@ -220,6 +225,63 @@ __device__ __forceinline__ void load_row8(const bf16_t* __restrict__ src, int H,
 
 __device__ __forceinline__ float qround(float t, float qmax, float qmin) { return fminf(fmaxf(rintf(t), qmin), qmax); }
 
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+
+// E8M0 scale byte and value of a 32-channel block (4 lanes x 8 values): 2^(floor(log2 amax) - emax)
+__device__ __forceinline__ int mx_scale_byte(float am, int emax) {
+  const int e = am > 0.f ? (int)((__float_as_uint(am) >> 23) & 0xff) - 127 : -127;   // denormal amax -> -127
+  const int sb = e - emax + 127;
+  return sb < 0 ? 0 : (sb > 254 ? 254 : sb);
+}
+__device__ __forceinline__ float e8m0_value(int sb) { return sb ? __uint_as_float((uint32_t)sb << 23) : __uint_as_float(0x00400000u); }
+
+__device__ __forceinline__ void mx_pack8(uint8_t* __restrict__ row, int H, int col, int fmt, const float (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+  float am = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[e]));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  const int sb = mx_scale_byte(am, fmt == FMT_MXFP4 ? 2 : 8);
+  const float X = e8m0_value(sb);
+  if (fmt == FMT_MXFP4) {
+    uint32_t w = 0;
+    w = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(w, v[0], v[1], X, 0);
+    w = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(w, v[2], v[3], X, 1);
+    w = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(w, v[4], v[5], X, 2);
+    w = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(w, v[6], v[7], X, 3);
+    *(uint32_t*)(row + col / 2) = w;
+    if ((lane & 3) == 0) row[H / 2 + col / 32] = (uint8_t)sb;
+  } else {
+    s16x2_t a = {0, 0}, b = {0, 0};
+    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(a, v[0], v[1], X, false);
+    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(a, v[2], v[3], X, true);
+    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(b, v[4], v[5], X, false);
+    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(b, v[6], v[7], X, true);
+    u32x2_t w;
+    w[0] = (uint32_t)(uint16_t)a[0] | ((uint32_t)(uint16_t)a[1] << 16);
+    w[1] = (uint32_t)(uint16_t)b[0] | ((uint32_t)(uint16_t)b[1] << 16);
+    *(u32x2_t*)(row + col) = w;
+    if ((lane & 3) == 0) row[H + col / 32] = (uint8_t)sb;
+  }
+}
+
+__device__ __forceinline__ void mx_unpack8(const uint8_t* __restrict__ row, int H, int col, int fmt, float (&o)[8]) {
+  if (fmt == FMT_MXFP4) {
+    const float X = e8m0_value(row[H / 2 + col / 32]);
+    const uint32_t w = *(const uint32_t*)(row + col / 2);
+    f32x2_t p0 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(w, X, 0), p1 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(w, X, 1);
+    f32x2_t p2 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(w, X, 2), p3 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp4(w, X, 3);
+    o[0] = p0[0]; o[1] = p0[1]; o[2] = p1[0]; o[3] = p1[1]; o[4] = p2[0]; o[5] = p2[1]; o[6] = p3[0]; o[7] = p3[1];
+  } else {
+    const float X = e8m0_value(row[H + col / 32]);
+    const u32x2_t w = *(const u32x2_t*)(row + col);
+    f32x2_t p0 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[0], X, false), p1 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[0], X, true);
+    f32x2_t p2 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[1], X, false), p3 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(w[1], X, true);
+    o[0] = p0[0]; o[1] = p0[1]; o[2] = p1[0]; o[3] = p1[1]; o[4] = p2[0]; o[5] = p2[1]; o[6] = p3[0]; o[7] = p3[1];
+  }
+}
+
 template <int NCH, class T>
 __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -249,7 +311,7 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
 
   // scale / quantiser for this row
   float inv = 0.f, mul = 0.f;  // code = round(x * inv) for token & channel; window mode uses ref formula
-  const bool raw = fmt == FMT_BF16 || fmt == FMT_F32;
+  const bool raw = fmt == FMT_BF16 || fmt == FMT_F32 || fmt == FMT_MXFP4 || fmt == FMT_MXFP8;
   if (raw && a.scale_mode == SC_TOKEN && lane == 0) scales[row] = 0.f;
   if (!raw) {
     if (a.scale_mode == SC_TOKEN) {
@@ -276,6 +338,10 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
     if (fmt == FMT_F32) {
       *(f32x4_t*)(dst + col * 4) = f32x4_t{v[c][0], v[c][1], v[c][2], v[c][3]};
       *(f32x4_t*)(dst + col * 4 + 16) = f32x4_t{v[c][4], v[c][5], v[c][6], v[c][7]};
+      continue;
+    }
+    if (fmt == FMT_MXFP4 || fmt == FMT_MXFP8) {
+      mx_pack8(dst, a.H, col, fmt, v[c]);
       continue;
     }
     if (fmt == FMT_BF16) {
@@ -359,7 +425,7 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
   }
   const float* scales = (const float*)(a.msg + a.off_scale);
   float s = 0.f;
-  if (fmt != FMT_BF16 && fmt != FMT_F32) {
+  if (fmt != FMT_BF16 && fmt != FMT_F32 && fmt != FMT_MXFP4 && fmt != FMT_MXFP8) {
     if (a.scale_mode == SC_TOKEN) s = scales[row];
     else if (a.scale_mode == SC_WINDOW) s = scales[b];
   }
@@ -379,6 +445,12 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) { o[2 * e] = bf_lo(w[e]); o[2 * e + 1] = bf_hi(w[e]); }
       }
+      store8(out + col, o);
+      continue;
+    }
+    if (fmt == FMT_MXFP4 || fmt == FMT_MXFP8) {
+      float o[8];
+      mx_unpack8(src, a.H, col, fmt, o);
       store8(out + col, o);
       continue;
     }

@@ -1134,6 +1134,228 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
   if (wm == 0) __builtin_amdgcn_s_barrier();  // group 0 matches group 1's extra barrier
 }
 
+// ---- 256x256 eight-phase GEMM (variant 10, "256e"): full-line K-tiles, half-tile DMA stream, wave ping-pong ----
+// K-tiles of BK = 64 (128-byte LDS rows: every DMA row is one whole L2 line, where the K-half ring above moves
+// 64-byte half lines and so issues twice the L2 requests per MFMA), double-buffered: 2 x 64 KiB.  A K-tile buffer
+// holds four 16 KiB half-tiles:
+//   A-half h = the quadrant-row band h of both wave rows   (tile rows wm*128 + h*64 + 0..63, local row wm*64 + r)
+//   B-half h = the quadrant-column band h of all wave cols (tile cols wn*64 + h*32 + 0..31, local row wn*32 + c)
+// A wave (wm, wn) owns a 128x64 output = 4 quadrants of 64x32.  Sub-phase s of a K-tile computes quadrant
+// s=0 (0,0)  s=1 (0,1)  s=2 (1,1)  s=3 (1,0) over the K-tile (16 MFMAs).  Fragments stay in registers across sub-
+// phases, so the LDS reads are: s=0 A-band 0 + B-band 0, s=1 B-band 1, s=2 A-band 1, s=3 none.
+// Phase = R-section (this phase's ds_reads, then ONE half-tile DMA: 2 glds per thread) | barrier | M-section
+// (lgkmcnt(0), 16 MFMAs at raised priority, counted vmcnt) | barrier.  Waves 4-7 run one barrier behind waves 0-3,
+// so on every SIMD one wave's MFMAs overlap the other's reads and DMA issue.
+// DMA stream: items u = 0, 1, ... = half-tiles in the order A0 B0 B1 A1 of K-tile u/4 (the walk of this workgroup's
+// tiles, the next tile's operands streaming under the current tile's last K-tiles); the prologue issues items 0-5,
+// phase p issues item p + 6, and the end of phase p retires item p + 3 (vmcnt(6): three half-tiles stay in flight).
+//   RAW: item u is retired at the end of phase u - 3 and first read in phase >= u - 1, i.e. behind two barriers
+//        (one for each wave group; MI355X_MICROARCH.md §Two waves per SIMD: a DMA is ordered for a reader only by the
+//        issuer's vmcnt plus a barrier the reader passed after it).
+//   WAR: item u overwrites the half-tile of K-tile u/4 - 2 whose last read was >= 2 phases before phase u - 6, the
+//        partner group's reads of it retired by its lgkmcnt(0) and a barrier.
+namespace e8 {
+constexpr int BUF = 65536, HA0 = 0, HA1 = 16384, HB0 = 32768, HB1 = 49152;
+}
+
+template <int EPI, int RH>
+__global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs a) {
+  using CF = C256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tm = (a.M + 255) / 256, tn = (a.N + 255) / 256, ntiles = tm * tn;
+  const TileWalk walk = tile_walk(blockIdx.x, gridDim.x, ntiles, a.walk);
+  const int tile0 = walk.first, G = walk.stride;
+  if (tile0 >= walk.end) return;
+  const int nk = a.K / 64;
+  const int total = 4 * ((walk.end - 1 - tile0) / G + 1) * nk;   // DMA items of this workgroup
+
+  // ---- DMA side: per half h and glds i, this lane's 32-bit byte offset inside the staging tile (fixed per tile)
+  const char* sa = nullptr;
+  const char* sb = nullptr;
+  uint32_t oA[2][2], oB[2][2];
+  auto set_stage_tile = [&](int t) {
+    int m0, n0;
+    tile_origin(t, a.M, a.N, 256, 256, m0, n0);
+    sa = (const char*)(a.A + (size_t)m0 * a.lda);
+    sb = (const char*)(a.B + (size_t)n0 * a.ldb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int lr = (i * 8 + wave) * 8 + (lane >> 3);          // local row of the half-tile (0..127)
+      const int ch = (lane & 7) ^ swz(lr);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ra = min((lr >> 6) * 128 + h * 64 + (lr & 63), a.M - 1 - m0);
+        const int rb = min((lr >> 5) * 64 + h * 32 + (lr & 31), a.N - 1 - n0);
+        oA[h][i] = (uint32_t)(ra * a.lda + ch * 8) * 2u;
+        oB[h][i] = (uint32_t)(rb * a.ldb + ch * 8) * 2u;
+      }
+    }
+  };
+  int st_u = 0, st_kt = 0, st_tile = tile0;
+  set_stage_tile(tile0);
+  auto issue = [&]() {
+    if (st_u >= total) return;
+    const int hk = st_u & 3;                 // 0 A0, 1 B0, 2 B1, 3 A1
+    char* buf = smem + ((st_u >> 2) & 1) * e8::BUF;
+    const int kb = st_kt * 128;
+    if (hk == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(sa + kb + oA[0][i], buf + e8::HA0 + (i * 8 + wave) * 1024);
+    } else if (hk == 1) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(sb + kb + oB[0][i], buf + e8::HB0 + (i * 8 + wave) * 1024);
+    } else if (hk == 2) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(sb + kb + oB[1][i], buf + e8::HB1 + (i * 8 + wave) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds16(sa + kb + oA[1][i], buf + e8::HA1 + (i * 8 + wave) * 1024);
+    }
+    ++st_u;
+    if (hk == 3 && ++st_kt == nk && st_u < total) {
+      st_kt = 0;
+      st_tile += G;
+      set_stage_tile(st_tile);
+    }
+  };
+
+  // ---- compute side
+  const int sw = ((lane & 15) >> 1) & 7;
+  uint32_t aoff[2], boff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = ks * 4 + (lane >> 4);
+    aoff[ks] = lds_addr(smem) + (wm * 64 + (lane & 15)) * 128 + ((c ^ sw) << 4);
+    boff[ks] = lds_addr(smem) + (wn * 32 + (lane & 15)) * 128 + ((c ^ sw) << 4);
+  }
+  bf16x8_t FA[2][4], FB[2][2][2];   // FA[ks][i] (current A band), FB[band][ks][j]
+  auto read_a = [&](uint32_t bo, int band) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint32_t va = aoff[ks] + bo + (band ? e8::HA1 : e8::HA0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) DS_READ_B128(FA[ks][i], va, i * 2048);
+    }
+  };
+  auto read_b = [&](uint32_t bo, int band) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint32_t vb = boff[ks] + bo + (band ? e8::HB1 : e8::HB0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) DS_READ_B128(FB[band][ks][j], vb, j * 2048);
+    }
+  };
+  f32x4_t acc[8][4];
+  zero_acc<8>(acc);
+  auto mma = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm * 4 + i][qn * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[qn][ks][j], FA[ks][i], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto wait_end = [&](int p) {  // retire item p + 3 (those after it that exist stay in flight)
+    const int after = min(total, p + 7) - (p + 4);
+    if (after >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (after == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  // prologue: items 0..5 issued, items 0..2 retired and visible
+#pragma unroll 1
+  for (int i = 0; i < 6; ++i) issue();
+  wait_end(-1);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+
+  int tile = tile0, kt = 0, m0, n0;
+  tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
+  // Row scales (fused RMSNorm) of the current tile, loaded one tile ahead into registers that nothing touches until
+  // the epilogue: a load whose destination is read or rewritten inside the K loop makes the compiler drain vmcnt
+  // (and with it the DMA pipeline) at the loop head.
+  float rs[8];
+  auto load_rs = [&](int mt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = min(mt + wm * 128 + i * 16 + (lane & 15), a.M - 1);
+      rs[i] = a.rscale ? a.rscale[m] : 1.f;
+    }
+  };
+  load_rs(m0);
+  const int nphase = total;   // 4 phases per K-tile = one DMA item per phase
+#pragma unroll 1
+  for (int p = 0; p < nphase; p += 4) {
+    const uint32_t bo = ((p >> 2) & 1) * e8::BUF;
+    // s = 0: A-band 0, B-band 0 -> quadrant (0, 0)
+    read_a(bo, 0);
+    read_b(bo, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    issue();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_end(p);
+    __builtin_amdgcn_s_barrier();
+    // s = 1: B-band 1 -> quadrant (0, 1)
+    read_b(bo, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    issue();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_end(p + 1);
+    __builtin_amdgcn_s_barrier();
+    // s = 2: A-band 1 -> quadrant (1, 1)
+    read_a(bo, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    issue();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_end(p + 2);
+    __builtin_amdgcn_s_barrier();
+    // s = 3: no reads -> quadrant (1, 0)
+    issue();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_end(p + 3);
+    __builtin_amdgcn_s_barrier();
+    if (++kt == nk) {  // tile done: epilogue in this wave's next R window
+      if (n0 + wn * 64 < a.N) gemm_epilogue<EPI, RH, CF>(a, acc, m0, n0, lane, wm, wn, rs);
+      zero_acc<8>(acc);
+      kt = 0;
+      tile += G;
+      if (tile < walk.end) {
+        tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
+        load_rs(m0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // group 0 matches group 1's extra barrier
+}
+
 // ---- 256x224 persistent GEMM for N = 896 (Qwen2 hidden size: O-proj and MLP down, both residual epilogues) ----
 // 896 = 3.5 x 256: the 256x256 tile computes a half-empty last column tile (1/8 of all MFMAs wasted, its
 // waves' SIMDs idle), and no power-of-two tile both avoids that and gives a tile count that divides the 256
@@ -1489,6 +1711,20 @@ static int launch_pp(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+template <int EPI, int RH>
+static int launch_8p(const GemmArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const int grid = std::min(tiles, num_cus());
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_8p_kernel<EPI, RH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * e8::BUF);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_8p_kernel<EPI, RH>), dim3(grid), dim3(512), 2 * e8::BUF, st, a);
+  return (int)hipGetLastError();
+}
+
 static int g_w7 = 1;  // 256x224 tiles for N % 224 == 0 shapes that 256 does not divide (N = 896)
 
 // The 256x224 kernel takes the plain / bias / residual epilogues of N % 224 == 0 shapes that 256 does not
@@ -1555,10 +1791,12 @@ static int launch(const GemmArgs& args, hipStream_t st) {
     const bool use256 = g_tile_override ? g_tile_override == 256 && fits : big;
     if (!use256) return launch_cfg<EPI, RH, C128>(a, st);
     const int variant = g_c256_variant >= 0 ? g_c256_variant : (a.K >= 2048 ? 4 : 1);
-    if constexpr (epi_f32(EPI)) {  // fp32 execution: K is always >= 6 x 64; the two production main loops only
+    if constexpr (epi_f32(EPI)) {  // fp32 execution: K is always >= 6 x 64; the production main loops only
+      if (variant == 10) return launch_8p<EPI, RH>(a, st);
       return variant == 4 ? launch_pp<EPI, RH>(a, st) : launch_cfg<EPI, RH, C256, true>(a, st);
     } else {
       switch (variant) {
+        case 10: return launch_8p<EPI, RH>(a, st);
         case 0: return launch_cfg<EPI, RH, C256, false>(a, st);
         case 2: return launch_ring<EPI, RH, false>(a, st);
         case 3: return launch_ring<EPI, RH, true>(a, st);

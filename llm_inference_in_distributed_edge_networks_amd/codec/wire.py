@@ -35,7 +35,8 @@ from ..ops._native import call, ptr, stream
 
 MAGIC = 0x45444742
 VERSION = 1
-FMT_BF16, FMT_INT8, FMT_INT4, FMT_INT2, FMT_F32 = 0, 1, 2, 3, 4
+FMT_BF16, FMT_INT8, FMT_INT4, FMT_INT2, FMT_F32, FMT_MXFP4, FMT_MXFP8 = 0, 1, 2, 3, 4, 5, 6
+MX_FORMATS = (FMT_MXFP4, FMT_MXFP8)
 SC_TOKEN, SC_WINDOW, SC_CHANNEL, SC_NONE = 0, 1, 2, 3
 CH_MAXABS, CH_MEAN = 0, 1
 NATIVE = -1  # "keep in the activation dtype" (bf16 on GPU, fp32 in the CPU reference mode)
@@ -67,6 +68,11 @@ CODECS = {c.name: c for c in [
     CodecSpec("channel_1_mean", 8, FMT_INT2, FMT_INT2, SC_CHANNEL, 1, 1, CH_MEAN, False, False),
     CodecSpec("channel_1_max", 9, FMT_INT2, FMT_INT2, SC_CHANNEL, 1, 1, CH_MAXABS, False, False),
     CodecSpec("int8_token_keep", 10, NATIVE, FMT_INT8, SC_TOKEN, 0, 127),
+    # OCP microscaling (32-channel blocks, E8M0 scales inline in the row; gfx950 scaled converts)
+    CodecSpec("mxfp4", 11, FMT_MXFP4, FMT_MXFP4, SC_NONE, uses_ratio=False, needs_importance=False),
+    CodecSpec("mxfp8", 12, FMT_MXFP8, FMT_MXFP8, SC_NONE, uses_ratio=False, needs_importance=False),
+    CodecSpec("mixed_mxfp4_mxfp8", 13, FMT_MXFP8, FMT_MXFP4, SC_NONE),
+    CodecSpec("mxfp4_keep", 14, NATIVE, FMT_MXFP4, SC_NONE),
 ]}
 
 
@@ -81,7 +87,8 @@ def _a16(n: int) -> int:
 
 
 def _row_bytes(fmt: int, H: int) -> int:
-    return {FMT_BF16: 2 * H, FMT_INT8: H, FMT_INT4: H // 2, FMT_INT2: H // 4, FMT_F32: 4 * H}[fmt]
+    return {FMT_BF16: 2 * H, FMT_INT8: H, FMT_INT4: H // 2, FMT_INT2: H // 4, FMT_F32: 4 * H,
+            FMT_MXFP4: H // 2 + H // 32, FMT_MXFP8: H + H // 32}[fmt]
 
 
 @dataclass(frozen=True)
@@ -271,6 +278,59 @@ def _dequant(q: torch.Tensor, spec: CodecSpec, is_lo: bool, scale_row, ch_scale)
     return q * ch_scale / float(qmax)
 
 
+# ---- OCP microscaling rows (csrc/codec.hip mx_pack8 / mx_unpack8) ----------------------------------------------
+_FP4_GRID = torch.tensor([0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0])
+
+
+def _fp4_codes(v: torch.Tensor) -> torch.Tensor:
+    """E2M1 codes of v (round to nearest, ties to even code, saturating at 6), sign in bit 3."""
+    a = v.abs()
+    # thresholds between grid points; a tie goes to the even code (0, 2, 4, 6)
+    c = torch.zeros_like(a, dtype=torch.int64)
+    for lo, hi_excl, code in ((0.25, True, 1), (0.75, False, 2), (1.25, True, 3), (1.75, False, 4), (2.5, True, 5),
+                              (3.5, False, 6), (5.0, True, 7)):
+        c = torch.where(a > lo if hi_excl else a >= lo, torch.full_like(c, code), c)
+    return c | ((v < 0) & (c > 0)).to(torch.int64) << 3
+
+
+def _mx_exp(am: torch.Tensor, emax: int) -> torch.Tensor:
+    """E8M0 scale byte: clamp(floor(log2 amax) - emax + 127, 0, 254); amax 0 / denormal -> exponent -127."""
+    bits = am.float().contiguous().view(torch.int32).to(torch.int64)
+    e = ((bits >> 23) & 0xFF) - 127
+    e = torch.where(am > 0, e, torch.full_like(e, -127))
+    return (e - emax + 127).clamp(0, 254)
+
+
+def _e8m0(sb: torch.Tensor) -> torch.Tensor:
+    v = (sb.to(torch.int64) << 23).to(torch.int32).view(torch.float32)
+    return torch.where(sb == 0, torch.full_like(v, 2.0 ** -127), v)
+
+
+def _mx_pack(rows: torch.Tensor, fmt: int) -> torch.Tensor:
+    n, H = rows.shape
+    blk = rows.float().reshape(n, H // 32, 32)
+    sb = _mx_exp(blk.abs().amax(-1), 2 if fmt == FMT_MXFP4 else 8)           # [n, H/32]
+    y = blk / _e8m0(sb)[..., None]
+    if fmt == FMT_MXFP4:
+        c = _fp4_codes(y).reshape(n, H // 2, 2)
+        codes = (c[..., 0] | (c[..., 1] << 4)).to(torch.uint8)
+    else:
+        codes = y.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8).reshape(n, H)
+    return torch.cat([codes.reshape(n, -1), sb.to(torch.uint8)], 1).reshape(-1)
+
+
+def _mx_unpack(b: torch.Tensor, fmt: int, n: int, H: int) -> torch.Tensor:
+    r = b.reshape(n, _row_bytes(fmt, H))
+    nc = H // 2 if fmt == FMT_MXFP4 else H
+    codes, sb = r[:, :nc], r[:, nc:].to(torch.int64)
+    if fmt == FMT_MXFP4:
+        c = torch.stack([codes & 15, codes >> 4], -1).reshape(n, H).to(torch.int64)
+        v = _FP4_GRID[c & 7] * torch.where(c >= 8, -1.0, 1.0)
+    else:
+        v = codes.contiguous().view(torch.float8_e4m3fn).float()
+    return (v.reshape(n, H // 32, 32) * _e8m0(sb)[..., None]).reshape(n, H)
+
+
 def _header(spec: CodecSpec, L: Layout) -> torch.Tensor:
     return torch.tensor([MAGIC, VERSION, spec.cid, L.B, L.S, L.H, -1 if L.kvar else L.k, L.hi_fmt], dtype=torch.int32)
 
@@ -292,7 +352,7 @@ def _encode_cpu(x, spec, L, lo_mask):
     if spec.scale_mode == SC_TOKEN:
         scales = torch.zeros(B, S)
         for is_lo, fmt, qmax in ((False, L.hi_fmt, spec.qmax_hi), (True, L.lo_fmt, spec.qmax_lo)):
-            if fmt in (FMT_BF16, FMT_F32):
+            if fmt in (FMT_BF16, FMT_F32) or fmt in MX_FORMATS:
                 continue
             sel = lo_mask if is_lo else ~lo_mask
             am = xf.abs().amax(-1)
@@ -317,6 +377,8 @@ def _encode_cpu(x, spec, L, lo_mask):
             data = rows.contiguous().view(torch.uint8).reshape(-1)
         elif fmt == FMT_BF16:
             data = rows.to(torch.bfloat16).contiguous().view(torch.uint8).reshape(-1)
+        elif fmt in MX_FORMATS:
+            data = _mx_pack(rows, fmt)
         else:
             if spec.scale_mode == SC_TOKEN:
                 srow = scales[sel]
@@ -359,6 +421,8 @@ def _decode_cpu(msg, spec, L, dtype):
             rows = raw.view(torch.float32).reshape(n, H)
         elif fmt == FMT_BF16:
             rows = raw.view(torch.bfloat16).reshape(n, H).float()
+        elif fmt in MX_FORMATS:
+            rows = _mx_unpack(raw, fmt, n, H)
         else:
             q = _unpack_rows(raw, fmt, n, H)
             if spec.scale_mode == SC_TOKEN:

@@ -145,13 +145,13 @@ def set_gemm_tile(tile: int) -> None:
 
 
 # s-a*: timing ablations with wrong results, only in a tuning build of the library (-DEDGE_TUNING_BUILD=1)
-GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8, "s-a4": 9}
+GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8, "s-a4": 9, "e": 10}
 
 
 def set_gemm_variant(v: int) -> None:
     """256x256 GEMM main loop (A/B and tests): 0 K-tile double buffer with compiler-waited fragment loads,
     1 the same with hand-counted asm reads, 2 the K-half ring, 3 the ring with s_setprio, 4 the ring with
-    wave-group ping-pong."""
+    wave-group ping-pong, 8 the ping-pong ring with 5 slots, 10 the eight-phase full-line K-tile kernel."""
     call("edge_gemm_set_variant", int(v))
 
 

@@ -182,3 +182,33 @@ def test_top_rho_message_roundtrip(codec):
             assert torch.equal(yb, y.view(B, S, H)[b])
     kt = int(ks.sum())
     assert C.wire.message_payload(msg, L) == L.payload_bytes(kt) <= L.total
+
+
+def test_mx_formats_oracle():
+    """OCP MX rows: E8M0 block scale 2^(floor(log2 amax) - emax); E2M1 / E4M3 round-to-nearest-even, saturating."""
+    x = torch.tensor([[0.0, 0.25, 0.5, 0.75, 1.0, 1.25, 1.5, 2.5, 3.0, 5.0, 6.0, 7.0, -1.0, -3.5, 100.0, 0.3] * 2])
+    y4, nb4 = C.fake_quant(x, C.get_codec("mxfp4"), 1, 1)
+    # amax 100 -> scale 2^(6 - 2) = 16: 100/16 = 6.25 -> 6 (96); 7/16 -> 0.5 (8); 5/16 = 0.3125 -> 0.5 (8)
+    assert y4[0, :16].tolist() == [0, 0, 0, 0, 0, 0, 0, 0, 0, 8, 8, 8, 0, 0, 96, 0]
+    y8, nb8 = C.fake_quant(x, C.get_codec("mxfp8"), 1, 1)
+    assert y8[0, 14] == 96 and y8[0, 15] == 0.3125 and torch.equal(y8[0, :14], x[0, :14])
+    assert nb4 > 32 // 2 and nb8 > 32
+
+
+@pytest.mark.parametrize("codec", ["mxfp4", "mxfp8", "mixed_mxfp4_mxfp8", "mxfp4_keep"])
+def test_mx_codecs_error_and_bytes(codec):
+    g = torch.Generator().manual_seed(0)
+    B, S, H = 2, 64, 256
+    x = torch.randn(B * S, H, generator=g)
+    x[:, 7] *= 50          # an outlier channel: block scales confine it to its 32-channel block
+    imp = torch.rand(B, S, generator=g)
+    spec = C.get_codec(codec)
+    y, nb = C.fake_quant(x, spec, B, S, 0.5, imp)
+    err = ((y - x) ** 2).mean() / (x ** 2).mean()
+    assert err < (0.03 if "fp4" in codec else 0.002)
+    bits = 8 * nb / (B * S * H)
+    assert bits < {"mxfp4": 4.6, "mxfp8": 8.6, "mixed_mxfp4_mxfp8": 6.6, "mxfp4_keep": 18.5}[codec]
+    # block scaling beats one per-token scale under the outlier channel at equal nominal width
+    if codec == "mxfp4":
+        yt, _ = C.fake_quant(x, C.get_codec("int4_token"), B, S, 1.0, imp)
+        assert err < ((yt - x) ** 2).mean() / (x ** 2).mean()

@@ -236,3 +236,34 @@ def test_full_model_nll_matches_cpu_fp32(name, B, S):
     cpu, gpu = _full_model_nll(get_config(name), B, S)
     rel = ((gpu - cpu).abs() / cpu.abs()).max().item()
     assert rel < 1e-4, (rel, cpu.tolist(), gpu.tolist())
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(32768, 9728, 896, "swiglu"), (4096, 2048, 512, "gelu"),
+                                       (1000, 1024, 896, "resid"), (700, 2048, 512, "bias")])
+def test_linear_x6_eight_phase(M, N, K, epi):
+    """The X6 (fp32-mode) GEMMs on the eight-phase main loop (variant 10)."""
+    ops.set_gemm_config("256e")
+    try:
+        test_linear_x6_fp32_accuracy(M, N, K, {"resid": "resid", "gelu": "gelu", "swiglu": "swiglu",
+                                                "bias": "bias"}[epi])
+    finally:
+        ops.set_gemm_config("0")
+
+
+@pytest.mark.parametrize("codec", ["mxfp4", "mxfp8", "mixed_mxfp4_mxfp8", "mxfp4_keep"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mx_codecs_gpu_equal_cpu(codec, dtype):
+    """gfx950 scaled converts (v_cvt_scalef32_pk_*) decode to exactly the CPU oracle's values."""
+    B, S, H = 3, 256, 896
+    x = (rnd(B * S, H, seed=80) * 3).to(dtype)
+    x[:, 5] *= 40
+    imp = torch.rand(B, S, generator=torch.Generator().manual_seed(81))
+    spec = C.get_codec(codec)
+    m_cpu, L = C.encode(x.float(), spec, B, S, 0.5, imp)
+    m_gpu, L2 = C.encode(x.to(DEV), spec, B, S, 0.5, imp.to(DEV))
+    y_cpu = C.decode(m_cpu, spec, L, torch.float32)
+    y_gpu = C.decode(m_gpu, spec, L2, dtype).float().cpu()
+    if dtype == torch.float32:
+        assert torch.equal(y_gpu, y_cpu)
+    else:   # bf16 activations: the hi class is bf16 on the GPU, the MX values are exact in bf16 or rounded once
+        assert (y_gpu - y_cpu).abs().max() <= 0.01 * y_cpu.abs().max()

@@ -23,6 +23,11 @@ SHAPES = {  # name: (M, N, K, act, bias, resid)
     "gate_up_b64": (32768, 9728, 896, "swiglu_il", False, False),
     "big": (8192, 8192, 8192, None, False, False),
     "qkv_rope_b64": (32768, 1152, 896, "qkv_rope", True, False),   # fused QKV + bias + RoPE + scatter epilogue
+    # fp32 execution mode (X6 split-bf16 operands, K' = 6K): TF/s below count the bf16 MFMA work (6x the fp32 FLOPs)
+    "x6_gate_up_b64": (32768, 9728, 6 * 896, "x6_swiglu", False, False),
+    "x6_down_b64": (32768, 896, 6 * 4864, "x6", False, True),
+    "x6_o_proj_b64": (32768, 896, 6 * 896, "x6", False, True),
+    "x6_big": (8192, 8192, 6 * 1024, "x6", False, False),
 }
 
 
@@ -55,10 +60,11 @@ def main():
         M = a.m or M if name != "lm_head" else M
         x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
         w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
-        b = torch.randn(N, device=dev).to(torch.bfloat16) if bias else None
-        No = N // 2 if act == "swiglu_il" else N
-        r = torch.randn(M, No, device=dev).to(torch.bfloat16) if resid else None
-        out = torch.empty(M, No, device=dev, dtype=torch.bfloat16)
+        x6 = act is not None and act.startswith("x6")
+        b = torch.randn(N, device=dev).to(torch.float32 if x6 else torch.bfloat16) if bias else None
+        No = N // 2 if act in ("swiglu_il", "x6_swiglu") else N
+        r = torch.randn(M, No, device=dev).to(torch.float32 if x6 else torch.bfloat16) if resid else None
+        out = torch.empty(M, No, device=dev, dtype=torch.float32 if x6 else torch.bfloat16)
         tiles = a.tiles.split(",")
 
         def mk(spec):  # spec may end in "/w0" = strided persistent tile walk instead of XCD chunks, or "/noepi" =
@@ -76,6 +82,10 @@ def main():
                 ops._native.lib().edge_gemm_set_w7_mode(mode)
                 if act == "qkv_rope":
                     ops.qkv_rope(x, w, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
+                elif act == "x6_swiglu":
+                    ops.linear_x6(x, w, act="swiglu_il")
+                elif act == "x6":
+                    ops.linear_x6(x, w, bias=b, residual=r, out=out)
                 else:
                     ops.linear(x, w, bias=b, residual=r, act=act, out=out)
                 ops._native.lib().edge_gemm_set_skip_epi(0)

@@ -37,11 +37,16 @@ def main():
     ap.add_argument("--codecs", default="ref_int4_global,int4_token,mixed_int4_int8,mixed_int2_int8")
     ap.add_argument("--relevance-windows", type=int, default=256)
     ap.add_argument("--json-out", default="gpurun_out/quality_sweep.json")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="execution mode of the sweep (fp32 = the reference's precision)")
     a = ap.parse_args()
     dev = "cuda" if torch.cuda.is_available() else "cpu"
-    dtype = torch.bfloat16 if dev == "cuda" else torch.float32
+    dtype = torch.bfloat16 if (dev == "cuda" and a.dtype == "bf16") else torch.float32
     cfg = get_config(a.model)
     m = DecoderLM.load_native(cfg, a.weights, dev, dtype)
+    # the explicit LRP engine runs the bf16 kernels on the GPU: calibrate head weights on a bf16 copy
+    m_rel = m if (dev == "cpu" or dtype == torch.bfloat16) else DecoderLM.load_native(cfg, a.weights, dev,
+                                                                                      torch.bfloat16)
     layers = [int(x) for x in a.layers.split(",")]
     ratios = [float(x) for x in a.ratios.split(",")]
 
@@ -49,7 +54,7 @@ def main():
     t0 = time.time()
     tr = local_text_bytes("train")
     wins = sliding_windows(tr.shape[1], 512, 512)[: a.relevance_windows]
-    eng = RelevanceEngine(m)
+    eng = RelevanceEngine(m_rel)
     acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=dev)
     for b in batches(tr, wins, a.batch):
         rel, _, _ = eng.head_relevance(b.ids)
@@ -59,7 +64,7 @@ def main():
 
     ev = local_text_bytes("eval")
     wins = sliding_windows(ev.shape[1], 512, 32)[: a.windows]
-    out = {"model": cfg.name, "weights": a.weights, "data": f"python-stdlib-bytes/eval, {len(wins)} windows "
+    out = {"model": cfg.name, "weights": a.weights, "dtype": a.dtype if dev == "cuda" else "fp32", "data": f"python-stdlib-bytes/eval, {len(wins)} windows "
            "(max_length 512, stride 32)", "methods": METHODS, "layers": layers, "ratios": ratios,
            "head_weights": hw.tolist(), "codecs": {}}
     for codec in a.codecs.split(","):
