@@ -253,11 +253,16 @@ __device__ __forceinline__ void mx_pack8(uint8_t* __restrict__ row, int H, int c
     *(uint32_t*)(row + col / 2) = w;
     if ((lane & 3) == 0) row[H / 2 + col / 32] = (uint8_t)sb;
   } else {
+    // x / X can reach 2^9 > 448 (E4M3 max): clamp first - the fp8 convert does not saturate (NaN code)
+    const float lim = 448.f * X;
+    float c[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) c[e] = fminf(fmaxf(v[e], -lim), lim);
     s16x2_t a = {0, 0}, b = {0, 0};
-    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(a, v[0], v[1], X, false);
-    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(a, v[2], v[3], X, true);
-    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(b, v[4], v[5], X, false);
-    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(b, v[6], v[7], X, true);
+    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(a, c[0], c[1], X, false);
+    a = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(a, c[2], c[3], X, true);
+    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(b, c[4], c[5], X, false);
+    b = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(b, c[6], c[7], X, true);
     u32x2_t w;
     w[0] = (uint32_t)(uint16_t)a[0] | ((uint32_t)(uint16_t)a[1] << 16);
     w[1] = (uint32_t)(uint16_t)b[0] | ((uint32_t)(uint16_t)b[1] << 16);
