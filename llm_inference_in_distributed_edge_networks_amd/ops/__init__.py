@@ -145,13 +145,14 @@ def set_gemm_tile(tile: int) -> None:
 
 
 # s-a*: timing ablations with wrong results, only in a tuning build of the library (-DEDGE_TUNING_BUILD=1)
-GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8, "s-a4": 9, "e": 10}
+GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8, "s-a4": 9, "e": 10, "w": 11, "wp": 12}
 
 
 def set_gemm_variant(v: int) -> None:
     """256x256 GEMM main loop (A/B and tests): 0 K-tile double buffer with compiler-waited fragment loads,
     1 the same with hand-counted asm reads, 2 the K-half ring, 3 the ring with s_setprio, 4 the ring with
-    wave-group ping-pong, 8 the ping-pong ring with 5 slots, 10 the eight-phase full-line K-tile kernel."""
+    wave-group ping-pong, 8 the ping-pong ring with 5 slots, 10 the eight-phase full-line K-tile kernel, 11 the
+    four-wave kernel with 128x128 wave tiles (default), 12 the same with an L2 prefetch stream."""
     call("edge_gemm_set_variant", int(v))
 
 
@@ -166,9 +167,10 @@ def gemm_ssq_parts(M: int, N: int, K: int, act=None, bias=False, residual=False)
     return int(lib().edge_gemm_ssq_parts(M, N, K, _ACT[act], int(bool(bias)), int(bool(residual))))
 
 
-def set_gemm_walk(chunked: bool) -> None:
-    """Persistent 256x256 GEMMs: XCD-contiguous tile chunks (default) or the grid-strided walk.  A/B only."""
-    call("edge_gemm_set_walk", int(bool(chunked)))
+def set_gemm_walk(chunked) -> None:
+    """Persistent 256x256 GEMMs: XCD-contiguous tile chunks (default) or the grid-strided walk.  A/B only.
+    2 = chunked for the four-wave kernel too (it walks strided otherwise)."""
+    call("edge_gemm_set_walk", int(chunked) if not isinstance(chunked, bool) else int(chunked))
 
 
 def set_gemm_config(spec: str) -> None:

@@ -240,9 +240,10 @@ def test_full_model_nll_matches_cpu_fp32(name, B, S):
 
 @pytest.mark.parametrize("M,N,K,epi", [(32768, 9728, 896, "swiglu"), (4096, 2048, 512, "gelu"),
                                        (1000, 1024, 896, "resid"), (700, 2048, 512, "bias")])
-def test_linear_x6_eight_phase(M, N, K, epi):
-    """The X6 (fp32-mode) GEMMs on the eight-phase main loop (variant 10)."""
-    ops.set_gemm_config("256e")
+@pytest.mark.parametrize("tile", ["256e", "256w", "256wp"])
+def test_linear_x6_eight_phase(M, N, K, epi, tile):
+    """The X6 (fp32-mode) GEMMs on the eight-phase (variant 10) and four-wave (variant 11) main loops."""
+    ops.set_gemm_config(tile)
     try:
         test_linear_x6_fp32_accuracy(M, N, K, {"resid": "resid", "gelu": "gelu", "swiglu": "swiglu",
                                                 "bias": "bias"}[epi])

@@ -131,7 +131,7 @@ def _gemm_case(M, N, K, epi):
     close(y, ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("tile", ["128", "256", "256r", "256s", "256s5", "256e"])
+@pytest.mark.parametrize("tile", ["128", "256", "256r", "256s", "256s5", "256e", "256w"])
 def test_gemm_asymmetric_identity(tile):
     # A = I, asymmetric B: catches a transposed C-write
     K = 256
@@ -371,10 +371,12 @@ def test_fused_norm_model_matches_unfused():
 @pytest.mark.parametrize("M,N,K,epi", [(4352 + 37, 4096, 192, "resid"), (4352, 4096, 64, "swiglu"),
                                        (4400, 3968, 128, "bias_resid"), (300, 1024, 896, "none"),
                                        (32768, 9728, 896, "swiglu"), (8192, 2048, 4864, "gelu")])
-def test_gemm_eight_phase(M, N, K, epi):
-    """Variant 10 (eight-phase full-line K-tiles, half-tile DMA stream across tile boundaries): partial row/column
-    tiles, K = one K-tile (64: the prologue's items span tiles), more tiles than CUs."""
-    ops.set_gemm_config("256e")
+@pytest.mark.parametrize("tile", ["256e", "256w", "256wp"])
+def test_gemm_eight_phase(M, N, K, epi, tile):
+    """Variant 10 (eight-phase full-line K-tiles, half-tile DMA stream across tile boundaries) and variant 11
+    (four waves of 128x128, K-tile stream across tile boundaries): partial row/column tiles, K = one K-tile (64:
+    the prologue's K-tiles span tiles), more tiles than CUs."""
+    ops.set_gemm_config(tile)
     try:
         _gemm_case(M, N, K, epi)
     finally:

@@ -28,6 +28,9 @@ SHAPES = {  # name: (M, N, K, act, bias, resid)
     "x6_down_b64": (32768, 896, 6 * 4864, "x6", False, True),
     "x6_o_proj_b64": (32768, 896, 6 * 896, "x6", False, True),
     "x6_big": (8192, 8192, 6 * 1024, "x6", False, False),
+    # epilogue-cost ablations of the x6 gate/up shape: plain fp32 output, plain bf16 output
+    "x6_gate_up_f32out": (32768, 9728, 6 * 896, "x6", False, False),
+    "gate_up_k5376_bf16out": (32768, 9728, 6 * 896, None, False, False),
 }
 
 
@@ -77,7 +80,7 @@ def main():
 
             def f():
                 ops.set_gemm_config(cfg)
-                ops.set_gemm_walk(walk != "0")
+                ops.set_gemm_walk(int(walk) if walk else 1)
                 ops._native.lib().edge_gemm_set_skip_epi(int(noepi))
                 ops._native.lib().edge_gemm_set_w7_mode(mode)
                 if act == "qkv_rope":
@@ -96,7 +99,7 @@ def main():
         variants = {t: mk(t) for t in tiles}
         ours = variants[tiles[0]]
         lib = lambda: torch.matmul(x, w.t())  # noqa: E731
-        if resid:  # hipBLASLt with the residual as beta*C (what a library route for RESID GEMMs would run)
+        if resid and not x6:  # hipBLASLt with the residual as beta*C (what a library route for RESID GEMMs would run)
             variants["libr"] = lambda: torch.addmm(r, x, w.t())
         for _ in range(3):
             ours(); lib()
