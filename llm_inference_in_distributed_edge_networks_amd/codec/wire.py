@@ -283,14 +283,15 @@ _FP4_GRID = torch.tensor([0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0])
 
 
 def _fp4_codes(v: torch.Tensor) -> torch.Tensor:
-    """E2M1 codes of v (round to nearest, ties to even code, saturating at 6), sign in bit 3."""
+    """E2M1 codes of v (round to nearest, ties to even code, saturating at 6), sign in bit 3 - kept on values that
+    round to zero (-0, code 8), as the gfx950 scaled convert does."""
     a = v.abs()
     # thresholds between grid points; a tie goes to the even code (0, 2, 4, 6)
     c = torch.zeros_like(a, dtype=torch.int64)
     for lo, hi_excl, code in ((0.25, True, 1), (0.75, False, 2), (1.25, True, 3), (1.75, False, 4), (2.5, True, 5),
                               (3.5, False, 6), (5.0, True, 7)):
         c = torch.where(a > lo if hi_excl else a >= lo, torch.full_like(c, code), c)
-    return c | ((v < 0) & (c > 0)).to(torch.int64) << 3
+    return c | torch.signbit(v).to(torch.int64) << 3
 
 
 def _mx_exp(am: torch.Tensor, emax: int) -> torch.Tensor:
