@@ -1366,272 +1366,6 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs a) {
   if (wm == 0) __builtin_amdgcn_s_barrier();  // group 0 matches group 1's extra barrier
 }
 
-// ---- 256x256 four-wave GEMM (variant 11, "256w"): 128x128 wave tiles, one wave per SIMD ----------------------
-// Four waves (2 x 2), each owning a 128x128 output block = 8 x 8 v_mfma_f32_16x16x32_bf16 accumulators (256 VGPRs:
-// the 512-entry unified register file of a one-wave-per-SIMD kernel).  Per 32-wide K-half a wave reads 8 A + 8 B
-// fragments for 64 MFMAs - half the LDS reads per MFMA of a 128x64 wave tile - and no partner wave shares its
-// SIMD's matrix pipe.  K-tiles of BK = 64 (full 128-byte LDS rows, the C256 swizzled image), double-buffered
-// (2 x 64 KiB); fragments double-buffered in registers (X = K-half 0, Y = K-half 1).  Per K-tile t (buffer t & 1):
-//   M(t,0): 64 MFMAs on X, interleaved with the 16 ds_reads of K-half 1 into Y
-//   lgkmcnt(0) (Y landed), vmcnt(0) (K-tile t+1's DMA, issued during M(t-1,1), landed), ONE barrier
-//   M(t,1): 64 MFMAs on Y, interleaved with the 16 glds of K-tile t+2 into buffer t & 1 (every wave's reads of it
-//           retired before the barrier) and the 16 ds_reads of K-tile t+1's K-half 0 into X
-// so each DMA has two K-halves (128 MFMAs per wave) to land.  The K-tile stream runs through all of the workgroup's
-// tiles (persistent, XCD-chunked walk); a tile's epilogue runs after its last M(t,1), on the two 64-column halves
-// of the wave's block with the C256 epilogue.
-// PF > 0 (variant 12): each wave also touches one 128-B line per row of the A and B tiles of K-tile t+PF (two 4-byte
-// LDS-DMA loads into a scratch area past the buffers) at the end of M(t,1), so the tile DMA of two K-tiles later
-// hits L2; the barrier waits then leave those two loads outstanding (vmcnt(2)).
-template <int EPI, int RH, int PF>
-__global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
-  using CQ = Cfg<256, 256, 4, 4>;   // epilogue view: 64x64 quarters
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TB = 65536, BOFF = 32768;   // K-tile buffer bytes, B tile offset inside it
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tm = (a.M + 255) / 256, tn = (a.N + 255) / 256, ntiles = tm * tn;
-  // strided walk: at any time the whole chip works on ~256 consecutive grouped-M tiles, so every XCD shares the same
-  // 8 A panels through the Infinity Cache (the per-XCD chunked walk was 3-8 % slower on the M = 32768 shapes)
-  const TileWalk walk = tile_walk(blockIdx.x, gridDim.x, ntiles, a.walk == 2 ? 1 : 0);
-  const int tile0 = walk.first, G = walk.stride;
-  if (tile0 >= walk.end) return;
-  const int nk = a.K / 64;
-  const int total = ((walk.end - 1 - tile0) / G + 1) * nk;   // K-tiles of this workgroup
-
-  // ---- DMA: wave w stages 1-KiB blocks w, w+4, ..., w+28 of each 32 KiB operand tile (8 rows of 128 B each)
-  const char* sa = nullptr;
-  const char* sb = nullptr;
-  uint32_t oa[8], ob[8];
-  auto set_stage_tile = [&](int t) {
-    int m0, n0;
-    tile_origin(t, a.M, a.N, 256, 256, m0, n0);
-    sa = (const char*)(a.A + (size_t)m0 * a.lda);
-    sb = (const char*)(a.B + (size_t)n0 * a.ldb);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = (i * 4 + wave) * 8 + (lane >> 3);
-      const int ch = (lane & 7) ^ swz(r);
-      oa[i] = (uint32_t)(min(r, a.M - 1 - m0) * a.lda + ch * 8) * 2u;
-      ob[i] = (uint32_t)(min(r, a.N - 1 - n0) * a.ldb + ch * 8) * 2u;
-    }
-  };
-  int st_q = 0, st_kt = 0, st_tile = tile0;
-  set_stage_tile(tile0);
-  auto stage_part = [&](int part) {  // part 0 / 1: A / B rows of K-tile st_q (B advances the stream)
-    char* buf = smem + (st_q & 1) * TB;
-    const int kb = st_kt * 128;
-    if (part == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) glds16(sa + kb + oa[i], buf + (i * 4 + wave) * 1024);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) glds16(sb + kb + ob[i], buf + BOFF + (i * 4 + wave) * 1024);
-      ++st_q;
-      if (++st_kt == nk && st_q < total) {
-        st_kt = 0;
-        st_tile += G;
-        set_stage_tile(st_tile);
-      }
-    }
-  };
-
-  // ---- L2 prefetch stream (PF K-tiles ahead of the compute)
-  const char* pa_ = nullptr;
-  const char* pb_ = nullptr;
-  int pf_q = PF, pf_kt = 0, pf_tile = tile0;
-  auto set_pf_tile = [&](int t) {
-    int pm0, pn0;
-    tile_origin(t, a.M, a.N, 256, 256, pm0, pn0);
-    const int r = wave * 64 + lane;
-    pa_ = (const char*)(a.A + (size_t)(pm0 + min(r, a.M - 1 - pm0)) * a.lda);
-    pb_ = (const char*)(a.B + (size_t)(pn0 + min(r, a.N - 1 - pn0)) * a.ldb);
-  };
-  if constexpr (PF > 0) {
-    pf_kt = PF % nk;
-    pf_tile = tile0 + (PF / nk) * G;
-    if (pf_tile >= walk.end) pf_tile = tile0;
-    set_pf_tile(pf_tile);
-  }
-  auto prefetch = [&]() {
-    if constexpr (PF > 0) {
-      char* scratch = smem + 2 * TB + wave * 256;
-      __builtin_amdgcn_global_load_lds(pa_ + pf_kt * 128, LDS_PTR(scratch), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds(pb_ + pf_kt * 128, LDS_PTR(scratch), 4, 0, 0);
-      ++pf_q;
-      if (pf_q < total && ++pf_kt == nk) {
-        pf_kt = 0;
-        pf_tile += G;
-        set_pf_tile(pf_tile);
-      }
-    }
-  };
-
-  // ---- fragments
-  const int sw = ((lane & 15) >> 1) & 7;
-  uint32_t abase[2], bbase[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int c = ks * 4 + (lane >> 4);
-    abase[ks] = lds_addr(smem) + (wm * 128 + (lane & 15)) * 128 + ((c ^ sw) << 4);
-    bbase[ks] = lds_addr(smem) + BOFF + (wn * 128 + (lane & 15)) * 128 + ((c ^ sw) << 4);
-  }
-  bf16x8_t XA[8], XB[8], YA[8], YB[8];
-  f32x4_t acc[2][8][4];   // [column half][row group][column group]
-
-#define W4_RD(F, base, idx) DS_READ_B128(F, base, (idx) * 2048)
-  // 64 MFMAs on (FA, FB) with 16 ds_reads (8 A + 8 B fragments of K-half ks of buffer bo into GA / GB) interleaved:
-  // one read after every 4 MFMAs; read_on = false issues the MFMAs only.
-  // first_c = true: the tile's first MFMAs start from zero (no accumulator zeroing, no tied input)
-  auto mma_rd = [&](const bf16x8_t(&FA)[8], const bf16x8_t(&FB)[8], bf16x8_t(&GA)[8], bf16x8_t(&GB)[8],
-                    uint32_t bo, int ks, auto first_c) {
-    const uint32_t va = abase[ks] + bo, vb = bbase[ks] + bo;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if constexpr (decltype(first_c)::value) MFMA_AGPR_FIRST(acc[j >> 2][i][j & 3], FB[j], FA[i]);
-        else MFMA_AGPR(acc[j >> 2][i][j & 3], FB[j], FA[i]);
-        if ((j & 3) == 3) {
-          const int q = i * 2 + (j >> 2);   // 0..15
-          __builtin_amdgcn_sched_barrier(0);
-          if (q < 8) W4_RD(GA[q], va, q);
-          else W4_RD(GB[q - 8], vb, q - 8);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    }
-  };
-  // the same with the 16 glds of one K-tile interleaved too (one glds every 4 MFMAs, after the read); the read /
-  // DMA switches are compile-time (runtime-predicated asm register writes make the allocator spill the fragments)
-  auto mma_rd_dma = [&](const bf16x8_t(&FA)[8], const bf16x8_t(&FB)[8], bf16x8_t(&GA)[8], bf16x8_t(&GB)[8],
-                        uint32_t bo, auto read_c, auto dma_c) {
-    constexpr bool read_on = decltype(read_c)::value, dma_on = decltype(dma_c)::value;
-    const uint32_t va = abase[0] + bo, vb = bbase[0] + bo;
-    char* dbuf = smem + (st_q & 1) * TB;
-    const int kb = st_kt * 128;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        MFMA_AGPR(acc[j >> 2][i][j & 3], FB[j], FA[i]);
-        if ((j & 3) == 3) {
-          const int q = i * 2 + (j >> 2);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (read_on) {
-            if (q < 8) W4_RD(GA[q], va, q);
-            else W4_RD(GB[q - 8], vb, q - 8);
-          }
-          if constexpr (dma_on) {
-            if (q < 8) glds16(sa + kb + oa[q], dbuf + (q * 4 + wave) * 1024);
-            else glds16(sb + kb + ob[q - 8], dbuf + BOFF + ((q - 8) * 4 + wave) * 1024);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    }
-    if constexpr (dma_on) {  // advance the DMA stream by one K-tile (both parts issued above); it stops at the end
-      ++st_q;
-      if (st_q >= total) {
-        st_kt = nk - 1;
-      } else if (++st_kt == nk) {
-        st_kt = 0;
-        st_tile += G;
-        set_stage_tile(st_tile);
-      }
-    }
-  };
-#undef W4_RD
-
-  // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed and visible, its K-half 0 fragments in X
-  stage_part(0);
-  stage_part(1);
-  if (total > 1) {
-    stage_part(0);
-    stage_part(1);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) DS_READ_B128(XA[i], abase[0], i * 2048);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) DS_READ_B128(XB[j], bbase[0], j * 2048);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-  int tile = tile0, kt = 0, m0, n0;
-  tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
-  float rs[8];
-  auto load_rs = [&](int mt) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = min(mt + wm * 128 + i * 16 + (lane & 15), a.M - 1);
-      rs[i] = a.rscale ? a.rscale[m] : 1.f;
-    }
-  };
-  load_rs(m0);
-#pragma unroll 1
-  for (int t = 0; t < total; ++t) {
-    const uint32_t bo = (t & 1) * TB, bn = ((t + 1) & 1) * TB;
-    // M(t,0) on X, K-half 1 of K-tile t -> Y
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt == 0) mma_rd(XA, XB, YA, YB, bo, 1, std::true_type{});
-    else mma_rd(XA, XB, YA, YB, bo, 1, std::false_type{});
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < total) {
-      if constexpr (PF > 0) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // M(t,1) on Y, K-tile t+2 -> buffer t & 1, K-half 0 of K-tile t+1 -> X
-    // unconditional: past the end of the stream the DMA re-reads the last K-tile into a buffer nobody reads again
-    // and the fragment reads fill X with values nobody consumes
-    mma_rd_dma(YA, YB, XA, XB, bn, std::true_type{}, std::true_type{});
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PF > 0) {
-      if (pf_q < total) prefetch();
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the count rule exact at the end
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (++kt == nk) {
-      // all MFMAs of the tile were issued; the epilogue reads the accumulators after they drain
-      MFMA_DRAIN();
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int qd = 0; qd < 4; ++qd) {
-        // one 64x64 quarter at a time (row half ih, column half h), as virtual wave (2 wm + ih, 2 wn + h) of a 4x4
-        // layout: its accumulators are copied to VGPRs here (the scheduler would otherwise hoist all 256 reads)
-        const int ih = qd >> 1, h = qd & 1;
-        f32x4_t c[4][4];
-        float rq[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          rq[i] = rs[ih * 4 + i];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            c[i][j] = acc[h][ih * 4 + i][j];
-            asm volatile("" : "+v"(c[i][j]));
-          }
-        }
-        if (n0 + wn * 128 + h * 64 < a.N) gemm_epilogue<EPI, RH, CQ>(a, c, m0, n0, lane, wm * 2 + ih, wn * 2 + h, rq);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      kt = 0;
-      tile += G;
-      if (tile < walk.end) {
-        tile_origin(tile, a.M, a.N, 256, 256, m0, n0);
-        load_rs(m0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // ---- 256x224 persistent GEMM for N = 896 (Qwen2 hidden size: O-proj and MLP down, both residual epilogues) ----
 // 896 = 3.5 x 256: the 256x256 tile computes a half-empty last column tile (1/8 of all MFMAs wasted, its
 // waves' SIMDs idle), and no power-of-two tile both avoids that and gives a tile count that divides the 256
@@ -1755,6 +1489,287 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
       if (ok && g == 0) a.ssq_out[(size_t)m * P + nw / 112] = ss;
     }
   }
+}
+
+// ---- four-wave GEMM (variant 11, "256w"): 128 x (BN/2) wave tiles, one wave per SIMD ---------------------------
+// Four waves (2 x 2) per 256 x BN tile (BN = 256, or 224 for the N = 896 residual GEMMs), each owning a 128 x BN/2
+// block = 8 x NJ v_mfma_f32_16x16x32_bf16 accumulators (NJ = BN/32: 256 / 224 AGPRs, the accumulator half of the
+// 512-entry unified register file of a one-wave-per-SIMD kernel; see MFMA_AGPR).  Per 32-wide K-half a wave reads
+// 8 A + NJ B fragments for 8 NJ MFMAs - about half the LDS reads per MFMA of the eight-wave 128x64 / 64x112 wave
+// tiles - and no partner wave shares its SIMD's matrix pipe.  K-tiles of BK = 64 (full 128-byte LDS rows, the
+// swizzled C256 image), double-buffered (2 x (32 + BN/8) KiB); fragments double-buffered in registers (X = K-half
+// 0, Y = K-half 1).  Per K-tile t (buffer t & 1):
+//   M(t,0): 8 NJ MFMAs on X, interleaved with the ds_reads of K-half 1 into Y
+//   lgkmcnt(0) (Y landed), vmcnt(0) (K-tile t+1's DMA, issued during M(t-1,1), landed), ONE barrier
+//   M(t,1): 8 NJ MFMAs on Y, interleaved with the 8 + NJ glds of K-tile t+2 into buffer t & 1 (every wave's reads
+//           of it retired before the barrier) and the ds_reads of K-tile t+1's K-half 0 into X
+// so each DMA has two K-halves to land.  The K-tile stream runs through all of the workgroup's tiles (persistent,
+// grid-strided walk); a tile's epilogue runs after its last M(t,1), one 64-row quarter / half at a time with the
+// shared epilogues (gemm_epilogue for BN = 256 as a 4 x 4 layout of 64 x 64 slabs, w7_epilogue for BN = 224 as
+// 4 x 2 slabs of 64 x 112).
+// PF > 0 (variant 12): each wave also touches one 128-B line per row of the A and B tiles of K-tile t+PF (two 4-byte
+// LDS-DMA loads into a scratch area past the buffers) at the end of M(t,1), so the tile DMA two K-tiles later hits
+// L2; the barrier waits then leave those two loads outstanding (vmcnt(2)).  (Measured slower: kept for A/B.)
+namespace w4 {
+template <int BN> struct Geo {
+  static constexpr int NJ = BN / 32;                    // wave column groups of 16
+  static constexpr int NB = BN / 32;                    // B glds blocks per wave per K-tile (BN/8 blocks of 1 KiB)
+  static constexpr int BOFF = 32768, TB = 32768 + BN * 128;   // B tile offset, K-tile buffer bytes
+  static constexpr int NR = 8 + NJ;                     // fragment reads (and glds) per wave per K-half (K-tile)
+  static constexpr int MF = 8 * NJ;                     // MFMAs per wave per K-half
+  static constexpr int LDS = 2 * TB;
+};
+// position (MFMA index) after which work item r of NR is issued: evenly spread over the MF MFMAs
+template <int MF, int NR>
+__device__ constexpr int slot_pos(int r) { return (r + 1) * MF / NR - 1; }
+}  // namespace w4
+
+template <int EPI, int RH, int PF, int BN>
+__global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
+  using Gm = w4::Geo<BN>;
+  constexpr int NJ = Gm::NJ, NB = Gm::NB, BOFF = Gm::BOFF, TB = Gm::TB, NR = Gm::NR, MF = Gm::MF;
+  using CQ = Cfg<256, 256, 4, 4>;   // BN = 256 epilogue view: 64x64 slabs
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tm = (a.M + 255) / 256, tn = (a.N + BN - 1) / BN, ntiles = tm * tn;
+  // strided walk: at any time the whole chip works on ~256 consecutive grouped-M tiles, so every XCD shares the same
+  // 8 A panels through the Infinity Cache (the per-XCD chunked walk was 3-8 % slower on the M = 32768 shapes)
+  const TileWalk walk = tile_walk(blockIdx.x, gridDim.x, ntiles, a.walk == 2 ? 1 : 0);
+  const int tile0 = walk.first, G = walk.stride;
+  if (tile0 >= walk.end) return;
+  const int nk = a.K / 64;
+  const int total = ((walk.end - 1 - tile0) / G + 1) * nk;   // K-tiles of this workgroup
+
+  // ---- DMA: wave w stages 1-KiB blocks w, w+4, ... of each operand tile (8 rows of 128 B each)
+  const char* sa = nullptr;
+  const char* sb = nullptr;
+  uint32_t oa[8], ob[NB];
+  auto set_stage_tile = [&](int t) {
+    int m0, n0;
+    tile_origin(t, a.M, a.N, 256, BN, m0, n0);
+    sa = (const char*)(a.A + (size_t)m0 * a.lda);
+    sb = (const char*)(a.B + (size_t)n0 * a.ldb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = (i * 4 + wave) * 8 + (lane >> 3);
+      oa[i] = (uint32_t)(min(r, a.M - 1 - m0) * a.lda + ((lane & 7) ^ swz(r)) * 8) * 2u;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int r = (i * 4 + wave) * 8 + (lane >> 3);
+      ob[i] = (uint32_t)(min(r, a.N - 1 - n0) * a.ldb + ((lane & 7) ^ swz(r)) * 8) * 2u;
+    }
+  };
+  int st_q = 0, st_kt = 0, st_tile = tile0;
+  set_stage_tile(tile0);
+  auto dma_item = [&](int r, char* buf, int kb) {   // item r < 8: A block, else B block r - 8
+    if (r < 8) glds16(sa + kb + oa[r], buf + (r * 4 + wave) * 1024);
+    else glds16(sb + kb + ob[r - 8], buf + BOFF + ((r - 8) * 4 + wave) * 1024);
+  };
+  auto advance_stage = [&]() {   // the DMA stream stops (repeats its last K-tile) at the end
+    ++st_q;
+    if (st_q >= total) {
+      st_kt = nk - 1;
+    } else if (++st_kt == nk) {
+      st_kt = 0;
+      st_tile += G;
+      set_stage_tile(st_tile);
+    }
+  };
+  auto stage_all = [&]() {
+    char* buf = smem + (st_q & 1) * TB;
+    const int kb = st_kt * 128;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) dma_item(r, buf, kb);
+    advance_stage();
+  };
+
+  // ---- L2 prefetch stream (PF K-tiles ahead of the compute)
+  const char* pa_ = nullptr;
+  const char* pb_ = nullptr;
+  int pf_q = PF, pf_kt = 0, pf_tile = tile0;
+  auto set_pf_tile = [&](int t) {
+    int pm0, pn0;
+    tile_origin(t, a.M, a.N, 256, BN, pm0, pn0);
+    const int r = wave * 64 + lane;
+    pa_ = (const char*)(a.A + (size_t)(pm0 + min(r, a.M - 1 - pm0)) * a.lda);
+    pb_ = (const char*)(a.B + (size_t)(pn0 + min(min(r, BN - 1), a.N - 1 - pn0)) * a.ldb);
+  };
+  if constexpr (PF > 0) {
+    pf_kt = PF % nk;
+    pf_tile = tile0 + (PF / nk) * G;
+    if (pf_tile >= walk.end) pf_tile = tile0;
+    set_pf_tile(pf_tile);
+  }
+  auto prefetch = [&]() {
+    if constexpr (PF > 0) {
+      char* scratch = smem + 2 * TB + wave * 256;
+      __builtin_amdgcn_global_load_lds(pa_ + pf_kt * 128, LDS_PTR(scratch), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(pb_ + pf_kt * 128, LDS_PTR(scratch), 4, 0, 0);
+      ++pf_q;
+      if (pf_q < total && ++pf_kt == nk) {
+        pf_kt = 0;
+        pf_tile += G;
+        set_pf_tile(pf_tile);
+      }
+    }
+  };
+
+  // ---- fragments
+  const int sw = ((lane & 15) >> 1) & 7;
+  uint32_t abase[2], bbase[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = ks * 4 + (lane >> 4);
+    abase[ks] = lds_addr(smem) + (wm * 128 + (lane & 15)) * 128 + ((c ^ sw) << 4);
+    bbase[ks] = lds_addr(smem) + BOFF + (wn * (BN / 2) + (lane & 15)) * 128 + ((c ^ sw) << 4);
+  }
+  bf16x8_t XA[8], XB[NJ], YA[8], YB[NJ];
+  f32x4_t acc[8][NJ];
+
+  // 8 NJ MFMAs on (FA, FB) with the NR fragment reads of K-half ks of buffer bo into (GA, GB) and, with DMA, the NR
+  // glds of the stream's next K-tile spread evenly between them.  The switches are compile-time (runtime-predicated
+  // asm register writes make the allocator spill the fragments); first_c: the tile's first MFMAs start from zero.
+  auto mma = [&](const bf16x8_t(&FA)[8], const bf16x8_t(&FB)[NJ], bf16x8_t(&GA)[8], bf16x8_t(&GB)[NJ], uint32_t bo,
+                 int ks, auto first_c, auto dma_c, auto read_c) {
+    constexpr bool first = decltype(first_c)::value, dma_on = decltype(dma_c)::value;
+    constexpr bool read_on = decltype(read_c)::value;
+    const uint32_t va = abase[ks] + bo, vb = bbase[ks] + bo;
+    char* dbuf = smem + (st_q & 1) * TB;
+    const int kb = st_kt * 128;
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      // MFMAs slot_pos(rr-1)+1 .. slot_pos(rr), then work item rr
+#pragma unroll
+      for (int n = (rr == 0 ? 0 : w4::slot_pos<MF, NR>(rr - 1) + 1); n <= w4::slot_pos<MF, NR>(rr); ++n) {
+        const int i = n / NJ, j = n % NJ;
+        if constexpr (first) MFMA_AGPR_FIRST(acc[i][j], FB[j], FA[i]);
+        else MFMA_AGPR(acc[i][j], FB[j], FA[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (read_on) {
+        if (rr < 8) DS_READ_B128(GA[rr], va, rr * 2048);
+        else DS_READ_B128(GB[rr - 8], vb, (rr - 8) * 2048);
+      }
+      if constexpr (dma_on) dma_item(rr, dbuf, kb);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (dma_on) advance_stage();
+  };
+
+  // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed and visible, its K-half 0 fragments in X
+  stage_all();
+  if (total > 1) {
+    stage_all();
+    if constexpr (NR == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) DS_READ_B128(XA[i], abase[0], i * 2048);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) DS_READ_B128(XB[j], bbase[0], j * 2048);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  int tile = tile0, kt = 0, m0, n0;
+  tile_origin(tile, a.M, a.N, 256, BN, m0, n0);
+  float rs[8];
+  auto load_rs = [&](int mt) {
+    if constexpr (BN == 256) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = min(mt + wm * 128 + i * 16 + (lane & 15), a.M - 1);
+        rs[i] = a.rscale ? a.rscale[m] : 1.f;
+      }
+    }
+  };
+  load_rs(m0);
+#pragma unroll 1
+  for (int t = 0; t < total; ++t) {
+    const uint32_t bo = (t & 1) * TB, bn = ((t + 1) & 1) * TB;
+    // M(t,0) on X, K-half 1 of K-tile t -> Y
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt == 0) mma(XA, XB, YA, YB, bo, 1, std::true_type{}, std::false_type{}, std::true_type{});
+    else mma(XA, XB, YA, YB, bo, 1, std::false_type{}, std::false_type{}, std::true_type{});
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < total) {
+      if constexpr (PF > 0) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // M(t,1) on Y, K-tile t+2 -> buffer t & 1, K-half 0 of K-tile t+1 -> X.  Unconditional: past the end of the
+    // stream the DMA re-reads the last K-tile into a buffer nobody reads again and X gets values nobody consumes.
+    // (A runtime switch between read / no-read copies of this loop makes the allocator spill the fragments.)
+    mma(YA, YB, XA, XB, bn, 0, std::false_type{}, std::true_type{}, std::true_type{});
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PF > 0) {
+      if (pf_q < total) prefetch();
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the count rule exact at the end
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (++kt == nk) {
+      // all MFMAs of the tile were issued; the epilogue reads the accumulators after they drain
+      MFMA_DRAIN();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (BN == 256) {
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          // one 64x64 slab at a time (row half ih, column half h), as virtual wave (2 wm + ih, 2 wn + h) of a 4x4
+          // layout: its accumulators are copied to VGPRs here (the scheduler would otherwise hoist all the reads)
+          const int ih = qd >> 1, h = qd & 1;
+          f32x4_t c[4][4];
+          float rq[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            rq[i] = rs[ih * 4 + i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              c[i][j] = acc[ih * 4 + i][h * 4 + j];
+              asm volatile("" : "+v"(c[i][j]));
+            }
+          }
+          if (n0 + wn * 128 + h * 64 < a.N) gemm_epilogue<EPI, RH, CQ>(a, c, m0, n0, lane, wm * 2 + ih, wn * 2 + h, rq);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih) {   // 64 x 112 halves as virtual waves (2 wm + ih, wn) of the W7 layout
+          f32x4_t c[4][NJ];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              c[i][j] = acc[ih * 4 + i][j];
+              asm volatile("" : "+v"(c[i][j]));
+            }
+          w7_epilogue<EPI, 0>(a, c, m0, n0, lane, wm * 2 + ih, wn);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      kt = 0;
+      tile += G;
+      if (tile < walk.end) {
+        tile_origin(tile, a.M, a.N, 256, BN, m0, n0);
+        load_rs(m0);
+      }
+      // the next tile's first K-half fragments again (K-tile t+1 landed in buffer bn before this K-tile's barrier):
+      // re-reading them here leaves the copies read during M(t,1) dead across the epilogue, which gets their VGPRs
+#pragma unroll
+      for (int i = 0; i < 8; ++i) DS_READ_B128(XA[i], abase[0] + bn, i * 2048);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) DS_READ_B128(XB[j], bbase[0] + bn, j * 2048);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Staging offsets (elements, 32-bit: the operands are < 2^31 elements) of this wave's glds blocks; instruction
@@ -2001,21 +2016,23 @@ static int launch_8p(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <int EPI, int RH, int PF = 0>
+template <int EPI, int RH, int PF = 0, int BN = 256>
 static int launch_4w(const GemmArgs& a, hipStream_t st) {
-  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   const int grid = std::min(tiles, num_cus());
-  constexpr int lds = 131072 + (PF > 0 ? 1024 : 0);
+  constexpr int lds = w4::Geo<BN>::LDS + (PF > 0 ? 1024 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, PF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, PF, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, PF>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, PF, BN>), dim3(grid), dim3(256), lds, st, a);
   return (int)hipGetLastError();
 }
 
-static int g_w7 = 1;  // 256x224 tiles for N % 224 == 0 shapes that 256 does not divide (N = 896)
+static int g_w7 = 2;  // 256x224 tiles for N % 224 == 0 shapes that 256 does not divide (N = 896): 1 eight-wave
+                      // 64x112 wave tiles, 2 four-wave 128x112 wave tiles (default: 10-17 % faster on N = 896)
 
 // The 256x224 kernel takes the plain / bias / residual epilogues of N % 224 == 0 shapes that 256 does not
 // divide, when 256-row tiles fill the chip; tests force it at small M with tile override 224.
@@ -2044,6 +2061,8 @@ static int launch_w7m(const GemmArgs& a, hipStream_t st) {
 
 template <int EPI>
 static int launch_w7(const GemmArgs& a, hipStream_t st) {
+  // g_w7 == 2 (or variant 11 forced): the four-wave kernel with 256x224 tiles (128x112 wave tiles)
+  if (g_c256_variant == 11 || (g_c256_variant < 0 && g_w7 == 2)) return launch_4w<EPI, 0, 0, 224>(a, st);
   if constexpr (epi_f32(EPI)) return launch_w7m<EPI, 0>(a, st);  // the modes A/B the bf16 epilogue's traffic
   switch (g_w7_mode) {
     case 1: return launch_w7m<EPI, 1>(a, st);

@@ -156,9 +156,10 @@ def set_gemm_variant(v: int) -> None:
     call("edge_gemm_set_variant", int(v))
 
 
-def set_gemm_w7(on: bool) -> None:
-    """Automatic use of the 256x224 tiles for N = 896-like shapes (default on; A/B only)."""
-    call("edge_gemm_set_w7", int(bool(on)))
+def set_gemm_w7(on) -> None:
+    """Automatic use of the 256x224 tiles for N = 896-like shapes (A/B only): 0 off, 1 / True the eight-wave
+    kernel, 2 the four-wave kernel."""
+    call("edge_gemm_set_w7", int(on))
 
 
 def gemm_ssq_parts(M: int, N: int, K: int, act=None, bias=False, residual=False) -> int:

@@ -251,6 +251,16 @@ def test_linear_x6_eight_phase(M, N, K, epi, tile):
         ops.set_gemm_config("0")
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 896, 896), (32768, 896, 896), (32768, 896, 4864), (256 * 3 + 5, 2688, 128)])
+def test_linear_x6_four_wave_224(M, N, K):
+    """The fp32-residual O-proj / down GEMMs on the four-wave 256x224 kernel."""
+    ops.set_gemm_config("224w")
+    try:
+        test_linear_x6_fp32_accuracy(M, N, K, "resid")
+    finally:
+        ops.set_gemm_config("0")
+
+
 @pytest.mark.parametrize("codec", ["mxfp4", "mxfp8", "mixed_mxfp4_mxfp8", "mxfp4_keep"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_mx_codecs_gpu_equal_cpu(codec, dtype):

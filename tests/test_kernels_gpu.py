@@ -87,10 +87,12 @@ def test_gemm_persistent_multi_tile(M, N, K, epi, tile):
 @pytest.mark.parametrize("M,N,K", [(300, 896, 896), (256 * 70 + 37, 896, 128), (1000, 896, 4864), (64, 896, 192),
                                    (300, 2688, 256)])
 @pytest.mark.parametrize("epi", ["none", "bias", "resid", "bias_resid"])
-def test_gemm_w7(M, N, K, epi):
-    """256x224 tiles (N % 224 == 0, N % 256 != 0): partial last row tile, the shortest K loop (two K-tiles, the
-    staging stream crosses tile boundaries every K-tile), more tiles than CUs, several column tiles."""
-    ops.set_gemm_config("224")
+@pytest.mark.parametrize("tile", ["224", "224w"])
+def test_gemm_w7(M, N, K, epi, tile):
+    """256x224 tiles (N % 224 == 0, N % 256 != 0), eight-wave and four-wave kernels: partial last row tile, the
+    shortest K loop (two K-tiles, the staging stream crosses tile boundaries every K-tile), more tiles than CUs,
+    several column tiles."""
+    ops.set_gemm_config(tile)
     try:
         _gemm_case(M, N, K, epi)
     finally:
@@ -310,7 +312,7 @@ def test_row_ssq(H):
     close(s, R.row_ssq(x), atol=1e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("tile", ["128", "224", "256", "256r", "256s", "256s5"])
+@pytest.mark.parametrize("tile", ["128", "224", "224w", "256", "256r", "256s", "256s5", "256w"])
 @pytest.mark.parametrize("act", [None, "swiglu_il"])
 def test_gemm_fused_norm_and_ssq_out(tile, act):
     M, K, N = 700, 896, 1024
@@ -334,7 +336,7 @@ def test_gemm_fused_norm_and_ssq_out(tile, act):
     if y2._edge_ssq.shape == ref_ssq.shape:
         close(y2._edge_ssq, ref_ssq, atol=1e-2, rtol=1e-4)
     else:
-        assert tile == "224" and y2._edge_ssq.shape == (M, 896 // 112)
+        assert tile.startswith("224") and y2._edge_ssq.shape == (M, 896 // 112)
         ref_ssq = y2.cpu().float().pow(2).reshape(M, 8, 112).sum(-1)
         close(y2._edge_ssq, ref_ssq, atol=1e-2, rtol=1e-4)
 

@@ -46,7 +46,7 @@ def test_qwen2_production_shapes_w7_vs_256():
         assert ops.gemm_ssq_parts(32768, 896, 896, residual=True) == 14
         c256 = LocalPipeline(m, plan, bcfg, use_graphs=False).run_batch(b).clone()
     finally:
-        ops.set_gemm_w7(True)
+        ops.set_gemm_w7(2)
     assert torch.isfinite(w7).all()
     # same math, different tiling / partial-sum order: bf16-level differences through 24 layers
     assert torch.allclose(w7, c256, rtol=2e-2, atol=2e-2), (w7 - c256).abs().max()
