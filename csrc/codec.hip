@@ -17,7 +17,11 @@
 // its un-selected tokens in fp32, Experiments/Qwen2-0.5B/qwen_layer_wise.py:54-70).
 #include "common.h"
 
-enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3, FMT_F32 = 4, FMT_MXFP4 = 5, FMT_MXFP8 = 6 };
+enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3, FMT_F32 = 4, FMT_MXFP4 = 5, FMT_MXFP8 = 6, FMT_GRP = 7 };
+// Head-group rows (FMT_GRP): every 64-channel group g (one head's width) has its own bit width b_g in {2, 4, 8}
+// (the plan: one byte per group in the message at off_plan, chosen from the boundary's channel-group relevance) and
+// its own max-abs scale s = max|x| / qmax_b (qmax 1 / 7 / 127): row = [group 0 codes (8 b_0 bytes)] ... [group G-1
+// codes][G fp32 scales]; codes are two's-complement int2 / int4 / int8 packed as the uniform formats.
 // OCP microscaling rows (FMT_MXFP4: E2M1 codes, FMT_MXFP8: E4M3 codes): blocks of 32 consecutive channels share one
 // E8M0 scale 2^(floor(log2 max|x|) - emax) (emax 2 / 8), stored after the row's codes: [codes][H/32 scale bytes].
 // Quantize / dequantize with gfx950's scaled converts (v_cvt_scalef32_pk_fp4_f32 / _fp8_f32 and the inverses:
@@ -29,13 +33,18 @@ struct CodecArgs {
   void* x; uint8_t* msg;
   long long off_mask, off_scale, off_hi, off_lo;
   long long off_kvec;           // >= 0: variable-k layout (k per window at msg + off_kvec), else fixed k
+  long long off_plan;           // >= 0: FMT_GRP bit plan (one byte per 64-channel group)
   int B, S, H, k, mw;           // mw: mask words per window
   int hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo, ch_kind;
+  int grp_code_bytes;           // FMT_GRP: sum over groups of 8 b_g (row = codes + 4 G scale bytes)
 };
 
 __device__ __forceinline__ int fmt_row_bytes(int fmt, int H) {
   return fmt == FMT_F32 ? 4 * H : fmt == FMT_BF16 ? 2 * H : fmt == FMT_INT8 ? H : fmt == FMT_INT4 ? H / 2 :
          fmt == FMT_MXFP4 ? H / 2 + H / 32 : fmt == FMT_MXFP8 ? H + H / 32 : H / 4;
+}
+__device__ __forceinline__ int row_bytes(const CodecArgs& a, int fmt) {
+  return fmt == FMT_GRP ? a.grp_code_bytes + 4 * (a.H / 64) : fmt_row_bytes(fmt, a.H);
 }
 
 __device__ __forceinline__ int wave_isum(int v) {
@@ -287,6 +296,80 @@ __device__ __forceinline__ void mx_unpack8(const uint8_t* __restrict__ row, int 
   }
 }
 
+// FMT_GRP: the 8 lanes holding channels [64 g, 64 g + 64) of a row (8 values each) quantize their group.
+// Byte offset of group g's codes = sum_{g' < g} 8 b_g'.
+__device__ __forceinline__ int grp_offset(const uint8_t* __restrict__ plan, int g) {
+  int o = 0;
+  for (int i = 0; i < g; ++i) o += 8 * plan[i];
+  return o;
+}
+__device__ __forceinline__ void grp_pack8(uint8_t* __restrict__ row, const CodecArgs& a, int col,
+                                          const float (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+  const uint8_t* plan = a.msg + a.off_plan;
+  const int g = col >> 6, bits = plan[g];
+  const int qmax = (1 << (bits - 1)) - 1;
+  float am = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[e]));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  am = fmaxf(am, __shfl_xor(am, 4, 64));
+  const float s = am / (float)qmax;
+  const float inv = am > 0.f ? 1.f / s : 0.f;
+  const float qf = (float)qmax;
+  int q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = (int)qround(v[e] * inv, qf, -qf);
+  uint8_t* dst = row + grp_offset(plan, g);
+  const int sub = lane & 7;
+  if (bits == 8) {
+    u32x2_t w;
+    w[0] = (q[0] & 255) | ((q[1] & 255) << 8) | ((q[2] & 255) << 16) | ((uint32_t)(q[3] & 255) << 24);
+    w[1] = (q[4] & 255) | ((q[5] & 255) << 8) | ((q[6] & 255) << 16) | ((uint32_t)(q[7] & 255) << 24);
+    *(u32x2_t*)(dst + sub * 8) = w;
+  } else if (bits == 4) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w |= (uint32_t)(q[e] & 15) << (4 * e);
+    *(uint32_t*)(dst + sub * 4) = w;
+  } else {
+    uint32_t w = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w |= (uint32_t)(q[e] & 3) << (2 * e);
+    *(uint16_t*)(dst + sub * 2) = (uint16_t)w;
+  }
+  if (sub == 0) *(float*)(row + a.grp_code_bytes + 4 * g) = s;
+}
+__device__ __forceinline__ void grp_unpack8(const uint8_t* __restrict__ row, const CodecArgs& a, int col,
+                                            float (&o)[8]) {
+  const int lane = threadIdx.x & 63;
+  const uint8_t* plan = a.msg + a.off_plan;
+  const int g = col >> 6, bits = plan[g];
+  const uint8_t* src = row + grp_offset(plan, g);
+  const int sub = lane & 7;
+  const float s = *(const float*)(row + a.grp_code_bytes + 4 * g);
+  int q[8];
+  if (bits == 8) {
+    const u32x2_t w = *(const u32x2_t*)(src + sub * 8);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      q[e] = (int)(int8_t)((w[0] >> (8 * e)) & 255);
+      q[4 + e] = (int)(int8_t)((w[1] >> (8 * e)) & 255);
+    }
+  } else if (bits == 4) {
+    const uint32_t w = *(const uint32_t*)(src + sub * 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = ((int)(w << (28 - 4 * e))) >> 28;
+  } else {
+    const uint32_t w = *(const uint16_t*)(src + sub * 2);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = ((int)(w << (30 - 2 * e))) >> 30;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (float)q[e] * s;
+}
+
 template <int NCH, class T>
 __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -298,12 +381,12 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
   const int slot_lo = lo_prefix(mask, a.mw, j, is_lo);
   const int fmt = is_lo ? a.lo_fmt : a.hi_fmt;
   const int qmax = is_lo ? a.qmax_lo : a.qmax_hi;
-  const int rb = fmt_row_bytes(fmt, a.H);
+  const int rb = row_bytes(a, fmt);
   uint8_t* dst;
   if (a.off_kvec >= 0) {
     int Kb, Kt;
     kvar_prefix(a, b, Kb, Kt);
-    const long long off_hi = a.off_lo + (((long long)Kt * fmt_row_bytes(a.lo_fmt, a.H) + 15) & ~15ll);
+    const long long off_hi = a.off_lo + (((long long)Kt * row_bytes(a, a.lo_fmt) + 15) & ~15ll);
     dst = is_lo ? a.msg + a.off_lo + ((size_t)Kb + slot_lo) * rb
                 : a.msg + off_hi + ((size_t)b * a.S - Kb + (j - slot_lo)) * rb;
   } else {
@@ -316,7 +399,7 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
 
   // scale / quantiser for this row
   float inv = 0.f, mul = 0.f;  // code = round(x * inv) for token & channel; window mode uses ref formula
-  const bool raw = fmt == FMT_BF16 || fmt == FMT_F32 || fmt == FMT_MXFP4 || fmt == FMT_MXFP8;
+  const bool raw = fmt == FMT_BF16 || fmt == FMT_F32 || fmt == FMT_MXFP4 || fmt == FMT_MXFP8 || fmt == FMT_GRP;
   if (raw && a.scale_mode == SC_TOKEN && lane == 0) scales[row] = 0.f;
   if (!raw) {
     if (a.scale_mode == SC_TOKEN) {
@@ -347,6 +430,10 @@ __global__ __launch_bounds__(256) void pack_kernel(CodecArgs a) {
     }
     if (fmt == FMT_MXFP4 || fmt == FMT_MXFP8) {
       mx_pack8(dst, a.H, col, fmt, v[c]);
+      continue;
+    }
+    if (fmt == FMT_GRP) {
+      grp_pack8(dst, a, col, v[c]);
       continue;
     }
     if (fmt == FMT_BF16) {
@@ -416,12 +503,12 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
   const int slot_lo = lo_prefix(mask, a.mw, j, is_lo);
   const int fmt = is_lo ? a.lo_fmt : a.hi_fmt;
   const int qmax = is_lo ? a.qmax_lo : a.qmax_hi;
-  const int rb = fmt_row_bytes(fmt, a.H);
+  const int rb = row_bytes(a, fmt);
   const uint8_t* src;
   if (a.off_kvec >= 0) {
     int Kb, Kt;
     kvar_prefix(a, b, Kb, Kt);
-    const long long off_hi = a.off_lo + (((long long)Kt * fmt_row_bytes(a.lo_fmt, a.H) + 15) & ~15ll);
+    const long long off_hi = a.off_lo + (((long long)Kt * row_bytes(a, a.lo_fmt) + 15) & ~15ll);
     src = is_lo ? a.msg + a.off_lo + ((size_t)Kb + slot_lo) * rb
                 : a.msg + off_hi + ((size_t)b * a.S - Kb + (j - slot_lo)) * rb;
   } else {
@@ -430,7 +517,7 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
   }
   const float* scales = (const float*)(a.msg + a.off_scale);
   float s = 0.f;
-  if (fmt != FMT_BF16 && fmt != FMT_F32 && fmt != FMT_MXFP4 && fmt != FMT_MXFP8) {
+  if (fmt != FMT_BF16 && fmt != FMT_F32 && fmt != FMT_MXFP4 && fmt != FMT_MXFP8 && fmt != FMT_GRP) {
     if (a.scale_mode == SC_TOKEN) s = scales[row];
     else if (a.scale_mode == SC_WINDOW) s = scales[b];
   }
@@ -456,6 +543,12 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
     if (fmt == FMT_MXFP4 || fmt == FMT_MXFP8) {
       float o[8];
       mx_unpack8(src, a.H, col, fmt, o);
+      store8(out + col, o);
+      continue;
+    }
+    if (fmt == FMT_GRP) {
+      float o[8];
+      grp_unpack8(src, a, col, o);
       store8(out + col, o);
       continue;
     }
@@ -502,11 +595,12 @@ __global__ __launch_bounds__(256) void unpack_kernel(CodecArgs a) {
   } while (0)
 
 static CodecArgs make_args(void* x, void* msg, long long om, long long os, long long oh, long long ol, long long okv,
-                           int B, int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi,
-                           int qmax_lo, int ch_kind) {
+                           long long opl, int B, int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode,
+                           int qmax_hi, int qmax_lo, int ch_kind, int grp_code_bytes) {
   CodecArgs a;
   a.x = x; a.msg = (uint8_t*)msg;
-  a.off_mask = om; a.off_scale = os; a.off_hi = oh; a.off_lo = ol; a.off_kvec = okv;
+  a.off_mask = om; a.off_scale = os; a.off_hi = oh; a.off_lo = ol; a.off_kvec = okv; a.off_plan = opl;
+  a.grp_code_bytes = grp_code_bytes;
   a.B = B; a.S = S; a.H = H; a.k = k; a.mw = ((S + 63) / 64) * 2;
   a.hi_fmt = hi_fmt; a.lo_fmt = lo_fmt; a.scale_mode = scale_mode; a.qmax_hi = qmax_hi; a.qmax_lo = qmax_lo;
   a.ch_kind = ch_kind;
@@ -555,12 +649,15 @@ EDGE_API int edge_rowmax(const float* in, float* out, int R, int H, hipStream_t 
   return (int)hipGetLastError();
 }
 
+// grp_code_bytes: FMT_GRP rows' code bytes (sum 8 b_g over the plan at msg + opl; 0 without FMT_GRP)
 EDGE_API int edge_pack(const void* x, void* msg, long long om, long long os, long long oh, long long ol, long long okv,
-                       int B, int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi, int qmax_lo,
-                       int ch_kind, int x_f32, hipStream_t st) {
+                       long long opl, int B, int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi,
+                       int qmax_lo, int ch_kind, int grp_code_bytes, int x_f32, hipStream_t st) {
   if (H % 32) return (int)hipErrorInvalidValue;
-  CodecArgs a = make_args((void*)x, msg, om, os, oh, ol, okv, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
-                          ch_kind);
+  if ((hi_fmt == FMT_GRP || lo_fmt == FMT_GRP) && (H % 64 || opl < 0 || grp_code_bytes <= 0))
+    return (int)hipErrorInvalidValue;
+  CodecArgs a = make_args((void*)x, msg, om, os, oh, ol, okv, opl, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi,
+                          qmax_lo, ch_kind, grp_code_bytes);
   const int rows = B * S;
   if (rows <= 0) return 0;
   if (x_f32) DISPATCH_NCH(H, hipLaunchKernelGGL((pack_kernel<NCH, float>), dim3((rows + 3) / 4), dim3(256), 0, st, a));
@@ -569,11 +666,14 @@ EDGE_API int edge_pack(const void* x, void* msg, long long om, long long os, lon
 }
 
 EDGE_API int edge_unpack(void* x, const void* msg, long long om, long long os, long long oh, long long ol,
-                         long long okv, int B, int S, int H, int k, int hi_fmt, int lo_fmt, int scale_mode, int qmax_hi,
-                         int qmax_lo, int ch_kind, int x_f32, hipStream_t st) {
+                         long long okv, long long opl, int B, int S, int H, int k, int hi_fmt, int lo_fmt,
+                         int scale_mode, int qmax_hi, int qmax_lo, int ch_kind, int grp_code_bytes, int x_f32,
+                         hipStream_t st) {
   if (H % 32) return (int)hipErrorInvalidValue;
-  CodecArgs a = make_args(x, (void*)msg, om, os, oh, ol, okv, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi, qmax_lo,
-                          ch_kind);
+  if ((hi_fmt == FMT_GRP || lo_fmt == FMT_GRP) && (H % 64 || opl < 0 || grp_code_bytes <= 0))
+    return (int)hipErrorInvalidValue;
+  CodecArgs a = make_args(x, (void*)msg, om, os, oh, ol, okv, opl, B, S, H, k, hi_fmt, lo_fmt, scale_mode, qmax_hi,
+                          qmax_lo, ch_kind, grp_code_bytes);
   const int rows = B * S;
   if (rows <= 0) return 0;
   if (x_f32) DISPATCH_NCH(H, hipLaunchKernelGGL((unpack_kernel<NCH, float>), dim3((rows + 3) / 4), dim3(256), 0, st, a));

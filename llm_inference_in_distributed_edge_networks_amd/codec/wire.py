@@ -35,7 +35,7 @@ from ..ops._native import call, ptr, stream
 
 MAGIC = 0x45444742
 VERSION = 1
-FMT_BF16, FMT_INT8, FMT_INT4, FMT_INT2, FMT_F32, FMT_MXFP4, FMT_MXFP8 = 0, 1, 2, 3, 4, 5, 6
+FMT_BF16, FMT_INT8, FMT_INT4, FMT_INT2, FMT_F32, FMT_MXFP4, FMT_MXFP8, FMT_GRP = 0, 1, 2, 3, 4, 5, 6, 7
 MX_FORMATS = (FMT_MXFP4, FMT_MXFP8)
 SC_TOKEN, SC_WINDOW, SC_CHANNEL, SC_NONE = 0, 1, 2, 3
 CH_MAXABS, CH_MEAN = 0, 1
@@ -54,6 +54,7 @@ class CodecSpec:
     ch_kind: int = CH_MAXABS
     uses_ratio: bool = True      # lo class = int(ratio*S) least important tokens
     needs_importance: bool = True
+    plan: tuple | None = None    # FMT_GRP rows: bits (2 / 4 / 8) of every 64-channel group (with_plan)
 
 
 CODECS = {c.name: c for c in [
@@ -73,7 +74,62 @@ CODECS = {c.name: c for c in [
     CodecSpec("mxfp8", 12, FMT_MXFP8, FMT_MXFP8, SC_NONE, uses_ratio=False, needs_importance=False),
     CodecSpec("mixed_mxfp4_mxfp8", 13, FMT_MXFP8, FMT_MXFP4, SC_NONE),
     CodecSpec("mxfp4_keep", 14, NATIVE, FMT_MXFP4, SC_NONE),
+    # head-group rows (FMT_GRP): every 64-channel group (one head's width) has its own bit width and max-abs scale;
+    # the widths come from the relevance of the boundary's channel groups (group_bits / allocate_group_bits)
+    CodecSpec("rgroup", 15, FMT_GRP, FMT_GRP, SC_NONE, uses_ratio=False, needs_importance=False),
+    CodecSpec("mixed_rgroup_int8", 16, FMT_INT8, FMT_GRP, SC_TOKEN, 127, 0),
 ]}
+GROUP = 64                  # channels per group of FMT_GRP rows
+GROUP_BITS = (2, 4, 8)
+
+
+def needs_plan(spec: CodecSpec) -> bool:
+    return FMT_GRP in (spec.hi_fmt, spec.lo_fmt)
+
+
+def with_plan(spec: CodecSpec, plan) -> CodecSpec:
+    """The codec with a group bit plan (one entry per 64-channel group, each 2, 4 or 8)."""
+    from dataclasses import replace
+    plan = tuple(int(b) for b in plan)
+    if any(b not in GROUP_BITS for b in plan):
+        raise ValueError(f"group bits must be in {GROUP_BITS}, got {plan}")
+    return replace(spec, plan=plan)
+
+
+def allocate_group_bits(relevance, avg_bits: float = 4.0) -> tuple:
+    """Relevance-driven bit allocation over the 64-channel groups of a boundary.
+
+    First-order (LRP) error model: quantizing group g with a max-abs step amax_g / qmax_b moves the output by
+    about sum_c |dx_c| * step / 2, which scales with the group's relevance R_g = sum |x * dx| (the LRP pass,
+    ``channel_group_relevance.json``) over qmax_b (1 / 7 / 127 for 2 / 4 / 8 bits).  Greedy: start every group at
+    2 bits and spend the budget ``avg_bits * G`` on the upgrade with the largest R_g (1/qmax_b - 1/qmax_b') per
+    bit (2 -> 4 -> 8); equal relevance gives the uniform plan."""
+    w = [max(float(r), 0.0) for r in relevance]
+    G = len(w)
+    if not any(w):
+        w = [1.0] * G
+    d = {2: 1.0, 4: 1.0 / 7.0, 8: 1.0 / 127.0}
+    bits = [2] * G
+    budget = int(round(avg_bits * G)) - 2 * G
+    while budget > 0:
+        best, best_gain = -1, 0.0
+        for g in range(G):
+            b = bits[g]
+            if b == 8:
+                continue
+            nb = 4 if b == 2 else 8
+            cost = nb - b
+            if cost > budget:
+                continue
+            gain = w[g] * (d[b] - d[nb]) / cost
+            if gain > best_gain or (gain == best_gain and best >= 0 and w[g] > w[best]):
+                best, best_gain = g, gain
+        if best < 0:
+            break
+        nb = 4 if bits[best] == 2 else 8
+        budget -= nb - bits[best]
+        bits[best] = nb
+    return tuple(bits)
 
 
 def get_codec(name: str) -> CodecSpec:
@@ -86,7 +142,9 @@ def _a16(n: int) -> int:
     return (n + 15) // 16 * 16
 
 
-def _row_bytes(fmt: int, H: int) -> int:
+def _row_bytes(fmt: int, H: int, plan=None) -> int:
+    if fmt == FMT_GRP:   # codes of every group (8 * bits bytes), then one fp32 scale per group
+        return sum(8 * b for b in plan) + 4 * len(plan)
     return {FMT_BF16: 2 * H, FMT_INT8: H, FMT_INT4: H // 2, FMT_INT2: H // 4, FMT_F32: 4 * H,
             FMT_MXFP4: H // 2 + H // 32, FMT_MXFP8: H + H // 32}[fmt]
 
@@ -107,6 +165,11 @@ class Layout:
     total: int        # bytes of the message buffer (the capacity when kvar)
     kvar: bool = False
     off_kvec: int = -1
+    plan: tuple | None = None   # FMT_GRP group bits (also stored in the message at off_plan, one byte each)
+    off_plan: int = -1
+
+    def row_bytes(self, fmt: int) -> int:
+        return _row_bytes(fmt, self.H, self.plan)
 
     @property
     def payload_bytes_per_token(self) -> float:
@@ -116,11 +179,11 @@ class Layout:
         """Bytes of the message proper: ``total`` for fixed k; for variable k with ``k_total`` lo rows in all."""
         if not self.kvar:
             return self.total
-        return self.off_lo + _a16(k_total * _row_bytes(self.lo_fmt, self.H)) + \
-            (self.B * self.S - k_total) * _row_bytes(self.hi_fmt, self.H)
+        return self.off_lo + _a16(k_total * self.row_bytes(self.lo_fmt)) + \
+            (self.B * self.S - k_total) * self.row_bytes(self.hi_fmt)
 
     def hi_offset(self, k_total: int) -> int:
-        return self.off_hi if not self.kvar else self.off_lo + _a16(k_total * _row_bytes(self.lo_fmt, self.H))
+        return self.off_hi if not self.kvar else self.off_lo + _a16(k_total * self.row_bytes(self.lo_fmt))
 
 
 def native_fmt(dtype: torch.dtype) -> int:
@@ -146,20 +209,32 @@ def layout(spec: CodecSpec, B: int, S: int, H: int, k: int, dtype: torch.dtype =
     nf = native_fmt(dtype)
     hi = nf if spec.hi_fmt == NATIVE else spec.hi_fmt
     lo = nf if spec.lo_fmt == NATIVE else spec.lo_fmt
+    plan = None
+    if FMT_GRP in (hi, lo):
+        if H % GROUP:
+            raise ValueError(f"head-group rows need a hidden size multiple of {GROUP}")
+        plan = spec.plan if spec.plan is not None else (4,) * (H // GROUP)
+        if len(plan) != H // GROUP:
+            raise ValueError(f"group plan has {len(plan)} entries, hidden size {H} has {H // GROUP} groups")
+    rb = lambda f: _row_bytes(f, H, plan)  # noqa: E731
     mw = 2 * ((S + 63) // 64)
     off_mask = 32
     n_scale = {SC_TOKEN: B * S, SC_WINDOW: B, SC_CHANNEL: B * H, SC_NONE: 0}[spec.scale_mode]
+    # the group plan section (one byte per group) follows the mask (and the k vector)
+    plan_bytes = _a16(len(plan)) if plan is not None else 0
     if kvar:
         off_kvec = off_mask + _a16(B * mw * 4)
-        off_scale = off_kvec + _a16(B * 4)
+        off_plan = off_kvec + _a16(B * 4) if plan is not None else -1
+        off_scale = off_kvec + _a16(B * 4) + plan_bytes
         off_lo = off_scale + _a16(n_scale * 4)
-        total = off_lo + _a16(B * S * max(_row_bytes(hi, H), _row_bytes(lo, H))) + 16
-        return Layout(B, S, H, -1, mw, hi, lo, off_mask, off_scale, -1, off_lo, total, True, off_kvec)
-    off_scale = off_mask + _a16(B * mw * 4)
+        total = off_lo + _a16(B * S * max(rb(hi), rb(lo))) + 16
+        return Layout(B, S, H, -1, mw, hi, lo, off_mask, off_scale, -1, off_lo, total, True, off_kvec, plan, off_plan)
+    off_plan = off_mask + _a16(B * mw * 4) if plan is not None else -1
+    off_scale = off_mask + _a16(B * mw * 4) + plan_bytes
     off_hi = off_scale + _a16(n_scale * 4)
-    off_lo = off_hi + _a16(B * (S - k) * _row_bytes(hi, H))
-    total = off_lo + _a16(B * k * _row_bytes(lo, H))
-    return Layout(B, S, H, k, mw, hi, lo, off_mask, off_scale, off_hi, off_lo, total)
+    off_lo = off_hi + _a16(B * (S - k) * rb(hi))
+    total = off_lo + _a16(B * k * rb(lo))
+    return Layout(B, S, H, k, mw, hi, lo, off_mask, off_scale, off_hi, off_lo, total, False, -1, plan, off_plan)
 
 
 def message_bytes(spec: CodecSpec, B: int, S: int, H: int, ratio: float, dtype=torch.bfloat16) -> int:
@@ -332,6 +407,38 @@ def _mx_unpack(b: torch.Tensor, fmt: int, n: int, H: int) -> torch.Tensor:
     return (v.reshape(n, H // 32, 32) * _e8m0(sb)[..., None]).reshape(n, H)
 
 
+def _grp_pack(rows: torch.Tensor, plan) -> torch.Tensor:
+    """FMT_GRP rows: per 64-channel group g of b_g bits, s = max|x| / qmax_b (qmax 1 / 7 / 127), codes
+    clamp(round(x * (1 / s)), -qmax, qmax) packed as int2 / int4 / int8 (csrc/codec.hip grp_pack8); then the G
+    fp32 scales."""
+    n, H = rows.shape
+    parts, scales = [], []
+    for g, b in enumerate(plan):
+        blk = rows[:, g * GROUP:(g + 1) * GROUP].float()
+        qmax = (1 << (b - 1)) - 1
+        am = blk.abs().amax(-1)
+        s = am / float(qmax)
+        inv = torch.where(am > 0, 1.0 / torch.where(am > 0, s, torch.ones_like(s)), torch.zeros_like(s))
+        q = torch.round(blk * inv[:, None]).clamp(-qmax, qmax)
+        parts.append(_pack_rows(q, {2: FMT_INT2, 4: FMT_INT4, 8: FMT_INT8}[b]).reshape(n, -1))
+        scales.append(s)
+    sc = torch.stack(scales, 1).contiguous().view(torch.uint8).reshape(n, -1)
+    return torch.cat(parts + [sc], 1).reshape(-1)
+
+
+def _grp_unpack(b: torch.Tensor, plan, n: int, H: int) -> torch.Tensor:
+    r = b.reshape(n, _row_bytes(FMT_GRP, H, plan))
+    cb = sum(8 * x for x in plan)
+    sc = r[:, cb:].contiguous().view(torch.float32).reshape(n, len(plan))
+    out, off = [], 0
+    for g, bits in enumerate(plan):
+        nb = 8 * bits
+        q = _unpack_rows(r[:, off:off + nb].contiguous(), {2: FMT_INT2, 4: FMT_INT4, 8: FMT_INT8}[bits], n, GROUP)
+        out.append(q * sc[:, g:g + 1])
+        off += nb
+    return torch.cat(out, 1)
+
+
 def _header(spec: CodecSpec, L: Layout) -> torch.Tensor:
     return torch.tensor([MAGIC, VERSION, spec.cid, L.B, L.S, L.H, -1 if L.kvar else L.k, L.hi_fmt], dtype=torch.int32)
 
@@ -346,6 +453,8 @@ def _encode_cpu(x, spec, L, lo_mask):
     if L.kvar:
         kv = lo_mask.sum(1).to(torch.int32).contiguous().view(torch.uint8)
         msg[L.off_kvec:L.off_kvec + kv.numel()] = kv
+    if L.plan is not None:
+        msg[L.off_plan:L.off_plan + len(L.plan)] = torch.tensor(L.plan, dtype=torch.uint8)
     xf = x.float().reshape(B, S, H)
     # statistics
     scales = None
@@ -353,7 +462,7 @@ def _encode_cpu(x, spec, L, lo_mask):
     if spec.scale_mode == SC_TOKEN:
         scales = torch.zeros(B, S)
         for is_lo, fmt, qmax in ((False, L.hi_fmt, spec.qmax_hi), (True, L.lo_fmt, spec.qmax_lo)):
-            if fmt in (FMT_BF16, FMT_F32) or fmt in MX_FORMATS:
+            if fmt in (FMT_BF16, FMT_F32, FMT_GRP) or fmt in MX_FORMATS:
                 continue
             sel = lo_mask if is_lo else ~lo_mask
             am = xf.abs().amax(-1)
@@ -380,6 +489,8 @@ def _encode_cpu(x, spec, L, lo_mask):
             data = rows.to(torch.bfloat16).contiguous().view(torch.uint8).reshape(-1)
         elif fmt in MX_FORMATS:
             data = _mx_pack(rows, fmt)
+        elif fmt == FMT_GRP:
+            data = _grp_pack(rows, L.plan)
         else:
             if spec.scale_mode == SC_TOKEN:
                 srow = scales[sel]
@@ -416,7 +527,7 @@ def _decode_cpu(msg, spec, L, dtype):
         if n == 0:
             continue
         off = L.off_lo if is_lo else L.hi_offset(kt)
-        nb = n * _row_bytes(fmt, H)
+        nb = n * L.row_bytes(fmt)
         raw = msg[off:off + nb]
         if fmt == FMT_F32:
             rows = raw.view(torch.float32).reshape(n, H)
@@ -424,6 +535,8 @@ def _decode_cpu(msg, spec, L, dtype):
             rows = raw.view(torch.bfloat16).reshape(n, H).float()
         elif fmt in MX_FORMATS:
             rows = _mx_unpack(raw, fmt, n, H)
+        elif fmt == FMT_GRP:
+            rows = _grp_unpack(raw, L.plan, n, H)
         else:
             q = _unpack_rows(raw, fmt, n, H)
             if spec.scale_mode == SC_TOKEN:
@@ -451,8 +564,21 @@ def _gpu_header(spec, L, device):
 
 
 def _args(spec, L):
-    return (L.off_mask, L.off_scale, L.off_hi, L.off_lo, L.off_kvec, L.B, L.S, L.H, max(L.k, 0), L.hi_fmt, L.lo_fmt,
-            spec.scale_mode, spec.qmax_hi, spec.qmax_lo, spec.ch_kind)
+    gcb = sum(8 * b for b in L.plan) if L.plan is not None else 0
+    return (L.off_mask, L.off_scale, L.off_hi, L.off_lo, L.off_kvec, L.off_plan, L.B, L.S, L.H, max(L.k, 0),
+            L.hi_fmt, L.lo_fmt, spec.scale_mode, spec.qmax_hi, spec.qmax_lo, spec.ch_kind, gcb)
+
+
+_PLAN_CACHE: dict = {}
+
+
+def _gpu_plan(L, device):
+    key = (L.plan, device)
+    t = _PLAN_CACHE.get(key)
+    if t is None:
+        t = torch.tensor(L.plan, dtype=torch.uint8).to(device)
+        _PLAN_CACHE[key] = t
+    return t
 
 
 def _encode_gpu(x, spec, L, imp, msg, mass=0.0):
@@ -461,6 +587,8 @@ def _encode_gpu(x, spec, L, imp, msg, mass=0.0):
     xf32 = int(x.dtype == torch.float32)
     st = stream()
     msg[:32].copy_(_gpu_header(spec, L, x.device))
+    if L.plan is not None:
+        msg[L.off_plan:L.off_plan + len(L.plan)].copy_(_gpu_plan(L, x.device))
     if L.kvar:
         if imp is None:
             raise ValueError("top-rho selection needs token importance")

@@ -41,6 +41,8 @@ class Params:
     num_stages: int = 1                      # pipeline stages for the distributed runner
     split_layers: list = field(default_factory=list)   # explicit stage boundaries (last layer of each stage but the last)
     head_weights: str = ""                   # path to attention_head_weights.json (weighted_importance)
+    group_relevance: str = ""                # channel_group_relevance.json (head-group codecs rgroup / mixed_rgroup_int8)
+    group_avg_bits: float = 4.0              # head-group codecs: average bits per channel of a group-quantized row
     output_dir: str = "."
     checkpoint_every: int = 1000             # windows between partial-result dumps (reference: 1000)
     resume: bool = True

@@ -22,6 +22,7 @@ import time
 
 import torch
 
+from .. import codec as C
 from ..config import Params, dump_json, resolve_device, resolve_dtype
 from ..importance import canonical, load_head_weights
 from ..models import build_model, get_config
@@ -192,6 +193,15 @@ def initial_experiment(p: Params) -> dict:
     return out
 
 
+def _default_group_relevance() -> str | None:
+    for c in ("channel_group_relevance.json", "../Relevance/channel_group_relevance.json",
+              os.path.join(os.path.dirname(__file__), "..", "..", "Experiments", "Relevance",
+                           "channel_group_relevance.json")):
+        if os.path.exists(c):
+            return c
+    return None
+
+
 def _default_head_weights() -> str | None:
     for c in ("attention_head_weights.json", "../Relevance/attention_head_weights.json",
               "../../attention_head_weights.json"):
@@ -250,12 +260,22 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
             raise FileNotFoundError("weighted_importance needs attention_head_weights.json "
                                     "(run Experiments/Relevance/main.py or set params['head_weights'])")
         hw = load_head_weights(path)
+    grel = None
+    if C.wire.needs_plan(C.get_codec(p.codec)):
+        path = p.group_relevance or _default_group_relevance()
+        if p.group_relevance and not os.path.exists(path):
+            raise FileNotFoundError(f"group_relevance {path} not found (run Experiments/Relevance/main.py)")
+        if path and os.path.exists(path):
+            with open(path) as f:
+                grel = torch.tensor(json.load(f), dtype=torch.float32)
+        else:
+            log("head-group codec without channel_group_relevance.json: every group gets the same width")
     log(f"pipeline: model={cfg.name} weights={prov} data={data_prov} stages={plan.num_stages} "
         f"boundaries={plan.boundary_layers()} world={env.world_size} codec={p.codec} windows={len(wins)}")
     results: dict = {}
     for m in methods:
         for r in p.ratios:
-            bcfg = BoundaryConfig(p.codec, float(r), m, hw)
+            bcfg = BoundaryConfig(p.codec, float(r), m, hw, group_relevance=grel, group_avg_bits=p.group_avg_bits)
             bl = list(batches(ids, wins, p.window_batch))
             t0 = time.perf_counter()
             if distributed:

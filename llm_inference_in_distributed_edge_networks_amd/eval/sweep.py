@@ -64,6 +64,8 @@ class SweepConfig:
     head_weights: torch.Tensor | None = None
     max_fork_tokens: int = 1 << 17     # cap on tokens per stacked suffix forward
     ratio_scale: float = 1.0           # Pythia 'initial' uses ratio in 0..10 meaning 0.1*ratio
+    group_relevance: object = None     # head-group codecs: [layers][H / 64] channel-group relevance (plan source)
+    group_avg_bits: float = 4.0
 
     def rows(self) -> list:
         out = []
@@ -138,6 +140,16 @@ class SweepEngine:
         imp = {(meth, L): trackers[meth].importance(L) for meth, ls in need.items() for L in ls}
         return base, saved, imp
 
+    def _spec_at(self, name: str, L: int) -> C.CodecSpec:
+        """Codec ``name`` at the boundary after layer L (relevance-allocated group plan for head-group codecs)."""
+        spec = C.get_codec(name)
+        if not C.wire.needs_plan(spec):
+            return spec
+        G = self.m.cfg.hidden_size // C.wire.GROUP
+        rel = [1.0] * G if self.sc.group_relevance is None else \
+            [float(v) for v in torch.as_tensor(self.sc.group_relevance, dtype=torch.float32)[L + 1]]
+        return C.wire.with_plan(spec, C.wire.allocate_group_bits(rel, self.sc.group_avg_bits))
+
     def _k(self, ratio, S, spec=None):
         return C.wire.num_lo(spec or self.spec, float(ratio) * self.sc.ratio_scale, S)
 
@@ -176,7 +188,7 @@ class SweepEngine:
                 xs = []
                 for key in chunk:
                     src, kk, cname = key[0], key[1], key[-1]
-                    spec = C.get_codec(cname)
+                    spec = self._spec_at(cname, L)
                     im = None if src == "all" else imp[src]
                     if kk == "top_rho":
                         xq, nbytes = C.fake_quant(saved[L], spec, B, S, key[2], importance=im, selection="top_rho")

@@ -54,7 +54,8 @@ _SIGS = {
     "edge_set_mask": [c_p, c_ll, c_i, c_i, c_i, c_p],
     "edge_channel_stats": [c_p, c_p, c_ll, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_rowmax": [c_p, c_p, c_i, c_i, c_p],
-    "edge_pack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_pack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
+                  c_i, c_p],
     "edge_lrp_attn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_lrp_rope_pack": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_swiglu_il": [c_p, c_p, c_ll, c_i, c_p],
@@ -62,7 +63,8 @@ _SIGS = {
     "edge_lrp_gelu_bwd": [c_p, c_p, c_ll, c_p],
     "edge_lrp_ln_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_ln_rstd": [c_p, c_p, c_i, c_i, c_f, c_p],
-    "edge_unpack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "edge_unpack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
+                    c_i, c_i, c_p],
     # fp32 execution mode (X6 split-bf16 GEMM operands, fp32 attention / norms / codec)
     "edge_gemm_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p, c_p],
     "edge_gemm_qkv_rope_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p],

@@ -42,10 +42,26 @@ class BoundaryConfig:
     method: str = "last_row"
     head_weights: torch.Tensor | None = None
     selection: str = "ratio"      # "ratio": int(ratio*S) least important; "top_rho": keep mass 1 - ratio
+    # head-group codecs (rgroup, mixed_rgroup_int8): channel-group relevance [layers][H / 64] of the residual stream
+    # entering each layer (channel_group_relevance.json of the relevance pass) and the average bits per channel;
+    # without a table every group gets the same width
+    group_relevance: object = None
+    group_avg_bits: float = 4.0
 
     @property
     def spec(self) -> C.CodecSpec:
         return C.get_codec(self.codec)
+
+    def spec_for(self, boundary: int | None, hidden: int) -> C.CodecSpec:
+        """The codec of the boundary after layer ``boundary``: with its relevance-allocated group plan for the
+        head-group codecs (the tensor crossing it enters layer boundary + 1)."""
+        spec = self.spec
+        if boundary is None or not C.wire.needs_plan(spec):
+            return spec
+        G = hidden // C.wire.GROUP
+        rel = [1.0] * G if self.group_relevance is None else \
+            [float(v) for v in torch.as_tensor(self.group_relevance, dtype=torch.float32)[boundary + 1]]
+        return C.wire.with_plan(spec, C.wire.allocate_group_bits(rel, self.group_avg_bits))
 
     @property
     def kvar(self) -> bool:
@@ -86,6 +102,9 @@ class StageRunner:
         # LRP head table resident on the stage's device once (no host->device copy inside a captured graph)
         hw = bcfg.head_weights
         self.head_weights = None if hw is None else torch.as_tensor(hw).to(model.device, torch.float32).contiguous()
+        H = model.cfg.hidden_size
+        self.spec_out = bcfg.spec_for(self.boundary, H)
+        self.spec_in = bcfg.spec_for(None if self.first else self.layers[0] - 1, H)
 
     def _tracker(self, S: int):
         if self.boundary is None or not self.bcfg.needs_importance(S):
@@ -118,11 +137,11 @@ class StageRunner:
         return x, imp, (tr.carry() if tr is not None else None)
 
     def encode(self, x, batch: WindowBatch, imp, out=None):
-        msg, L = C.encode(x, self.bcfg.spec, batch.B, batch.S, self.bcfg.ratio, imp, out=out,
+        msg, L = C.encode(x, self.spec_out, batch.B, batch.S, self.bcfg.ratio, imp, out=out,
                           selection=self.bcfg.selection)
         if L.kvar and not prerun_active():   # compact message payload, summed on the device (capturable, no sync)
             kt = msg[L.off_kvec:L.off_kvec + 4 * L.B].view(torch.int32).sum().to(torch.float64)
-            rl, rh = C.wire._row_bytes(L.lo_fmt, L.H), C.wire._row_bytes(L.hi_fmt, L.H)
+            rl, rh = L.row_bytes(L.lo_fmt), L.row_bytes(L.hi_fmt)
             pay = L.off_lo + torch.ceil(kt * rl / 16) * 16 + (L.B * L.S - kt) * rh
             if self.stats.kvar_bytes is None or self.stats.kvar_bytes.device != msg.device:
                 self.stats.kvar_bytes = torch.zeros((), dtype=torch.float64, device=msg.device)
@@ -147,7 +166,7 @@ class StageRunner:
         x = None
         if not self.first:
             L = self.layout_in(b)
-            x = C.decode(msg_in, self.bcfg.spec, L, self.model.dtype)
+            x = C.decode(msg_in, self.spec_in, L, self.model.dtype)
         x, imp, c = self.run(b, x, carry_in if (carry_in is not None and carry_in.numel()) else None)
         if self.last:
             return self.finish(x, b)
@@ -155,10 +174,10 @@ class StageRunner:
         return msg, (c if c is not None else torch.empty(0, device=msg.device))
 
     def layout_in(self, batch) -> C.Layout:
-        return self.layout(batch)
+        return self.layout(batch, self.spec_in)
 
-    def layout(self, batch: WindowBatch) -> C.Layout:
-        spec = self.bcfg.spec
+    def layout(self, batch: WindowBatch, spec: C.CodecSpec | None = None) -> C.Layout:
+        spec = self.spec_out if spec is None else spec
         if self.bcfg.kvar:
             return C.layout(spec, batch.B, batch.S, self.model.cfg.hidden_size, -1, self.model.dtype, kvar=True)
         k = C.wire.num_lo(spec, self.bcfg.ratio, batch.S)

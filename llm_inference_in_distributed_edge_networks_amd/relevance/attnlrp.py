@@ -106,13 +106,14 @@ def _lin(x, w, b=None):
     return y + b if b is not None else y
 
 
-def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32, keep_probs: bool = True):
+def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32, keep_probs: bool = True, keep_x: bool = False):
     """Differentiable forward with AttnLRP rules.
 
-    Returns (logits_last [V], embeds, per-layer tensors): the attention probabilities A (S x S per head,
-    ``keep_probs``) or the per-head attention outputs O = A V (S x D per head).  Under the uniform rule
-    on A V, dA = 0.5 dO V^T, hence sum_ij A_ij dA_ij = 0.5 sum_i dO_i . O_i: the head relevance needs
-    only O and its gradient - an S/D-times smaller tensor than A (8x at S=512)."""
+    Returns (logits_last [B, V], embeds, per-layer tensors[, layer inputs]): the attention probabilities A
+    (S x S per head, ``keep_probs``) or the per-head attention outputs O = A V (S x D per head).  Under the
+    uniform rule on A V, dA = 0.5 dO V^T, hence sum_ij A_ij dA_ij = 0.5 sum_i dO_i . O_i: the head relevance
+    needs only O and its gradient - an S/D-times smaller tensor than A (8x at S=512).  ``keep_x`` also returns
+    the residual stream entering every layer (gradients retained: the boundary-channel relevance)."""
     cfg = model.cfg
     f = lambda t: None if t is None else t.to(dtype)  # noqa: E731
     B, S = ids.shape
@@ -121,7 +122,12 @@ def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32, keep_probs: bool 
     x = emb
     cos, sin = model.cos[:S].to(dtype), model.sin[:S].to(dtype)
     probs = []
+    xs = []
     for L in model.layers:
+        if keep_x:
+            if x is not emb:
+                x.retain_grad()
+            xs.append(x)
         if cfg.arch == "qwen2":
             h = _rmsnorm_id(x, f(L["ln1_w"]), cfg.norm_eps)
         else:
@@ -160,6 +166,8 @@ def lrp_forward(model, ids: torch.Tensor, dtype=torch.float32, keep_probs: bool 
     else:
         hN = _layernorm_id(last, f(model.w["norm_w"]), f(model.w["norm_b"]), cfg.norm_eps)
     logits = _lin(hN, f(model.w["head"]))
+    if keep_x:
+        return logits, emb, probs, xs
     return logits, emb, probs
 
 
@@ -176,6 +184,25 @@ def head_relevance(model, ids: torch.Tensor, dtype=torch.float32, via_probs: boo
     rel = torch.stack([scale * (T * T.grad).sum(dim=(0, 2, 3)) for T in probs]).detach()
     in_rel = (emb * emb.grad).sum().detach()
     return rel, in_rel, mx.detach()
+
+
+def head_relevance_batched(model, ids: torch.Tensor, dtype=torch.float32, group: int = 64):
+    """``head_relevance`` for B windows at once (windows are independent: each seeds its own max logit), plus the
+    relevance of the residual stream entering every layer per ``group``-channel block (head-sized groups):
+    chan[b, l, g] = sum over tokens and the group's channels of |x * dx| (LRP Gradient x Input, magnitude: the
+    bit-allocation signal of the head-group boundary codec).  Returns (rel [B, layers, heads], in_rel [B],
+    seed logit [B], chan [B, layers, H / group]).  Plain PyTorch ops (autograd, library GEMMs): the reference-
+    precision path of the offline calibration on any device."""
+    B, S = ids.shape
+    with torch.enable_grad():
+        logits, emb, outs, xs = lrp_forward(model, ids, dtype, keep_probs=False, keep_x=True)
+        mx = logits.max(-1).values
+        torch.autograd.backward(mx, grad_tensors=mx.detach())
+    rel = torch.stack([0.5 * (T * T.grad).sum(dim=(2, 3)) for T in outs], 1).detach()
+    in_rel = (emb * emb.grad).view(B, S, -1).sum((1, 2)).detach()
+    H = emb.shape[-1]
+    chan = torch.stack([(x * x.grad).abs().view(B, S, H // group, group).sum((1, 3)) for x in xs], 1).detach()
+    return rel.float(), in_rel.float(), mx.detach().float(), chan.float()
 
 
 def normalize_per_layer(rel: torch.Tensor) -> torch.Tensor:
@@ -198,34 +225,45 @@ def relevance_main(p) -> list:
     env = init_distributed(p.device)
     device = str(env.device)
     cfg = get_config(p.model or "qwen2-0.5b")
-    # the explicit LRP engine's GPU kernels (csrc/lrp.hip) are bf16: dtype "auto" picks bf16 on the GPU for this
-    # offline calibration, fp32 on the CPU oracle path
-    dtype = torch.bfloat16 if (device.startswith("cuda") and p.dtype == "auto") else resolve_dtype(p, device)
-    if device.startswith("cuda") and dtype == torch.float32:
-        raise NotImplementedError("the GPU LRP engine runs bf16 (dtype: bf16 or auto); fp32 relevance runs on CPU")
+    # engine: the reference's precision (fp32, "auto") runs the AttnLRP rules as autograd on plain PyTorch ops
+    # (head_relevance_batched); dtype "bf16" on the GPU runs the explicit-backward HIP engine (csrc/lrp.hip, ~10x
+    # faster, bf16 storage: head table within ~10 % of the fp32 one, tests/test_lrp_gpu.py)
+    dtype = resolve_dtype(p, device) if p.dtype != "auto" else torch.float32
+    fast = device.startswith("cuda") and dtype == torch.bfloat16
     model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed)
     ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed,
                                   strict=p.strict_data)
     wins = sliding_windows(ids.shape[1], p.max_length or 512, p.stride)
     if p.max_windows:
         wins = wins[: p.max_windows]
-    log(f"relevance: model={cfg.name} weights={prov} data={data_prov} windows={len(wins)}")
+    log(f"relevance: model={cfg.name} weights={prov} data={data_prov} windows={len(wins)} "
+        f"engine={'hip-bf16' if fast else 'autograd-' + str(dtype).replace('torch.', '')}")
     from ..eval.windows import batches
     from .engine import RelevanceEngine
-    eng = RelevanceEngine(model)
+    eng = RelevanceEngine(model) if fast else None
+    G = cfg.hidden_size // 64
     acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=device)
+    cacc = torch.zeros(cfg.num_layers, G, dtype=torch.float64, device=device)
     pb = progress_bar(len(wins), env.is_main)
     for bi, b in enumerate(batches(ids, wins, max(1, p.window_batch))):
         if bi % env.world_size != env.rank:
             continue
-        rel, _, _ = eng.head_relevance(b.ids)
+        if fast:
+            rel, _, _, chan = eng.head_relevance(b.ids, want_channels=True)
+        else:
+            rel, _, _, chan = head_relevance_batched(model, b.ids.to(device), dtype)
         acc += rel.double().sum(0)
+        cacc += chan.double().sum(0)
         pb.update(b.B * env.world_size)
     pb.close()
     all_reduce_sum(acc)
+    all_reduce_sum(cacc)
     weights = normalize_per_layer(acc).float().cpu().tolist()
+    chan_w = normalize_per_layer(cacc).float().cpu().tolist()
     if env.is_main:
         out = os.path.join(p.output_dir, "attention_head_weights.json")
         dump_json(weights, out)
-        log(f"wrote {out}")
+        cout = os.path.join(p.output_dir, "channel_group_relevance.json")
+        dump_json(chan_w, cout)
+        log(f"wrote {out} and {cout}")
     return weights

@@ -59,7 +59,7 @@ class RelevanceEngine:
         saves = []
         for i, L in enumerate(m.layers):
             t = self.T[i]
-            sv = {}
+            sv = {"x": x}
             if self.qwen:
                 ssq1 = ops.row_ssq(x)
                 sv["rs1"] = ops.row_rscale(ssq1, H, cfg.norm_eps)
@@ -112,9 +112,11 @@ class RelevanceEngine:
         return dx, mx
 
     @torch.no_grad()
-    def head_relevance(self, ids: torch.Tensor):
+    def head_relevance(self, ids: torch.Tensor, want_channels: bool = False, group: int = 64):
         """ids [B, S] (B windows of equal length) -> (rel [B, layers, heads] fp32, input relevance [B],
-        seed logit [B]).  rel[b, l, h] = sum_{i,j} A_ij dA_ij of head h, layer l, window b."""
+        seed logit [B][, chan [B, layers, H / group]]).  rel[b, l, h] = sum_{i,j} A_ij dA_ij of head h, layer l,
+        window b; chan (``want_channels``) = sum over tokens and the group's channels of |x * dx| of the residual
+        stream entering layer l (as ``attnlrp.head_relevance_batched``)."""
         m, cfg = self.m, self.m.cfg
         ids = ids.to(m.device)
         B, S = ids.shape
@@ -122,6 +124,9 @@ class RelevanceEngine:
         emb, x, saves = self._forward(ids)
         dx, mx = self._seed(x, B, S)
         rel = torch.zeros(B, cfg.num_layers, Hq, dtype=torch.float32, device=m.device)
+        H = cfg.hidden_size
+        chan = torch.zeros(B, cfg.num_layers, H // group, dtype=torch.float32, device=m.device) if want_channels \
+            else None
         for i in range(cfg.num_layers - 1, -1, -1):
             L, t, sv = m.layers[i], self.T[i], saves[i]
             if self.qwen:
@@ -140,6 +145,10 @@ class RelevanceEngine:
             else:
                 dh1 = ops.linear(dqkv, t["wqkvT"])
                 dx = ops.lrp_ln_bwd(dh1, sv["rs1"], L["ln1_w"], dh2, sv["rs1"], L["ln2_w"], dx)
+            if want_channels:
+                chan[:, i] = (sv["x"].float() * dx.float()).abs().view(B, S, H // group, group).sum((1, 3))
             saves[i] = None
         in_rel = (emb.float() * dx.float()).view(B, S, -1).sum((1, 2))
+        if want_channels:
+            return rel, in_rel, mx, chan
         return rel, in_rel, mx

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo BUILD_FAIL; tail gpurun_out/build.log; exit 1; }
 (cd Experiments/Relevance && timeout -k 10 300 python main.py --max-windows 64 > $R/gpurun_out/configs/relevance.log 2>&1) || { echo RELEVANCE_FAIL; tail $R/gpurun_out/configs/relevance.log; exit 1; }
-echo "[relevance] ok"; cp Experiments/Relevance/attention_head_weights.json gpurun_out/configs/
+echo "[relevance] ok"; cp Experiments/Relevance/attention_head_weights.json Experiments/Relevance/channel_group_relevance.json gpurun_out/configs/
 cd Experiments/Pipeline
 for c in configs/config2_*.json configs/config3_*.json configs/config4_*.json configs/config5_*.json; do
   n=$(basename $c .json)

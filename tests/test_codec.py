@@ -212,3 +212,48 @@ def test_mx_codecs_error_and_bytes(codec):
     if codec == "mxfp4":
         yt, _ = C.fake_quant(x, C.get_codec("int4_token"), B, S, 1.0, imp)
         assert err < ((yt - x) ** 2).mean() / (x ** 2).mean()
+
+
+def test_group_bits_allocation():
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import allocate_group_bits
+    rel = [0.30, 0.01, 0.20, 0.02, 0.25, 0.01, 0.10, 0.11]
+    bits = allocate_group_bits(rel, 4.0)
+    assert sum(bits) == 4 * len(rel) and set(bits) <= {2, 4, 8}
+    order = sorted(range(len(rel)), key=lambda g: -rel[g])
+    # more relevant groups never get fewer bits than less relevant ones
+    assert all(bits[order[i]] >= bits[order[i + 1]] for i in range(len(rel) - 1)), bits
+    assert allocate_group_bits([1.0] * 14, 4.0) == (4,) * 14
+    assert allocate_group_bits([0.0] * 6, 2.0) == (2,) * 6
+    assert sum(allocate_group_bits(rel, 3.0)) <= 3 * len(rel)
+
+
+@pytest.mark.parametrize("name", ["rgroup", "mixed_rgroup_int8"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_group_codec_roundtrip(name, dtype):
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import with_plan
+    B, S, H = 2, 48, 256
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(B * S, H, generator=g) * 2).to(dtype)
+    x[:, 64:128] *= 10          # a loud group
+    imp = torch.rand(B, S, generator=g)
+    plan = (8, 2, 4, 4)
+    spec = with_plan(C.get_codec(name), plan)
+    msg, L = C.encode(x, spec, B, S, 0.5, imp)
+    assert L.plan == plan and L.total == msg.numel()
+    assert bytes(msg[L.off_plan:L.off_plan + 4].tolist()) == bytes(plan)
+    y = C.decode(msg, spec, L, torch.float32)
+    xf = x.float()
+    lo = torch.ones(B * S, dtype=torch.bool) if name == "rgroup" else C.wire.select_mask(imp, S // 2).reshape(-1)
+    for gi, b in enumerate(plan):
+        blk = slice(64 * gi, 64 * gi + 64)
+        qmax = (1 << (b - 1)) - 1
+        step = xf[lo][:, blk].abs().amax(-1, keepdim=True) / qmax
+        assert ((y[lo][:, blk] - xf[lo][:, blk]).abs() <= step / 2 + 1e-6).all(), gi
+    if name == "mixed_rgroup_int8":
+        step = xf[~lo].abs().amax(-1, keepdim=True) / 127
+        assert ((y[~lo] - xf[~lo]).abs() <= step / 2 + 1e-6).all()
+    # row bytes: codes 8 * sum(bits) + 4 scale bytes per group
+    assert L.row_bytes(C.wire.FMT_GRP) == 8 * sum(plan) + 16
+    # default plan without relevance: 4 bits everywhere
+    L4 = C.layout(C.get_codec(name), B, S, H, S // 2 if name != "rgroup" else 0, dtype)
+    assert L4.plan == (4, 4, 4, 4)

@@ -62,6 +62,15 @@ def test_qwen2_importance_and_relevance(tmp_path):
                                  "head_weights": str(d / "attention_head_weights.json")}, tmp_path)
     res = json.loads((d2 / "avg_ppl_results.json").read_text())
     assert len(res["avg_ppl_results"]) == 4 and res["wire_bytes_per_token"][0][0][2] < res["wire_bytes_per_token"][0][0][0]
+    # the relevance pass also writes the channel-group table; the config-5 pipeline uses it for its group plans
+    gr = json.loads((d / "channel_group_relevance.json").read_text())
+    assert len(gr) == 4 and len(gr[0]) == 4 and all(abs(sum(r) - 1) < 1e-3 for r in gr)
+    d3 = run_main("Pipeline", {"model": "tiny-qwen2", "num_stages": 2, "codec": "mixed_rgroup_int8",
+                               "methods": ["weighted_importance"], "ratios": [0, 1], "max_length": 64,
+                               "head_weights": str(d / "attention_head_weights.json"),
+                               "group_relevance": str(d / "channel_group_relevance.json")}, tmp_path)
+    res = json.loads((d3 / "pipeline_results.json").read_text())["results"]["weighted_importance"]
+    assert res["1"]["wire_bytes_per_token"] < res["0"]["wire_bytes_per_token"]
 
 
 def test_qwen2_channel(tmp_path):

@@ -43,6 +43,16 @@ def test_relevance_then_weighted_pipeline_and_sweep(tmp_path):
                                 "head_weights": hwp}, tmp_path)
     sweep = json.loads((q / "avg_ppl_results.json").read_text())["avg_ppl_results"]
     assert len(sweep) == 2 and all(v > 0 for row in sweep for r in row for v in r)
+    # config 5 style: relevance-weighted importance + the head-group codec with the LRP channel-group plans
+    grp = str(d / "channel_group_relevance.json")
+    gr = json.loads(open(grp).read())
+    assert len(gr) == 4 and all(len(r) == 256 // 64 for r in gr)
+    g = run_main("Pipeline", {"model": "tiny-qwen2", "num_stages": 3, "codec": "mixed_rgroup_int8",
+                              "methods": ["weighted_importance"], "ratios": [0, 0.5, 1], "max_length": 128,
+                              "head_weights": hwp, "group_relevance": grp, "group_avg_bits": 3}, tmp_path,
+                 name="Pipeline_rgroup")
+    res = json.loads((g / "pipeline_results.json").read_text())["results"]["weighted_importance"]
+    assert res["1"]["wire_bytes_per_token"] < res["0"]["wire_bytes_per_token"] and res["1"]["ppl"] > 0
 
 
 def test_pythia_entry_point_gpu(tmp_path):

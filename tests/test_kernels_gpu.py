@@ -383,3 +383,29 @@ def test_gemm_eight_phase(M, N, K, epi, tile):
         _gemm_case(M, N, K, epi)
     finally:
         ops.set_gemm_config("0")
+
+
+@pytest.mark.parametrize("name", ["rgroup", "mixed_rgroup_int8"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_group_codec_gpu_equals_cpu(name, dtype):
+    """Head-group rows with a non-uniform relevance plan: GPU message bytes == CPU oracle bytes (fp32
+    activations; bf16 activations: same bytes from the bf16-rounded input), decode equal."""
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import allocate_group_bits, with_plan
+    B, S, H = 3, 200, 896
+    x = (rnd(B * S, H, seed=60) * 2).to(dtype)
+    x[:, 128:192] *= 30
+    imp = torch.rand(B, S, generator=torch.Generator().manual_seed(61))
+    rel = torch.rand(H // 64, generator=torch.Generator().manual_seed(62)).tolist()
+    spec = with_plan(C.get_codec(name), allocate_group_bits(rel, 4.0))
+    assert len(set(spec.plan)) > 1
+    m_cpu, L = C.encode(x.float(), spec, B, S, 0.4, imp)
+    m_gpu, L2 = C.encode(x.to(DEV), spec, B, S, 0.4, imp.to(DEV))
+    assert L2.plan == L.plan
+    if dtype == torch.float32:
+        assert torch.equal(m_gpu.cpu(), m_cpu)
+    y_cpu = C.decode(m_cpu, spec, L, torch.float32)
+    y_gpu = C.decode(m_gpu, spec, L2, torch.float32).cpu()
+    if dtype == torch.float32:
+        assert torch.equal(y_gpu, y_cpu)
+    else:
+        assert (y_gpu - y_cpu).abs().max() <= 1e-5 * y_cpu.abs().max() + 1e-6

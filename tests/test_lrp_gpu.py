@@ -96,3 +96,28 @@ def test_relevance_engine_gpu_vs_cpu(cfg):
     # the calibrated table (normalised per layer over all windows) is what weighted_importance consumes
     wg, wc = rg.sum(0), rc.sum(0)
     assert rel_err(wg / wg.sum(-1, keepdim=True), wc / wc.sum(-1, keepdim=True)) < 0.1
+
+
+def test_fp32_calibration_table_matches_cpu_full_qwen2():
+    """The reference-precision calibration (dtype fp32 / auto: AttnLRP as autograd on the GPU) on the full
+    24-layer Qwen2-0.5B shape: normalised head table within 2 % (relative L2) of the CPU fp32 oracle on the same
+    random weights and windows, and the channel-group relevance too; the bf16 HIP engine's deviation is printed."""
+    from llm_inference_in_distributed_edge_networks_amd.models import get_config
+    from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import (head_relevance_batched,
+                                                                                  normalize_per_layer)
+    from llm_inference_in_distributed_edge_networks_amd.relevance.engine import RelevanceEngine
+    cfg = get_config("qwen2-0.5b")
+    mc = DecoderLM.random_init(cfg, 7, std=0.02)
+    mg = DecoderLM.random_init(cfg, 7, device=DEV, std=0.02, x6=False)
+    ids = torch.randint(0, cfg.vocab_size, (2, 128), generator=torch.Generator().manual_seed(3))
+    rc, _, _, cc = head_relevance_batched(mc, ids)
+    rg, _, _, cg = head_relevance_batched(mg, ids.to(DEV))
+    tc, tg = normalize_per_layer(rc.sum(0)), normalize_per_layer(rg.sum(0))
+    e_head = rel_err(tg, tc)
+    e_chan = rel_err(normalize_per_layer(cg.sum(0)), normalize_per_layer(cc.sum(0)))
+    mb = DecoderLM.random_init(cfg, 7, device=DEV, dtype=torch.bfloat16, std=0.02)
+    rb, _, _ = RelevanceEngine(mb).head_relevance(ids.to(DEV))
+    e_bf16 = rel_err(normalize_per_layer(rb.sum(0)), tc)
+    print(f"normalised head table vs CPU fp32: fp32 GPU {e_head:.2e}, bf16 HIP engine {e_bf16:.2e}; "
+          f"channel groups {e_chan:.2e}")
+    assert e_head < 0.02 and e_chan < 0.02

@@ -88,3 +88,24 @@ def test_lrp_reference_ops_match_autograd():
     assert torch.allclose(dq, qa.grad, rtol=1e-4, atol=1e-5)
     assert torch.allclose(dk.view(B, Hkv, 2, S, D).sum(2), ka.grad, rtol=1e-4, atol=1e-5)
     assert torch.allclose(dv.view(B, Hkv, 2, S, D).sum(2), va.grad, rtol=1e-4, atol=1e-5)
+
+
+def test_batched_autograd_and_channel_relevance():
+    """head_relevance_batched (the fp32 calibration path on any device) == per-window head_relevance, and its
+    channel-group relevance == the explicit engine's (want_channels)."""
+    from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import head_relevance_batched
+    from llm_inference_in_distributed_edge_networks_amd.relevance.engine import RelevanceEngine
+    for cfg in (TINY_QWEN2, TINY_NEOX):
+        m = DecoderLM.random_init(cfg, 4, std=0.05)
+        ids = torch.randint(0, cfg.vocab_size, (3, 48), generator=torch.Generator().manual_seed(2))
+        rel, in_rel, mx, chan = head_relevance_batched(m, ids)
+        G = cfg.hidden_size // 64
+        assert chan.shape == (3, cfg.num_layers, G) and (chan >= 0).all() and (chan.sum(-1) > 0).all()
+        for b in range(3):
+            r0, in0, mx0 = head_relevance(m, ids[b:b + 1])
+            assert torch.allclose(rel[b], r0, rtol=1e-4, atol=1e-5)
+            assert abs(float(in_rel[b]) - float(in0)) < 1e-3 * max(1.0, abs(float(in0)))
+            assert abs(float(mx[b]) - float(mx0)) < 1e-4
+        rel_e, _, _, chan_e = RelevanceEngine(m).head_relevance(ids, want_channels=True)
+        assert torch.allclose(rel_e, rel, rtol=1e-4, atol=1e-5)
+        assert torch.allclose(chan_e, chan, rtol=1e-4, atol=1e-6)

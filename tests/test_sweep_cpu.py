@@ -83,3 +83,28 @@ def test_initial_rows_batched_equals_per_window():
     assert torch.allclose(a, b, atol=2e-5), (a - b).abs().max()
     # ratio 10 with top-rho: mass 0 -> every token quantized == the ratio-form ratio 10
     assert abs(a[3, 0, 3] - a[0, 0, 3]) < 1e-6
+
+
+def test_sweep_group_codec_equals_split_runner():
+    """Head-group codec with relevance-allocated plans (per boundary layer): sweep engine == pipeline runtime, and
+    the plans differ between boundaries when the relevance does."""
+    G = TINY_QWEN2.hidden_size // 64
+    grel = torch.rand(TINY_QWEN2.num_layers, G, generator=torch.Generator().manual_seed(3))
+    grel[1] = torch.tensor([1.0] + [0.02] * (G - 1))    # one dominant group: 8 bits for it, 2 for some others
+    sc = SweepConfig(["regular_importance"], [0, 2], [0.5, 1], codec="mixed_rgroup_int8", group_relevance=grel,
+                     group_avg_bits=4.0)
+    eng = SweepEngine(M, sc)
+    res = run_sweep(eng, batches(TOK, WINS, 4))
+    for li, L in enumerate([0, 2]):
+        for ri, r in enumerate([0.5, 1]):
+            bc = BoundaryConfig("mixed_rgroup_int8", r, "regular_importance", group_relevance=grel, group_avg_bits=4.0)
+            pipe = LocalPipeline(M, PipelinePlan.from_split_layers(4, [L]), bc)
+            assert pipe.stages[0].spec_out.plan == eng._spec_at("mixed_rgroup_int8", L).plan
+            ppl = pipe.evaluate(batches(TOK, WINS, 4)).ppl()
+            assert abs(ppl - res["avg_ppl_results"][0][li][ri]) / ppl < 1e-6, (L, r)
+    assert eng._spec_at("mixed_rgroup_int8", 0).plan == (8, 4, 2, 2)
+    # 3 stages: each boundary decodes with the plan its sender used
+    bc = BoundaryConfig("mixed_rgroup_int8", 0.5, "regular_importance", group_relevance=grel)
+    pipe = LocalPipeline(M, PipelinePlan.from_split_layers(4, [0, 2]), bc)
+    assert pipe.stages[1].spec_in.plan == pipe.stages[0].spec_out.plan
+    assert pipe.evaluate(batches(TOK, WINS, 4)).ppl() > 0

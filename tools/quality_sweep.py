@@ -56,23 +56,37 @@ def main():
     wins = sliding_windows(tr.shape[1], 512, 512)[: a.relevance_windows]
     eng = RelevanceEngine(m_rel)
     acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=dev)
+    cacc = torch.zeros(cfg.num_layers, cfg.hidden_size // 64, dtype=torch.float64, device=dev)
     for b in batches(tr, wins, a.batch):
-        rel, _, _ = eng.head_relevance(b.ids)
+        rel, _, _, chan = eng.head_relevance(b.ids, want_channels=True)
         acc += rel.double().sum(0)
+        cacc += chan.double().sum(0)
     hw = normalize_per_layer(acc).float().cpu()
+    grel = normalize_per_layer(cacc).float().cpu()     # channel-group relevance: the head-group codecs' bit plans
     print(f"relevance: {len(wins)} windows in {time.time() - t0:.1f}s", flush=True)
 
     ev = local_text_bytes("eval")
     wins = sliding_windows(ev.shape[1], 512, 32)[: a.windows]
     out = {"model": cfg.name, "weights": a.weights, "dtype": a.dtype if dev == "cuda" else "fp32", "data": f"python-stdlib-bytes/eval, {len(wins)} windows "
            "(max_length 512, stride 32)", "methods": METHODS, "layers": layers, "ratios": ratios,
-           "head_weights": hw.tolist(), "codecs": {}}
+           "head_weights": hw.tolist(), "channel_group_relevance": grel.tolist(), "codecs": {}}
     for codec in a.codecs.split(","):
         t0 = time.time()
-        sc = SweepConfig(METHODS, layers, ratios, codec=codec, head_weights=hw)
+        # head-group codecs: "name@bits" = relevance-allocated plans of that average width, "name@bitsu" = the
+        # same width in every group (uniform plan, the ablation)
+        base, _, bits = codec.partition("@")
+        uniform = bits.endswith("u")
+        avg = float(bits.rstrip("u") or 4.0)
+        sc = SweepConfig(METHODS, layers, ratios, codec=base, head_weights=hw,
+                         group_relevance=None if uniform else grel, group_avg_bits=avg)
         res = run_sweep(SweepEngine(m, sc), batches(ev, wins, a.batch))
         out["codecs"][codec] = {"avg_ppl_results": res["avg_ppl_results"],
                                 "wire_bytes_per_token": res["wire_bytes_per_token"], "seconds": res["seconds"]}
+        if C.wire.needs_plan(C.get_codec(base)):
+            eng_ = SweepEngine(m, sc)
+            plans = {L: list(eng_._spec_at(base, L).plan) for L in layers}
+            out["codecs"][codec]["group_plans"] = plans
+            print("group plans: " + "; ".join(f"layer {L}: {''.join(str(b) for b in p)}" for L, p in plans.items()))
         print(f"\n### {codec}  ({time.time() - t0:.1f}s)\n", flush=True)
         print("| method | layer | " + " | ".join(f"{r:g}" for r in ratios) + " |")
         print("|---|---|" + "---|" * len(ratios))
