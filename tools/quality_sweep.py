@@ -82,11 +82,6 @@ def main():
         res = run_sweep(SweepEngine(m, sc), batches(ev, wins, a.batch))
         out["codecs"][codec] = {"avg_ppl_results": res["avg_ppl_results"],
                                 "wire_bytes_per_token": res["wire_bytes_per_token"], "seconds": res["seconds"]}
-        if C.wire.needs_plan(C.get_codec(base)):
-            eng_ = SweepEngine(m, sc)
-            plans = {L: list(eng_._spec_at(base, L).plan) for L in layers}
-            out["codecs"][codec]["group_plans"] = plans
-            print("group plans: " + "; ".join(f"layer {L}: {''.join(str(b) for b in p)}" for L, p in plans.items()))
         print(f"\n### {codec}  ({time.time() - t0:.1f}s)\n", flush=True)
         print("| method | layer | " + " | ".join(f"{r:g}" for r in ratios) + " |")
         print("|---|---|" + "---|" * len(ratios))
@@ -96,6 +91,12 @@ def main():
                 print(f"| {meth} | {L} | " + " | ".join(f"{v:.4f}" if v < 1e4 else f"{v:.3g}" for v in row) + " |")
         bpt = res["wire_bytes_per_token"][0][0]
         print("wire B/token per ratio: " + ", ".join(f"{b:.1f}" for b in bpt), flush=True)
+        if C.wire.needs_plan(C.get_codec(base)):
+            eng_ = SweepEngine(m, sc)
+            plans = {L: list(eng_._spec_at(base, L).plan) for L in layers}
+            out["codecs"][codec]["group_plans"] = plans
+            print("group plans: " + "; ".join(f"layer {L}: {''.join(str(b) for b in p)}" for L, p in plans.items()))
+
     os.makedirs(os.path.dirname(os.path.abspath(a.json_out)), exist_ok=True)
     with open(a.json_out, "w") as f:
         json.dump(out, f, indent=1)
