@@ -12,7 +12,7 @@
 //   attn_colsum_f32    : sum_i P[i, j] per head from Q, K and the row LSE (second sweep, key block outer).
 //
 // Layouts as the bf16 kernels (attention.hip): q [B,Hq,S,64] (RoPE applied, pre-scaled), k [B,Hkv,S,64],
-// vt [B,Hkv,64,s_pad] (V^T, zero padded), o [B*S, Hq*64] (fp32) or [B*S, 6*Hq*64] (X6).
+// vt [B,Hkv,64,s_pad] (V^T, zero padded), o [B*S, Hq*64] (fp32) or [B*S, 3*Hq*64] (3-plane X6).
 //
 // 16x16x4 f32 MFMA operand layout: lane l supplies A[m = l&15][k = l>>4] and B[k = l>>4][n = l&15]; the result
 // D[m][n] sits in lane l, register r at m = 4(l>>4) + r, n = l&15.  The contraction index k of MFMA number kk is
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_fwd_f32_kernel(const float*
     const float inv = 1.f / l_run;
     const int W = Hq * 64;
     if constexpr (X6OUT) {
-      bf16_t* orow = (bf16_t*)o + ((size_t)b * S + qrow) * (size_t)(X6_TERMS * W);
+      bf16_t* orow = (bf16_t*)o + ((size_t)b * S + qrow) * (size_t)(3 * W);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
@@ -315,7 +315,8 @@ __global__ __launch_bounds__(256) void attn_colsum_f32_kernel(const float* __res
   }
 }
 
-// out_x6 != 0: O in the X6 layout [B*S, 6*Hq*64] (bf16 planes) for the O-projection; else fp32 [B*S, Hq*64].
+// out_x6 != 0: O as a 3-plane X6 activation [B*S, 3*Hq*64] (bf16 planes) for the O-projection; else fp32
+// [B*S, Hq*64].
 EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float* vt, void* o, float* lse,
                                      const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, int out_x6,
                                      hipStream_t st) {

@@ -28,10 +28,11 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 // x = x0 + x1 + x2 exactly, each a bf16 (8 significant bits; the residual after two round-to-nearest steps has at
 // most 8 significant bits left).  A product x*y is then sum_{i+j<=2} xi*yj up to terms of relative size 2^-27,
 // below fp32's own rounding (2^-24), and every bf16 x bf16 product is exact in the fp32 MFMA accumulator.
-// The six terms are laid out as a K-concatenation, so an ordinary bf16 MFMA GEMM over K' = 6K computes the
-// fp32-accurate product:  A' row = [a2 | a0 | a1 | a1 | a0 | a0],  B' row = [b0 | b2 | b1 | b0 | b1 | b0]
-// (the small terms first: they are accumulated before the large ones).  X6_APLANE / X6_BPLANE give the plane
-// of each K-block.  Activations that feed a GEMM are stored in this "X6" layout [rows, 6K] by their producer.
+// The six terms are a K-concatenation, so an ordinary bf16 MFMA GEMM over K' = 6K computes the fp32-accurate
+// product with the K-blocks  A' = [a2 | a0 | a1 | a1 | a0 | a0],  B' = [b0 | b2 | b1 | b0 | b1 | b0]
+// (the small terms first: they are accumulated before the large ones).  Weights are stored as B' [N, 6K]; an
+// activation is stored once per plane, [a0 | a1 | a2] ([rows, 3K], half the bytes of A'), and the GEMM's A loader
+// reads K-block j of A' from plane x6_aplane(j) (x6_acol).
 constexpr int X6_TERMS = 6;
 __device__ __forceinline__ void split3(float x, float& p0, float& p1, float& p2) {
   p0 = (float)(__bf16)x;
@@ -39,41 +40,36 @@ __device__ __forceinline__ void split3(float x, float& p0, float& p1, float& p2)
   p1 = (float)(__bf16)r;
   p2 = (float)(__bf16)(r - p1);
 }
-// Store 4 consecutive values v[0..3] at column `col` of an X6 row (block width K): six 8-byte stores.
+// column of the 3-plane activation row holding column kp of A' (K = plane width; K-blocks never straddle a K-tile)
+__device__ __forceinline__ int x6_acol(int kp, int K) {
+  const int j = kp / K;                          // A' block 0..5, planes 2 0 1 1 0 0
+  return ((0x1102 >> (4 * j)) & 3) * K + (kp - j * K);
+}
+// Store 4 consecutive values v[0..3] at column `col` of an X6 activation row (plane width K): three 8-byte stores.
 __device__ __forceinline__ void store_x6_4(bf16_t* __restrict__ row, int K, int col, const float (&v)[4]) {
   float p[3][4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) split3(v[e], p[0][e], p[1][e], p[2][e]);
-  u32x2_t w[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    w[i][0] = pack_bf2(p[i][0], p[i][1]);
-    w[i][1] = pack_bf2(p[i][2], p[i][3]);
+    u32x2_t w;
+    w[0] = pack_bf2(p[i][0], p[i][1]);
+    w[1] = pack_bf2(p[i][2], p[i][3]);
+    *(u32x2_t*)(row + i * (size_t)K + col) = w;
   }
-  // A-side plane order of the six K-blocks: 2 0 1 1 0 0
-  *(u32x2_t*)(row + 0 * (size_t)K + col) = w[2];
-  *(u32x2_t*)(row + 1 * (size_t)K + col) = w[0];
-  *(u32x2_t*)(row + 2 * (size_t)K + col) = w[1];
-  *(u32x2_t*)(row + 3 * (size_t)K + col) = w[1];
-  *(u32x2_t*)(row + 4 * (size_t)K + col) = w[0];
-  *(u32x2_t*)(row + 5 * (size_t)K + col) = w[0];
 }
-// 8 consecutive values: six 16-byte stores.
+// 8 consecutive values: three 16-byte stores.
 __device__ __forceinline__ void store_x6_8(bf16_t* __restrict__ row, int K, int col, const float (&v)[8]) {
   float p[3][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) split3(v[e], p[0][e], p[1][e], p[2][e]);
-  u32x4_t w[3];
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < 3; ++i) {
+    u32x4_t w;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) w[i][e] = pack_bf2(p[i][2 * e], p[i][2 * e + 1]);
-  *(u32x4_t*)(row + 0 * (size_t)K + col) = w[2];
-  *(u32x4_t*)(row + 1 * (size_t)K + col) = w[0];
-  *(u32x4_t*)(row + 2 * (size_t)K + col) = w[1];
-  *(u32x4_t*)(row + 3 * (size_t)K + col) = w[1];
-  *(u32x4_t*)(row + 4 * (size_t)K + col) = w[0];
-  *(u32x4_t*)(row + 5 * (size_t)K + col) = w[0];
+    for (int e = 0; e < 4; ++e) w[e] = pack_bf2(p[i][2 * e], p[i][2 * e + 1]);
+    *(u32x4_t*)(row + i * (size_t)K + col) = w;
+  }
 }
 
 // silu(x) = x / (1 + e^-x) on the hardware transcendentals (v_exp_f32, v_rcp_f32, ~1 ulp): a plain '/' compiles

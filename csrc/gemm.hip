@@ -52,7 +52,11 @@ struct GemmArgs {
   int rs_lds;    // persistent 256x256: row scales DMA'd to LDS in the last K-tile (default 1; 0 = A/B baseline)
   int skip_epi;  // timing ablation only (wrong results): 1 = no epilogue (gemm_bf16 / w7 kernels); 2 = persistent
                  // 256x256 SwiGLU epilogue computed but not stored
+  int x6k;       // > 0: A is a 3-plane X6 activation [M, 3 x6k] (common.h x6_acol) of the K' = 6 x6k GEMM
 };
+
+// element column of A holding GEMM column k (k a K-tile start)
+__device__ __forceinline__ int a_kcol(const GemmArgs& a, int k) { return a.x6k ? x6_acol(k, a.x6k) : k; }
 
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
@@ -649,7 +653,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
         acc[mg * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[mg * 4 + i][j], 0, 0, 0);
   };
   auto stage = [&](int k0, char* buf) {
-    stage_issue<CF::A_INSTR, NW>(pa, k0, buf, wave);
+    stage_issue<CF::A_INSTR, NW>(pa, a_kcol(a, k0), buf, wave);
     stage_issue<CF::B_INSTR, NW>(pb, k0, buf + CF::A_BYTES, wave);
   };
   const int nk = a.K / BK;
@@ -1564,8 +1568,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   };
   int st_q = 0, st_kt = 0, st_tile = tile0;
   set_stage_tile(tile0);
-  auto dma_item = [&](int r, char* buf, int kb) {   // item r < 8: A block, else B block r - 8
-    if (r < 8) glds16(sa + kb + oa[r], buf + (r * 4 + wave) * 1024);
+  auto dma_item = [&](int r, char* buf, int kba, int kb) {   // item r < 8: A block, else B block r - 8
+    if (r < 8) glds16(sa + kba + oa[r], buf + (r * 4 + wave) * 1024);
     else glds16(sb + kb + ob[r - 8], buf + BOFF + ((r - 8) * 4 + wave) * 1024);
   };
   auto advance_stage = [&]() {   // the DMA stream stops (repeats its last K-tile) at the end
@@ -1580,9 +1584,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   };
   auto stage_all = [&]() {
     char* buf = smem + (st_q & 1) * TB;
-    const int kb = st_kt * 128;
+    const int kb = st_kt * 128, kba = a_kcol(a, st_kt * 64) * 2;
 #pragma unroll
-    for (int r = 0; r < NR; ++r) dma_item(r, buf, kb);
+    for (int r = 0; r < NR; ++r) dma_item(r, buf, kba, kb);
     advance_stage();
   };
 
@@ -1606,7 +1610,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   auto prefetch = [&]() {
     if constexpr (PF > 0) {
       char* scratch = smem + 2 * TB + wave * 256;
-      __builtin_amdgcn_global_load_lds(pa_ + pf_kt * 128, LDS_PTR(scratch), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(pa_ + a_kcol(a, pf_kt * 64) * 2, LDS_PTR(scratch), 4, 0, 0);
       __builtin_amdgcn_global_load_lds(pb_ + pf_kt * 128, LDS_PTR(scratch), 4, 0, 0);
       ++pf_q;
       if (pf_q < total && ++pf_kt == nk) {
@@ -1638,7 +1642,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     constexpr bool read_on = decltype(read_c)::value;
     const uint32_t va = abase[ks] + bo, vb = bbase[ks] + bo;
     char* dbuf = smem + (st_q & 1) * TB;
-    const int kb = st_kt * 128;
+    const int kb = st_kt * 128, kba = dma_on ? a_kcol(a, st_kt * 64) * 2 : 0;
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
       // MFMAs slot_pos(rr-1)+1 .. slot_pos(rr), then work item rr
@@ -1653,7 +1657,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
         if (rr < 8) DS_READ_B128(GA[rr], va, rr * 2048);
         else DS_READ_B128(GB[rr - 8], vb, (rr - 8) * 2048);
       }
-      if constexpr (dma_on) dma_item(rr, dbuf, kb);
+      if constexpr (dma_on) dma_item(rr, dbuf, kba, kb);
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (dma_on) advance_stage();
@@ -1680,6 +1684,13 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   float rs[8];
   auto load_rs = [&](int mt) {
     if constexpr (BN == 256) {
+      if constexpr (EPI == EPI_QKV_ROPE) {
+        if (a.ssq_in) {   // fused RMSNorm from the producer's sum-of-squares partials (the bf16 QKV GEMM)
+          if (a.ssq_parts == 8) rscale_from_partials<8, 128, 8>(a, mt, wm, lane, rs);
+          else rscale_from_partials<8, 128, 14>(a, mt, wm, lane, rs);
+          return;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int m = min(mt + wm * 128 + i * 16 + (lane & 15), a.M - 1);
@@ -2031,6 +2042,8 @@ static int launch_4w(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+static int g_qkv256 = 1;  // QKV+RoPE GEMMs on the four-wave 256x256 kernel when it fills the chip (else 128x128):
+                          // 0 never, 1 the fp32-mode QKV, 2 both
 static int g_w7 = 2;  // 256x224 tiles for N % 224 == 0 shapes that 256 does not divide (N = 896): 1 eight-wave
                       // 64x112 wave tiles, 2 four-wave 128x112 wave tiles (default: 10-17 % faster on N = 896)
 
@@ -2061,8 +2074,8 @@ static int launch_w7m(const GemmArgs& a, hipStream_t st) {
 
 template <int EPI>
 static int launch_w7(const GemmArgs& a, hipStream_t st) {
-  // g_w7 == 2 (or variant 11 forced): the four-wave kernel with 256x224 tiles (128x112 wave tiles)
-  if (g_c256_variant == 11 || (g_c256_variant < 0 && g_w7 == 2)) return launch_4w<EPI, 0, 0, 224>(a, st);
+  // g_w7 == 2 (or variant 11 forced), and every 3-plane X6 operand: the four-wave kernel with 256x224 tiles
+  if (g_c256_variant == 11 || (g_c256_variant < 0 && g_w7 == 2) || a.x6k) return launch_4w<EPI, 0, 0, 224>(a, st);
   if constexpr (epi_f32(EPI)) return launch_w7m<EPI, 0>(a, st);  // the modes A/B the bf16 epilogue's traffic
   switch (g_w7_mode) {
     case 1: return launch_w7m<EPI, 1>(a, st);
@@ -2085,6 +2098,12 @@ static int launch(const GemmArgs& args, hipStream_t st) {
   // FLOP), 128x128 otherwise (N not a multiple of 256, or too few 256-row panels).  The QKV/RoPE and
   // LSE epilogues stay on 128x128 (register budget; their N is never a multiple of 256 in practice).
   if constexpr (EPI == EPI_QKV_ROPE || EPI == EPI_F32_QKV_ROPE) {
+    // persistent 256x256 four-wave tiles when they fill the chip (N = 1152: the last column tile is half used)
+    const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+    // (default for the fp32-mode X6 QKV, K' = 6K; the bf16 QKV's K = 896 loop is shorter than the 128x128 kernel's
+    // tail advantage: g_qkv256 = 2 forces it there too)
+    const bool on = EPI == EPI_F32_QKV_ROPE ? g_qkv256 >= 1 : g_qkv256 >= 2;
+    if (on && tiles >= 256 && g_tile_override != 128) return launch_4w<EPI, RH>(a, st);
     return launch_cfg<EPI, RH, C128>(a, st);
   } else if constexpr (EPI == EPI_LSE) {
     // LM head on the scored rows (M = 2048 at the bench batch, N = vocab): 256x256 persistent tiles when they
@@ -2102,11 +2121,11 @@ static int launch(const GemmArgs& args, hipStream_t st) {
     // default: the four-wave 128x128-wave-tile loop (variant 11; +3-20 % over the eight-wave loops on the gate/up,
     // X6 gate/up and 8192^3 shapes, profiles/r02_gemm_4w.md)
     const int variant = g_c256_variant >= 0 ? g_c256_variant : 11;
-    if constexpr (epi_f32(EPI)) {  // fp32 execution: K is always >= 6 x 64; the production main loops only
-      if (variant == 10) return launch_8p<EPI, RH>(a, st);
-      if (variant == 11) return launch_4w<EPI, RH>(a, st);
+    if constexpr (epi_f32(EPI)) {  // fp32 execution (3-plane X6 A operand): the kernels with the plane-remapping
+      // A loader - the four-wave loop (default, and for the eight-wave variants) or the C256 loop (variants 0 / 1)
       if (variant == 12) return launch_4w<EPI, RH, 4>(a, st);
-      return variant == 4 ? launch_pp<EPI, RH>(a, st) : launch_cfg<EPI, RH, C256, true>(a, st);
+      if (variant == 0 || variant == 1) return launch_cfg<EPI, RH, C256, true>(a, st);
+      return launch_4w<EPI, RH>(a, st);
     } else {
       switch (variant) {
         case 10: return launch_8p<EPI, RH>(a, st);
@@ -2152,6 +2171,11 @@ EDGE_API int edge_gemm_set_rs_lds(int on) {
 EDGE_API int edge_gemm_set_skip_epi(int on) {
   if (!EDGE_TUNING_BUILD && on) return (int)hipErrorNotSupported;
   g_skip_epi = on;
+  return 0;
+}
+
+EDGE_API int edge_gemm_set_qkv256(int on) {
+  g_qkv256 = on;
   return 0;
 }
 
@@ -2247,19 +2271,20 @@ EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, 
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B;
   a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.biasf = bias; a.residf = resid; a.ldr = ldr;
-  if (Kx % (X6_TERMS * BK)) return (int)hipErrorInvalidValue;
+  a.x6k = Kx / X6_TERMS;   // A: 3-plane activation rows (lda >= 3 Kx / 6)
+  if (Kx % (X6_TERMS * BK) || lda < 3 * a.x6k) return (int)hipErrorInvalidValue;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
   if (((uintptr_t)C & 15) || ldc % 4 || (resid && (ldr % 4 || ((uintptr_t)resid & 15))) ||
       (bias && ((uintptr_t)bias & 15)))
     return (int)hipErrorInvalidValue;
   if (act == 2) {
-    if (bias || resid || ldc != 3 * N) return (int)hipErrorInvalidValue;
+    if (bias || resid || ldc != 3 * (N / 2)) return (int)hipErrorInvalidValue;
     a.C = (bf16_t*)C;
     return launch<EPI_X6_SWIGLU>(a, st);
   }
   if (act == 1) {
-    if (resid || !bias || ldc != 6 * N) return (int)hipErrorInvalidValue;
+    if (resid || !bias || ldc != 3 * N) return (int)hipErrorInvalidValue;
     a.C = (bf16_t*)C;
     return launch<EPI_X6_BIAS_GELU>(a, st);
   }
@@ -2277,7 +2302,8 @@ EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* b
                                     int rot_dim, int s_pad, float q_scale, hipStream_t st) {
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
-  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = Kx; a.ldb = Kx;
+  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = Kx / 2; a.ldb = Kx;
+  a.x6k = Kx / X6_TERMS;   // X: 3-plane activation rows [M, 3 Kx / 6]
   a.biasf = bias; a.qf = q; a.kf = k; a.vtf = vt;
   a.cosT = cosT; a.sinT = sinT; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.s_pad = s_pad;
   a.q_scale = q_scale;
@@ -2294,11 +2320,14 @@ EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* b
   }
 }
 
+// x6 != 0: fp32 execution, X a 3-plane X6 activation [M, K / 2] and W the X6 weight [N, K] (K = 6 x plane width)
 EDGE_API int edge_gemm_lse(const void* X, const void* W, const int64_t* targets, float* part_max, float* part_sum,
-                           float* tgt_logit, int M, int N, int K, hipStream_t st) {
+                           float* tgt_logit, int M, int N, int K, int x6, hipStream_t st) {
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
-  a.M = M; a.N = N; a.K = K; a.lda = K; a.ldb = K;
+  a.M = M; a.N = N; a.K = K; a.lda = x6 ? K / 2 : K; a.ldb = K;
+  if (x6 && K % (X6_TERMS * BK)) return (int)hipErrorInvalidValue;
+  a.x6k = x6 ? K / X6_TERMS : 0;
   a.targets = targets; a.part_max = part_max; a.part_sum = part_sum; a.tgt_logit = tgt_logit; a.nparts = N / 64;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;

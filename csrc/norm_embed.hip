@@ -218,8 +218,8 @@ EDGE_API int edge_row_rscale(const float* ssq, float* rs, int R, int P, int H, f
 }
 
 // =============================================================================================
-// fp32 execution mode: fp32 activations in, fp32 statistics, and GEMM-input outputs written in the X6 split-bf16
-// layout [R, 6H] (common.h) that the fp32-mode GEMMs consume (out_x6 = 0: plain fp32 [R, H] instead).
+// fp32 execution mode: fp32 activations in, fp32 statistics, and GEMM-input outputs written as 3-plane X6 split-bf16
+// activations [R, 3H] (common.h) that the fp32-mode GEMMs consume (out_x6 = 0: plain fp32 [R, H] instead).
 template <int NCH>
 __device__ __forceinline__ void load_row_f32(const float* __restrict__ src, int H, float (&v)[NCH][8]) {
   const int lane = threadIdx.x & 63;
@@ -255,7 +255,7 @@ __device__ __forceinline__ void store_row_f32_or_x6(void* __restrict__ dst, int 
   }
 }
 
-__device__ __forceinline__ size_t out_row_elems(int H, bool x6) { return x6 ? (size_t)X6_TERMS * H : (size_t)H; }
+__device__ __forceinline__ size_t out_row_elems(int H, bool x6) { return x6 ? (size_t)3 * H : (size_t)H; }
 __device__ __forceinline__ void* out_row(void* y, size_t r, int H, bool x6) {
   return x6 ? (void*)((bf16_t*)y + r * out_row_elems(H, true)) : (void*)((float*)y + r * (size_t)H);
 }
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* __restr
   }
 }
 
-// fp32 [R, H] (rows optionally gathered) -> X6 [R, 6H]
+// fp32 [R, H] (rows optionally gathered) -> 3-plane X6 activation [R, 3H]
 template <int NCH>
 __global__ __launch_bounds__(256) void split6_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
                                                      const int* __restrict__ rows, int R, int H) {
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256) void split6_kernel(const float* __restrict__ x
   if (r >= R) return;
   float v[NCH][8];
   load_row_f32<NCH>(x + (size_t)(rows ? rows[r] : r) * H, H, v);
-  store_row_f32_or_x6<NCH>(y + (size_t)r * X6_TERMS * H, H, v, true);
+  store_row_f32_or_x6<NCH>(y + (size_t)r * 3 * H, H, v, true);
 }
 
 __global__ __launch_bounds__(256) void embedding_f32_kernel(const int64_t* __restrict__ ids,

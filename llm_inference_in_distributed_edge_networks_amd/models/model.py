@@ -29,8 +29,8 @@ Precision.  The reference evaluates fp32 models (``qwen_layer_wise.py:17`` and
 attention, softmax statistics and the boundary codec are fp32, and every GEMM takes its
 operands in the X6 split-bf16 layout (``ops.reference.x6_act`` / ``x6_weight``: six bf16
 MFMA products per fp32 product, exact to 2^-27 relative).  Producers of GEMM inputs (norms,
-attention, the SwiGLU / GELU epilogues) write X6 directly; weights are expanded once at
-load.  ``dtype=torch.bfloat16`` is the faster bf16 mode.
+attention, the SwiGLU / GELU epilogues) write the three bf16 planes of their output directly
+(3-plane activations, the GEMM's A loader expands them); weights are expanded once at load.  ``dtype=torch.bfloat16`` is the faster bf16 mode.
 """
 from __future__ import annotations
 

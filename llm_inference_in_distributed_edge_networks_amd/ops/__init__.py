@@ -43,10 +43,14 @@ def _check_f32(*ts):
             raise ValueError("HIP kernels take contiguous tensors")
 
 
-def _check_x6(*ts):
-    for t in ts:
-        if t is not None and (t.dtype != torch.bfloat16 or t.shape[-1] % 6 or not t.is_contiguous()):
-            raise TypeError("X6 operands are contiguous bf16 [rows, 6K] tensors (reference.x6_act / x6_weight)")
+def _check_x6(x6, w6):
+    """x6: 3-plane activation [rows, 3K] (reference.x6_act), w6: X6 weight [N, 6K] (reference.x6_weight)."""
+    for t, m, what in ((x6, 3, "activations [rows, 3K] (reference.x6_act)"), (w6, 6, "weights [N, 6K] "
+                                                                               "(reference.x6_weight)")):
+        if t.dtype != torch.bfloat16 or t.shape[-1] % m or not t.is_contiguous():
+            raise TypeError(f"X6 {what} must be contiguous bf16")
+    if 2 * x6.shape[-1] != w6.shape[-1]:
+        raise ValueError(f"X6 activation width {x6.shape[-1]} does not match the weight width {w6.shape[-1]}")
 
 
 def _check_bf16(*ts):
@@ -74,7 +78,7 @@ def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
 
 
 def _out_f32_or_x6(R: int, H: int, x6: bool, device) -> torch.Tensor:
-    return torch.empty(R, 6 * H, dtype=torch.bfloat16, device=device) if x6 else \
+    return torch.empty(R, 3 * H, dtype=torch.bfloat16, device=device) if x6 else \
         torch.empty(R, H, dtype=torch.float32, device=device)
 
 
@@ -166,6 +170,12 @@ def gemm_ssq_parts(M: int, N: int, K: int, act=None, bias=False, residual=False)
     """Row sum-of-squares partials ``linear(..., want_ssq=True)`` produces for this shape: N/64 (64-column
     slabs), or N/112 (wave slabs) when the 256x224 kernel runs it."""
     return int(lib().edge_gemm_ssq_parts(M, N, K, _ACT[act], int(bool(bias)), int(bool(residual))))
+
+
+def set_gemm_qkv256(mode: int) -> None:
+    """QKV+RoPE GEMMs on the four-wave 256x256 kernel when the shape fills the chip: 0 never, 1 the fp32-mode (X6)
+    QKV (default), 2 the bf16 QKV too."""
+    call("edge_gemm_set_qkv256", int(mode))
 
 
 def set_gemm_walk(chunked) -> None:
@@ -290,7 +300,7 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, x6: bool = False):
     ``n_rows`` ([B] fp32, scored rows per window as in ``WindowBatch.n_rows``): only query rows
     >= S-1-n_rows[b] are needed (last layer of the model); other 64-row blocks may be skipped and their
     output rows are then undefined.  fp32 q/k/vt run the f32 matrix-core kernel; ``x6`` then writes o in
-    the X6 layout [B*S, 6*Hq*64] the O-projection consumes."""
+    the 3-plane X6 layout [B*S, 3*Hq*64] the O-projection consumes."""
     if not _gpu(q):
         o, lse = ref.attention(q, k, vt, S, need_lse)
         return (ref.x6_act(o) if x6 else o), lse
@@ -372,34 +382,35 @@ def head_nll(h, w, targets):
     tgt = torch.empty(R, dtype=torch.float32, device=h.device)
     nll = torch.empty(R, dtype=torch.float32, device=h.device)
     t64 = targets.to(torch.int64).contiguous()
-    call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, stream())
+    call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, 0, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
 
 
 # ---- fp32 execution mode: X6 GEMMs (csrc/gemm.hip EPI_F32*, EPI_X6_*) ---------------------------------------
 def split6(x: torch.Tensor, rows: torch.Tensor | None = None) -> torch.Tensor:
-    """fp32 [R, K] (optionally rows gathered) -> X6 [R, 6K]."""
+    """fp32 [R, K] (optionally rows gathered) -> 3-plane X6 activation [R, 3K]."""
     if not _gpu(x):
         return ref.x6_act(x if rows is None else x.index_select(0, rows.long()))
     _check_f32(x)
     R = x.shape[0] if rows is None else rows.numel()
     rows32 = None if rows is None else rows.to(torch.int32).contiguous()
-    y = torch.empty(R, 6 * x.shape[1], dtype=torch.bfloat16, device=x.device)
+    y = torch.empty(R, 3 * x.shape[1], dtype=torch.bfloat16, device=x.device)
     call("edge_split6", ptr(x), ptr(y), ptr(rows32), R, x.shape[1], stream())
     return y
 
 
 def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=None, out=None,
               rscale=None) -> torch.Tensor:
-    """fp32-accurate ``act(rscale * (x @ w.T) + bias) + residual`` from X6 operands (x6 [M, 6K], w6 [N, 6K]).
+    """fp32-accurate ``act(rscale * (x @ w.T) + bias) + residual`` from X6 operands (x6 [M, 3K] 3-plane
+    activation, w6 [N, 6K] X6 weight).
 
-    act None -> fp32 [M, N] (``residual`` fp32, may alias ``out``); act "gelu" / "swiglu_il" -> the activation in
-    the X6 layout ([M, 6N] / [M, 3N]) for the next GEMM."""
-    M, Kx = x6.shape
-    N = w6.shape[0]
+    act None -> fp32 [M, N] (``residual`` fp32, may alias ``out``); act "gelu" / "swiglu_il" -> the activation as
+    a 3-plane X6 activation ([M, 3N] / [M, 3N/2]) for the next GEMM."""
+    M = x6.shape[0]
+    N, Kx = w6.shape
     if not _gpu(x6):
-        y = ref.x6_to_f32(x6) @ ref.x6_to_f32(w6).t()
+        y = ref.x6_to_f32(x6) @ ref.x6w_to_f32(w6).t()
         if rscale is not None:
             y = y * rscale.float().view(-1, 1)
         if bias is not None:
@@ -417,7 +428,6 @@ def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=
         return y
     _check_x6(x6, w6)
     _check_f32(bias, residual, rscale)
-    assert w6.shape[1] == Kx
     if act is None:
         if out is None:
             out = torch.empty(M, N, dtype=torch.float32, device=x6.device)
@@ -425,8 +435,8 @@ def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=
         code = 0
     else:
         No = N // 2 if act == "swiglu_il" else N
-        out = torch.empty(M, 6 * No, dtype=torch.bfloat16, device=x6.device)
-        ldc = 6 * No
+        out = torch.empty(M, 3 * No, dtype=torch.bfloat16, device=x6.device)
+        ldc = 3 * No
         code = _ACT[act]
     call("edge_gemm_f32", ptr(x6), ptr(w6), ptr(out), M, N, Kx, x6.stride(0), w6.stride(0), ldc, ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), code, ptr(rscale), stream())
@@ -436,12 +446,12 @@ def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=
 def qkv_rope_x6(x6, w6, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
     """fp32 fused QKV projection + bias + RoPE + head-major scatter from X6 operands -> fp32 (q, k, vt)."""
     if not _gpu(x6):
-        return ref.qkv_rope(ref.x6_to_f32(x6), ref.x6_to_f32(w6), bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim,
+        return ref.qkv_rope(ref.x6_to_f32(x6), ref.x6w_to_f32(w6), bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim,
                             q_scale)
     _check_x6(x6, w6)
     _check_f32(bias)
     assert D == 64, "HIP attention path is specialised for head_dim 64"
-    M, Kx = x6.shape
+    M, Kx = x6.shape[0], w6.shape[1]
     sp = s_pad(S)
     f32 = dict(dtype=torch.float32, device=x6.device)
     q = torch.empty(B, Hq, S, D, **f32)
@@ -455,16 +465,16 @@ def qkv_rope_x6(x6, w6, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
 def head_nll_x6(h6: torch.Tensor, w6: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
     """fp32 fused LM head + cross entropy on the scored rows from X6 operands: per-row NLL."""
     if not _gpu(h6):
-        return ref.head_nll(ref.x6_to_f32(h6), ref.x6_to_f32(w6), targets)
+        return ref.head_nll(ref.x6_to_f32(h6), ref.x6w_to_f32(w6), targets)
     _check_x6(h6, w6)
-    R, Kx = h6.shape
+    R, Kx = h6.shape[0], w6.shape[1]
     V = w6.shape[0]
     nparts = V // 64
     f32 = dict(dtype=torch.float32, device=h6.device)
     pmax, psum = torch.empty(R, nparts, **f32), torch.empty(R, nparts, **f32)
     tgt, nll = torch.empty(R, **f32), torch.empty(R, **f32)
     t64 = targets.to(torch.int64).contiguous()
-    call("edge_gemm_lse", ptr(h6), ptr(w6), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, stream())
+    call("edge_gemm_lse", ptr(h6), ptr(w6), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, 1, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
 

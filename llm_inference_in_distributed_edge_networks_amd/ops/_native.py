@@ -36,6 +36,7 @@ _SIGS = {
     "edge_gemm_set_variant": [c_i],
     "edge_gemm_set_walk": [c_i],
     "edge_gemm_set_w7": [c_i],
+    "edge_gemm_set_qkv256": [c_i],
     "edge_gemm_set_skip_epi": [c_i],
     "edge_gemm_set_rs_lds": [c_i],
     "edge_gemm_set_lse256": [c_i],
@@ -43,7 +44,7 @@ _SIGS = {
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],
-    "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
+    "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_set_variant": [c_i],

@@ -186,6 +186,8 @@ def head_nll(h, w, targets):
 # x = x0 + x1 + x2 exactly (three bf16 planes); a GEMM over the K-concatenations
 #   A' = [a2 | a0 | a1 | a1 | a0 | a0],  B' = [b0 | b2 | b1 | b0 | b1 | b0]
 # sums the six products a_i b_j with i + j <= 2, i.e. the fp32 product up to terms of relative size 2^-27.
+# Weights are stored as B' [N, 6K]; activations once per plane, [a0 | a1 | a2] [R, 3K] (the GEMM's A loader reads
+# block j of A' from plane X6_APLANES[j]).
 X6_APLANES = (2, 0, 1, 1, 0, 0)
 X6_BPLANES = (0, 2, 1, 0, 1, 0)
 
@@ -200,9 +202,15 @@ def split3(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
 
 
 def x6_act(x: torch.Tensor) -> torch.Tensor:
-    """fp32 [R, K] -> X6 activation layout [R, 6K] bf16 (what the fp32-mode kernels emit for GEMM inputs)."""
-    p = split3(x)
-    return torch.cat([p[i] for i in X6_APLANES], -1).contiguous()
+    """fp32 [R, K] -> 3-plane X6 activation [R, 3K] bf16 = [a0 | a1 | a2] (what the fp32-mode kernels emit for
+    GEMM inputs)."""
+    return torch.cat(split3(x), -1).contiguous()
+
+
+def x6_expand(x6: torch.Tensor) -> torch.Tensor:
+    """3-plane activation [R, 3K] -> the A' K-concatenation [R, 6K] the GEMM reads (X6_APLANES)."""
+    K = x6.shape[-1] // 3
+    return torch.cat([x6[..., i * K:(i + 1) * K] for i in X6_APLANES], -1)
 
 
 def x6_weight(w: torch.Tensor) -> torch.Tensor:
@@ -212,9 +220,15 @@ def x6_weight(w: torch.Tensor) -> torch.Tensor:
 
 
 def x6_to_f32(x6: torch.Tensor) -> torch.Tensor:
-    """Inverse of ``x6_act``: the fp32 value is the sum of the three distinct planes (blocks 1, 2, 0)."""
-    K = x6.shape[-1] // 6
-    return x6[..., K:2 * K].float() + x6[..., 2 * K:3 * K].float() + x6[..., :K].float()
+    """Inverse of ``x6_act``: the fp32 value is the sum of the three planes (exact: a0 + a1 + a2 in fp32)."""
+    K = x6.shape[-1] // 3
+    return (x6[..., :K].float() + x6[..., K:2 * K].float()) + x6[..., 2 * K:].float()
+
+
+def x6w_to_f32(w6: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``x6_weight``: the sum of the three distinct planes (blocks 0, 2, 1)."""
+    K = w6.shape[-1] // 6
+    return (w6[..., :K].float() + w6[..., 2 * K:3 * K].float()) + w6[..., K:2 * K].float()
 
 
 # ---- fused RMSNorm (GPU fast path) semantics -------------------------------------------------------

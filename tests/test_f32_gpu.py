@@ -108,8 +108,10 @@ def test_linear_x6_inplace_residual():
     assert rel_err(y, x.double() @ w.double().t() + r.double()) < 2e-6
 
 
-@pytest.mark.parametrize("B,S,Hq,Hkv,rot", [(2, 512, 14, 2, 64), (2, 100, 14, 2, 64), (1, 2048, 8, 8, 16)])
+@pytest.mark.parametrize("B,S,Hq,Hkv,rot", [(2, 512, 14, 2, 64), (2, 100, 14, 2, 64), (1, 2048, 8, 8, 16),
+                                             (64, 512, 14, 2, 64), (24, 2048, 8, 8, 16)])
 def test_qkv_rope_x6(B, S, Hq, Hkv, rot):
+    """fp32 QKV+RoPE from X6 operands: 128x128 tiles (small M) and the four-wave 256x256 kernel (production M)."""
     H = 896 if Hq == 14 else 512
     Nq = (Hq + 2 * Hkv) * 64
     x = rnd(B * S, H, seed=30)

@@ -341,17 +341,28 @@ def test_gemm_fused_norm_and_ssq_out(tile, act):
         close(y2._edge_ssq, ref_ssq, atol=1e-2, rtol=1e-4)
 
 
-def test_qkv_rope_fused_norm():
-    B, S, Hq, Hkv, Hd = 2, 256, 14, 2, 896
-    cos, sin = R.rope_tables(1024, 64, 1e6)
+@pytest.mark.parametrize("B,S,mode,rot", [(2, 256, 1, 64), (64, 512, 2, 64), (64, 512, 0, 64), (40, 512, 2, 16)])
+def test_qkv_rope_fused_norm(B, S, mode, rot):
+    """QKV + bias + RoPE + fused RMSNorm (ssq partials): 128x128 tiles, and the four-wave 256x256 kernel (mode 2)
+    at production row counts (partial last column tile N = 1152), full and partial rotary."""
+    Hq, Hkv, Hd = 14, 2, 896
+    cos, sin = R.rope_tables(1024, max(rot, 2), 1e6)
+    ops.set_gemm_qkv256(mode)
+    try:
+        _qkv_case(B, S, Hq, Hkv, Hd, cos, sin, rot)
+    finally:
+        ops.set_gemm_qkv256(1)
+
+
+def _qkv_case(B, S, Hq, Hkv, Hd, cos, sin, rot):
     x = rnd(B * S, Hd, seed=96)
     nw = rnd(Hd, s=0.1, seed=97) + 1
     N = (Hq + 2 * Hkv) * 64
     w = rnd(N, Hd, s=0.04, seed=98)
     b = rnd(N, s=0.3, seed=99)
     q, k, vt = ops.qkv_rope(x.to(DEV), R.fold_norm_weight(w, nw).to(DEV), b.to(DEV), cos.to(DEV), sin.to(DEV),
-                            B, S, Hq, Hkv, 64, 64, 0.125, norm=(R.row_ssq(x).to(DEV), 1e-6))
-    rq, rk, rvt = R.qkv_rope(R.rmsnorm(x, nw, 1e-6), w, b, cos, sin, B, S, Hq, Hkv, 64, 64, 0.125)
+                            B, S, Hq, Hkv, 64, rot, 0.125, norm=(R.row_ssq(x).to(DEV), 1e-6))
+    rq, rk, rvt = R.qkv_rope(R.rmsnorm(x, nw, 1e-6), w, b, cos, sin, B, S, Hq, Hkv, 64, rot, 0.125)
     close(q, rq, atol=3e-2, rtol=3e-2)
     close(k, rk, atol=4e-2, rtol=3e-2)
     close(vt, rvt, atol=4e-2, rtol=3e-2)

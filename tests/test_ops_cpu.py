@@ -73,3 +73,24 @@ def test_native_library_exports_every_bound_entry_point():
         pytest.skip("kernel library not built")
     L = ctypes.CDLL(_native.LIB_PATH)
     assert [n for n in _native._SIGS if not hasattr(L, n)] == []
+
+
+def test_x6_three_plane_activation_layout():
+    """3-plane X6 activations [a0|a1|a2] expand to the A' K-concatenation the GEMM reads (blocks 2 0 1 1 0 0), and
+    A' @ B'^T over the six bf16 products is fp32-accurate."""
+    import torch
+
+    from llm_inference_in_distributed_edge_networks_amd.ops import reference as R
+    g = torch.Generator().manual_seed(0)
+    x, w = torch.randn(64, 128, generator=g), torch.randn(96, 128, generator=g) / 11
+    a3 = R.x6_act(x)
+    assert a3.shape == (64, 384) and a3.dtype == torch.bfloat16
+    assert torch.equal(R.x6_to_f32(a3), (a3[:, :128].float() + a3[:, 128:256].float()) + a3[:, 256:].float())
+    assert (R.x6_to_f32(a3) - x).abs().max() <= 1e-6 * x.abs().max()
+    ap = R.x6_expand(a3)
+    for j, p in enumerate(R.X6_APLANES):
+        assert torch.equal(ap[:, 128 * j:128 * (j + 1)], a3[:, 128 * p:128 * (p + 1)])
+    y = ap.double() @ R.x6_weight(w).double().t()
+    ref = x.double() @ w.double().t()
+    assert ((y - ref).abs().max() / ref.abs().max()) < 1e-6
+    assert torch.allclose(R.x6w_to_f32(R.x6_weight(w)), w, rtol=0, atol=1e-6)

@@ -28,6 +28,7 @@ SHAPES = {  # name: (M, N, K, act, bias, resid)
     "x6_down_b64": (32768, 896, 6 * 4864, "x6", False, True),
     "x6_o_proj_b64": (32768, 896, 6 * 896, "x6", False, True),
     "x6_big": (8192, 8192, 6 * 1024, "x6", False, False),
+    "x6_qkv_rope_b64": (32768, 1152, 6 * 896, "x6_qkv_rope", True, False),
     # epilogue-cost ablations of the x6 gate/up shape: plain fp32 output, plain bf16 output
     "x6_gate_up_f32out": (32768, 9728, 6 * 896, "x6", False, False),
     "gate_up_k5376_bf16out": (32768, 9728, 6 * 896, None, False, False),
@@ -85,6 +86,8 @@ def main():
                 ops._native.lib().edge_gemm_set_w7_mode(mode)
                 if act == "qkv_rope":
                     ops.qkv_rope(x, w, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
+                elif act == "x6_qkv_rope":
+                    ops.qkv_rope_x6(x, w, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
                 elif act == "x6_swiglu":
                     ops.linear_x6(x, w, act="swiglu_il")
                 elif act == "x6":
@@ -94,7 +97,7 @@ def main():
                 ops._native.lib().edge_gemm_set_skip_epi(0)
                 ops._native.lib().edge_gemm_set_w7_mode(0)
             return f
-        if act == "qkv_rope":
+        if act in ("qkv_rope", "x6_qkv_rope"):
             cos, sin = (t.to(dev) for t in ops.rope_tables(512, 64, 1e6))
         variants = {t: mk(t) for t in tiles}
         ours = variants[tiles[0]]
