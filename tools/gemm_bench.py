@@ -62,9 +62,10 @@ def main():
         if a.only and name not in a.only.split(","):
             continue
         M = a.m or M if name != "lm_head" else M
-        x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
-        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         x6 = act is not None and act.startswith("x6")
+        # X6 shapes: K is the GEMM's K' = 6 x plane width; the activation is stored once per plane ([M, K'/2])
+        x = (torch.rand(M, K // 2 if x6 else K, device=dev) * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
         b = torch.randn(N, device=dev).to(torch.float32 if x6 else torch.bfloat16) if bias else None
         No = N // 2 if act in ("swiglu_il", "x6_swiglu") else N
         r = torch.randn(M, No, device=dev).to(torch.float32 if x6 else torch.bfloat16) if resid else None
@@ -101,7 +102,8 @@ def main():
             cos, sin = (t.to(dev) for t in ops.rope_tables(512, 64, 1e6))
         variants = {t: mk(t) for t in tiles}
         ours = variants[tiles[0]]
-        lib = lambda: torch.matmul(x, w.t())  # noqa: E731
+        xl = torch.cat([x, x], 1) if x6 else x   # hipBLASLt reference: the same K' GEMM on plain operands
+        lib = lambda: torch.matmul(xl, w.t())  # noqa: E731
         if resid and not x6:  # hipBLASLt with the residual as beta*C (what a library route for RESID GEMMs would run)
             variants["libr"] = lambda: torch.addmm(r, x, w.t())
         for _ in range(3):
