@@ -41,6 +41,7 @@ class Params:
     num_stages: int = 1                      # pipeline stages for the distributed runner
     split_layers: list = field(default_factory=list)   # explicit stage boundaries (last layer of each stage but the last)
     head_weights: str = ""                   # path to attention_head_weights.json (weighted_importance)
+    selection: str = "ratio"                 # "ratio" (int(ratio*S) least important) | "top_rho" (mass 1 - ratio kept)
     group_relevance: str = ""                # channel_group_relevance.json (head-group codecs rgroup / mixed_rgroup_int8)
     group_avg_bits: float = 4.0              # head-group codecs: average bits per channel of a group-quantized row
     output_dir: str = "."
@@ -88,6 +89,8 @@ class Params:
                 raise ValueError(f"bad ratio {r!r}")
         if self.num_stages < 1:
             raise ValueError("num_stages must be >= 1")
+        if self.selection not in ("ratio", "top_rho"):
+            raise ValueError(f"selection must be 'ratio' or 'top_rho', got {self.selection!r}")
 
 
 def resolve_device(p: Params) -> str:

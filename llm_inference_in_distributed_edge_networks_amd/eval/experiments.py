@@ -88,7 +88,8 @@ def importance_sweep(p: Params, default_model: str, out_name: str) -> dict:
         if hw is None:
             raise FileNotFoundError("weighted_importance needs attention_head_weights.json "
                                     "(run Experiments/Relevance/main.py or set params['head_weights'])")
-    sc = SweepConfig(methods, p.layers_of_interest, p.ratios, p.codec, hw)
+    rows = [SweepMethod(m, m, selection=p.selection) for m in methods]
+    sc = SweepConfig(rows, p.layers_of_interest, p.ratios, p.codec, hw)
     eng = SweepEngine(model, sc)
     state = _state(p, env, out_name)
     pb = progress_bar(len(wins), env.is_main)
@@ -275,7 +276,8 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
     results: dict = {}
     for m in methods:
         for r in p.ratios:
-            bcfg = BoundaryConfig(p.codec, float(r), m, hw, group_relevance=grel, group_avg_bits=p.group_avg_bits)
+            bcfg = BoundaryConfig(p.codec, float(r), m, hw, selection=p.selection, group_relevance=grel,
+                                  group_avg_bits=p.group_avg_bits)
             bl = list(batches(ids, wins, p.window_batch))
             t0 = time.perf_counter()
             if distributed:

@@ -85,3 +85,16 @@ def test_analysis_js(tmp_path):
     res = json.loads((d / "js_divergence.json").read_text())
     m = res["js_divergence"]
     assert len(m) == 4 and m[0][0] == 0 and abs(m[0][1] - m[1][0]) < 1e-12 and all(0 <= v <= 1 for r in m for v in r)
+
+
+def test_top_rho_selection_from_params(tmp_path):
+    """params['selection'] = 'top_rho' drives the sweep and the pipeline (variable-k boundary messages)."""
+    d = run_main("Qwen2-0.5B", {"model": "tiny-qwen2", "max_length": 128, "ratios": [0.5], "layers_of_interest": [1],
+                                "methods": ["last_row"], "codec": "mixed_int4_int8", "selection": "top_rho"},
+                 tmp_path)
+    sw = json.loads((d / "avg_ppl_results.json").read_text())
+    p = run_main("Pipeline", {"model": "tiny-qwen2", "split_layers": [1], "codec": "mixed_int4_int8",
+                              "methods": ["last_row"], "ratios": [0.5], "max_length": 128, "selection": "top_rho"},
+                 tmp_path)
+    res = json.loads((p / "pipeline_results.json").read_text())["results"]["last_row"]["0.5"]
+    assert abs(res["ppl"] - sw["avg_ppl_results"][0][0][0]) / res["ppl"] < 1e-6
