@@ -2109,7 +2109,10 @@ static int launch(const GemmArgs& args, hipStream_t st) {
     // LM head on the scored rows (M = 2048 at the bench batch, N = vocab): 256x256 persistent tiles when they
     // fill the chip (A/B: g_lse256), else 128x128
     const bool big = g_lse256 && a.N % 128 == 0 && (long long)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 256;
-    if (big && g_tile_override != 128) return launch_cfg<EPI, RH, C256, true>(a, st);
+    if (big && g_tile_override != 128) {
+      if (g_c256_variant == 0 || g_c256_variant == 1) return launch_cfg<EPI, RH, C256, true>(a, st);
+      return launch_4w<EPI, RH>(a, st);   // the four-wave loop (per-64-column LSE partials per quarter)
+    }
     return launch_cfg<EPI, RH, C128>(a, st);
   } else {
     // a partial last column tile (N % 256 == 128) wastes at most 1/(2*tn) of the MFMA work

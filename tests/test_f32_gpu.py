@@ -167,14 +167,18 @@ def test_importance_stats_f32(B, S, Hq, Hkv):
     assert rel_err(cs, R.attn_colsum(q.double(), k.double(), rl, S)) < 5e-6
 
 
-def test_head_nll_x6():
-    R_, H, V = 200, 896, 151936
+@pytest.mark.parametrize("R_", [200, 2048])
+def test_head_nll_x6(R_):
+    """fp32 LM head + CE from X6 operands: 128x128 tiles (200 rows) and the four-wave 256x256 kernel (2048 rows,
+    partial last vocabulary tile); the first 96 rows against fp64."""
+    H, V = 896, 151936
     h = rnd(R_, H, seed=60)
     w = rnd(V, H, s=0.05, seed=61)
     t = torch.randint(0, V, (R_,))
+    t[:3] = torch.tensor([0, V - 1, V - 100])
     nll = ops.head_nll_x6(R.x6_act(h).to(DEV), R.x6_weight(w).to(DEV), t.to(DEV))
-    ref = R.head_nll(h.double(), w.double(), t)
-    assert float((nll.cpu().double() - ref).abs().max()) < 2e-5
+    ref = R.head_nll(h[:96].double(), w.double(), t[:96])
+    assert float((nll[:96].cpu().double() - ref).abs().max()) < 2e-5
 
 
 @pytest.mark.parametrize("codec", ["ref_int4_global", "mixed_int4_int8", "int4_token", "passthrough", "channel_4",
