@@ -1572,6 +1572,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     if (r < 8) glds16(sa + kba + oa[r], buf + (r * 4 + wave) * 1024);
     else glds16(sb + kb + ob[r - 8], buf + BOFF + ((r - 8) * 4 + wave) * 1024);
   };
+  int st_kba = a_kcol(a, 0) * 2;   // byte offset of the stream K-tile's A columns (3-plane X6 operands: the plane remap, computed
+                    // once per K-tile where the wave waits anyway, not on the MFMA issue path)
   auto advance_stage = [&]() {   // the DMA stream stops (repeats its last K-tile) at the end
     ++st_q;
     if (st_q >= total) {
@@ -1581,10 +1583,11 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       st_tile += G;
       set_stage_tile(st_tile);
     }
+    st_kba = a_kcol(a, st_kt * 64) * 2;
   };
   auto stage_all = [&]() {
     char* buf = smem + (st_q & 1) * TB;
-    const int kb = st_kt * 128, kba = a_kcol(a, st_kt * 64) * 2;
+    const int kb = st_kt * 128, kba = st_kba;
 #pragma unroll
     for (int r = 0; r < NR; ++r) dma_item(r, buf, kba, kb);
     advance_stage();
@@ -1642,7 +1645,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     constexpr bool read_on = decltype(read_c)::value;
     const uint32_t va = abase[ks] + bo, vb = bbase[ks] + bo;
     char* dbuf = smem + (st_q & 1) * TB;
-    const int kb = st_kt * 128, kba = dma_on ? a_kcol(a, st_kt * 64) * 2 : 0;
+    const int kb = st_kt * 128, kba = st_kba;
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
       // MFMAs slot_pos(rr-1)+1 .. slot_pos(rr), then work item rr
