@@ -74,8 +74,9 @@ def parse():
     p.add_argument("--ratio", type=float, default=0.5)
     p.add_argument("--method", default="regular_importance")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--transport", default="torch", choices=["torch", "rccl"],
-                   help="stage hand-off: torch.distributed p2p (RCCL) or the native RCCL wrapper")
+    p.add_argument("--transport", default="torch", choices=["torch", "rccl", "ipc"],
+                   help="stage hand-off: torch.distributed p2p (RCCL), the native RCCL wrapper, or peer copies into "
+                        "IPC-mapped receive slots (ipc)")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--json-out", default="")
     return p.parse_args()

@@ -252,6 +252,10 @@ class DistributedPipeline:
         elif transport == "torch":
             from .rccl import TorchP2P
             self.tr = TorchP2P()
+        elif transport == "ipc":
+            from .ipc import IpcP2P
+            self.tr = IpcP2P(model.device)
+            self.tr.setup(rank, self.prev, self.next)
         else:
             raise ValueError(f"unknown transport {transport!r}")
         if check is None:
@@ -377,6 +381,8 @@ class DistributedPipeline:
         if wd:
             wd.stop()
         self.runner.stats.compute_s += time.perf_counter() - t0
+        if hasattr(self.tr, "quiesce"):      # peer-copy transport: no flow-control message left unmatched
+            self.tr.quiesce()
         all_reduce_sum(acc_local)
         acc = PPLAccumulator()
         acc.total_nll, acc.n_tokens = float(acc_local[0]), float(acc_local[1])

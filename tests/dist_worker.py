@@ -24,9 +24,13 @@ def run(rank, world, port, pp, codec, ratio, method, out_path, split):
     model, _ = build_model(cfg, "cpu", torch.float32, seed=0, layers=plan.stage_layers(stage),
                            with_embed=stage == 0, with_head=stage == pp - 1)
     hw = torch.linspace(-1, 2, cfg.num_layers * cfg.num_heads).view(cfg.num_layers, cfg.num_heads)
-    pipe = DistributedPipeline(model, plan, BoundaryConfig(codec, ratio, method, hw), grid, rank)
+    pipe = DistributedPipeline(model, plan, BoundaryConfig(codec, ratio, method, hw), grid, rank,
+                               transport=os.environ.get("EDGE_TEST_TRANSPORT", "torch"))
     toks = synthetic_stream(1500, cfg.vocab_size, 2)
-    acc, info = pipe.evaluate(list(batches(toks, sliding_windows(1500, 128, 32), 3)))
+    bl = list(batches(toks, sliding_windows(1500, 128, 32), 3))
+    acc, info = pipe.evaluate(bl)
+    if os.environ.get("EDGE_TEST_TWICE"):          # a second run on the same transport state (sequence numbers go on)
+        acc, info = pipe.evaluate(bl)
     if rank == 0:
         with open(out_path, "w") as f:
             json.dump({"ppl": acc.ppl(), "n": acc.n_tokens}, f)

@@ -81,3 +81,20 @@ def test_distributed_checked_pipeline(tmp_path, monkeypatch):
     mp.spawn(dist_worker.run, args=args, nprocs=3, join=True)
     ref = local_ppl(PipelinePlan.from_split_layers(4, [0, 2]), "mixed_int4_int8", 0.5, "aggregate_till")
     assert abs(json.loads(out.read_text())["ppl"] - ref) / ref < 1e-6
+
+
+@pytest.mark.parametrize("world,pp,method,split,slot_kb", [(2, 2, "regular_importance", [1], 160),
+                                                          (3, 3, "aggregate_till", [0, 2], 160),
+                                                          (3, 3, "aggregate_till", [0, 2], 32)])
+def test_distributed_peer_copy_transport(tmp_path, monkeypatch, world, pp, method, split, slot_kb):
+    """transport='ipc' (sender copies into the receiver's slot ring, flags / credits over the process group; here
+    /dev/shm mappings): equal to the local pipeline, with small slots (oversized messages take the fallback path)
+    and a second evaluation on the same transport state."""
+    monkeypatch.setenv("EDGE_TEST_TRANSPORT", "ipc")
+    monkeypatch.setenv("EDGE_TEST_TWICE", "1")
+    monkeypatch.setenv("EDGE_IPC_SLOT_BYTES", str(slot_kb << 10))   # 32 KiB: the messages fall back, carries fit
+    out = tmp_path / "res.json"
+    mp.spawn(dist_worker.run, args=(world, free_port(), pp, "mixed_int4_int8", 0.5, method, str(out), split),
+             nprocs=world, join=True)
+    ref = local_ppl(PipelinePlan.from_split_layers(4, split), "mixed_int4_int8", 0.5, method)
+    assert abs(json.loads(out.read_text())["ppl"] - ref) / ref < 1e-6

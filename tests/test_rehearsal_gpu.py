@@ -59,3 +59,15 @@ def test_serialized_kernel_mode_same_result():
     fast = _run(2, ["--no-bf16"])
     ser = _run(2, ["--no-bf16", "--no-graphs"], {"AMD_SERIALIZE_KERNEL": "3", "HIP_LAUNCH_BLOCKING": "1"})
     assert ser["ppl_random_weights"] == fast["ppl_random_weights"]
+
+
+def test_peer_copy_transport_one_gpu():
+    """--transport ipc: boundary messages copied by the sender straight into the receiver's IPC-mapped slot ring
+    (CUDA IPC between the two processes; flags / credits over gloo here) == the single-process run."""
+    one = _run(1, ["--no-bf16"])
+    ipc = _run(2, ["--no-bf16", "--transport", "ipc"])
+    assert ipc["config"]["transport"] == "ipc"
+    assert ipc["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
+    three = _run(3, ["--no-bf16", "--transport", "ipc", "--pp", "3"], {"EDGE_IPC_SLOT_BYTES": str(1 << 16)})
+    one3 = _run(1, ["--no-bf16", "--pp", "3"])
+    assert three["ppl_random_weights"] == pytest.approx(one3["ppl_random_weights"], rel=1e-9)
