@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--sizes", default="1024,65536,1048576,11075584,29360128")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--transport", default="torch", choices=["torch", "ipc"],
+                    help="torch: isend/irecv (RCCL); ipc: peer copies into the receiver's IPC-mapped slot ring "
+                         "(parallel/ipc.py, the hipMemcpyPeerAsync baseline)")
     a = ap.parse_args()
     env = init_distributed("auto")
     assert env.world_size == 2, "run with exactly 2 ranks"
@@ -52,7 +55,23 @@ def main():
             r.wait()
         sync()
         dt = time.perf_counter() - t0
-        res.append({"bytes": n, "half_rtt_us": lat * 1e6, "stream_GBps": n * a.iters / dt / 1e9})
+        rec = {"bytes": n, "half_rtt_us": lat * 1e6, "stream_GBps": n * a.iters / dt / 1e9}
+        if a.transport == "ipc":
+            # one-way stream of the same messages through the peer-copy transport (rank 0 -> rank 1)
+            from llm_inference_in_distributed_edge_networks_amd.parallel.ipc import IpcP2P
+            tr = IpcP2P(dev, capacity=max(n, 1 << 20))
+            tr.setup(env.rank, 0 if env.rank == 1 else None, 1 if env.rank == 0 else None)
+            sync()
+            t0 = time.perf_counter()
+            hs = [tr.send(buf, 1) if env.rank == 0 else tr.recv(buf, 0) for _ in range(a.iters)]
+            for h in hs:
+                h.wait()
+            tr.quiesce()
+            sync()
+            dist.barrier()
+            rec["ipc_stream_GBps"] = n * a.iters / (time.perf_counter() - t0) / 1e9
+            tr.close()
+        res.append(rec)
         if env.rank == 0:
             print(json.dumps(res[-1]), flush=True)
     if env.rank == 0 and a.json_out:
