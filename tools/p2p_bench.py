@@ -63,9 +63,10 @@ def main():
             tr.setup(env.rank, 0 if env.rank == 1 else None, 1 if env.rank == 0 else None)
             sync()
             t0 = time.perf_counter()
-            hs = [tr.send(buf, 1) if env.rank == 0 else tr.recv(buf, 0) for _ in range(a.iters)]
-            for h in hs:
-                h.wait()
+            for _ in range(a.iters):   # the receiver consumes each message before posting the next receive
+                h = tr.send(buf, 1) if env.rank == 0 else tr.recv(buf, 0)
+                if env.rank == 1:
+                    h.wait()
             tr.quiesce()
             sync()
             dist.barrier()
