@@ -2,9 +2,9 @@
 // attention half of the framework's fp32 execution mode (the reference evaluates its models in fp32:
 // Experiments/Qwen2-0.5B/qwen_layer_wise.py:17, Experiments/Pythia-70M/pythia_model.py:25 load without a dtype).
 //
-// Matrix work runs on the gfx950 f32 matrix cores, v_mfma_f32_16x16x4_f32: exact fp32 products and fp32
-// accumulation (the GEMMs of the same mode use the split-bf16 X6 scheme instead, see common.h; attention is ~3 %
-// of the FLOPs at S = 512 and takes the f32 instruction, which needs no operand splitting).
+// flash_attn_fwd_x6 (default) runs the matrix work as split-bf16 products on the bf16 matrix cores (the X6 scheme of
+// the GEMMs, common.h): 1.5x the native f32 kernel, flash_attn_fwd_f32, which runs v_mfma_f32_16x16x4_f32 (exact
+// fp32 products and fp32 accumulation) and stays for A/B and the importance scorers.
 //
 //   flash_attn_fwd_f32 : O = softmax(Q K^T) V, online softmax, optional row LSE; O written as fp32 rows or
 //                        directly in the X6 layout the O-projection GEMM consumes.
@@ -207,6 +207,233 @@ __global__ __launch_bounds__(256, 2) void flash_attn_fwd_f32_kernel(const float*
   }
 }
 
+// ---- split-bf16 ("X6") flash attention: the same fp32-accurate result on the bf16 matrix cores -------------------
+// q, k, v and the probabilities are split into three bf16 planes (common.h split3) and every product is the sum of
+// the six plane products a_i b_j with i + j <= 2 (v_mfma_f32_16x16x32_bf16; dropped terms 2^-27 relative, every
+// bf16 x bf16 product exact in the fp32 accumulator): 96 bf16 MFMAs of 16 cycles per 16-query x 64-key tile against
+// 128 f32 MFMAs of 32 cycles.  Same S^T = K Q^T / O^T += V^T P^T orientation as flash_attn_fwd_f32 (lane holds 4
+// keys of one query; the probabilities are the lane's own P^T operand).  K and V^T tiles are read from global fp32
+// into registers one tile ahead, split, and written to LDS as planes of 64 rows x 128 B (16-byte chunks swizzled by
+// (row >> 1) & 7, the GEMM image); V^T keys are stored in the order the P^T operand holds them - within a 32-key
+// block a lane's k-slots 8g..8g+7 are keys {4g..4g+3, 16+4g..16+4g+3} - so each A fragment is one ds_read_b128.
+namespace {
+constexpr int XPL = 64 * 128;                 // one bf16 plane of a 64 x 64 tile
+__device__ __forceinline__ int xsw(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ void split_frag(const float (&v)[8], bf16x8_t& a, bf16x8_t& b, bf16x8_t& c) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float p0, p1, p2;
+    split3(v[e], p0, p1, p2);
+    a[e] = (__bf16)p0;
+    b[e] = (__bf16)p1;
+    c[e] = (__bf16)p2;
+  }
+}
+__device__ __forceinline__ bf16x8_t xfrag(const char* plane, int row, int chunk) {
+  return *(const bf16x8_t*)(plane + row * 128 + ((chunk ^ xsw(row)) << 4));
+}
+__device__ __forceinline__ f32x4_t mfma_bf(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// the six plane products, small terms first
+__device__ __forceinline__ f32x4_t x6_dot(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4_t c) {
+  c = mfma_bf(a[2], b[0], c);
+  c = mfma_bf(a[0], b[2], c);
+  c = mfma_bf(a[1], b[1], c);
+  c = mfma_bf(a[1], b[0], c);
+  c = mfma_bf(a[0], b[1], c);
+  return mfma_bf(a[0], b[0], c);
+}
+}  // namespace
+
+// NW waves of 16 query rows per workgroup (4: 64 rows, 8: 128 rows sharing each staged K / V^T tile)
+template <bool X6OUT, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(const float* __restrict__ q,
+                                                                  const float* __restrict__ k,
+                                                                  const float* __restrict__ vt, void* __restrict__ o,
+                                                                  float* __restrict__ lse,
+                                                                  const float* __restrict__ n_rows, int B, int Hq,
+                                                                  int Hkv, int S, int s_pad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // K planes (3 x 8 KiB), V^T planes (3 x 8 KiB)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
+  constexpr int QB = 16 * NW;          // query rows per workgroup
+  const int nqb = (S + QB - 1) / QB;
+  const int G = Hq / Hkv, NG = B * Hkv;
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int cnt = (NG - xcd + 7) >> 3;
+  const int per_qb = cnt * G;
+  if (j >= per_qb * nqb) return;
+  const int qb = nqb - 1 - j / per_qb;
+  const int rem = j - (nqb - 1 - qb) * per_qb;
+  const int grp = xcd + 8 * (rem / G);
+  const int b = grp / Hkv, hk = grp - b * Hkv, h = hk * G + rem % G;
+  if (n_rows && qb * QB + QB - 1 < S - 1 - (int)n_rows[b]) return;  // scored-rows mode (last layer)
+
+  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
+  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const float* vh = vt + ((size_t)b * Hkv + hk) * 64 * (size_t)s_pad;
+  char* const lk = smem;
+  char* const lv = smem + 3 * XPL;
+
+  const int q0 = qb * QB + wave * 16;
+  const int qrow = q0 + ql;
+  const int qld = qrow < S ? qrow : S - 1;
+  // Q^T operand planes: lane (query ql, g) holds d = 32 ks + 8g .. +7
+  bf16x8_t qp[2][3];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    float v[8];
+    const f32x4_t a = *(const f32x4_t*)(qh + (size_t)qld * 64 + 32 * ks + 8 * g);
+    const f32x4_t c = *(const f32x4_t*)(qh + (size_t)qld * 64 + 32 * ks + 8 * g + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = c[e]; }
+    split_frag(v, qp[ks][0], qp[ks][1], qp[ks][2]);
+  }
+  f32x4_t oacc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m2 = -INFINITY, l_run = 0.f;
+
+  // staging: this lane's NF consecutive floats of K row / V^T row srow (64 rows over the NW waves)
+  constexpr int NF = 64 * 64 / (NW * 64), LPR = 64 / NF;   // floats per lane, lanes per row
+  const int srow = (wave * 64 + lane) / LPR, scol = (lane % LPR) * NF;
+  f32x4_t kreg[NF / 4], vreg[NF / 4];
+  auto load_tile = [&](int kb) {
+    const int kr = min(kb * 64 + srow, S - 1);
+    const float* kp = kh + (size_t)kr * 64 + scol;
+    const float* vp = vh + (size_t)srow * s_pad + kb * 64 + scol;
+#pragma unroll
+    for (int i = 0; i < NF / 4; ++i) {
+      kreg[i] = *(const f32x4_t*)(kp + 4 * i);
+      vreg[i] = *(const f32x4_t*)(vp + 4 * i);
+    }
+  };
+  auto write_tile = [&]() {
+    // K row srow: d = scol .. + NF - 1 = chunks scol / 8 .. of each plane
+#pragma unroll
+    for (int hc = 0; hc < NF / 8; ++hc) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] = kreg[2 * hc][e]; v[4 + e] = kreg[2 * hc + 1][e]; }
+      bf16x8_t p[3];
+      split_frag(v, p[0], p[1], p[2]);
+      const int c = scol / 8 + hc;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *(bf16x8_t*)(lk + pl * XPL + srow * 128 + ((c ^ xsw(srow)) << 4)) = p[pl];
+    }
+    // V^T row srow (= d): keys scol .. + NF - 1 in groups of 4; the group of keys 32 s + 16 hf + 4a .. +3 goes to
+    // chunk 4 s + a, half hf
+#pragma unroll
+    for (int a4 = 0; a4 < NF / 4; ++a4) {
+      const int key = scol + 4 * a4;
+      const int sblk = key >> 5, hf = (key >> 4) & 1, a = (key >> 2) & 3;
+      float p0[4], p1[4], p2[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split3(vreg[a4][e], p0[e], p1[e], p2[e]);
+      const int off = srow * 128 + (((4 * sblk + a) ^ xsw(srow)) << 4) + hf * 8;
+      *(u32x2_t*)(lv + 0 * XPL + off) = u32x2_t{pack_bf2(p0[0], p0[1]), pack_bf2(p0[2], p0[3])};
+      *(u32x2_t*)(lv + 1 * XPL + off) = u32x2_t{pack_bf2(p1[0], p1[1]), pack_bf2(p1[2], p1[3])};
+      *(u32x2_t*)(lv + 2 * XPL + off) = u32x2_t{pack_bf2(p2[0], p2[1]), pack_bf2(p2[2], p2[3])};
+    }
+  };
+
+  const int nkb = min((qb + 1) * QB, S + 63) / 64;   // key tiles up to this block's last query row
+  const int kmax = (q0 + 15) / 64;  // last key tile this wave needs (wave-uniform)
+  load_tile(0);
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();                 // every wave's reads of the previous tile retired
+    write_tile();
+    __syncthreads();                 // planes of tile kb visible
+    if (kb + 1 < nkb) load_tile(kb + 1);
+    if (kb > kmax) continue;
+    // S^T = K Q^T over the 4 key blocks of 16
+    f32x4_t st[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const int row = kt * 16 + ql;
+      st[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t kf[3] = {xfrag(lk, row, 4 * ks + g), xfrag(lk + XPL, row, 4 * ks + g),
+                                xfrag(lk + 2 * XPL, row, 4 * ks + g)};
+        st[kt] = x6_dot(kf, qp[ks], st[kt]);
+      }
+    }
+    if (kb * 64 + 63 > q0 || kb * 64 + 63 >= S) {   // causal / sequence-end mask (wave-uniform branch)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * 64 + kt * 16 + 4 * g + r;
+          if (key > qrow || key >= S) st[kt][r] = -INFINITY;
+        }
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[kt][r]);
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float mc = mloc * FLOG2E;
+    if (__builtin_amdgcn_ballot_w64(mc > m2 + FTAU)) {  // wave-uniform lazy rescale
+      const float mn = fmaxf(m2, mc);
+      const float alpha = exp2f(m2 - mn);
+      m2 = mn;
+      l_run *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) oacc[d] *= alpha;
+    }
+    float ps = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = exp2f(fmaf(st[kt][r], FLOG2E, -m2));
+        st[kt][r] = pv;
+        ps += pv;
+      }
+    l_run += ps;
+    // O^T += V^T P^T: k-step s contracts the keys {32 s + 4g + r, 32 s + 16 + 4g + r}
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      float pv8[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { pv8[r] = st[2 * sk][r]; pv8[4 + r] = st[2 * sk + 1][r]; }
+      bf16x8_t pp[3];
+      split_frag(pv8, pp[0], pp[1], pp[2]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int row = dt * 16 + ql;
+        const bf16x8_t vf[3] = {xfrag(lv, row, 4 * sk + g), xfrag(lv + XPL, row, 4 * sk + g),
+                                xfrag(lv + 2 * XPL, row, 4 * sk + g)};
+        oacc[dt] = x6_dot(vf, pp, oacc[dt]);
+      }
+    }
+  }
+
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (qrow < S) {
+    const float inv = 1.f / l_run;
+    const int W = Hq * 64;
+    if constexpr (X6OUT) {
+      bf16_t* orow = (bf16_t*)o + ((size_t)b * S + qrow) * (size_t)(3 * W);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
+        store_x6_4(orow, W, h * 64 + dt * 16 + 4 * g, v);
+      }
+    } else {
+      float* orow = (float*)o + ((size_t)b * S + qrow) * (size_t)W + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(orow + dt * 16 + 4 * g) = oacc[dt] * inv;
+    }
+    if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = m2 * 0.6931471805599453f + logf(l_run);
+  }
+}
+
 // Last-row probabilities: one workgroup per (b, h); P[S-1, j] = softmax_j(q_{S-1} . k_j), fp32 throughout.
 __global__ __launch_bounds__(256) void attn_lastrow_f32_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                                float* __restrict__ out, int Hq, int Hkv, int S) {
@@ -315,6 +542,13 @@ __global__ __launch_bounds__(256) void attn_colsum_f32_kernel(const float* __res
   }
 }
 
+static int g_attn_f32_variant = 2;   // 0: split-bf16 (X6) MFMA kernel, 64 query rows per workgroup; 2 (default): the same
+                                     // with 128 rows (8 waves); 1: native f32 MFMA kernel (A/B)
+EDGE_API int edge_attn_f32_set_variant(int v) {
+  g_attn_f32_variant = v;
+  return 0;
+}
+
 // out_x6 != 0: O as a 3-plane X6 activation [B*S, 3*Hq*64] (bf16 planes) for the O-projection; else fp32
 // [B*S, Hq*64].
 EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float* vt, void* o, float* lse,
@@ -324,12 +558,30 @@ EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float
   if (Hq % Hkv || s_pad % 64 || s_pad < S) return (int)hipErrorInvalidValue;
   const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
   const dim3 grid(8 * maxcnt * G * ((S + 63) / 64));
-  if (out_x6)
+  if (g_attn_f32_variant == 0 || g_attn_f32_variant == 2) {   // split-bf16 matrix cores (0: 64 query rows / WG)
+    const bool w8 = g_attn_f32_variant == 2;
+    const dim3 gx(8 * maxcnt * G * ((S + (w8 ? 127 : 63)) / (w8 ? 128 : 64)));
+    if (w8) {
+      if (out_x6)
+        hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<true, 8>), gx, dim3(512), 6 * XPL, st, q, k, vt, o, lse, n_rows,
+                           B, Hq, Hkv, S, s_pad);
+      else
+        hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<false, 8>), gx, dim3(512), 6 * XPL, st, q, k, vt, o, lse, n_rows,
+                           B, Hq, Hkv, S, s_pad);
+    } else if (out_x6) {
+      hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<true, 4>), gx, dim3(256), 6 * XPL, st, q, k, vt, o, lse, n_rows,
+                         B, Hq, Hkv, S, s_pad);
+    } else {
+      hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<false, 4>), gx, dim3(256), 6 * XPL, st, q, k, vt, o, lse, n_rows,
+                         B, Hq, Hkv, S, s_pad);
+    }
+  } else if (out_x6) {             // f32 matrix cores
     hipLaunchKernelGGL(flash_attn_fwd_f32_kernel<true>, grid, dim3(256), 4 * FTILE, st, q, k, vt, o, lse, n_rows, B,
                        Hq, Hkv, S, s_pad);
-  else
+  } else {
     hipLaunchKernelGGL(flash_attn_fwd_f32_kernel<false>, grid, dim3(256), 4 * FTILE, st, q, k, vt, o, lse, n_rows, B,
                        Hq, Hkv, S, s_pad);
+  }
   return (int)hipGetLastError();
 }
 

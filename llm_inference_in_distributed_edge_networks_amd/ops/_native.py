@@ -48,6 +48,7 @@ _SIGS = {
     "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_set_variant": [c_i],
+    "edge_attn_f32_set_variant": [c_i],
     "edge_attn_lastrow": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_colsum": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_head_combine": [c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p],

@@ -127,7 +127,19 @@ def test_qkv_rope_x6(B, S, Hq, Hkv, rot):
 
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (3, 100, 14, 2), (1, 2048, 8, 8), (2, 64, 4, 1)])
 @pytest.mark.parametrize("x6", [False, True])
-def test_attention_f32(B, S, Hq, Hkv, x6):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_attention_f32(B, S, Hq, Hkv, x6, variant):
+    """fp32 attention vs fp64: split-bf16 MFMA kernel (variant 0, 64 query rows per workgroup; 2: 128 rows) and the
+    native f32 MFMA kernel (1).  The error is dominated by the fp32 exp2 (~5e-6 relative L2 for both kernels; bf16
+    attention is ~1e-3)."""
+    ops._native.lib().edge_attn_f32_set_variant(variant)
+    try:
+        _attention_f32_case(B, S, Hq, Hkv, x6)
+    finally:
+        ops._native.lib().edge_attn_f32_set_variant(2)
+
+
+def _attention_f32_case(B, S, Hq, Hkv, x6):
     q = rnd(B, Hq, S, 64, seed=40) * 0.5
     k = rnd(B, Hkv, S, 64, seed=41) * 2
     v = rnd(B, Hkv, S, 64, seed=42)
@@ -138,7 +150,7 @@ def test_attention_f32(B, S, Hq, Hkv, x6):
     ro, rl = R.attention(q.double(), k.double(), vt.double(), S, need_lse=True)
     if x6:
         o = R.x6_to_f32(o)
-    assert rel_err(o, ro) < 5e-6
+    assert rel_err(o, ro) < 1e-5
     assert float((lse.cpu().double() - rl).abs().max()) < 5e-5
 
 

@@ -18,7 +18,10 @@ def main():
     ap.add_argument("--Hkv", type=int, default=2)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--fp32", action="store_true", help="the fp32-mode kernels: split-bf16 (x6) vs native f32 MFMA")
     a = ap.parse_args()
+    if a.fp32:
+        return bench_fp32(a)
     B, S, Hq, Hkv = a.B, a.S, a.Hq, a.Hkv
     g = torch.Generator().manual_seed(0)
     q = (torch.randn(B, Hq, S, 64, generator=g) * 0.125).bfloat16().cuda()
@@ -43,6 +46,32 @@ def main():
     ops.set_attn_variant(4)
     out = {k_: {"us": round(min(v), 2), "TFLOPs": round(flop / min(v) * 1e-6, 1)} for k_, v in res.items()}
     print(json.dumps({"shape": [B, S, Hq, Hkv], **out}))
+
+
+def bench_fp32(a):
+    B, S, Hq, Hkv = a.B, a.S, a.Hq, a.Hkv
+    g = torch.Generator().manual_seed(0)
+    q = (torch.randn(B, Hq, S, 64, generator=g) * 0.125).cuda()
+    k = torch.randn(B, Hkv, S, 64, generator=g).cuda()
+    vt = torch.randn(B, Hkv, 64, ops.s_pad(S), generator=g).cuda()
+    flop = 4.0 * B * Hq * 64 * sum(i + 1 for i in range(S))
+    res = {}
+    lib = ops._native.lib()
+    for _ in range(a.rounds):
+        for v, name in ((0, "x6_bf16_mfma"), (2, "x6_bf16_mfma_128rows"), (1, "f32_mfma")):
+            lib.edge_attn_f32_set_variant(v)
+            for x6 in (False, True):
+                ops.attention(q, k, vt, S, need_lse=True, x6=x6)
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                for _ in range(a.iters):
+                    ops.attention(q, k, vt, S, need_lse=True, x6=x6)
+                en.record()
+                torch.cuda.synchronize()
+                res.setdefault(f"{name}{'_x6out' if x6 else ''}", []).append(st.elapsed_time(en) / a.iters * 1e3)
+    lib.edge_attn_f32_set_variant(2)
+    out = {k_: {"us": round(min(v), 2), "TFLOPs_fp32": round(flop / min(v) * 1e-6, 1)} for k_, v in res.items()}
+    print(json.dumps({"shape": [B, S, Hq, Hkv], "dtype": "fp32", **out}))
 
 
 if __name__ == "__main__":
