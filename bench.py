@@ -15,7 +15,7 @@ the same stages in one process on the one GPU (the boundary is still encoded and
 
 Precision: ``--dtype fp32`` (default) is the reference's precision (it loads its models without a torch_dtype,
 ``Experiments/Qwen2-0.5B/qwen_layer_wise.py:17``): fp32 residual stream, norms, softmax, attention (f32 matrix
-cores) and codec, GEMMs on X6 split-bf16 operands (fp32-accurate, see ``ops.reference.x6_act``).  A second, separately
+cores) and codec, GEMMs on h3 split-fp16 operands (fp32-accurate, see ``ops.reference.h3_act``).  A second, separately
 timed run of the bf16 mode is reported as ``value_bf16`` (``--no-bf16`` skips it).
 
 ``value`` = window tokens processed per second over the whole job (every window is a full 512-token forward, as in
@@ -201,7 +201,7 @@ def main():
                    "stage_layers": [[r.start, r.stop - 1] for r in (plan.stage_layers(s) for s in range(pp))],
                    "codec": a.codec, "ratio": a.ratio, "importance": a.method,
                    "transport": a.transport if dist_pp else "local", "hip_graphs": not a.no_graphs,
-                   "gemm_precision": "x6 split-bf16 (fp32-accurate)" if dname == "fp32" else "bf16"},
+                   "gemm_precision": "h3 split-fp16 (fp32-accurate)" if dname == "fp32" else "bf16"},
         "baseline_note": "T4 fp32, 1 eager + 100 split forwards of 512 tokens per window in 16.2 s (BASELINE.md)",
         "scored_tokens_per_s": round(scored_per_step * a.steps / dt, 1),
         "wire_bytes_per_token": [round(w, 2) for w in wires],

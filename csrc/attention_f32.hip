@@ -2,17 +2,17 @@
 // attention half of the framework's fp32 execution mode (the reference evaluates its models in fp32:
 // Experiments/Qwen2-0.5B/qwen_layer_wise.py:17, Experiments/Pythia-70M/pythia_model.py:25 load without a dtype).
 //
-// flash_attn_fwd_x6 (default) runs the matrix work as split-bf16 products on the bf16 matrix cores (the X6 scheme of
-// the GEMMs, common.h): 1.5x the native f32 kernel, flash_attn_fwd_f32, which runs v_mfma_f32_16x16x4_f32 (exact
+// flash_attn_fwd_x6 (default) runs the matrix work as split-bf16 products on the bf16 matrix cores (three bf16 planes,
+// six plane products per fp32 product, common.h split3): 1.5x the native f32 kernel, flash_attn_fwd_f32, which runs v_mfma_f32_16x16x4_f32 (exact
 // fp32 products and fp32 accumulation) and stays for A/B and the importance scorers.
 //
 //   flash_attn_fwd_f32 : O = softmax(Q K^T) V, online softmax, optional row LSE; O written as fp32 rows or
-//                        directly in the X6 layout the O-projection GEMM consumes.
+//                        directly in the h3 layout (common.h) the O-projection GEMM consumes.
 //   attn_lastrow_f32   : P[S-1, :] per head.
 //   attn_colsum_f32    : sum_i P[i, j] per head from Q, K and the row LSE (second sweep, key block outer).
 //
 // Layouts as the bf16 kernels (attention.hip): q [B,Hq,S,64] (RoPE applied, pre-scaled), k [B,Hkv,S,64],
-// vt [B,Hkv,64,s_pad] (V^T, zero padded), o [B*S, Hq*64] (fp32) or [B*S, 3*Hq*64] (3-plane X6).
+// vt [B,Hkv,64,s_pad] (V^T, zero padded), o [B*S, Hq*64] (fp32) or [B*S, 2*Hq*64] (2-plane h3).
 //
 // 16x16x4 f32 MFMA operand layout: lane l supplies A[m = l&15][k = l>>4] and B[k = l>>4][n = l&15]; the result
 // D[m][n] sits in lane l, register r at m = 4(l>>4) + r, n = l&15.  The contraction index k of MFMA number kk is
@@ -126,13 +126,13 @@ __device__ __forceinline__ void f32_tile(const char* lk, const char* lv, const f
 // One workgroup = 4 waves = 64 query rows of one (window, head); each wave owns 16 rows.  K / V^T tiles of 64
 // keys are DMA'd to LDS (global_load_lds, swizzled source) and double-buffered; XCD-aware block order as the bf16
 // v2 kernel: the query blocks and heads of one (window, kv head) group run on one XCD, heavy blocks first.
-template <bool X6OUT>
+template <bool H3OUT>
 __global__ __launch_bounds__(256, 2) void flash_attn_fwd_f32_kernel(const float* __restrict__ q,
                                                                    const float* __restrict__ k,
                                                                    const float* __restrict__ vt, void* __restrict__ o,
                                                                    float* __restrict__ lse,
                                                                    const float* __restrict__ n_rows, int B, int Hq,
-                                                                   int Hkv, int S, int s_pad) {
+                                                                   int Hkv, int S, int s_pad, float h3s) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
   const int nqb = (S + 63) / 64;
@@ -191,12 +191,12 @@ __global__ __launch_bounds__(256, 2) void flash_attn_fwd_f32_kernel(const float*
   if (qrow < S) {
     const float inv = 1.f / l_run;
     const int W = Hq * 64;
-    if constexpr (X6OUT) {
-      bf16_t* orow = (bf16_t*)o + ((size_t)b * S + qrow) * (size_t)(3 * W);
+    if constexpr (H3OUT) {
+      f16_t* orow = (f16_t*)o + ((size_t)b * S + qrow) * (size_t)(2 * W);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
-        store_x6_4(orow, W, h * 64 + dt * 16 + 4 * g, v);
+        store_h3_4(orow, W, h * 64 + dt * 16 + 4 * g, v, h3s);
       }
     } else {
       float* orow = (float*)o + ((size_t)b * S + qrow) * (size_t)W + h * 64;
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_fwd_f32_kernel(const float*
   }
 }
 
-// ---- split-bf16 ("X6") flash attention: the same fp32-accurate result on the bf16 matrix cores -------------------
+// ---- split-bf16 ("x6") flash attention: the same fp32-accurate result on the bf16 matrix cores -------------------
 // q, k, v and the probabilities are split into three bf16 planes (common.h split3) and every product is the sum of
 // the six plane products a_i b_j with i + j <= 2 (v_mfma_f32_16x16x32_bf16; dropped terms 2^-27 relative, every
 // bf16 x bf16 product exact in the fp32 accumulator): 96 bf16 MFMAs of 16 cycles per 16-query x 64-key tile against
@@ -248,13 +248,13 @@ __device__ __forceinline__ f32x4_t x6_dot(const bf16x8_t (&a)[3], const bf16x8_t
 }  // namespace
 
 // NW waves of 16 query rows per workgroup (4: 64 rows, 8: 128 rows sharing each staged K / V^T tile)
-template <bool X6OUT, int NW>
+template <bool H3OUT, int NW>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(const float* __restrict__ q,
                                                                   const float* __restrict__ k,
                                                                   const float* __restrict__ vt, void* __restrict__ o,
                                                                   float* __restrict__ lse,
                                                                   const float* __restrict__ n_rows, int B, int Hq,
-                                                                  int Hkv, int S, int s_pad) {
+                                                                  int Hkv, int S, int s_pad, float h3s) {
   extern __shared__ __attribute__((aligned(16))) char smem[];   // K planes (3 x 8 KiB), V^T planes (3 x 8 KiB)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
   constexpr int QB = 16 * NW;          // query rows per workgroup
@@ -418,12 +418,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
   if (qrow < S) {
     const float inv = 1.f / l_run;
     const int W = Hq * 64;
-    if constexpr (X6OUT) {
-      bf16_t* orow = (bf16_t*)o + ((size_t)b * S + qrow) * (size_t)(3 * W);
+    if constexpr (H3OUT) {
+      f16_t* orow = (f16_t*)o + ((size_t)b * S + qrow) * (size_t)(2 * W);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
-        store_x6_4(orow, W, h * 64 + dt * 16 + 4 * g, v);
+        store_h3_4(orow, W, h * 64 + dt * 16 + 4 * g, v, h3s);
       }
     } else {
       float* orow = (float*)o + ((size_t)b * S + qrow) * (size_t)W + h * 64;
@@ -542,45 +542,45 @@ __global__ __launch_bounds__(256) void attn_colsum_f32_kernel(const float* __res
   }
 }
 
-static int g_attn_f32_variant = 2;   // 0: split-bf16 (X6) MFMA kernel, 64 query rows per workgroup; 2 (default): the same
+static int g_attn_f32_variant = 2;   // 0: split-bf16 (x6) MFMA kernel, 64 query rows per workgroup; 2 (default): the same
                                      // with 128 rows (8 waves); 1: native f32 MFMA kernel (A/B)
 EDGE_API int edge_attn_f32_set_variant(int v) {
   g_attn_f32_variant = v;
   return 0;
 }
 
-// out_x6 != 0: O as a 3-plane X6 activation [B*S, 3*Hq*64] (bf16 planes) for the O-projection; else fp32
-// [B*S, Hq*64].
+// out_h3_scale > 0: O as a 2-plane h3 activation [B*S, 2*Hq*64] (fp16 planes at that scale) for the O-projection;
+// 0: fp32 [B*S, Hq*64].
 EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float* vt, void* o, float* lse,
-                                     const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, int out_x6,
+                                     const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float out_h3_scale,
                                      hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
-  if (Hq % Hkv || s_pad % 64 || s_pad < S) return (int)hipErrorInvalidValue;
+  if (Hq % Hkv || s_pad % 64 || s_pad < S || out_h3_scale < 0.f) return (int)hipErrorInvalidValue;
   const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
   const dim3 grid(8 * maxcnt * G * ((S + 63) / 64));
   if (g_attn_f32_variant == 0 || g_attn_f32_variant == 2) {   // split-bf16 matrix cores (0: 64 query rows / WG)
     const bool w8 = g_attn_f32_variant == 2;
     const dim3 gx(8 * maxcnt * G * ((S + (w8 ? 127 : 63)) / (w8 ? 128 : 64)));
     if (w8) {
-      if (out_x6)
+      if (out_h3_scale > 0.f)
         hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<true, 8>), gx, dim3(512), 6 * XPL, st, q, k, vt, o, lse, n_rows,
-                           B, Hq, Hkv, S, s_pad);
+                           B, Hq, Hkv, S, s_pad, out_h3_scale);
       else
         hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<false, 8>), gx, dim3(512), 6 * XPL, st, q, k, vt, o, lse, n_rows,
-                           B, Hq, Hkv, S, s_pad);
-    } else if (out_x6) {
+                           B, Hq, Hkv, S, s_pad, out_h3_scale);
+    } else if (out_h3_scale > 0.f) {
       hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<true, 4>), gx, dim3(256), 6 * XPL, st, q, k, vt, o, lse, n_rows,
-                         B, Hq, Hkv, S, s_pad);
+                         B, Hq, Hkv, S, s_pad, out_h3_scale);
     } else {
       hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<false, 4>), gx, dim3(256), 6 * XPL, st, q, k, vt, o, lse, n_rows,
-                         B, Hq, Hkv, S, s_pad);
+                         B, Hq, Hkv, S, s_pad, out_h3_scale);
     }
-  } else if (out_x6) {             // f32 matrix cores
+  } else if (out_h3_scale > 0.f) {             // f32 matrix cores
     hipLaunchKernelGGL(flash_attn_fwd_f32_kernel<true>, grid, dim3(256), 4 * FTILE, st, q, k, vt, o, lse, n_rows, B,
-                       Hq, Hkv, S, s_pad);
+                       Hq, Hkv, S, s_pad, out_h3_scale);
   } else {
     hipLaunchKernelGGL(flash_attn_fwd_f32_kernel<false>, grid, dim3(256), 4 * FTILE, st, q, k, vt, o, lse, n_rows, B,
-                       Hq, Hkv, S, s_pad);
+                       Hq, Hkv, S, s_pad, out_h3_scale);
   }
   return (int)hipGetLastError();
 }

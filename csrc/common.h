@@ -24,52 +24,65 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// ---- fp32 execution by split-bf16 MFMA ("x6") -------------------------------------------------------------
-// x = x0 + x1 + x2 exactly, each a bf16 (8 significant bits; the residual after two round-to-nearest steps has at
-// most 8 significant bits left).  A product x*y is then sum_{i+j<=2} xi*yj up to terms of relative size 2^-27,
-// below fp32's own rounding (2^-24), and every bf16 x bf16 product is exact in the fp32 MFMA accumulator.
-// The six terms are a K-concatenation, so an ordinary bf16 MFMA GEMM over K' = 6K computes the fp32-accurate
-// product with the K-blocks  A' = [a2 | a0 | a1 | a1 | a0 | a0],  B' = [b0 | b2 | b1 | b0 | b1 | b0]
-// (the small terms first: they are accumulated before the large ones).  Weights are stored as B' [N, 6K]; an
-// activation is stored once per plane, [a0 | a1 | a2] ([rows, 3K], half the bytes of A'), and the GEMM's A loader
-// reads K-block j of A' from plane x6_aplane(j) (x6_acol).
-constexpr int X6_TERMS = 6;
+// x = x0 + x1 + x2 exactly, each a bf16 (8 significant bits): the split-bf16 products of the fp32 attention kernel
+// (attention_f32.hip x6_dot: the six plane products with i + j <= 2, exact to 2^-27 relative).
 __device__ __forceinline__ void split3(float x, float& p0, float& p1, float& p2) {
   p0 = (float)(__bf16)x;
   const float r = x - p0;
   p1 = (float)(__bf16)r;
   p2 = (float)(__bf16)(r - p1);
 }
-// column of the 3-plane activation row holding column kp of A' (K = plane width; K-blocks never straddle a K-tile)
-__device__ __forceinline__ int x6_acol(int kp, int K) {
-  const int j = kp / K;                          // A' block 0..5, planes 2 0 1 1 0 0
-  return ((0x1102 >> (4 * j)) & 3) * K + (kp - j * K);
+
+// ---- fp32 GEMMs by split-fp16 MFMA ("h3") ---------------------------------------------------------------
+// A GEMM operand is scaled by a power of two s (exact) and split into two fp16 planes, s x = hi + lo with
+// hi = fp16(s x) (11 significant bits) and lo = fp16(s x - hi) (the residual, exact in fp32; 11 more bits).  The
+// fp32 product is then hi_a hi_b + hi_a lo_b + lo_a hi_b (the dropped lo_a lo_b is 2^-22 relative and the residual
+// rounding 2^-23: measured error below the CPU fp32 GEMM's own, tools/h3_error.py), and every fp16 x fp16 product
+// is exact in the fp32 MFMA accumulator.  The three terms are a K-concatenation, so an ordinary fp16 MFMA GEMM over
+// K' = 3K computes it with the K-blocks  A' = [a_lo | a_hi | a_hi],  B' = [b_hi | b_lo | b_hi]  (small terms
+// first), at the bf16/fp16 matrix-core rate - half the MFMAs of a three-plane bf16 split (six products).  The
+// epilogue multiplies by alpha = 1 / (s_a s_b).  The scales keep every plane inside the fp16 range: the model
+// derives s_a per GEMM input from a bound on |x| that holds for any input (models/model.py h3 scales: RMSNorm /
+// LayerNorm outputs, attention outputs and SwiGLU / GELU outputs are bounded by the weights), s_b from max |w|.
+// Weights are stored as B' [N, 3K]; an activation once per plane, [hi | lo] ([rows, 2K]), and the GEMM's A loader
+// reads K-block j of A' from plane (1 0 0)[j] (h3_acol).
+typedef uint16_t f16_t;   // fp16 storage as raw 16-bit words
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+constexpr int H3_TERMS = 3;
+__device__ __forceinline__ void split2h(float x, float& hi, float& lo) {
+  hi = (float)(_Float16)x;
+  lo = (float)(_Float16)(x - hi);
 }
-// Store 4 consecutive values v[0..3] at column `col` of an X6 activation row (plane width K): three 8-byte stores.
-__device__ __forceinline__ void store_x6_4(bf16_t* __restrict__ row, int K, int col, const float (&v)[4]) {
-  float p[3][4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) split3(v[e], p[0][e], p[1][e], p[2][e]);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    u32x2_t w;
-    w[0] = pack_bf2(p[i][0], p[i][1]);
-    w[1] = pack_bf2(p[i][2], p[i][3]);
-    *(u32x2_t*)(row + i * (size_t)K + col) = w;
-  }
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, f16x2_t{(_Float16)a, (_Float16)b});
 }
-// 8 consecutive values: three 16-byte stores.
-__device__ __forceinline__ void store_x6_8(bf16_t* __restrict__ row, int K, int col, const float (&v)[8]) {
-  float p[3][8];
+// column of the 2-plane activation row holding column kp of A' (K = plane width; K-blocks never straddle a K-tile)
+__device__ __forceinline__ int h3_acol(int kp, int K) {
+  const int j = kp / K;                          // A' block 0..2: planes lo hi hi
+  return (j == 0 ? K : 0) + (kp - j * K);
+}
+// Store s * v[0..3] at column `col` of an h3 activation row (plane width K): two 8-byte stores.
+__device__ __forceinline__ void store_h3_4(f16_t* __restrict__ row, int K, int col, const float (&v)[4], float s) {
+  float hi[4], lo[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) split3(v[e], p[0][e], p[1][e], p[2][e]);
+  for (int e = 0; e < 4; ++e) split2h(v[e] * s, hi[e], lo[e]);
+  *(u32x2_t*)(row + col) = u32x2_t{pack_h2(hi[0], hi[1]), pack_h2(hi[2], hi[3])};
+  *(u32x2_t*)(row + (size_t)K + col) = u32x2_t{pack_h2(lo[0], lo[1]), pack_h2(lo[2], lo[3])};
+}
+// 8 consecutive values: two 16-byte stores.
+__device__ __forceinline__ void store_h3_8(f16_t* __restrict__ row, int K, int col, const float (&v)[8], float s) {
+  float hi[8], lo[8];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    u32x4_t w;
+  for (int e = 0; e < 8; ++e) split2h(v[e] * s, hi[e], lo[e]);
+  u32x4_t wh, wl;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) w[e] = pack_bf2(p[i][2 * e], p[i][2 * e + 1]);
-    *(u32x4_t*)(row + i * (size_t)K + col) = w;
+  for (int e = 0; e < 4; ++e) {
+    wh[e] = pack_h2(hi[2 * e], hi[2 * e + 1]);
+    wl[e] = pack_h2(lo[2 * e], lo[2 * e + 1]);
   }
+  *(u32x4_t*)(row + col) = wh;
+  *(u32x4_t*)(row + (size_t)K + col) = wl;
 }
 
 // silu(x) = x / (1 + e^-x) on the hardware transcendentals (v_exp_f32, v_rcp_f32, ~1 ulp): a plain '/' compiles

@@ -18,10 +18,11 @@
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_GELU = 4, EPI_SWIGLU = 5,
        EPI_QKV_ROPE = 6, EPI_LSE = 7,
-       // fp32 execution (operands in the X6 split-bf16 layout, common.h; K is the concatenated 6K): fp32 outputs,
-       // fp32 bias / residual, or X6-layout outputs for epilogues whose result feeds the next GEMM
-       EPI_F32 = 8, EPI_F32_BIAS = 9, EPI_F32_RESID = 10, EPI_F32_BIAS_RESID = 11, EPI_X6_BIAS_GELU = 12,
-       EPI_X6_SWIGLU = 13, EPI_F32_QKV_ROPE = 14 };
+       // fp32 execution (operands in the h3 split-fp16 layout, common.h; K is the concatenated 3K; fp16 MFMAs): fp32
+       // outputs, fp32 bias / residual, h3-layout outputs for epilogues whose result feeds the next GEMM, or the LM
+       // head's LSE partials
+       EPI_F32 = 8, EPI_F32_BIAS = 9, EPI_F32_RESID = 10, EPI_F32_BIAS_RESID = 11, EPI_H3_BIAS_GELU = 12,
+       EPI_H3_SWIGLU = 13, EPI_F32_QKV_ROPE = 14, EPI_F32_LSE = 15 };
 constexpr bool epi_f32(int e) { return e >= EPI_F32; }
 constexpr bool epi_plain(int e) {  // none / bias / residual epilogues (the 256x224 kernel's set)
   return e == EPI_NONE || e == EPI_BIAS || e == EPI_RESID || e == EPI_BIAS_RESID || e == EPI_F32 ||
@@ -32,7 +33,8 @@ struct GemmArgs {
   const bf16_t* A; const bf16_t* B; bf16_t* C;
   int M, N, K, lda, ldb, ldc;
   const bf16_t* bias; const bf16_t* resid; int ldr;
-  // fp32 epilogues: fp32 output / bias / residual (C may alias resid), X6 outputs go to C with ldc = 6 * width
+  // fp32 epilogues: fp32 output / bias / residual (C may alias resid), h3 outputs go to C (fp16 planes) with
+  // ldc = 2 * width
   float* Cf; const float* biasf; const float* residf;
   float* qf; float* kf; float* vtf;
   // QKV_ROPE
@@ -52,11 +54,23 @@ struct GemmArgs {
   int rs_lds;    // persistent 256x256: row scales DMA'd to LDS in the last K-tile (default 1; 0 = A/B baseline)
   int skip_epi;  // timing ablation only (wrong results): 1 = no epilogue (gemm_bf16 / w7 kernels); 2 = persistent
                  // 256x256 SwiGLU epilogue computed but not stored
-  int x6k;       // > 0: A is a 3-plane X6 activation [M, 3 x6k] (common.h x6_acol) of the K' = 6 x6k GEMM
+  int h3k;       // > 0: A is a 2-plane h3 activation [M, 2 h3k] (common.h h3_acol) of the K' = 3 h3k GEMM
+  float alpha = 1.f;      // h3: 1 / (s_a s_b), the product's scale (applied with the row scale)
+  float out_scale = 1.f;  // h3 outputs (SwiGLU / GELU): the next GEMM's input scale s_a
 };
 
 // element column of A holding GEMM column k (k a K-tile start)
-__device__ __forceinline__ int a_kcol(const GemmArgs& a, int k) { return a.x6k ? x6_acol(k, a.x6k) : k; }
+__device__ __forceinline__ int a_kcol(const GemmArgs& a, int k) { return a.h3k ? h3_acol(k, a.h3k) : k; }
+
+// 16x16x32 MFMA on bf16 (bf16 mode) or fp16 (h3 planes of the fp32 mode) operands held as raw 16-bit words
+template <bool F16>
+__device__ __forceinline__ f32x4_t mfma16x32(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
@@ -123,7 +137,7 @@ __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
 
 // ---- fp32-execution epilogues (EPI >= EPI_F32).  Same ownership as gemm_epilogue below: lane owns rows
 // m0 + wm*WTM + i*16 + (lane&15) and columns nw + j*16 + 4*(lane>>4) + r of the wave's 64-column slab, so every
-// output is 4 consecutive fp32 values (one 16-byte store) or 4 consecutive values of each of the six X6 blocks.
+// output is 4 consecutive fp32 values (one 16-byte store) or 4 consecutive values of each of the two h3 planes.
 template <int EPI, int RH, class CF>
 __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&acc)[CF::MI][4], int m0, int nw,
                                                   int lane, int wm) {
@@ -205,11 +219,11 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
     if (m >= a.M) continue;
-    if constexpr (EPI == EPI_X6_SWIGLU) {
+    if constexpr (EPI == EPI_H3_SWIGLU) {
       // gate/up interleaved in 16-column blocks: acc[i][2p] gate, acc[i][2p+1] up of output columns
-      // nw/2 + 16p + 4g + r; silu via v_exp_f32 / v_rcp_f32 (about 1 ulp each: fp32-level, as the X6 products; the
+      // nw/2 + 16p + 4g + r; silu via v_exp_f32 / v_rcp_f32 (about 1 ulp each: fp32-level, as the h3 products; the
       // IEEE-exact expf and division were a third of this epilogue's VALU time)
-      bf16_t* row = a.C + (size_t)m * a.ldc;
+      f16_t* row = a.C + (size_t)m * a.ldc;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         float o[4];
@@ -218,22 +232,22 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
           const float gg = acc[i][2 * p][r], uu = acc[i][2 * p + 1][r];
           o[r] = gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * uu;
         }
-        store_x6_4(row, a.N / 2, nw / 2 + p * 16 + g * 4, o);
+        store_h3_4(row, a.N / 2, nw / 2 + p * 16 + g * 4, o, a.out_scale);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = nw + j * 16 + g * 4;
         float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID || EPI == EPI_X6_BIAS_GELU) {
+        if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID || EPI == EPI_H3_BIAS_GELU) {
           const f32x4_t bw = *(const f32x4_t*)(a.biasf + n);
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] += bw[r];
         }
-        if constexpr (EPI == EPI_X6_BIAS_GELU) {
+        if constexpr (EPI == EPI_H3_BIAS_GELU) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
-          store_x6_4(a.C + (size_t)m * a.ldc, a.N, n, o);
+          store_h3_4(a.C + (size_t)m * a.ldc, a.N, n, o, a.out_scale);
         } else {
           if constexpr (EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID) {
             const f32x4_t rw = *(const f32x4_t*)(a.residf + (size_t)m * a.ldr + n);
@@ -257,17 +271,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
   const int nw = n0 + wn * 64;  // first column of this wave's 64-wide slab
   if (nw >= a.N) return;        // slab beyond N in a partial last column tile (wave-uniform)
 
-  if (a.rscale || a.ssq_in) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
+  if constexpr (epi_f32(EPI)) {  // h3 operands: the product's scale alpha with the optional row scale
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const float f = rs[i] * a.alpha;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] *= f;
+    }
+    if constexpr (EPI != EPI_F32_LSE) return gemm_epilogue_f32<EPI, RH, CF>(a, acc, m0, nw, lane, wm);
+  } else if (a.rscale || a.ssq_in) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] *= rs[i];
   }
-  if constexpr (epi_f32(EPI)) {
-    return gemm_epilogue_f32<EPI, RH, CF>(a, acc, m0, nw, lane, wm);
-  }
 
-  if constexpr (EPI == EPI_LSE) {
+  if constexpr (EPI == EPI_LSE || EPI == EPI_F32_LSE) {
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
@@ -572,6 +591,9 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #define MFMA_DRAIN() asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory")
 #define ACC_SETTLE() asm volatile("s_nop 4" ::: "memory")
 #define MFMA_AGPR_FIRST(acc, a, b) asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b))
+// fp16 operands (the h3 planes of the fp32 mode)
+#define MFMA_AGPR_H(acc, a, b) asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b))
+#define MFMA_AGPR_FIRST_H(acc, a, b) asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b))
 
 // Persistent tile walk of workgroup bid out of G.  Workgroups are dispatched round-robin over the 8 XCDs
 // (bid & 7), and xcd_remap numbers the workgroups of one XCD consecutively (base .. base+cx-1).
@@ -650,7 +672,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[mg * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[mg * 4 + i][j], 0, 0, 0);
+        acc[mg * 4 + i][j] = mfma16x32<epi_f32(EPI)>(FB[j], FA[i], acc[mg * 4 + i][j]);
   };
   auto stage = [&](int k0, char* buf) {
     stage_issue<CF::A_INSTR, NW>(pa, a_kcol(a, k0), buf, wave);
@@ -1416,7 +1438,7 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
         const int m = m0 + wm * 64 + (ih + i) * 16 + (lane & 15);
         if (m >= a.M) continue;
         float* row = a.Cf + (size_t)m * a.ldc + nw + g * 4;
-        const float rsm = a.rscale ? a.rscale[m] : 1.f;
+        const float rsm = (a.rscale ? a.rscale[m] : 1.f) * a.alpha;
 #pragma unroll
         for (int j = 0; j < w7::NJ; ++j) {
           f32x4_t o = acc[ih + i][j] * rsm;
@@ -1572,7 +1594,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     if (r < 8) glds16(sa + kba + oa[r], buf + (r * 4 + wave) * 1024);
     else glds16(sb + kb + ob[r - 8], buf + BOFF + ((r - 8) * 4 + wave) * 1024);
   };
-  int st_kba = a_kcol(a, 0) * 2;   // byte offset of the stream K-tile's A columns (3-plane X6 operands: the plane remap, computed
+  int st_kba = a_kcol(a, 0) * 2;   // byte offset of the stream K-tile's A columns (2-plane h3 operands: the plane remap, computed
                     // once per K-tile where the wave waits anyway, not on the MFMA issue path)
   auto advance_stage = [&]() {   // the DMA stream stops (repeats its last K-tile) at the end
     ++st_q;
@@ -1652,8 +1674,13 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
 #pragma unroll
       for (int n = (rr == 0 ? 0 : w4::slot_pos<MF, NR>(rr - 1) + 1); n <= w4::slot_pos<MF, NR>(rr); ++n) {
         const int i = n / NJ, j = n % NJ;
-        if constexpr (first) MFMA_AGPR_FIRST(acc[i][j], FB[j], FA[i]);
-        else MFMA_AGPR(acc[i][j], FB[j], FA[i]);
+        if constexpr (epi_f32(EPI)) {
+          if constexpr (first) MFMA_AGPR_FIRST_H(acc[i][j], FB[j], FA[i]);
+          else MFMA_AGPR_H(acc[i][j], FB[j], FA[i]);
+        } else {
+          if constexpr (first) MFMA_AGPR_FIRST(acc[i][j], FB[j], FA[i]);
+          else MFMA_AGPR(acc[i][j], FB[j], FA[i]);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (read_on) {
@@ -1853,7 +1880,7 @@ __global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (h == 1 && j == 3) continue;
-        acc[i][h * 4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j], FA[i], acc[i][h * 4 + j], 0, 0, 0);
+        acc[i][h * 4 + j] = mfma16x32<epi_f32(EPI)>(FB[j], FA[i], acc[i][h * 4 + j]);
       }
   };
   auto stage = [&](int k0, char* buf) {
@@ -2077,8 +2104,8 @@ static int launch_w7m(const GemmArgs& a, hipStream_t st) {
 
 template <int EPI>
 static int launch_w7(const GemmArgs& a, hipStream_t st) {
-  // g_w7 == 2 (or variant 11 forced), and every 3-plane X6 operand: the four-wave kernel with 256x224 tiles
-  if (g_c256_variant == 11 || (g_c256_variant < 0 && g_w7 == 2) || a.x6k) return launch_4w<EPI, 0, 0, 224>(a, st);
+  // g_w7 == 2 (or variant 11 forced), and every 2-plane h3 operand: the four-wave kernel with 256x224 tiles
+  if (g_c256_variant == 11 || (g_c256_variant < 0 && g_w7 == 2) || a.h3k) return launch_4w<EPI, 0, 0, 224>(a, st);
   if constexpr (epi_f32(EPI)) return launch_w7m<EPI, 0>(a, st);  // the modes A/B the bf16 epilogue's traffic
   switch (g_w7_mode) {
     case 1: return launch_w7m<EPI, 1>(a, st);
@@ -2103,12 +2130,12 @@ static int launch(const GemmArgs& args, hipStream_t st) {
   if constexpr (EPI == EPI_QKV_ROPE || EPI == EPI_F32_QKV_ROPE) {
     // persistent 256x256 four-wave tiles when they fill the chip (N = 1152: the last column tile is half used)
     const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
-    // (default for the fp32-mode X6 QKV, K' = 6K; the bf16 QKV's K = 896 loop is shorter than the 128x128 kernel's
+    // (default for the fp32-mode h3 QKV, K' = 3K; the bf16 QKV's K = 896 loop is shorter than the 128x128 kernel's
     // tail advantage: g_qkv256 = 2 forces it there too)
     const bool on = EPI == EPI_F32_QKV_ROPE ? g_qkv256 >= 1 : g_qkv256 >= 2;
     if (on && tiles >= 256 && g_tile_override != 128) return launch_4w<EPI, RH>(a, st);
     return launch_cfg<EPI, RH, C128>(a, st);
-  } else if constexpr (EPI == EPI_LSE) {
+  } else if constexpr (EPI == EPI_LSE || EPI == EPI_F32_LSE) {
     // LM head on the scored rows (M = 2048 at the bench batch, N = vocab): 256x256 persistent tiles when they
     // fill the chip (A/B: g_lse256), else 128x128
     const bool big = g_lse256 && a.N % 128 == 0 && (long long)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 256;
@@ -2120,14 +2147,14 @@ static int launch(const GemmArgs& args, hipStream_t st) {
   } else {
     // a partial last column tile (N % 256 == 128) wastes at most 1/(2*tn) of the MFMA work
     const int tn = (a.N + 255) / 256;
-    const bool fits = a.N % 256 == 0 || (a.N % 128 == 0 && tn >= 4 && EPI != EPI_SWIGLU && EPI != EPI_X6_SWIGLU);
+    const bool fits = a.N % 256 == 0 || (a.N % 128 == 0 && tn >= 4 && EPI != EPI_SWIGLU && EPI != EPI_H3_SWIGLU);
     const bool big = fits && ((long long)((a.M + 255) / 256) * tn >= 256);
     const bool use256 = g_tile_override ? g_tile_override == 256 && fits : big;
     if (!use256) return launch_cfg<EPI, RH, C128>(a, st);
     // default: the four-wave 128x128-wave-tile loop (variant 11; +3-20 % over the eight-wave loops on the gate/up,
-    // X6 gate/up and 8192^3 shapes, profiles/r02_gemm_4w.md)
+    // gate/up and 8192^3 shapes, profiles/r02_gemm_4w.md)
     const int variant = g_c256_variant >= 0 ? g_c256_variant : 11;
-    if constexpr (epi_f32(EPI)) {  // fp32 execution (3-plane X6 A operand): the kernels with the plane-remapping
+    if constexpr (epi_f32(EPI)) {  // fp32 execution (2-plane h3 A operand): the kernels with the plane-remapping
       // A loader - the four-wave loop (default, and for the eight-wave variants) or the C256 loop (variants 0 / 1)
       if (variant == 12) return launch_4w<EPI, RH, 4>(a, st);
       if (variant == 0 || variant == 1) return launch_cfg<EPI, RH, C256, true>(a, st);
@@ -2266,33 +2293,35 @@ EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, 
   }
 }
 
-// fp32 execution (X6 operands, common.h): A [M, 6K], B [N, 6K] split-bf16 K-concatenations, so the K of the GEMM
-// is Kx = 6K.  act 0 none -> fp32 C [M, ldc] (+ fp32 bias, + fp32 residual, which may alias C); act 1 bias + GELU
-// -> X6 output [M, 6N] in C (bf16, ldc = 6N); act 2 interleaved SwiGLU -> X6 output [M, 6N/2] (ldc = 3N).
+// fp32 execution (h3 operands, common.h): A a 2-plane h3 activation [M, 2K] (lda >= 2K), B the h3 weight [N, 3K],
+// so the K of the GEMM is Kx = 3K; alpha = 1 / (s_a s_b).  act 0 none -> fp32 C [M, ldc] (+ fp32 bias, + fp32
+// residual, which may alias C); act 1 bias + GELU -> h3 output [M, 2N] in C (fp16 planes, ldc = 2N) at scale
+// out_scale; act 2 interleaved SwiGLU -> h3 output [M, 2 (N/2)] (ldc = N).
 EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, int Kx, int lda, int ldb, int ldc,
-                           const float* bias, const float* resid, int ldr, int act, const float* rscale,
-                           hipStream_t st) {
+                           const float* bias, const float* resid, int ldr, int act, const float* rscale, float alpha,
+                           float out_scale, hipStream_t st) {
   GemmArgs a{};
   a.rscale = rscale;  // optional per-row scale of the product (before bias / activation / residual)
+  a.alpha = alpha; a.out_scale = out_scale;
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B;
   a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.biasf = bias; a.residf = resid; a.ldr = ldr;
-  a.x6k = Kx / X6_TERMS;   // A: 3-plane activation rows (lda >= 3 Kx / 6)
-  if (Kx % (X6_TERMS * BK) || lda < 3 * a.x6k) return (int)hipErrorInvalidValue;
+  a.h3k = Kx / H3_TERMS;   // A: 2-plane activation rows (lda >= 2 Kx / 3)
+  if (Kx % (H3_TERMS * BK) || lda < 2 * a.h3k || !(alpha > 0.f) || !(out_scale > 0.f)) return (int)hipErrorInvalidValue;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
   if (((uintptr_t)C & 15) || ldc % 4 || (resid && (ldr % 4 || ((uintptr_t)resid & 15))) ||
       (bias && ((uintptr_t)bias & 15)))
     return (int)hipErrorInvalidValue;
   if (act == 2) {
-    if (bias || resid || ldc != 3 * (N / 2)) return (int)hipErrorInvalidValue;
+    if (bias || resid || ldc != 2 * (N / 2)) return (int)hipErrorInvalidValue;
     a.C = (bf16_t*)C;
-    return launch<EPI_X6_SWIGLU>(a, st);
+    return launch<EPI_H3_SWIGLU>(a, st);
   }
   if (act == 1) {
-    if (resid || !bias || ldc != 3 * N) return (int)hipErrorInvalidValue;
+    if (resid || !bias || ldc != 2 * N) return (int)hipErrorInvalidValue;
     a.C = (bf16_t*)C;
-    return launch<EPI_X6_BIAS_GELU>(a, st);
+    return launch<EPI_H3_BIAS_GELU>(a, st);
   }
   a.Cf = (float*)C;
   if (bias && resid) return launch<EPI_F32_BIAS_RESID>(a, st);
@@ -2301,19 +2330,22 @@ EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, 
   return launch<EPI_F32>(a, st);
 }
 
-// fp32 QKV projection + bias + RoPE + head-major scatter: X [M, 6K] (X6), W [(Hq+2Hkv)*64, 6K] (X6), fp32 bias,
-// fp32 outputs q [B,Hq,S,64] (x q_scale), k [B,Hkv,S,64], vt [B,Hkv,64,s_pad].
+// fp32 QKV projection + bias + RoPE + head-major scatter: X [M, 2K] (h3 activation), W [(Hq+2Hkv)*64, 3K] (h3
+// weight), alpha = 1 / (s_x s_w), fp32 bias, fp32 outputs q [B,Hq,S,64] (x q_scale), k [B,Hkv,S,64],
+// vt [B,Hkv,64,s_pad].
 EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* bias, float* q, float* k, float* vt,
                                     const float* cosT, const float* sinT, int M, int Kx, int S, int Hq, int Hkv,
-                                    int rot_dim, int s_pad, float q_scale, hipStream_t st) {
+                                    int rot_dim, int s_pad, float q_scale, float alpha, hipStream_t st) {
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
-  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = Kx / 2; a.ldb = Kx;
-  a.x6k = Kx / X6_TERMS;   // X: 3-plane activation rows [M, 3 Kx / 6]
+  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = 2 * (Kx / H3_TERMS); a.ldb = Kx;
+  a.h3k = Kx / H3_TERMS;   // X: 2-plane activation rows [M, 2 Kx / 3]
+  a.alpha = alpha;
   a.biasf = bias; a.qf = q; a.kf = k; a.vtf = vt;
   a.cosT = cosT; a.sinT = sinT; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.s_pad = s_pad;
   a.q_scale = q_scale;
-  if (!bias || M % S || Kx % (X6_TERMS * BK) || ((uintptr_t)bias & 15)) return (int)hipErrorInvalidValue;
+  if (!bias || M % S || Kx % (H3_TERMS * BK) || ((uintptr_t)bias & 15) || !(alpha > 0.f))
+    return (int)hipErrorInvalidValue;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
   switch (rot_dim) {
@@ -2326,18 +2358,21 @@ EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* b
   }
 }
 
-// x6 != 0: fp32 execution, X a 3-plane X6 activation [M, K / 2] and W the X6 weight [N, K] (K = 6 x plane width)
+// LM head + LSE partials.  alpha == 0: bf16 X [M, K], W [N, K].  alpha > 0: fp32 execution, X a 2-plane h3
+// activation [M, 2K/3] and W the h3 weight [N, K] (K = 3 x plane width), product scale alpha.
 EDGE_API int edge_gemm_lse(const void* X, const void* W, const int64_t* targets, float* part_max, float* part_sum,
-                           float* tgt_logit, int M, int N, int K, int x6, hipStream_t st) {
+                           float* tgt_logit, int M, int N, int K, float alpha, hipStream_t st) {
   GemmArgs a{};
+  const bool h3 = alpha > 0.f;
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
-  a.M = M; a.N = N; a.K = K; a.lda = x6 ? K / 2 : K; a.ldb = K;
-  if (x6 && K % (X6_TERMS * BK)) return (int)hipErrorInvalidValue;
-  a.x6k = x6 ? K / X6_TERMS : 0;
+  a.M = M; a.N = N; a.K = K; a.lda = h3 ? 2 * (K / H3_TERMS) : K; a.ldb = K;
+  if (h3 && K % (H3_TERMS * BK)) return (int)hipErrorInvalidValue;
+  a.h3k = h3 ? K / H3_TERMS : 0;
+  a.alpha = h3 ? alpha : 1.f;
   a.targets = targets; a.part_max = part_max; a.part_sum = part_sum; a.tgt_logit = tgt_logit; a.nparts = N / 64;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
-  return launch<EPI_LSE>(a, st);
+  return h3 ? launch<EPI_F32_LSE>(a, st) : launch<EPI_LSE>(a, st);
 }
 
 // Combine the LSE partials: nll[m] = logsumexp_m - logit[target_m].

@@ -218,8 +218,8 @@ EDGE_API int edge_row_rscale(const float* ssq, float* rs, int R, int P, int H, f
 }
 
 // =============================================================================================
-// fp32 execution mode: fp32 activations in, fp32 statistics, and GEMM-input outputs written as 3-plane X6 split-bf16
-// activations [R, 3H] (common.h) that the fp32-mode GEMMs consume (out_x6 = 0: plain fp32 [R, H] instead).
+// fp32 execution mode: fp32 activations in, fp32 statistics, and GEMM-input outputs written as 2-plane h3 split-fp16
+// activations [R, 2H] at scale s (common.h) that the fp32-mode GEMMs consume (s = 0: plain fp32 [R, H] instead).
 template <int NCH>
 __device__ __forceinline__ void load_row_f32(const float* __restrict__ src, int H, float (&v)[NCH][8]) {
   const int lane = threadIdx.x & 63;
@@ -238,15 +238,15 @@ __device__ __forceinline__ void load_row_f32(const float* __restrict__ src, int 
 }
 
 template <int NCH>
-__device__ __forceinline__ void store_row_f32_or_x6(void* __restrict__ dst, int H, const float (&v)[NCH][8],
-                                                    bool x6) {
+__device__ __forceinline__ void store_row_f32_or_h3(void* __restrict__ dst, int H, const float (&v)[NCH][8],
+                                                    float h3s) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (c * 64 + lane) * 8;
     if (col >= H) continue;
-    if (x6) {
-      store_x6_8((bf16_t*)dst, H, col, v[c]);
+    if (h3s > 0.f) {
+      store_h3_8((f16_t*)dst, H, col, v[c], h3s);
     } else {
       float* d = (float*)dst + col;
       *(f32x4_t*)d = f32x4_t{v[c][0], v[c][1], v[c][2], v[c][3]};
@@ -255,16 +255,15 @@ __device__ __forceinline__ void store_row_f32_or_x6(void* __restrict__ dst, int 
   }
 }
 
-__device__ __forceinline__ size_t out_row_elems(int H, bool x6) { return x6 ? (size_t)3 * H : (size_t)H; }
-__device__ __forceinline__ void* out_row(void* y, size_t r, int H, bool x6) {
-  return x6 ? (void*)((bf16_t*)y + r * out_row_elems(H, true)) : (void*)((float*)y + r * (size_t)H);
+__device__ __forceinline__ void* out_row(void* y, size_t r, int H, float h3s) {
+  return h3s > 0.f ? (void*)((f16_t*)y + r * 2 * (size_t)H) : (void*)((float*)y + r * (size_t)H);
 }
 
 // HF Qwen2RMSNorm in fp32: y = w * (x * rsqrt(mean(x^2) + eps)).
 template <int NCH>
 __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           void* __restrict__ y, const int* __restrict__ rows, int R,
-                                                          int H, float eps, int x6) {
+                                                          int H, float eps, float h3s) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
   const int src_row = rows ? rows[r] : r;
@@ -282,7 +281,7 @@ __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restric
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[c][j] = g[c][j] * (v[c][j] * rs);
-  store_row_f32_or_x6<NCH>(out_row(y, r, H, x6), H, v, x6);
+  store_row_f32_or_h3<NCH>(out_row(y, r, H, h3s), H, v, h3s);
 }
 
 template <int NCH, bool DUAL>
@@ -290,7 +289,7 @@ __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* __restr
                                                             const float* __restrict__ b1, const float* __restrict__ w2,
                                                             const float* __restrict__ b2, void* __restrict__ y1,
                                                             void* __restrict__ y2, const int* __restrict__ rows, int R,
-                                                            int H, float eps, int x6) {
+                                                            int H, float eps, float h3s1, float h3s2) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
   const int src_row = rows ? rows[r] : r;
@@ -321,7 +320,7 @@ __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* __restr
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[c][j] = fmaf(v[c][j] * rs, g[c][j], b[c][j]);
-  store_row_f32_or_x6<NCH>(out_row(y1, r, H, x6), H, o, x6);
+  store_row_f32_or_h3<NCH>(out_row(y1, r, H, h3s1), H, o, h3s1);
   if (DUAL) {
     load_row_f32<NCH>(w2, H, g);
     load_row_f32<NCH>(b2, H, b);
@@ -329,19 +328,19 @@ __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* __restr
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[c][j] = fmaf(v[c][j] * rs, g[c][j], b[c][j]);
-    store_row_f32_or_x6<NCH>(out_row(y2, r, H, x6), H, o, x6);
+    store_row_f32_or_h3<NCH>(out_row(y2, r, H, h3s2), H, o, h3s2);
   }
 }
 
-// fp32 [R, H] (rows optionally gathered) -> 3-plane X6 activation [R, 3H]
+// fp32 [R, H] (rows optionally gathered) -> 2-plane h3 activation [R, 2H] at scale s
 template <int NCH>
-__global__ __launch_bounds__(256) void split6_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
-                                                     const int* __restrict__ rows, int R, int H) {
+__global__ __launch_bounds__(256) void split_h3_kernel(const float* __restrict__ x, f16_t* __restrict__ y,
+                                                       const int* __restrict__ rows, int R, int H, float s) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
   float v[NCH][8];
   load_row_f32<NCH>(x + (size_t)(rows ? rows[r] : r) * H, H, v);
-  store_row_f32_or_x6<NCH>(y + (size_t)r * 3 * H, H, v, true);
+  store_row_f32_or_h3<NCH>(y + (size_t)r * 2 * H, H, v, s);
 }
 
 __global__ __launch_bounds__(256) void embedding_f32_kernel(const int64_t* __restrict__ ids,
@@ -356,32 +355,33 @@ __global__ __launch_bounds__(256) void embedding_f32_kernel(const int64_t* __res
   for (int c = threadIdx.x & 63; c < H / 4; c += 64) dst[c] = src[c];
 }
 
+// h3_scale > 0: output as a 2-plane h3 activation [R, 2H] at that scale; 0: fp32 [R, H]
 EDGE_API int edge_rmsnorm_f32(const float* x, const float* w, void* y, const int* rows, int R, int H, float eps,
-                              int out_x6, hipStream_t st) {
-  if (H % 8 || R <= 0) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+                              float h3_scale, hipStream_t st) {
+  if (H % 8 || R <= 0 || h3_scale < 0.f) return R == 0 ? 0 : (int)hipErrorInvalidValue;
   dim3 grid((R + 3) / 4);
-  DISPATCH_NCH(H, rmsnorm_f32_kernel<NCH><<<grid, 256, 0, st>>>(x, w, y, rows, R, H, eps, out_x6));
+  DISPATCH_NCH(H, rmsnorm_f32_kernel<NCH><<<grid, 256, 0, st>>>(x, w, y, rows, R, H, eps, h3_scale));
   return (int)hipGetLastError();
 }
 
 EDGE_API int edge_layernorm_f32(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
-                                void* y1, void* y2, const int* rows, int R, int H, float eps, int out_x6,
-                                hipStream_t st) {
-  if (H % 8 || R <= 0) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+                                void* y1, void* y2, const int* rows, int R, int H, float eps, float h3_scale1,
+                                float h3_scale2, hipStream_t st) {
+  if (H % 8 || R <= 0 || h3_scale1 < 0.f || h3_scale2 < 0.f) return R == 0 ? 0 : (int)hipErrorInvalidValue;
   dim3 grid((R + 3) / 4);
   if (y2) {
     DISPATCH_NCH(H, (layernorm_f32_kernel<NCH, true><<<grid, 256, 0, st>>>(x, w1, b1, w2, b2, y1, y2, rows, R, H, eps,
-                                                                           out_x6)));
+                                                                           h3_scale1, h3_scale2)));
   } else {
     DISPATCH_NCH(H, (layernorm_f32_kernel<NCH, false><<<grid, 256, 0, st>>>(x, w1, b1, nullptr, nullptr, y1, nullptr,
-                                                                            rows, R, H, eps, out_x6)));
+                                                                            rows, R, H, eps, h3_scale1, 0.f)));
   }
   return (int)hipGetLastError();
 }
 
-EDGE_API int edge_split6(const float* x, void* y, const int* rows, int R, int H, hipStream_t st) {
-  if (H % 8 || R <= 0) return R == 0 ? 0 : (int)hipErrorInvalidValue;
-  DISPATCH_NCH(H, split6_kernel<NCH><<<(R + 3) / 4, 256, 0, st>>>(x, (bf16_t*)y, rows, R, H));
+EDGE_API int edge_split_h3(const float* x, void* y, const int* rows, int R, int H, float s, hipStream_t st) {
+  if (H % 8 || R <= 0 || !(s > 0.f)) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+  DISPATCH_NCH(H, split_h3_kernel<NCH><<<(R + 3) / 4, 256, 0, st>>>(x, (f16_t*)y, rows, R, H, s));
   return (int)hipGetLastError();
 }
 

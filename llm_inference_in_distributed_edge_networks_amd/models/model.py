@@ -27,10 +27,13 @@ Precision.  The reference evaluates fp32 models (``qwen_layer_wise.py:17`` and
 ``pythia_model.py:25`` load without ``torch_dtype``).  On the GPU a model built with
 ``dtype=torch.float32`` runs the fp32 execution mode: the residual stream, norms,
 attention, softmax statistics and the boundary codec are fp32, and every GEMM takes its
-operands in the X6 split-bf16 layout (``ops.reference.x6_act`` / ``x6_weight``: six bf16
-MFMA products per fp32 product, exact to 2^-27 relative).  Producers of GEMM inputs (norms,
-attention, the SwiGLU / GELU epilogues) write the three bf16 planes of their output directly
-(3-plane activations, the GEMM's A loader expands them); weights are expanded once at load.  ``dtype=torch.bfloat16`` is the faster bf16 mode.
+operands in the h3 split-fp16 layout (``ops.reference.h3_act`` / ``h3_weight``: a power-of-two
+scaled operand as two fp16 planes, three fp16 MFMA products per fp32 product, error below the
+CPU fp32 GEMM's).  Producers of GEMM inputs (norms, attention, the SwiGLU / GELU epilogues) write
+the two planes of their scaled output directly (the GEMM's A loader expands them); weights are
+split once at load.  The activation scales come from bounds on every GEMM input that hold for
+any model input (``_h3_bounds``), so no plane can leave the fp16 range.  ``dtype=torch.bfloat16``
+is the faster bf16 mode.
 """
 from __future__ import annotations
 
@@ -53,28 +56,77 @@ class AttnStats:
     colsum: torch.Tensor | None = None    # [B, Hq, S] sum_i P[i, j]
 
 
-_X6_KEYS = ("wqkv", "wo", "wgu", "wd", "wfc", "wproj")
+_H3_KEYS = ("wqkv", "wo", "wgu", "wd", "wfc", "wproj")
+
+
+def _rownorm(w: torch.Tensor) -> torch.Tensor:
+    return w.float().norm(dim=1)
+
+
+def _h3_bounds(cfg: ModelConfig, L: dict) -> dict:
+    """Bounds on |x| of every GEMM input of one decoder layer, valid for any layer input (exact arithmetic; the
+    power-of-two scales leave a factor 2 of headroom for rounding):
+
+    * norm outputs: |x_hat_i| <= ||x_hat||_2 <= sqrt(H) for RMSNorm and LayerNorm, so |g_i x_hat_i + b_i| <=
+      sqrt(H) max|g| + max|b| and ||y||_2 <= sqrt(H) max|g| + ||b||_2 =: n;
+    * attention output: a convex combination of value rows, |o| <= max_j |v_j| <= max_j n ||Wv_j||_2 + |bv_j|;
+    * SwiGLU output: |silu(g) u| <= |g| |u| <= n^2 max_j ||Wg_j||_2 ||Wu_j||_2;
+    * GELU output: |gelu(f)| <= |f| <= max_j n ||Wfc_j||_2 + |bfc_j|."""
+    H = cfg.hidden_size
+    rH = math.sqrt(H)
+
+    def norm_bound(g, b):
+        e = rH * g.float().abs().max().item()
+        if b is None:
+            return e, e
+        return e + b.float().abs().max().item(), e + b.float().norm().item()
+
+    qkv, n1 = norm_bound(L["ln1_w"], L.get("ln1_b"))
+    mlp, n2 = norm_bound(L["ln2_w"], L.get("ln2_b"))
+    v0 = cfg.q_size + cfg.kv_size
+    wv, bv = L["wqkv"][v0:v0 + cfg.kv_size], L["bqkv"][v0:v0 + cfg.kv_size]
+    o = (n1 * _rownorm(wv) + bv.float().abs()).max().item()
+    if cfg.arch == "qwen2":
+        g, u = ops.deinterleave_gate_up(L["wgu"].t().contiguous())
+        down = n2 * n2 * (_rownorm(g.t()) * _rownorm(u.t())).max().item()
+    else:
+        down = (n2 * _rownorm(L["wfc"]) + L["bfc"].float().abs()).max().item()
+    return dict(qkv=qkv, o=o, mlp=mlp, down=down)
 
 
 class DecoderLM:
-    def __init__(self, cfg: ModelConfig, weights: dict, device="cpu", dtype=torch.float32, x6: bool | None = None):
+    def __init__(self, cfg: ModelConfig, weights: dict, device="cpu", dtype=torch.float32, h3: bool | None = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
         self.w = weights
         self.layers = weights["layers"]
-        # fp32 execution on the GPU: X6 operands (x6=True also runs the same op sequence on CPU, for tests)
-        self.x6 = (self.device.type == "cuda" and dtype == torch.float32) if x6 is None else bool(x6)
-        if self.x6:
+        # fp32 execution on the GPU: h3 operands (h3=True also runs the same op sequence on CPU, for tests)
+        self.h3 = (self.device.type == "cuda" and dtype == torch.float32) if h3 is None else bool(h3)
+        # per layer: activation scales s (GEMM inputs) and product scales alpha = 1 / (s_x s_w) of the h3 GEMMs
+        self.h3_layer: list[dict | None] = [None] * len(self.layers)
+        self.h3_head: dict | None = None
+        if self.h3:
             if dtype != torch.float32:
-                raise ValueError("the X6 (fp32) execution mode needs fp32 weights")
-            for L in self.layers:
-                if L is not None:
-                    for k in _X6_KEYS:
-                        if k in L:
-                            L[k + "6"] = ops.reference.x6_weight(L[k])
+                raise ValueError("the h3 (fp32) execution mode needs fp32 weights")
+            S = ops.reference.h3_scale
+            for i, L in enumerate(self.layers):
+                if L is None:
+                    continue
+                sc = {k: S(v) for k, v in _h3_bounds(cfg, L).items()}
+                ins = dict(wqkv="qkv", wo="o", wgu="mlp", wd="down", wfc="mlp", wproj="down")
+                for k in _H3_KEYS:
+                    if k in L:
+                        L[k + "3"], sw = ops.reference.h3_weight(L[k])
+                        sc["a_" + k] = 1.0 / (sc[ins[k]] * sw)
+                self.h3_layer[i] = sc
             if weights.get("head") is not None:
-                weights["head6"] = ops.reference.x6_weight(weights["head"])
+                g, b = weights["norm_w"], weights.get("norm_b")
+                bound = math.sqrt(cfg.hidden_size) * g.float().abs().max().item() + \
+                    (0.0 if b is None else b.float().abs().max().item())
+                weights["head3"], sw = ops.reference.h3_weight(weights["head"])
+                s_in = S(bound)
+                self.h3_head = dict(s=s_in, a=1.0 / (s_in * sw))
         cos, sin = ops.rope_tables(cfg.max_position, cfg.rotary_dim, cfg.rope_theta)
         self.cos = cos.to(self.device).contiguous()
         self.sin = sin.to(self.device).contiguous()
@@ -93,7 +145,7 @@ class DecoderLM:
     @classmethod
     def random_init(cls, cfg: ModelConfig, seed: int = 0, device="cpu", dtype=torch.float32, std: float = 0.02,
                     layers: range | None = None, with_embed: bool = True, with_head: bool = True,
-                    x6: bool | None = None):
+                    h3: bool | None = None):
         """Seeded random weights of the given architecture (HF ``_init_weights`` style: N(0, 0.02)).
 
         ``layers`` restricts allocation to a layer range (a pipeline stage only holds its own layers);
@@ -143,7 +195,7 @@ class DecoderLM:
             w["head"] = fin(hd) if with_head else None
         if not with_embed and not cfg.tie_embeddings:
             w["embed"] = None
-        return cls(cfg, w, device, dtype, x6=x6)
+        return cls(cfg, w, device, dtype, h3=h3)
 
     @classmethod
     def from_state_dict(cls, cfg: ModelConfig, sd: dict, device="cpu", dtype=torch.float32,
@@ -273,8 +325,8 @@ class DecoderLM:
         cfg, L = self.cfg, self.layers[i]
         if L is None:
             raise RuntimeError(f"layer {i} is not resident on this stage")
-        if self.x6:
-            return self._layer_x6(i, x, B, S, stats)
+        if self.h3:
+            return self._layer_h3(i, x, B, S, stats)
         Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
         if self.fuse_norm:
             ssq = getattr(x, "_edge_ssq", None)
@@ -321,37 +373,39 @@ class DecoderLM:
                 raise ValueError(kd)
         return kinds
 
-    def _attn_x6(self, i, x, B, S, need_lse=False, n_rows=None):
-        """fp32 mode: norm(s) -> X6 QKV GEMM (+bias+RoPE) -> fp32 attention with X6 output."""
-        cfg, L = self.cfg, self.layers[i]
-        h26 = None
+    def _attn_h3(self, i, x, B, S, need_lse=False, n_rows=None):
+        """fp32 mode: norm(s) -> h3 QKV GEMM (+bias+RoPE) -> fp32 attention with h3 output."""
+        cfg, L, sc = self.cfg, self.layers[i], self.h3_layer[i]
+        h23 = None
         if cfg.arch == "qwen2":
-            h6 = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps, x6=True)
+            h3 = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps, h3=sc["qkv"])
         else:
-            h6, h26 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps, x6=True)
-        q, k, vt = ops.qkv_rope_x6(h6, L["wqkv6"], L["bqkv"], self.cos, self.sin, B, S, cfg.num_heads,
+            h3, h23 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps,
+                                         h3=(sc["qkv"], sc["mlp"]))
+        q, k, vt = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S, cfg.num_heads,
                                    cfg.num_kv_heads, cfg.head_dim, cfg.rotary_dim, self.q_scale)
-        o6, lse = ops.attention(q, k, vt, S, need_lse=need_lse, n_rows=n_rows, x6=True)
-        return q, k, o6, lse, h26
+        o3, lse = ops.attention(q, k, vt, S, need_lse=need_lse, n_rows=n_rows, h3=sc["o"])
+        return q, k, o3, lse, h23
 
-    def _mlp_x6(self, i, o6, x, h26):
-        cfg, L = self.cfg, self.layers[i]
+    def _mlp_h3(self, i, o3, x, h23):
+        cfg, L, sc = self.cfg, self.layers[i], self.h3_layer[i]
         if cfg.arch == "qwen2":
-            y = ops.linear_x6(o6, L["wo6"], residual=x)
-            a6 = ops.linear_x6(ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps, x6=True), L["wgu6"], act="swiglu_il")
-            return ops.linear_x6(a6, L["wd6"], residual=y, out=y)
-        y = ops.linear_x6(o6, L["wo6"], L["bo"], residual=x)
-        f6 = ops.linear_x6(h26, L["wfc6"], L["bfc"], act="gelu")
-        return ops.linear_x6(f6, L["wproj6"], L["bproj"], residual=y, out=y)
+            y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], residual=x)
+            a3 = ops.linear_h3(ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps, h3=sc["mlp"]), L["wgu3"], sc["a_wgu"],
+                               act="swiglu_il", out_scale=sc["down"])
+            return ops.linear_h3(a3, L["wd3"], sc["a_wd"], residual=y, out=y)
+        y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], L["bo"], residual=x)
+        f3 = ops.linear_h3(h23, L["wfc3"], sc["a_wfc"], L["bfc"], act="gelu", out_scale=sc["down"])
+        return ops.linear_h3(f3, L["wproj3"], sc["a_wproj"], L["bproj"], residual=y, out=y)
 
-    def _layer_x6(self, i, x, B, S, stats):
+    def _layer_h3(self, i, x, B, S, stats):
         kinds = self._stat_kinds(stats)
-        q, k, o6, lse, h26 = self._attn_x6(i, x, B, S, need_lse="colsum" in kinds)
+        q, k, o3, lse, h23 = self._attn_h3(i, x, B, S, need_lse="colsum" in kinds)
         st = None
         if kinds:
             st = AttnStats(lastrow=ops.attn_lastrow(q, k, S) if "lastrow" in kinds else None,
                            colsum=ops.attn_colsum(q, k, lse, S) if "colsum" in kinds else None)
-        return self._mlp_x6(i, o6, x, h26), st
+        return self._mlp_h3(i, o3, x, h23), st
 
     def layer_rows(self, i: int, x: torch.Tensor, B: int, S: int, rows: torch.Tensor,
                    n_rows: torch.Tensor | None = None) -> torch.Tensor:
@@ -366,10 +420,10 @@ class DecoderLM:
             raise RuntimeError(f"layer {i} is not resident on this stage")
         Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
         rows = rows.to(self.device)
-        if self.x6:
-            _, _, o6, _, h26 = self._attn_x6(i, x, B, S, n_rows=n_rows)
-            return self._mlp_x6(i, o6.index_select(0, rows), x.index_select(0, rows),
-                                None if h26 is None else h26.index_select(0, rows))
+        if self.h3:
+            _, _, o3, _, h23 = self._attn_h3(i, x, B, S, n_rows=n_rows)
+            return self._mlp_h3(i, o3.index_select(0, rows), x.index_select(0, rows),
+                                None if h23 is None else h23.index_select(0, rows))
         h2 = None
         if self.fuse_norm:
             ssq = getattr(x, "_edge_ssq", None)
@@ -405,13 +459,13 @@ class DecoderLM:
 
     def row_nll(self, x: torch.Tensor, rows: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         """Per-row NLL of the scored rows only (final norm + LM head + CE fused)."""
-        if self.x6:
-            rows = rows.to(self.device)
+        if self.h3:
+            rows, hs = rows.to(self.device), self.h3_head
             if self.cfg.arch == "qwen2":
-                h6 = ops.rmsnorm(x, self.w["norm_w"], self.cfg.norm_eps, rows, x6=True)
+                h3 = ops.rmsnorm(x, self.w["norm_w"], self.cfg.norm_eps, rows, h3=hs["s"])
             else:
-                h6 = ops.layernorm(x, self.w["norm_w"], self.w["norm_b"], self.cfg.norm_eps, rows, x6=True)
-            return ops.head_nll_x6(h6, self.w["head6"], targets.to(self.device))
+                h3 = ops.layernorm(x, self.w["norm_w"], self.w["norm_b"], self.cfg.norm_eps, rows, h3=hs["s"])
+            return ops.head_nll_h3(h3, self.w["head3"], hs["a"], targets.to(self.device))
         h = self.final_norm(x, rows.to(self.device))
         return ops.head_nll(h, self.w["head"], targets.to(self.device))
 

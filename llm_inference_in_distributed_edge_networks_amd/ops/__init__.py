@@ -5,8 +5,9 @@ Every op has exactly two implementations with identical layouts and semantics:
 * CUDA/HIP tensors -> the hand-written gfx950 kernel from ``csrc/`` (``_native``);
   a missing library is an error, never a silent fallback.  Two GPU precisions:
   bf16 activations (bf16 MFMA), and fp32 activations - the reference's precision - where
-  GEMM operands travel in the X6 split-bf16 layout (``reference.x6_act`` / ``x6_weight``,
-  csrc/common.h) and attention runs on the f32 matrix cores (csrc/attention_f32.hip);
+  GEMM operands travel in the h3 split-fp16 layout (``reference.h3_act`` / ``h3_weight``,
+  csrc/common.h: two fp16 planes, three fp16 MFMA products per fp32 product, power-of-two
+  operand scales) and attention runs on split-bf16 matrix-core products (csrc/attention_f32.hip);
 * CPU tensors -> the fp32 PyTorch oracle in ``reference.py`` (used for the
   CPU WikiText-2 configuration and as the test oracle).
 """
@@ -43,14 +44,16 @@ def _check_f32(*ts):
             raise ValueError("HIP kernels take contiguous tensors")
 
 
-def _check_x6(x6, w6):
-    """x6: 3-plane activation [rows, 3K] (reference.x6_act), w6: X6 weight [N, 6K] (reference.x6_weight)."""
-    for t, m, what in ((x6, 3, "activations [rows, 3K] (reference.x6_act)"), (w6, 6, "weights [N, 6K] "
-                                                                               "(reference.x6_weight)")):
-        if t.dtype != torch.bfloat16 or t.shape[-1] % m or not t.is_contiguous():
-            raise TypeError(f"X6 {what} must be contiguous bf16")
-    if 2 * x6.shape[-1] != w6.shape[-1]:
-        raise ValueError(f"X6 activation width {x6.shape[-1]} does not match the weight width {w6.shape[-1]}")
+def _check_h3(a3, w3, alpha):
+    """a3: 2-plane activation [rows, 2K] (reference.h3_act), w3: h3 weight [N, 3K] (reference.h3_weight)."""
+    for t, m, what in ((a3, 2, "activations [rows, 2K] (reference.h3_act)"), (w3, 3, "weights [N, 3K] "
+                                                                               "(reference.h3_weight)")):
+        if t.dtype != torch.float16 or t.shape[-1] % m or not t.is_contiguous():
+            raise TypeError(f"h3 {what} must be contiguous fp16")
+    if 3 * a3.shape[-1] != 2 * w3.shape[-1]:
+        raise ValueError(f"h3 activation width {a3.shape[-1]} does not match the weight width {w3.shape[-1]}")
+    if not alpha > 0.0:
+        raise ValueError(f"h3 product scale alpha must be > 0, got {alpha}")
 
 
 def _check_bf16(*ts):
@@ -77,24 +80,25 @@ def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def _out_f32_or_x6(R: int, H: int, x6: bool, device) -> torch.Tensor:
-    return torch.empty(R, 3 * H, dtype=torch.bfloat16, device=device) if x6 else \
+def _out_f32_or_h3(R: int, H: int, h3: float, device) -> torch.Tensor:
+    return torch.empty(R, 2 * H, dtype=torch.float16, device=device) if h3 else \
         torch.empty(R, H, dtype=torch.float32, device=device)
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, rows: torch.Tensor | None = None,
-            x6: bool = False) -> torch.Tensor:
-    """RMSNorm of ``x[rows]`` (all rows if ``rows`` is None).  fp32 ``x`` with ``x6``: output in the X6 layout."""
+            h3: float = 0.0) -> torch.Tensor:
+    """RMSNorm of ``x[rows]`` (all rows if ``rows`` is None).  fp32 ``x`` with ``h3`` = s > 0: output as the
+    2-plane h3 activation of s * y (the next GEMM's input)."""
     if not _gpu(x):
         y = ref.rmsnorm(x if rows is None else x.index_select(0, rows.long()), w, eps)
-        return ref.x6_act(y) if x6 else y
+        return ref.h3_act(y, h3) if h3 else y
     R = x.shape[0] if rows is None else rows.numel()
     H = x.shape[1]
     rows32 = None if rows is None else rows.to(torch.int32).contiguous()
     if x.dtype == torch.float32:
         _check_f32(x, w)
-        y = _out_f32_or_x6(R, H, x6, x.device)
-        call("edge_rmsnorm_f32", ptr(x), ptr(w), ptr(y), ptr(rows32), R, H, float(eps), int(x6), stream())
+        y = _out_f32_or_h3(R, H, h3, x.device)
+        call("edge_rmsnorm_f32", ptr(x), ptr(w), ptr(y), ptr(rows32), R, H, float(eps), float(h3), stream())
         return y
     _check_bf16(x, w)
     y = torch.empty(R, H, dtype=x.dtype, device=x.device)
@@ -102,18 +106,18 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, rows: torch.Tensor | N
     return y
 
 
-def layernorm(x, w, b, eps, rows=None, x6: bool = False):
+def layernorm(x, w, b, eps, rows=None, h3: float = 0.0):
     if not _gpu(x):
         y = ref.layernorm(x if rows is None else x.index_select(0, rows.long()), w, b, eps)
-        return ref.x6_act(y) if x6 else y
+        return ref.h3_act(y, h3) if h3 else y
     R = x.shape[0] if rows is None else rows.numel()
     H = x.shape[1]
     rows32 = None if rows is None else rows.to(torch.int32).contiguous()
     if x.dtype == torch.float32:
         _check_f32(x, w, b)
-        y = _out_f32_or_x6(R, H, x6, x.device)
+        y = _out_f32_or_h3(R, H, h3, x.device)
         call("edge_layernorm_f32", ptr(x), ptr(w), ptr(b), None, None, ptr(y), None, ptr(rows32), R, H, float(eps),
-             int(x6), stream())
+             float(h3), 0.0, stream())
         return y
     _check_bf16(x, w, b)
     y = torch.empty(R, H, dtype=x.dtype, device=x.device)
@@ -121,17 +125,19 @@ def layernorm(x, w, b, eps, rows=None, x6: bool = False):
     return y
 
 
-def layernorm_dual(x, w1, b1, w2, b2, eps, x6: bool = False):
-    """Two LayerNorms of the same input (GPT-NeoX parallel residual reads ln1(x) and ln2(x))."""
+def layernorm_dual(x, w1, b1, w2, b2, eps, h3: tuple[float, float] = (0.0, 0.0)):
+    """Two LayerNorms of the same input (GPT-NeoX parallel residual reads ln1(x) and ln2(x)).  fp32 ``x`` with
+    ``h3`` = (s1, s2) > 0: both outputs as h3 activations at their scales."""
+    s1, s2 = h3
     if not _gpu(x):
         y1, y2 = ref.layernorm_dual(x, w1, b1, w2, b2, eps)
-        return (ref.x6_act(y1), ref.x6_act(y2)) if x6 else (y1, y2)
+        return (ref.h3_act(y1, s1), ref.h3_act(y2, s2)) if s1 else (y1, y2)
     if x.dtype == torch.float32:
         _check_f32(x, w1, b1, w2, b2)
         R, H = x.shape
-        y1, y2 = _out_f32_or_x6(R, H, x6, x.device), _out_f32_or_x6(R, H, x6, x.device)
+        y1, y2 = _out_f32_or_h3(R, H, s1, x.device), _out_f32_or_h3(R, H, s2, x.device)
         call("edge_layernorm_f32", ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(y1), ptr(y2), None, R, H,
-             float(eps), int(x6), stream())
+             float(eps), float(s1), float(s2), stream())
         return y1, y2
     _check_bf16(x, w1, b1, w2, b2)
     R, H = x.shape
@@ -173,7 +179,7 @@ def gemm_ssq_parts(M: int, N: int, K: int, act=None, bias=False, residual=False)
 
 
 def set_gemm_qkv256(mode: int) -> None:
-    """QKV+RoPE GEMMs on the four-wave 256x256 kernel when the shape fills the chip: 0 never, 1 the fp32-mode (X6)
+    """QKV+RoPE GEMMs on the four-wave 256x256 kernel when the shape fills the chip: 0 never, 1 the fp32-mode (h3)
     QKV (default), 2 the bf16 QKV too."""
     call("edge_gemm_set_qkv256", int(mode))
 
@@ -294,16 +300,16 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     return q, k, vt
 
 
-def attention(q, k, vt, S, need_lse=False, n_rows=None, x6: bool = False):
+def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0):
     """Causal GQA flash attention -> (o [B*S, Hq*64], lse [B,Hq,S] or None).
 
     ``n_rows`` ([B] fp32, scored rows per window as in ``WindowBatch.n_rows``): only query rows
     >= S-1-n_rows[b] are needed (last layer of the model); other 64-row blocks may be skipped and their
-    output rows are then undefined.  fp32 q/k/vt run the f32 matrix-core kernel; ``x6`` then writes o in
-    the 3-plane X6 layout [B*S, 3*Hq*64] the O-projection consumes."""
+    output rows are then undefined.  fp32 q/k/vt run the fp32 kernels; ``h3`` = s > 0 then writes s * o as the
+    2-plane h3 activation [B*S, 2*Hq*64] the O-projection consumes."""
     if not _gpu(q):
         o, lse = ref.attention(q, k, vt, S, need_lse)
-        return (ref.x6_act(o) if x6 else o), lse
+        return (ref.h3_act(o, h3) if h3 else o), lse
     B, Hq, _, D = q.shape
     Hkv = k.shape[1]
     lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device) if need_lse else None
@@ -314,9 +320,9 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, x6: bool = False):
     if q.dtype == torch.float32:
         _check_f32(q, k, vt)
         assert D == 64 and vt.shape[-1] % 64 == 0 and vt.shape[-1] >= S
-        o = _out_f32_or_x6(B * S, Hq * D, x6, q.device)
+        o = _out_f32_or_h3(B * S, Hq * D, h3, q.device)
         call("edge_flash_attn_fwd_f32", ptr(q), ptr(k), ptr(vt), ptr(o), ptr(lse), ptr(nr), B, Hq, Hkv, S,
-             vt.shape[-1], int(x6), stream())
+             vt.shape[-1], float(h3), stream())
         return o, lse
     _check_bf16(q, k, vt)
     o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)
@@ -382,99 +388,102 @@ def head_nll(h, w, targets):
     tgt = torch.empty(R, dtype=torch.float32, device=h.device)
     nll = torch.empty(R, dtype=torch.float32, device=h.device)
     t64 = targets.to(torch.int64).contiguous()
-    call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, 0, stream())
+    call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, 0.0, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
 
 
-# ---- fp32 execution mode: X6 GEMMs (csrc/gemm.hip EPI_F32*, EPI_X6_*) ---------------------------------------
-def split6(x: torch.Tensor, rows: torch.Tensor | None = None) -> torch.Tensor:
-    """fp32 [R, K] (optionally rows gathered) -> 3-plane X6 activation [R, 3K]."""
+# ---- fp32 execution mode: h3 GEMMs (csrc/gemm.hip EPI_F32*, EPI_H3_*) ---------------------------------------
+def split_h3(x: torch.Tensor, s: float, rows: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 [R, K] (optionally rows gathered) -> 2-plane h3 activation of s * x, [R, 2K] fp16."""
     if not _gpu(x):
-        return ref.x6_act(x if rows is None else x.index_select(0, rows.long()))
+        return ref.h3_act(x if rows is None else x.index_select(0, rows.long()), s)
     _check_f32(x)
     R = x.shape[0] if rows is None else rows.numel()
     rows32 = None if rows is None else rows.to(torch.int32).contiguous()
-    y = torch.empty(R, 3 * x.shape[1], dtype=torch.bfloat16, device=x.device)
-    call("edge_split6", ptr(x), ptr(y), ptr(rows32), R, x.shape[1], stream())
+    y = torch.empty(R, 2 * x.shape[1], dtype=torch.float16, device=x.device)
+    call("edge_split_h3", ptr(x), ptr(y), ptr(rows32), R, x.shape[1], float(s), stream())
     return y
 
 
-def linear_x6(x6: torch.Tensor, w6: torch.Tensor, bias=None, residual=None, act=None, out=None,
-              rscale=None) -> torch.Tensor:
-    """fp32-accurate ``act(rscale * (x @ w.T) + bias) + residual`` from X6 operands (x6 [M, 3K] 3-plane
-    activation, w6 [N, 6K] X6 weight).
+def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, residual=None, act=None, out=None,
+              rscale=None, out_scale: float = 1.0) -> torch.Tensor:
+    """fp32-accurate ``act(rscale * (x @ w.T) + bias) + residual`` from h3 operands (a3 [M, 2K] the 2-plane
+    activation of s_a x, w3 [N, 3K] the h3 weight of w at scale s_w, alpha = 1 / (s_a s_w)).
 
     act None -> fp32 [M, N] (``residual`` fp32, may alias ``out``); act "gelu" / "swiglu_il" -> the activation as
-    a 3-plane X6 activation ([M, 3N] / [M, 3N/2]) for the next GEMM."""
-    M = x6.shape[0]
-    N, Kx = w6.shape
-    if not _gpu(x6):
-        y = ref.x6_to_f32(x6) @ ref.x6w_to_f32(w6).t()
+    the 2-plane h3 activation of ``out_scale`` * act(...) ([M, 2N] / [M, N]) for the next GEMM."""
+    M = a3.shape[0]
+    N, Kx = w3.shape
+    if not _gpu(a3):
+        y = ref.h3_matmul(a3, w3, alpha)
         if rscale is not None:
             y = y * rscale.float().view(-1, 1)
         if bias is not None:
             y = y + bias.float()
         if act == "gelu":
-            return ref.x6_act(ref.gelu(y))
+            return ref.h3_act(ref.gelu(y), out_scale)
         if act == "swiglu_il":
             g, u = ref.deinterleave_gate_up(y)
-            return ref.x6_act(torch.nn.functional.silu(g) * u)
+            return ref.h3_act(torch.nn.functional.silu(g) * u, out_scale)
         if residual is not None:
             y = y + residual.float()
         if out is not None:
             out.copy_(y)
             return out
         return y
-    _check_x6(x6, w6)
+    _check_h3(a3, w3, alpha)
     _check_f32(bias, residual, rscale)
     if act is None:
         if out is None:
-            out = torch.empty(M, N, dtype=torch.float32, device=x6.device)
+            out = torch.empty(M, N, dtype=torch.float32, device=a3.device)
         ldc = out.stride(0)
         code = 0
     else:
         No = N // 2 if act == "swiglu_il" else N
-        out = torch.empty(M, 3 * No, dtype=torch.bfloat16, device=x6.device)
-        ldc = 3 * No
+        out = torch.empty(M, 2 * No, dtype=torch.float16, device=a3.device)
+        ldc = 2 * No
         code = _ACT[act]
-    call("edge_gemm_f32", ptr(x6), ptr(w6), ptr(out), M, N, Kx, x6.stride(0), w6.stride(0), ldc, ptr(bias),
-         ptr(residual), 0 if residual is None else residual.stride(0), code, ptr(rscale), stream())
+    call("edge_gemm_f32", ptr(a3), ptr(w3), ptr(out), M, N, Kx, a3.stride(0), w3.stride(0), ldc, ptr(bias),
+         ptr(residual), 0 if residual is None else residual.stride(0), code, ptr(rscale), float(alpha),
+         float(out_scale), stream())
     return out
 
 
-def qkv_rope_x6(x6, w6, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
-    """fp32 fused QKV projection + bias + RoPE + head-major scatter from X6 operands -> fp32 (q, k, vt)."""
-    if not _gpu(x6):
-        return ref.qkv_rope(ref.x6_to_f32(x6), ref.x6w_to_f32(w6), bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim,
-                            q_scale)
-    _check_x6(x6, w6)
+def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
+    """fp32 fused QKV projection + bias + RoPE + head-major scatter from h3 operands -> fp32 (q, k, vt)."""
+    if not _gpu(a3):
+        y = ref.h3_matmul(a3, w3, alpha)            # x @ w.T, then the rest of the fused op on fp32
+        eye = torch.eye(y.shape[1], dtype=torch.float32)
+        return ref.qkv_rope(y, eye, bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
+    _check_h3(a3, w3, alpha)
     _check_f32(bias)
     assert D == 64, "HIP attention path is specialised for head_dim 64"
-    M, Kx = x6.shape[0], w6.shape[1]
+    M, Kx = a3.shape[0], w3.shape[1]
     sp = s_pad(S)
-    f32 = dict(dtype=torch.float32, device=x6.device)
+    f32 = dict(dtype=torch.float32, device=a3.device)
     q = torch.empty(B, Hq, S, D, **f32)
     k = torch.empty(B, Hkv, S, D, **f32)
     vt = torch.zeros(B, Hkv, D, sp, **f32) if sp != S else torch.empty(B, Hkv, D, sp, **f32)
-    call("edge_gemm_qkv_rope_f32", ptr(x6), ptr(w6), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, S,
-         Hq, Hkv, rot_dim, sp, float(q_scale), stream())
+    call("edge_gemm_qkv_rope_f32", ptr(a3), ptr(w3), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, S,
+         Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), stream())
     return q, k, vt
 
 
-def head_nll_x6(h6: torch.Tensor, w6: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
-    """fp32 fused LM head + cross entropy on the scored rows from X6 operands: per-row NLL."""
-    if not _gpu(h6):
-        return ref.head_nll(ref.x6_to_f32(h6), ref.x6w_to_f32(w6), targets)
-    _check_x6(h6, w6)
-    R, Kx = h6.shape[0], w6.shape[1]
-    V = w6.shape[0]
+def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch.Tensor) -> torch.Tensor:
+    """fp32 fused LM head + cross entropy on the scored rows from h3 operands: per-row NLL."""
+    if not _gpu(a3):
+        logits = ref.h3_matmul(a3, w3, alpha)
+        return torch.logsumexp(logits, -1) - logits.gather(1, targets.long().view(-1, 1)).squeeze(1)
+    _check_h3(a3, w3, alpha)
+    R, Kx = a3.shape[0], w3.shape[1]
+    V = w3.shape[0]
     nparts = V // 64
-    f32 = dict(dtype=torch.float32, device=h6.device)
+    f32 = dict(dtype=torch.float32, device=a3.device)
     pmax, psum = torch.empty(R, nparts, **f32), torch.empty(R, nparts, **f32)
     tgt, nll = torch.empty(R, **f32), torch.empty(R, **f32)
     t64 = targets.to(torch.int64).contiguous()
-    call("edge_gemm_lse", ptr(h6), ptr(w6), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, 1, stream())
+    call("edge_gemm_lse", ptr(a3), ptr(w3), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, float(alpha), stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
 

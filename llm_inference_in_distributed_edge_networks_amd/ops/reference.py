@@ -182,53 +182,69 @@ def head_nll(h, w, targets):
     return torch.logsumexp(logits, -1) - logits.gather(1, targets.long().view(-1, 1)).squeeze(1)
 
 
-# ---- fp32 execution by split-bf16 MFMA ("X6", csrc/common.h) -------------------------------------------------
-# x = x0 + x1 + x2 exactly (three bf16 planes); a GEMM over the K-concatenations
-#   A' = [a2 | a0 | a1 | a1 | a0 | a0],  B' = [b0 | b2 | b1 | b0 | b1 | b0]
-# sums the six products a_i b_j with i + j <= 2, i.e. the fp32 product up to terms of relative size 2^-27.
-# Weights are stored as B' [N, 6K]; activations once per plane, [a0 | a1 | a2] [R, 3K] (the GEMM's A loader reads
-# block j of A' from plane X6_APLANES[j]).
-X6_APLANES = (2, 0, 1, 1, 0, 0)
-X6_BPLANES = (0, 2, 1, 0, 1, 0)
+# ---- fp32 GEMMs by split-fp16 MFMA ("h3", csrc/common.h) ---------------------------------------------------
+# s x = hi + lo with hi = fp16(s x), lo = fp16(s x - hi) (s a power of two that keeps both planes in the fp16
+# range); a GEMM over the K-concatenations
+#   A' = [a_lo | a_hi | a_hi],  B' = [b_hi | b_lo | b_hi]
+# sums hi_a hi_b + hi_a lo_b + lo_a hi_b = s_a s_b (a b) up to the dropped lo_a lo_b (2^-22 relative) and the
+# residual rounding (2^-23): below the CPU fp32 GEMM's own error (tools/h3_error.py).  Weights are stored as B'
+# [N, 3K] fp16; activations once per plane, [hi | lo] [R, 2K] fp16 (the GEMM's A loader reads block j of A' from
+# plane H3_APLANES[j]); the epilogue multiplies by alpha = 1 / (s_a s_b).
+H3_APLANES = (1, 0, 0)
+H3_BPLANES = (0, 1, 0)
+H3_TOP = 15   # the scaled bound is at most 2^15: hi and lo stay below the fp16 maximum 65504 (< 2^16)
 
 
-def split3(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    xf = _f(x)
-    p0 = xf.to(torch.bfloat16)
-    r = xf - p0.float()
-    p1 = r.to(torch.bfloat16)
-    p2 = (r - p1.float()).to(torch.bfloat16)
-    return p0, p1, p2
+def h3_scale(bound: float) -> float:
+    """Power-of-two s with s * bound <= 2^15 (largest such; 1 for a zero or non-finite bound)."""
+    bound = float(bound)
+    if not (bound > 0.0 and math.isfinite(bound)):
+        return 1.0
+    e = H3_TOP - math.ceil(math.log2(bound))
+    return float(2.0 ** max(-100, min(100, e)))
 
 
-def x6_act(x: torch.Tensor) -> torch.Tensor:
-    """fp32 [R, K] -> 3-plane X6 activation [R, 3K] bf16 = [a0 | a1 | a2] (what the fp32-mode kernels emit for
+def split2h(x: torch.Tensor, s: float) -> tuple[torch.Tensor, torch.Tensor]:
+    xs = _f(x) * s
+    hi = xs.to(torch.float16)
+    lo = (xs - hi.float()).to(torch.float16)
+    return hi, lo
+
+
+def h3_act(x: torch.Tensor, s: float) -> torch.Tensor:
+    """fp32 [R, K] -> 2-plane h3 activation [R, 2K] fp16 = [hi | lo] of s x (what the fp32-mode kernels emit for
     GEMM inputs)."""
-    return torch.cat(split3(x), -1).contiguous()
+    return torch.cat(split2h(x, s), -1).contiguous()
 
 
-def x6_expand(x6: torch.Tensor) -> torch.Tensor:
-    """3-plane activation [R, 3K] -> the A' K-concatenation [R, 6K] the GEMM reads (X6_APLANES)."""
-    K = x6.shape[-1] // 3
-    return torch.cat([x6[..., i * K:(i + 1) * K] for i in X6_APLANES], -1)
+def h3_expand(a3: torch.Tensor) -> torch.Tensor:
+    """2-plane activation [R, 2K] -> the A' K-concatenation [R, 3K] the GEMM reads (H3_APLANES)."""
+    K = a3.shape[-1] // 2
+    return torch.cat([a3[..., i * K:(i + 1) * K] for i in H3_APLANES], -1)
 
 
-def x6_weight(w: torch.Tensor) -> torch.Tensor:
-    """fp32 [N, K] nn.Linear weight -> X6 weight layout [N, 6K] bf16."""
-    p = split3(w)
-    return torch.cat([p[i] for i in X6_BPLANES], -1).contiguous()
+def h3_weight(w: torch.Tensor) -> tuple[torch.Tensor, float]:
+    """fp32 [N, K] nn.Linear weight -> (h3 weight [N, 3K] fp16, its scale s_w)."""
+    s = h3_scale(_f(w).abs().max().item())
+    p = split2h(w, s)
+    return torch.cat([p[i] for i in H3_BPLANES], -1).contiguous(), s
 
 
-def x6_to_f32(x6: torch.Tensor) -> torch.Tensor:
-    """Inverse of ``x6_act``: the fp32 value is the sum of the three planes (exact: a0 + a1 + a2 in fp32)."""
-    K = x6.shape[-1] // 3
-    return (x6[..., :K].float() + x6[..., K:2 * K].float()) + x6[..., 2 * K:].float()
+def h3_to_f32(a3: torch.Tensor, s: float = 1.0) -> torch.Tensor:
+    """Inverse of ``h3_act``: (hi + lo) / s (exact in fp32)."""
+    K = a3.shape[-1] // 2
+    return (a3[..., :K].float() + a3[..., K:].float()) / s
 
 
-def x6w_to_f32(w6: torch.Tensor) -> torch.Tensor:
-    """Inverse of ``x6_weight``: the sum of the three distinct planes (blocks 0, 2, 1)."""
-    K = w6.shape[-1] // 6
-    return (w6[..., :K].float() + w6[..., 2 * K:3 * K].float()) + w6[..., K:2 * K].float()
+def h3w_to_f32(w3: torch.Tensor, s: float = 1.0) -> torch.Tensor:
+    """Inverse of ``h3_weight``: (hi + lo) / s."""
+    K = w3.shape[-1] // 3
+    return (w3[..., :K].float() + w3[..., K:2 * K].float()) / s
+
+
+def h3_matmul(a3: torch.Tensor, w3: torch.Tensor, alpha: float) -> torch.Tensor:
+    """What the h3 GEMM computes: alpha * (A' @ B'^T), fp16 x fp16 products (exact) accumulated in fp32."""
+    return (h3_expand(a3).float() @ w3.float().t()) * alpha
 
 
 # ---- fused RMSNorm (GPU fast path) semantics -------------------------------------------------------

@@ -1,4 +1,4 @@
-"""fp32 execution mode (the reference's precision) on gfx950: X6 split-bf16 GEMMs, f32-MFMA attention, fp32 norms,
+"""fp32 execution mode (the reference's precision) on gfx950: h3 split-fp16 GEMMs, split-bf16 attention, fp32 norms,
 fp32 boundary codec - each kernel against the plain-PyTorch fp32 oracle (ops/reference.py), and whole models
 against the CPU fp32 model."""
 import math
@@ -31,12 +31,15 @@ def test_embedding_f32_exact():
     assert torch.equal(ops.embedding(ids.to(DEV), tab.to(DEV)).cpu(), R.embedding(ids, tab))
 
 
-def test_split6_bitwise():
+def test_split_h3_bitwise():
     x = rnd(300, 896, seed=2) * 10
-    x[0, :5] = torch.tensor([0.0, -0.0, 1e-30, 3.0e38, -7.5])
-    assert torch.equal(ops.split6(x.to(DEV)).cpu(), R.x6_act(x))
+    x[0, :5] = torch.tensor([0.0, -0.0, 1e-30, 1.0e3, -7.5])
+    s = R.h3_scale(x.abs().max().item())
+    assert torch.equal(ops.split_h3(x.to(DEV), s).cpu(), R.h3_act(x, s))
     rows = torch.tensor([7, 0, 299])
-    assert torch.equal(ops.split6(x.to(DEV), rows.to(DEV)).cpu(), R.x6_act(x[rows]))
+    assert torch.equal(ops.split_h3(x.to(DEV), s, rows.to(DEV)).cpu(), R.h3_act(x[rows], s))
+    # the planes hold s x to ~2^-22 relative; tiny entries keep their absolute accuracy
+    assert (R.h3_to_f32(R.h3_act(x, s), s) - x).abs().max() <= 2 ** -21 * x.abs().max()
 
 
 @pytest.mark.parametrize("H", [512, 896, 2048])
@@ -45,19 +48,22 @@ def test_rmsnorm_f32(H):
     w = rnd(H, s=0.2, seed=4) + 1
     ref = R.rmsnorm(x, w, 1e-6)
     assert rel_err(ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6), ref) < 2e-6
-    y6 = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6, x6=True)
-    assert rel_err(R.x6_to_f32(y6), ref) < 2e-6
+    s = R.h3_scale(math.sqrt(H) * w.abs().max().item())
+    y3 = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6, h3=s)
+    assert y3.dtype == torch.float16 and y3.shape == (300, 2 * H)
+    assert rel_err(R.h3_to_f32(y3, s), ref) < 2e-6
     rows = torch.tensor([5, 0, 299, 17])
-    y6r = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6, rows.to(DEV), x6=True)
-    assert rel_err(R.x6_to_f32(y6r), ref[rows]) < 2e-6
+    y3r = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6, rows.to(DEV), h3=s)
+    assert rel_err(R.h3_to_f32(y3r, s), ref[rows]) < 2e-6
 
 
 def test_layernorm_dual_f32():
     x = rnd(257, 512, seed=5) * 3 + 1
     w1, b1, w2, b2 = (rnd(512, s=0.3, seed=s) for s in range(6, 10))
-    y1, y2 = ops.layernorm_dual(*(t.to(DEV) for t in (x, w1, b1, w2, b2)), 1e-5, x6=True)
+    s1, s2 = 2.0 ** 9, 2.0 ** 7
+    y1, y2 = ops.layernorm_dual(*(t.to(DEV) for t in (x, w1, b1, w2, b2)), 1e-5, h3=(s1, s2))
     r1, r2 = R.layernorm_dual(x, w1, b1, w2, b2, 1e-5)
-    assert rel_err(R.x6_to_f32(y1), r1) < 3e-6 and rel_err(R.x6_to_f32(y2), r2) < 3e-6
+    assert rel_err(R.h3_to_f32(y1, s1), r1) < 3e-6 and rel_err(R.h3_to_f32(y2, s2), r2) < 3e-6
     z = ops.layernorm(x.to(DEV), w1.to(DEV), b1.to(DEV), 1e-5)
     assert rel_err(z, r1) < 3e-6
 
@@ -72,84 +78,100 @@ def _f32_matmul_err(x, w):
     (300, 896, 896, "resid"), (32768, 896, 896, "resid"), (32768, 896, 4864, "resid"),   # 256x224 (w7) kernel
     (4096, 9728, 896, "swiglu"), (300, 1152, 896, "none"), (2048, 2048, 512, "gelu"),    # 256x256 / 128x128
     (700, 512, 2048, "bias_resid"), (8192, 1024, 640, "bias"), (1000, 512, 512, "bias_resid")])
-def test_linear_x6_fp32_accuracy(M, N, K, epi):
+def test_linear_h3_fp32_accuracy(M, N, K, epi, slack=0):
+    """h3 GEMM vs fp64; ``slack`` binades of headroom between the activation's scaled maximum and the fp16 range
+    (the model's scales come from bounds, not from the data: the planes stay accurate far below the bound)."""
     x = rnd(M, K, seed=10)
     w = rnd(N, K, s=1 / math.sqrt(K), seed=11)
     b = rnd(N, s=0.1, seed=12) if "bias" in epi or epi == "gelu" else None
     r = rnd(M, N, seed=13) if "resid" in epi else None
     act = {"gelu": "gelu", "swiglu": "swiglu_il"}.get(epi)
-    y = ops.linear_x6(R.x6_act(x).to(DEV), R.x6_weight(w).to(DEV), None if b is None else b.to(DEV),
-                      None if r is None else r.to(DEV), act)
+    sx = R.h3_scale(x.abs().max().item()) / 2 ** slack
+    w3, sw = R.h3_weight(w)
     ref = x.double() @ w.double().t()
     if b is not None:
         ref = ref + b.double()
     if act == "gelu":
         ref = torch.nn.functional.gelu(ref)
-        y = R.x6_to_f32(y)
     elif act == "swiglu_il":
         g, u = R.deinterleave_gate_up(ref)
         ref = torch.nn.functional.silu(g) * u
-        y = R.x6_to_f32(y)
+    so = R.h3_scale(ref.abs().max().item())
+    y = ops.linear_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), None if b is None else b.to(DEV),
+                      None if r is None else r.to(DEV), act, out_scale=so)
+    if act is not None:
+        y = R.h3_to_f32(y, so)
     if r is not None:
         ref = ref + r.double()
     yard = _f32_matmul_err(x[:512], w)
     err = rel_err(y, ref)
-    # fp32-level: within a small factor of the CPU fp32 GEMM's own error (the X6 scheme drops 2^-27 terms;
-    # the X6 re-split of the epilogue output adds one fp32 rounding)
+    # fp32-level: within a small factor of the CPU fp32 GEMM's own error (the h3 scheme drops 2^-22 terms and
+    # rounds the residual plane at 2^-23; the h3 re-split of the epilogue output adds one more such rounding)
     assert err < max(4 * yard, 2e-6), (err, yard)
 
 
-def test_linear_x6_inplace_residual():
+@pytest.mark.parametrize("slack", [8, 14])
+def test_linear_h3_loose_scale(slack):
+    """Scales 2^8 / 2^14 below the data's own (the model's bounds are loose): still fp32-level."""
+    test_linear_h3_fp32_accuracy(2048, 896, 4864, "resid", slack)
+
+
+def test_linear_h3_inplace_residual():
     M, K, N = 32768, 896, 896
     x, w, r = rnd(M, K, seed=20), rnd(N, K, s=0.03, seed=21), rnd(M, N, seed=22)
     rd = r.to(DEV)
-    y = ops.linear_x6(R.x6_act(x).to(DEV), R.x6_weight(w).to(DEV), residual=rd, out=rd)
+    sx = R.h3_scale(x.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    y = ops.linear_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), residual=rd, out=rd)
     assert y.data_ptr() == rd.data_ptr()
     assert rel_err(y, x.double() @ w.double().t() + r.double()) < 2e-6
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv,rot", [(2, 512, 14, 2, 64), (2, 100, 14, 2, 64), (1, 2048, 8, 8, 16),
                                              (64, 512, 14, 2, 64), (24, 2048, 8, 8, 16)])
-def test_qkv_rope_x6(B, S, Hq, Hkv, rot):
-    """fp32 QKV+RoPE from X6 operands: 128x128 tiles (small M) and the four-wave 256x256 kernel (production M)."""
+def test_qkv_rope_h3(B, S, Hq, Hkv, rot):
+    """fp32 QKV+RoPE from h3 operands: 128x128 tiles (small M) and the four-wave 256x256 kernel (production M)."""
     H = 896 if Hq == 14 else 512
     Nq = (Hq + 2 * Hkv) * 64
     x = rnd(B * S, H, seed=30)
     w = rnd(Nq, H, s=1 / math.sqrt(H), seed=31)
     b = rnd(Nq, s=0.1, seed=32)
     cos, sin = R.rope_tables(4096, rot, 1e6 if rot == 64 else 1e4)
-    q, k, vt = ops.qkv_rope_x6(R.x6_act(x).to(DEV), R.x6_weight(w).to(DEV), b.to(DEV), cos.to(DEV), sin.to(DEV),
-                               B, S, Hq, Hkv, 64, rot, 0.125)
+    sx = R.h3_scale(x.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    q, k, vt = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV), cos.to(DEV),
+                               sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125)
     rq, rk, rv = R.qkv_rope(x.double(), w.double(), b.double(), cos.double(), sin.double(), B, S, Hq, Hkv, 64, rot,
                             0.125)
     assert rel_err(q, rq) < 4e-6 and rel_err(k, rk) < 4e-6 and rel_err(vt, rv) < 4e-6
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (3, 100, 14, 2), (1, 2048, 8, 8), (2, 64, 4, 1)])
-@pytest.mark.parametrize("x6", [False, True])
+@pytest.mark.parametrize("h3", [False, True])
 @pytest.mark.parametrize("variant", [0, 1, 2])
-def test_attention_f32(B, S, Hq, Hkv, x6, variant):
+def test_attention_f32(B, S, Hq, Hkv, h3, variant):
     """fp32 attention vs fp64: split-bf16 MFMA kernel (variant 0, 64 query rows per workgroup; 2: 128 rows) and the
     native f32 MFMA kernel (1).  The error is dominated by the fp32 exp2 (~5e-6 relative L2 for both kernels; bf16
     attention is ~1e-3)."""
     ops._native.lib().edge_attn_f32_set_variant(variant)
     try:
-        _attention_f32_case(B, S, Hq, Hkv, x6)
+        _attention_f32_case(B, S, Hq, Hkv, h3)
     finally:
         ops._native.lib().edge_attn_f32_set_variant(2)
 
 
-def _attention_f32_case(B, S, Hq, Hkv, x6):
+def _attention_f32_case(B, S, Hq, Hkv, h3):
     q = rnd(B, Hq, S, 64, seed=40) * 0.5
     k = rnd(B, Hkv, S, 64, seed=41) * 2
     v = rnd(B, Hkv, S, 64, seed=42)
     sp = R.s_pad(S)
     vt = torch.zeros(B, Hkv, 64, sp)
     vt[..., :S] = v.transpose(-1, -2)
-    o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True, x6=x6)
+    s = R.h3_scale(v.abs().max().item()) if h3 else 0.0
+    o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True, h3=s)
     ro, rl = R.attention(q.double(), k.double(), vt.double(), S, need_lse=True)
-    if x6:
-        o = R.x6_to_f32(o)
+    if h3:
+        o = R.h3_to_f32(o, s)
     assert rel_err(o, ro) < 1e-5
     assert float((lse.cpu().double() - rl).abs().max()) < 5e-5
 
@@ -180,15 +202,17 @@ def test_importance_stats_f32(B, S, Hq, Hkv):
 
 
 @pytest.mark.parametrize("R_", [200, 2048])
-def test_head_nll_x6(R_):
-    """fp32 LM head + CE from X6 operands: 128x128 tiles (200 rows) and the four-wave 256x256 kernel (2048 rows,
+def test_head_nll_h3(R_):
+    """fp32 LM head + CE from h3 operands: 128x128 tiles (200 rows) and the four-wave 256x256 kernel (2048 rows,
     partial last vocabulary tile); the first 96 rows against fp64."""
     H, V = 896, 151936
     h = rnd(R_, H, seed=60)
     w = rnd(V, H, s=0.05, seed=61)
     t = torch.randint(0, V, (R_,))
     t[:3] = torch.tensor([0, V - 1, V - 100])
-    nll = ops.head_nll_x6(R.x6_act(h).to(DEV), R.x6_weight(w).to(DEV), t.to(DEV))
+    sh = R.h3_scale(h.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    nll = ops.head_nll_h3(R.h3_act(h, sh).to(DEV), w3.to(DEV), 1.0 / (sh * sw), t.to(DEV))
     ref = R.head_nll(h[:96].double(), w.double(), t[:96])
     assert float((nll[:96].cpu().double() - ref).abs().max()) < 2e-5
 
@@ -258,23 +282,23 @@ def test_full_model_nll_matches_cpu_fp32(name, B, S):
 
 @pytest.mark.parametrize("M,N,K,epi", [(32768, 9728, 896, "swiglu"), (4096, 2048, 512, "gelu"),
                                        (1000, 1024, 896, "resid"), (700, 2048, 512, "bias")])
-@pytest.mark.parametrize("tile", ["256e", "256w", "256wp"])
-def test_linear_x6_eight_phase(M, N, K, epi, tile):
-    """The X6 (fp32-mode) GEMMs on the eight-phase (variant 10) and four-wave (variant 11) main loops."""
+@pytest.mark.parametrize("tile", ["256", "256w", "256wp"])
+def test_linear_h3_main_loops(M, N, K, epi, tile):
+    """The h3 (fp32-mode) GEMMs on the C256 (variant 1) and four-wave (variant 11 / 12) main loops."""
     ops.set_gemm_config(tile)
     try:
-        test_linear_x6_fp32_accuracy(M, N, K, {"resid": "resid", "gelu": "gelu", "swiglu": "swiglu",
+        test_linear_h3_fp32_accuracy(M, N, K, {"resid": "resid", "gelu": "gelu", "swiglu": "swiglu",
                                                 "bias": "bias"}[epi])
     finally:
         ops.set_gemm_config("0")
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 896, 896), (32768, 896, 896), (32768, 896, 4864), (256 * 3 + 5, 2688, 128)])
-def test_linear_x6_four_wave_224(M, N, K):
+def test_linear_h3_four_wave_224(M, N, K):
     """The fp32-residual O-proj / down GEMMs on the four-wave 256x224 kernel."""
     ops.set_gemm_config("224w")
     try:
-        test_linear_x6_fp32_accuracy(M, N, K, "resid")
+        test_linear_h3_fp32_accuracy(M, N, K, "resid")
     finally:
         ops.set_gemm_config("0")
 

@@ -108,7 +108,7 @@ def test_fp32_calibration_table_matches_cpu_full_qwen2():
     from llm_inference_in_distributed_edge_networks_amd.relevance.engine import RelevanceEngine
     cfg = get_config("qwen2-0.5b")
     mc = DecoderLM.random_init(cfg, 7, std=0.02)
-    mg = DecoderLM.random_init(cfg, 7, device=DEV, std=0.02, x6=False)
+    mg = DecoderLM.random_init(cfg, 7, device=DEV, std=0.02, h3=False)
     ids = torch.randint(0, cfg.vocab_size, (2, 128), generator=torch.Generator().manual_seed(3))
     rc, _, _, cc = head_relevance_batched(mc, ids)
     rg, _, _, cg = head_relevance_batched(mg, ids.to(DEV))

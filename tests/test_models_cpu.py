@@ -72,21 +72,56 @@ def test_presets():
 
 
 @pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX])
-def test_x6_execution_path_matches_fp32(cfg):
-    """The fp32 GPU mode's op sequence (X6 split-bf16 GEMM operands, ops.*_x6) run on CPU equals plain fp32."""
+def test_h3_execution_path_matches_fp32(cfg):
+    """The fp32 GPU mode's op sequence (h3 split-fp16 GEMM operands, ops.*_h3) run on CPU equals plain fp32."""
     ref_m = DecoderLM.random_init(cfg, 5)
-    x6_m = DecoderLM.random_init(cfg, 5, x6=True)
+    h3_m = DecoderLM.random_init(cfg, 5, h3=True)
     ids = torch.randint(0, cfg.vocab_size, (2, 48), generator=torch.Generator().manual_seed(3))
     B, S = ids.shape
-    xr, xx = ref_m.embed(ids), x6_m.embed(ids)
+    xr, xx = ref_m.embed(ids), h3_m.embed(ids)
     for i in range(cfg.num_layers):
         xr, sr = ref_m.layer(i, xr, B, S, stats=("lastrow", "colsum"))
-        xx, sx = x6_m.layer(i, xx, B, S, stats=("lastrow", "colsum"))
+        xx, sx = h3_m.layer(i, xx, B, S, stats=("lastrow", "colsum"))
         assert torch.allclose(sx.lastrow, sr.lastrow, atol=1e-6) and torch.allclose(sx.colsum, sr.colsum, atol=1e-5)
     assert (xx - xr).abs().max() < 1e-4
     rows = torch.arange(S - 8, S).repeat(B) + torch.arange(B).repeat_interleave(8) * S
     tg = torch.randint(0, cfg.vocab_size, (rows.numel(),))
-    assert torch.allclose(x6_m.row_nll(xx, rows, tg), ref_m.row_nll(xr, rows, tg), atol=1e-4)
+    assert torch.allclose(h3_m.row_nll(xx, rows, tg), ref_m.row_nll(xr, rows, tg), atol=1e-4)
     # last-layer scored-rows shortcut
-    xl = x6_m.layer_rows(cfg.num_layers - 1, x6_m.forward_hidden(ids, 0, cfg.num_layers - 1), B, S, rows)
+    xl = h3_m.layer_rows(cfg.num_layers - 1, h3_m.forward_hidden(ids, 0, cfg.num_layers - 1), B, S, rows)
     assert torch.allclose(xl, xr.index_select(0, rows), atol=1e-4)
+
+
+@pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX])
+def test_h3_bounds_hold(cfg):
+    """Every GEMM input of the fp32 mode stays below its bound (so s * |x| <= 2^15, inside fp16), for inputs far
+    outside the trained range: huge residual streams, one-hot rows, all-equal rows."""
+    from llm_inference_in_distributed_edge_networks_amd import ops
+    from llm_inference_in_distributed_edge_networks_amd.models.model import _h3_bounds
+    m = DecoderLM.random_init(cfg, 9)
+    g = torch.Generator().manual_seed(1)
+    B, S, H = 2, 40, cfg.hidden_size
+    x = torch.randn(B * S, H, generator=g) * 1e4
+    x[0] = 0.0
+    x[0, 3] = 5e5
+    x[1] = 7.0
+    for i, L in enumerate(m.layers):
+        bd = _h3_bounds(cfg, L)
+        if cfg.arch == "qwen2":
+            h = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps)
+        else:
+            h, h2 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps)
+        assert h.abs().max() <= bd["qkv"] * (1 + 1e-5)
+        q, k, vt = ops.qkv_rope(h, L["wqkv"], L["bqkv"], m.cos, m.sin, B, S, cfg.num_heads, cfg.num_kv_heads,
+                                cfg.head_dim, cfg.rotary_dim, m.q_scale)
+        o, _ = ops.attention(q, k, vt, S)
+        assert o.abs().max() <= bd["o"] * (1 + 1e-5)
+        y = ops.linear(o, L["wo"], L.get("bo"), residual=x)
+        if cfg.arch == "qwen2":
+            h2 = ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps)
+            a = ops.linear(h2, L["wgu"], act="swiglu_il")
+        else:
+            a = ops.linear(h2, L["wfc"], L["bfc"], act="gelu")
+        assert h2.abs().max() <= bd["mlp"] * (1 + 1e-5)
+        assert a.abs().max() <= bd["down"] * (1 + 1e-5)
+        x = y

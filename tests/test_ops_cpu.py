@@ -75,22 +75,33 @@ def test_native_library_exports_every_bound_entry_point():
     assert [n for n in _native._SIGS if not hasattr(L, n)] == []
 
 
-def test_x6_three_plane_activation_layout():
-    """3-plane X6 activations [a0|a1|a2] expand to the A' K-concatenation the GEMM reads (blocks 2 0 1 1 0 0), and
-    A' @ B'^T over the six bf16 products is fp32-accurate."""
+def test_h3_two_plane_activation_layout():
+    """2-plane h3 activations [hi|lo] of s x expand to the A' K-concatenation the GEMM reads (blocks 1 0 0), and
+    alpha A' @ B'^T over the three fp16 products is fp32-accurate (below the fp32 GEMM's own error)."""
     import torch
 
     from llm_inference_in_distributed_edge_networks_amd.ops import reference as R
     g = torch.Generator().manual_seed(0)
-    x, w = torch.randn(64, 128, generator=g), torch.randn(96, 128, generator=g) / 11
-    a3 = R.x6_act(x)
-    assert a3.shape == (64, 384) and a3.dtype == torch.bfloat16
-    assert torch.equal(R.x6_to_f32(a3), (a3[:, :128].float() + a3[:, 128:256].float()) + a3[:, 256:].float())
-    assert (R.x6_to_f32(a3) - x).abs().max() <= 1e-6 * x.abs().max()
-    ap = R.x6_expand(a3)
-    for j, p in enumerate(R.X6_APLANES):
-        assert torch.equal(ap[:, 128 * j:128 * (j + 1)], a3[:, 128 * p:128 * (p + 1)])
-    y = ap.double() @ R.x6_weight(w).double().t()
+    x, w = torch.randn(64, 896, generator=g), torch.randn(96, 896, generator=g) / 30
+    s = R.h3_scale(x.abs().max().item())
+    assert s * x.abs().max() <= 2 ** 15 < 2 * s * x.abs().max()
+    a3 = R.h3_act(x, s)
+    assert a3.shape == (64, 2 * 896) and a3.dtype == torch.float16
+    assert (R.h3_to_f32(a3, s) - x).abs().max() <= 2 ** -21 * x.abs().max()
+    ap = R.h3_expand(a3)
+    for j, p in enumerate(R.H3_APLANES):
+        assert torch.equal(ap[:, 896 * j:896 * (j + 1)], a3[:, 896 * p:896 * (p + 1)])
+    w3, sw = R.h3_weight(w)
+    y = ap.double() @ w3.double().t() / (s * sw)
     ref = x.double() @ w.double().t()
-    assert ((y - ref).abs().max() / ref.abs().max()) < 1e-6
-    assert torch.allclose(R.x6w_to_f32(R.x6_weight(w)), w, rtol=0, atol=1e-6)
+    e32 = ((x @ w.t()).double() - ref).norm() / ref.norm()
+    assert ((y - ref).norm() / ref.norm()) < max(e32, 1e-7)
+    assert (R.h3w_to_f32(w3, sw) - w).abs().max() <= 2 ** -21 * w.abs().max()
+
+
+def test_h3_scale_keeps_fp16_range():
+    from llm_inference_in_distributed_edge_networks_amd.ops import reference as R
+    for b in (1e-30, 3e-5, 0.7, 1.0, 1.5, 30.0, 65504.0, 1e9):
+        s = R.h3_scale(b)
+        assert s * b <= 2 ** 15 < 2 * s * b or s in (2.0 ** 100, 2.0 ** -100)
+    assert R.h3_scale(0.0) == 1.0 and R.h3_scale(float("inf")) == 1.0

@@ -60,15 +60,15 @@ def bench_fp32(a):
     for _ in range(a.rounds):
         for v, name in ((0, "x6_bf16_mfma"), (2, "x6_bf16_mfma_128rows"), (1, "f32_mfma")):
             lib.edge_attn_f32_set_variant(v)
-            for x6 in (False, True):
-                ops.attention(q, k, vt, S, need_lse=True, x6=x6)
+            for h3 in (0.0, 1.0):
+                ops.attention(q, k, vt, S, need_lse=True, h3=h3)
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 st.record()
                 for _ in range(a.iters):
-                    ops.attention(q, k, vt, S, need_lse=True, x6=x6)
+                    ops.attention(q, k, vt, S, need_lse=True, h3=h3)
                 en.record()
                 torch.cuda.synchronize()
-                res.setdefault(f"{name}{'_x6out' if x6 else ''}", []).append(st.elapsed_time(en) / a.iters * 1e3)
+                res.setdefault(f"{name}{'_h3out' if h3 else ''}", []).append(st.elapsed_time(en) / a.iters * 1e3)
     lib.edge_attn_f32_set_variant(2)
     out = {k_: {"us": round(min(v), 2), "TFLOPs_fp32": round(flop / min(v) * 1e-6, 1)} for k_, v in res.items()}
     print(json.dumps({"shape": [B, S, Hq, Hkv], "dtype": "fp32", **out}))

@@ -23,15 +23,14 @@ SHAPES = {  # name: (M, N, K, act, bias, resid)
     "gate_up_b64": (32768, 9728, 896, "swiglu_il", False, False),
     "big": (8192, 8192, 8192, None, False, False),
     "qkv_rope_b64": (32768, 1152, 896, "qkv_rope", True, False),   # fused QKV + bias + RoPE + scatter epilogue
-    # fp32 execution mode (X6 split-bf16 operands, K' = 6K): TF/s below count the bf16 MFMA work (6x the fp32 FLOPs)
-    "x6_gate_up_b64": (32768, 9728, 6 * 896, "x6_swiglu", False, False),
-    "x6_down_b64": (32768, 896, 6 * 4864, "x6", False, True),
-    "x6_o_proj_b64": (32768, 896, 6 * 896, "x6", False, True),
-    "x6_big": (8192, 8192, 6 * 1024, "x6", False, False),
-    "x6_qkv_rope_b64": (32768, 1152, 6 * 896, "x6_qkv_rope", True, False),
-    # epilogue-cost ablations of the x6 gate/up shape: plain fp32 output, plain bf16 output
-    "x6_gate_up_f32out": (32768, 9728, 6 * 896, "x6", False, False),
-    "gate_up_k5376_bf16out": (32768, 9728, 6 * 896, None, False, False),
+    # fp32 execution mode (h3 split-fp16 operands, K' = 3K): TF/s below count the fp16 MFMA work (3x the fp32 FLOPs)
+    "h3_gate_up_b64": (32768, 9728, 3 * 896, "h3_swiglu", False, False),
+    "h3_down_b64": (32768, 896, 3 * 4864, "h3", False, True),
+    "h3_o_proj_b64": (32768, 896, 3 * 896, "h3", False, True),
+    "h3_big": (8192, 8192, 3 * 1024, "h3", False, False),
+    "h3_qkv_rope_b64": (32768, 1152, 3 * 896, "h3_qkv_rope", True, False),
+    # epilogue-cost ablation of the h3 gate/up shape: plain fp32 output
+    "h3_gate_up_f32out": (32768, 9728, 3 * 896, "h3", False, False),
 }
 
 
@@ -62,14 +61,15 @@ def main():
         if a.only and name not in a.only.split(","):
             continue
         M = a.m or M if name != "lm_head" else M
-        x6 = act is not None and act.startswith("x6")
-        # X6 shapes: K is the GEMM's K' = 6 x plane width; the activation is stored once per plane ([M, K'/2])
-        x = (torch.rand(M, K // 2 if x6 else K, device=dev) * 2 - 1).to(torch.bfloat16)
-        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
-        b = torch.randn(N, device=dev).to(torch.float32 if x6 else torch.bfloat16) if bias else None
-        No = N // 2 if act in ("swiglu_il", "x6_swiglu") else N
-        r = torch.randn(M, No, device=dev).to(torch.float32 if x6 else torch.bfloat16) if resid else None
-        out = torch.empty(M, No, device=dev, dtype=torch.float32 if x6 else torch.bfloat16)
+        h3 = act is not None and act.startswith("h3")
+        # h3 shapes: K is the GEMM's K' = 3 x plane width; the activation is stored once per plane ([M, 2K'/3])
+        dt = torch.float16 if h3 else torch.bfloat16
+        x = (torch.rand(M, 2 * K // 3 if h3 else K, device=dev) * 2 - 1).to(dt)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(dt)
+        b = torch.randn(N, device=dev).to(torch.float32 if h3 else torch.bfloat16) if bias else None
+        No = N // 2 if act in ("swiglu_il", "h3_swiglu") else N
+        r = torch.randn(M, No, device=dev).to(torch.float32 if h3 else torch.bfloat16) if resid else None
+        out = torch.empty(M, No, device=dev, dtype=torch.float32 if h3 else torch.bfloat16)
         tiles = a.tiles.split(",")
 
         def mk(spec):  # spec may end in "/w0" = strided persistent tile walk instead of XCD chunks, or "/noepi" =
@@ -87,24 +87,24 @@ def main():
                 ops._native.lib().edge_gemm_set_w7_mode(mode)
                 if act == "qkv_rope":
                     ops.qkv_rope(x, w, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
-                elif act == "x6_qkv_rope":
-                    ops.qkv_rope_x6(x, w, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
-                elif act == "x6_swiglu":
-                    ops.linear_x6(x, w, act="swiglu_il")
-                elif act == "x6":
-                    ops.linear_x6(x, w, bias=b, residual=r, out=out)
+                elif act == "h3_qkv_rope":
+                    ops.qkv_rope_h3(x, w, 1.0, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
+                elif act == "h3_swiglu":
+                    ops.linear_h3(x, w, 1.0, act="swiglu_il")
+                elif act == "h3":
+                    ops.linear_h3(x, w, 1.0, bias=b, residual=r, out=out)
                 else:
                     ops.linear(x, w, bias=b, residual=r, act=act, out=out)
                 ops._native.lib().edge_gemm_set_skip_epi(0)
                 ops._native.lib().edge_gemm_set_w7_mode(0)
             return f
-        if act in ("qkv_rope", "x6_qkv_rope"):
+        if act in ("qkv_rope", "h3_qkv_rope"):
             cos, sin = (t.to(dev) for t in ops.rope_tables(512, 64, 1e6))
         variants = {t: mk(t) for t in tiles}
         ours = variants[tiles[0]]
-        xl = torch.cat([x, x], 1) if x6 else x   # hipBLASLt reference: the same K' GEMM on plain operands
+        xl = torch.cat([x, x[:, :K // 3]], 1) if h3 else x   # hipBLASLt reference: the same K' GEMM, plain operands
         lib = lambda: torch.matmul(xl, w.t())  # noqa: E731
-        if resid and not x6:  # hipBLASLt with the residual as beta*C (what a library route for RESID GEMMs would run)
+        if resid and not h3:  # hipBLASLt with the residual as beta*C (what a library route for RESID GEMMs would run)
             variants["libr"] = lambda: torch.addmm(r, x, w.t())
         for _ in range(3):
             ours(); lib()

@@ -4,7 +4,7 @@
 // `-Xarch_host -fsanitize=address` (host code instrumented, the gfx950 code objects unchanged - GPU ASan / XNACK
 // are not available on this pool) and linked with this driver into one executable, so the ASan runtime is linked
 // in (no preload).  It drives the C ABI entry points the Python layer uses - GEMMs with every epilogue family,
-// fp32 (X6) GEMM, norms, attention, codec select/pack/unpack, argument validation paths, and an RCCL world-1
+// fp32 (h3) GEMM, norms, attention, codec select/pack/unpack, argument validation paths, and an RCCL world-1
 // loopback - on small shapes, and checks the return codes.  Any heap / stack misuse in the host code (argument
 // structs, dispatch tables, layout arithmetic, communicator lifetime) aborts with an ASan report.
 #include <hip/hip_runtime.h>
@@ -17,11 +17,13 @@ extern "C" {
 int edge_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, const void* bias,
               const void* resid, int ldr, int act, const float* rscale, float* ssq_out, hipStream_t st);
 int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, int Kx, int lda, int ldb, int ldc,
-                  const float* bias, const float* resid, int ldr, int act, const float* rscale, hipStream_t st);
-int edge_rmsnorm_f32(const float* x, const float* w, void* y, const int* rows, int R, int H, float eps, int out_x6,
-                     hipStream_t st);
+                  const float* bias, const float* resid, int ldr, int act, const float* rscale, float alpha,
+                  float out_scale, hipStream_t st);
+int edge_rmsnorm_f32(const float* x, const float* w, void* y, const int* rows, int R, int H, float eps,
+                     float h3_scale, hipStream_t st);
 int edge_flash_attn_fwd_f32(const float* q, const float* k, const float* vt, void* o, float* lse,
-                            const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, int out_x6, hipStream_t st);
+                            const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float out_h3_scale,
+                            hipStream_t st);
 int edge_select(const float* imp, int B, int S, int k, void* msg, long long off_mask, int mode, float thr,
                 long long off_kvec, hipStream_t st);
 int edge_pack(const void* x, void* msg, long long om, long long os, long long oh, long long ol, long long okv,
@@ -95,17 +97,19 @@ int main() {
   EXPECT(edge_gemm(bufs[0], bufs[1], bufs[2], 0, 512, 256, 256, 256, 512, nullptr, nullptr, 0, 0, nullptr, nullptr,
                    st), 0);
 
-  // fp32 mode: X6 GEMM (3-plane activation [M, 3K], weight [N, 6K]), fp32 out + SwiGLU X6 out, RMSNorm -> X6
+  // fp32 mode: h3 GEMM (2-plane activation [M, 2K], weight [N, 3K]), fp32 out + SwiGLU h3 out, RMSNorm -> h3
   {
-    const int M = 4096, N = 512, K = 128, Kx = 6 * K;
-    void *a = A((size_t)M * 3 * K * 2), *b = A((size_t)N * Kx * 2), *c = A((size_t)M * N * 4),
-         *c6 = A((size_t)M * 3 * (N / 2) * 2);
-    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, 3 * K, Kx, N, nullptr, nullptr, 0, 0, nullptr, st), 0);
-    EXPECT(edge_gemm_f32(a, b, c6, M, N, Kx, 3 * K, Kx, 3 * (N / 2), nullptr, nullptr, 0, 2, nullptr, st), 0);
-    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, K, Kx, N, nullptr, nullptr, 0, 0, nullptr, st),
-           (int)hipErrorInvalidValue);   // lda smaller than the 3-plane row
+    const int M = 4096, N = 512, K = 128, Kx = 3 * K;
+    void *a = A((size_t)M * 2 * K * 2), *b = A((size_t)N * Kx * 2), *c = A((size_t)M * N * 4),
+         *c3 = A((size_t)M * 2 * (N / 2) * 2);
+    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, 2 * K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 1.f, 1.f, st), 0);
+    EXPECT(edge_gemm_f32(a, b, c3, M, N, Kx, 2 * K, Kx, 2 * (N / 2), nullptr, nullptr, 0, 2, nullptr, 1.f, 1.f, st), 0);
+    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 1.f, 1.f, st),
+           (int)hipErrorInvalidValue);   // lda smaller than the 2-plane row
+    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, 2 * K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 0.f, 1.f, st),
+           (int)hipErrorInvalidValue);   // no product scale
     float *x = (float*)A((size_t)M * K * 4), *w = (float*)A(K * 4);
-    EXPECT(edge_rmsnorm_f32(x, w, c6, nullptr, M, K, 1e-6f, 1, st), 0);
+    EXPECT(edge_rmsnorm_f32(x, w, c3, nullptr, M, K, 1e-6f, 1.f, st), 0);
   }
   // fp32 attention + LSE
   {
@@ -113,8 +117,8 @@ int main() {
     float *q = (float*)A((size_t)B * Hq * S * 64 * 4), *k = (float*)A((size_t)B * Hkv * S * 64 * 4),
           *vt = (float*)A((size_t)B * Hkv * 64 * sp * 4), *o = (float*)A((size_t)B * S * Hq * 64 * 4),
           *lse = (float*)A((size_t)B * Hq * S * 4);
-    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, sp, 0, st), 0);
-    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, 100, 0, st), (int)hipErrorInvalidValue);
+    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, sp, 0.f, st), 0);
+    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, 100, 0.f, st), (int)hipErrorInvalidValue);
   }
   // codec: mixed int4 / int8 per-token message, fixed k (layout of codec/wire.py for B 2, S 64, H 256, k 32)
   {
