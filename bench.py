@@ -14,9 +14,13 @@ split after layer ``--split``; ``--pp 4`` / ``--pp 8`` are BASELINE configs 4-5,
 the same stages in one process on the one GPU (the boundary is still encoded and decoded).
 
 Precision: ``--dtype fp32`` (default) is the reference's precision (it loads its models without a torch_dtype,
-``Experiments/Qwen2-0.5B/qwen_layer_wise.py:17``): fp32 residual stream, norms, softmax, attention (f32 matrix
-cores) and codec, GEMMs on h3 split-fp16 operands (fp32-accurate, see ``ops.reference.h3_act``).  A second, separately
-timed run of the bf16 mode is reported as ``value_bf16`` (``--no-bf16`` skips it).
+``Experiments/Qwen2-0.5B/qwen_layer_wise.py:17``): fp32 residual stream, norms, softmax, attention (split-bf16
+matrix-core products) and codec, GEMMs on h3 split-fp16 operands (fp32-accurate, see ``ops.reference.h3_act``).
+The random weights have bf16 VALUES held in fp32 tensors by default (``--weight-values``): that is what the reference
+computes with, since the HF Qwen2-0.5B checkpoint stores bf16 (``torch_dtype: bfloat16``) and the reference upcasts
+it to fp32.  Such weights are exact in fp16 after scaling, so their h3 GEMMs need two fp16 products instead of three
+(the third is exactly zero).  Separately timed runs: the same fp32 run on full-fp32 random weight values
+(``value_fp32_weights``, ``--no-fp32-weights`` skips it) and the bf16 mode (``value_bf16``, ``--no-bf16``).
 
 ``value`` = window tokens processed per second over the whole job (every window is a full 512-token forward, as in
 the reference); scored tokens/s, PPL and the measured wire bytes/token are reported alongside, plus a per-stage GPU
@@ -78,23 +82,29 @@ def parse():
                    help="stage hand-off: torch.distributed p2p (RCCL), the native RCCL wrapper, or peer copies into "
                         "IPC-mapped receive slots (ipc)")
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--weight-values", default="bf16", choices=["bf16", "fp32"],
+                   help="precision of the random weight VALUES (held in fp32 in the fp32 mode): bf16 = as the HF "
+                        "Qwen2-0.5B checkpoint the reference upcasts to fp32 (torch_dtype bfloat16); fp32 = full fp32 "
+                        "random values (reported as value_fp32_weights)")
+    p.add_argument("--no-fp32-weights", action="store_true", help="skip the fp32-valued-weights measurement")
     p.add_argument("--json-out", default="")
     return p.parse_args()
 
 
-def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup):
-    """Build the model/pipeline for ``dtype`` and time ``timed_steps`` steps after ``warmup``.  Returns a dict."""
+def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None):
+    """Build the model/pipeline for ``dtype`` (random weights with ``values`` precision) and time ``timed_steps``
+    steps after ``warmup``.  Returns a dict."""
     dev = env.device
     world = env.world_size
     dist_pp = world > 1 and pp > 1
     bcfg = BoundaryConfig(a.codec, a.ratio, a.method)
     if not dist_pp:
-        model, prov = build_model(cfg, dev, dtype, seed=a.seed)
+        model, prov = build_model(cfg, dev, dtype, seed=a.seed, values=values)
         runner = LocalPipeline(model, plan, bcfg, use_graphs=not a.no_graphs)
     else:
         _, stage = grid.coords(env.rank)
         model, prov = build_model(cfg, dev, dtype, seed=a.seed, layers=plan.stage_layers(stage),
-                                  with_embed=(stage == 0), with_head=(stage == pp - 1))
+                                  with_embed=(stage == 0), with_head=(stage == pp - 1), values=values)
         runner = DistributedPipeline(model, plan, bcfg, grid, env.rank, use_graphs=not a.no_graphs,
                                      transport=a.transport)
 
@@ -178,7 +188,8 @@ def main():
             PipelinePlan.balanced(cfg, pp, a.max_length, a.stride / a.max_length))
     dtype = DTYPES[a.dtype] if env.device.type == "cuda" else torch.float32
 
-    main_run = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup)
+    values = torch.bfloat16 if a.weight_values == "bf16" else None
+    main_run = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup, values)
     dt = main_run["dt"]
     tok_per_step = grid.dp * a.microbatches * a.batch * a.max_length
     scored_per_step = grid.dp * a.microbatches * a.batch * a.stride
@@ -186,16 +197,20 @@ def main():
     spec = C.get_codec(a.codec)
     wires = [C.message_bytes(spec, a.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
              / (a.batch * a.max_length)] * (pp - 1)
-    second = None
+    second = fp32w = None
+    if values is not None and not a.no_fp32_weights and dtype == torch.float32 and env.device.type == "cuda":
+        fp32w = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup, None)
     if not a.no_bf16 and dtype == torch.float32 and env.device.type == "cuda":
-        second = measure(a, env, cfg, torch.bfloat16, pp, grid, plan, a.steps, a.warmup)
+        second = measure(a, env, cfg, torch.bfloat16, pp, grid, plan, a.steps, a.warmup, values)
     dname = {torch.float32: "fp32", torch.bfloat16: "bf16"}[dtype]
     out = {
         "metric": METRIC,
         "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(1000 * dt / a.steps, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": round(value / BASELINE_TOKENS_PER_S, 2), "dtype": dname,
-        "data": "synthetic (WikiText-2-test-length Zipf token stream), random-init weights",
+        "data": "synthetic (WikiText-2-test-length Zipf token stream), random-init weights"
+                + (" with bf16 values held in fp32 (as the HF Qwen2-0.5B checkpoint, torch_dtype bfloat16, that the "
+                   "reference upcasts to fp32)" if values is not None else ""),
         "config": {"model": cfg.name, "global_batch": grid.dp * a.microbatches * a.batch, "seq_len": a.max_length,
                    "stride": a.stride, "parallelism": f"pp{pp}xdp{grid.dp}" if dist_pp else f"local-pp{pp}",
                    "stage_layers": [[r.start, r.stop - 1] for r in (plan.stage_layers(s) for s in range(pp))],
@@ -211,6 +226,10 @@ def main():
     }
     if main_run["stages"]:
         out["stages"] = main_run["stages"]
+    if fp32w is not None:   # the same fp32 run on full-fp32 random weight values (three-product h3 GEMMs)
+        out["value_fp32_weights"] = round(tok_per_step * a.steps / fp32w["dt"], 1)
+        out["ms_per_step_fp32_weights"] = round(1000 * fp32w["dt"] / a.steps, 3)
+        out["ppl_random_weights_fp32_weights"] = fp32w["ppl"]
     if second is not None:
         out["value_bf16"] = round(tok_per_step * a.steps / second["dt"], 1)
         out["ms_per_step_bf16"] = round(1000 * second["dt"] / a.steps, 3)

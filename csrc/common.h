@@ -45,11 +45,12 @@ __device__ __forceinline__ void split3(float x, float& p0, float& p1, float& p2)
 // derives s_a per GEMM input from a bound on |x| that holds for any input (models/model.py h3 scales: RMSNorm /
 // LayerNorm outputs, attention outputs and SwiGLU / GELU outputs are bounded by the weights), s_b from max |w|.
 // Weights are stored as B' [N, 3K]; an activation once per plane, [hi | lo] ([rows, 2K]), and the GEMM's A loader
-// reads K-block j of A' from plane (1 0 0)[j] (h3_acol).
+// reads K-block j of A' from plane (1 0 0)[j] (h3_acol).  A weight that is exact in fp16 after scaling (b_lo = 0: a
+// bf16 or fp16 checkpoint, as the HF Qwen2 / Pythia releases) needs only the two products a_lo b_hi + a_hi b_hi,
+// the K' = 2K GEMM on B' = [b_hi | b_hi] (the same result: the third term is exactly zero).
 typedef uint16_t f16_t;   // fp16 storage as raw 16-bit words
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
 typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
-constexpr int H3_TERMS = 3;
 __device__ __forceinline__ void split2h(float x, float& hi, float& lo) {
   hi = (float)(_Float16)x;
   lo = (float)(_Float16)(x - hi);

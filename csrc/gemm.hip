@@ -54,7 +54,7 @@ struct GemmArgs {
   int rs_lds;    // persistent 256x256: row scales DMA'd to LDS in the last K-tile (default 1; 0 = A/B baseline)
   int skip_epi;  // timing ablation only (wrong results): 1 = no epilogue (gemm_bf16 / w7 kernels); 2 = persistent
                  // 256x256 SwiGLU epilogue computed but not stored
-  int h3k;       // > 0: A is a 2-plane h3 activation [M, 2 h3k] (common.h h3_acol) of the K' = 3 h3k GEMM
+  int h3k;       // > 0: A is a 2-plane h3 activation [M, 2 h3k] (common.h h3_acol) of the K' = 3 h3k (or 2 h3k) GEMM
   float alpha = 1.f;      // h3: 1 / (s_a s_b), the product's scale (applied with the row scale)
   float out_scale = 1.f;  // h3 outputs (SwiGLU / GELU): the next GEMM's input scale s_a
 };
@@ -2293,21 +2293,28 @@ EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, 
   }
 }
 
-// fp32 execution (h3 operands, common.h): A a 2-plane h3 activation [M, 2K] (lda >= 2K), B the h3 weight [N, 3K],
-// so the K of the GEMM is Kx = 3K; alpha = 1 / (s_a s_b).  act 0 none -> fp32 C [M, ldc] (+ fp32 bias, + fp32
+// h3 operand geometry: K' = Kx = terms x kplane, terms 3 (B' = [b_hi | b_lo | b_hi]) or 2 (a weight exact in fp16,
+// b_lo = 0 - e.g. a bf16 or fp16 checkpoint: B' = [b_hi | b_hi], the A loader reads A' = [a_lo | a_hi])
+static bool h3_geometry_ok(int Kx, int kplane) {
+  return kplane > 0 && kplane % BK == 0 && (Kx == 2 * kplane || Kx == 3 * kplane);
+}
+
+// fp32 execution (h3 operands, common.h): A a 2-plane h3 activation [M, 2K] (K = kplane, lda >= 2K), B the h3
+// weight [N, Kx] with Kx = 3K (or 2K, h3_geometry_ok); alpha = 1 / (s_a s_b).  act 0 none -> fp32 C [M, ldc] (+ fp32 bias, + fp32
 // residual, which may alias C); act 1 bias + GELU -> h3 output [M, 2N] in C (fp16 planes, ldc = 2N) at scale
 // out_scale; act 2 interleaved SwiGLU -> h3 output [M, 2 (N/2)] (ldc = N).
-EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, int Kx, int lda, int ldb, int ldc,
-                           const float* bias, const float* resid, int ldr, int act, const float* rscale, float alpha,
-                           float out_scale, hipStream_t st) {
+EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, int Kx, int kplane, int lda, int ldb,
+                           int ldc, const float* bias, const float* resid, int ldr, int act, const float* rscale,
+                           float alpha, float out_scale, hipStream_t st) {
   GemmArgs a{};
   a.rscale = rscale;  // optional per-row scale of the product (before bias / activation / residual)
   a.alpha = alpha; a.out_scale = out_scale;
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B;
   a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.biasf = bias; a.residf = resid; a.ldr = ldr;
-  a.h3k = Kx / H3_TERMS;   // A: 2-plane activation rows (lda >= 2 Kx / 3)
-  if (Kx % (H3_TERMS * BK) || lda < 2 * a.h3k || !(alpha > 0.f) || !(out_scale > 0.f)) return (int)hipErrorInvalidValue;
+  a.h3k = kplane;   // A: 2-plane activation rows (lda >= 2 kplane)
+  if (!h3_geometry_ok(Kx, kplane) || lda < 2 * kplane || !(alpha > 0.f) || !(out_scale > 0.f))
+    return (int)hipErrorInvalidValue;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
   if (((uintptr_t)C & 15) || ldc % 4 || (resid && (ldr % 4 || ((uintptr_t)resid & 15))) ||
@@ -2334,17 +2341,17 @@ EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, 
 // weight), alpha = 1 / (s_x s_w), fp32 bias, fp32 outputs q [B,Hq,S,64] (x q_scale), k [B,Hkv,S,64],
 // vt [B,Hkv,64,s_pad].
 EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* bias, float* q, float* k, float* vt,
-                                    const float* cosT, const float* sinT, int M, int Kx, int S, int Hq, int Hkv,
-                                    int rot_dim, int s_pad, float q_scale, float alpha, hipStream_t st) {
+                                    const float* cosT, const float* sinT, int M, int Kx, int kplane, int S, int Hq,
+                                    int Hkv, int rot_dim, int s_pad, float q_scale, float alpha, hipStream_t st) {
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
-  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = 2 * (Kx / H3_TERMS); a.ldb = Kx;
-  a.h3k = Kx / H3_TERMS;   // X: 2-plane activation rows [M, 2 Kx / 3]
+  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = 2 * kplane; a.ldb = Kx;
+  a.h3k = kplane;   // X: 2-plane activation rows [M, 2 kplane]
   a.alpha = alpha;
   a.biasf = bias; a.qf = q; a.kf = k; a.vtf = vt;
   a.cosT = cosT; a.sinT = sinT; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.s_pad = s_pad;
   a.q_scale = q_scale;
-  if (!bias || M % S || Kx % (H3_TERMS * BK) || ((uintptr_t)bias & 15) || !(alpha > 0.f))
+  if (!bias || M % S || !h3_geometry_ok(Kx, kplane) || ((uintptr_t)bias & 15) || !(alpha > 0.f))
     return (int)hipErrorInvalidValue;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
@@ -2359,15 +2366,15 @@ EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* b
 }
 
 // LM head + LSE partials.  alpha == 0: bf16 X [M, K], W [N, K].  alpha > 0: fp32 execution, X a 2-plane h3
-// activation [M, 2K/3] and W the h3 weight [N, K] (K = 3 x plane width), product scale alpha.
+// activation [M, 2 kplane] and W the h3 weight [N, K] (h3_geometry_ok), product scale alpha.
 EDGE_API int edge_gemm_lse(const void* X, const void* W, const int64_t* targets, float* part_max, float* part_sum,
-                           float* tgt_logit, int M, int N, int K, float alpha, hipStream_t st) {
+                           float* tgt_logit, int M, int N, int K, int kplane, float alpha, hipStream_t st) {
   GemmArgs a{};
   const bool h3 = alpha > 0.f;
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
-  a.M = M; a.N = N; a.K = K; a.lda = h3 ? 2 * (K / H3_TERMS) : K; a.ldb = K;
-  if (h3 && K % (H3_TERMS * BK)) return (int)hipErrorInvalidValue;
-  a.h3k = h3 ? K / H3_TERMS : 0;
+  a.M = M; a.N = N; a.K = K; a.lda = h3 ? 2 * kplane : K; a.ldb = K;
+  if (h3 && !h3_geometry_ok(K, kplane)) return (int)hipErrorInvalidValue;
+  a.h3k = h3 ? kplane : 0;
   a.alpha = h3 ? alpha : 1.f;
   a.targets = targets; a.part_max = part_max; a.part_sum = part_sum; a.tgt_logit = tgt_logit; a.nparts = N / 64;
   const int chk = check_shapes(a);

@@ -145,11 +145,14 @@ class DecoderLM:
     @classmethod
     def random_init(cls, cfg: ModelConfig, seed: int = 0, device="cpu", dtype=torch.float32, std: float = 0.02,
                     layers: range | None = None, with_embed: bool = True, with_head: bool = True,
-                    h3: bool | None = None):
+                    h3: bool | None = None, values: torch.dtype | None = None):
         """Seeded random weights of the given architecture (HF ``_init_weights`` style: N(0, 0.02)).
 
         ``layers`` restricts allocation to a layer range (a pipeline stage only holds its own layers);
         the generator is advanced identically so every stage sees the same weights as a full model.
+        ``values`` = torch.bfloat16 / float16 rounds every weight to that storage precision (held in ``dtype``): the
+        HF checkpoints are released that way (Qwen2-0.5B ``torch_dtype: bfloat16``, Pythia fp16) and the reference
+        upcasts them to fp32 (``Experiments/Qwen2-0.5B/qwen_layer_wise.py:17``).
         """
         g = torch.Generator().manual_seed(seed)
         H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
@@ -159,6 +162,8 @@ class DecoderLM:
             return (torch.randn(*shape, generator=g) * s)
 
         def fin(t):
+            if values is not None:
+                t = t.to(values)
             return t.to(device=device, dtype=dtype).contiguous()
 
         w: dict = {"layers": []}
@@ -512,8 +517,10 @@ def find_hf_snapshot(hf_id: str) -> str | None:
 
 
 def build_model(cfg: ModelConfig, device="cpu", dtype=torch.float32, weights: str = "", seed: int = 0,
-                layers: range | None = None, with_embed=True, with_head=True) -> tuple[DecoderLM, str]:
-    """Model from explicit weights dir, else a local HF snapshot, else seeded random init.
+                layers: range | None = None, with_embed=True, with_head=True,
+                values: torch.dtype | None = None) -> tuple[DecoderLM, str]:
+    """Model from explicit weights dir, else a local HF snapshot, else seeded random init (``values``: the random
+    weights' storage precision, see ``DecoderLM.random_init``).
 
     Returns (model, provenance string)."""
     path = weights or find_hf_snapshot(cfg.hf_id)
@@ -521,5 +528,6 @@ def build_model(cfg: ModelConfig, device="cpu", dtype=torch.float32, weights: st
         return DecoderLM.load_native(cfg, path, device, dtype, layers), f"native:{path}"
     if path and os.path.isdir(path):
         return DecoderLM.from_pretrained_dir(cfg, path, device, dtype, layers), f"hf:{path}"
+    tag = "" if values is None else f", {str(values).replace('torch.', '')} values"
     return (DecoderLM.random_init(cfg, seed, device, dtype, layers=layers, with_embed=with_embed,
-                                  with_head=with_head), f"random-init(seed={seed})")
+                                  with_head=with_head, values=values), f"random-init(seed={seed}{tag})")

@@ -44,16 +44,16 @@ def _check_f32(*ts):
             raise ValueError("HIP kernels take contiguous tensors")
 
 
-def _check_h3(a3, w3, alpha):
-    """a3: 2-plane activation [rows, 2K] (reference.h3_act), w3: h3 weight [N, 3K] (reference.h3_weight)."""
-    for t, m, what in ((a3, 2, "activations [rows, 2K] (reference.h3_act)"), (w3, 3, "weights [N, 3K] "
-                                                                               "(reference.h3_weight)")):
-        if t.dtype != torch.float16 or t.shape[-1] % m or not t.is_contiguous():
+def _check_h3(a3, w3, alpha) -> int:
+    """a3: 2-plane activation [rows, 2K] (reference.h3_act), w3: h3 weight [N, 3K] or [N, 2K]
+    (reference.h3_weight).  Returns the plane width K."""
+    for t, what in ((a3, "activations [rows, 2K] (reference.h3_act)"), (w3, "weights (reference.h3_weight)")):
+        if t.dtype != torch.float16 or not t.is_contiguous():
             raise TypeError(f"h3 {what} must be contiguous fp16")
-    if 3 * a3.shape[-1] != 2 * w3.shape[-1]:
-        raise ValueError(f"h3 activation width {a3.shape[-1]} does not match the weight width {w3.shape[-1]}")
+    ref.h3_terms(a3, w3)
     if not alpha > 0.0:
         raise ValueError(f"h3 product scale alpha must be > 0, got {alpha}")
+    return a3.shape[-1] // 2
 
 
 def _check_bf16(*ts):
@@ -388,7 +388,7 @@ def head_nll(h, w, targets):
     tgt = torch.empty(R, dtype=torch.float32, device=h.device)
     nll = torch.empty(R, dtype=torch.float32, device=h.device)
     t64 = targets.to(torch.int64).contiguous()
-    call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, 0.0, stream())
+    call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, 0, 0.0, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
 
@@ -432,7 +432,7 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
             out.copy_(y)
             return out
         return y
-    _check_h3(a3, w3, alpha)
+    kp = _check_h3(a3, w3, alpha)
     _check_f32(bias, residual, rscale)
     if act is None:
         if out is None:
@@ -444,7 +444,7 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
         out = torch.empty(M, 2 * No, dtype=torch.float16, device=a3.device)
         ldc = 2 * No
         code = _ACT[act]
-    call("edge_gemm_f32", ptr(a3), ptr(w3), ptr(out), M, N, Kx, a3.stride(0), w3.stride(0), ldc, ptr(bias),
+    call("edge_gemm_f32", ptr(a3), ptr(w3), ptr(out), M, N, Kx, kp, a3.stride(0), w3.stride(0), ldc, ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), code, ptr(rscale), float(alpha),
          float(out_scale), stream())
     return out
@@ -456,7 +456,7 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
         y = ref.h3_matmul(a3, w3, alpha)            # x @ w.T, then the rest of the fused op on fp32
         eye = torch.eye(y.shape[1], dtype=torch.float32)
         return ref.qkv_rope(y, eye, bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
-    _check_h3(a3, w3, alpha)
+    kp = _check_h3(a3, w3, alpha)
     _check_f32(bias)
     assert D == 64, "HIP attention path is specialised for head_dim 64"
     M, Kx = a3.shape[0], w3.shape[1]
@@ -465,7 +465,7 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
     q = torch.empty(B, Hq, S, D, **f32)
     k = torch.empty(B, Hkv, S, D, **f32)
     vt = torch.zeros(B, Hkv, D, sp, **f32) if sp != S else torch.empty(B, Hkv, D, sp, **f32)
-    call("edge_gemm_qkv_rope_f32", ptr(a3), ptr(w3), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, S,
+    call("edge_gemm_qkv_rope_f32", ptr(a3), ptr(w3), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, kp, S,
          Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), stream())
     return q, k, vt
 
@@ -475,7 +475,7 @@ def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch
     if not _gpu(a3):
         logits = ref.h3_matmul(a3, w3, alpha)
         return torch.logsumexp(logits, -1) - logits.gather(1, targets.long().view(-1, 1)).squeeze(1)
-    _check_h3(a3, w3, alpha)
+    kp = _check_h3(a3, w3, alpha)
     R, Kx = a3.shape[0], w3.shape[1]
     V = w3.shape[0]
     nparts = V // 64
@@ -483,7 +483,8 @@ def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch
     pmax, psum = torch.empty(R, nparts, **f32), torch.empty(R, nparts, **f32)
     tgt, nll = torch.empty(R, **f32), torch.empty(R, **f32)
     t64 = targets.to(torch.int64).contiguous()
-    call("edge_gemm_lse", ptr(a3), ptr(w3), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, float(alpha), stream())
+    call("edge_gemm_lse", ptr(a3), ptr(w3), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, kp, float(alpha),
+         stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
 

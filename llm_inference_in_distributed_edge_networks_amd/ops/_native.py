@@ -44,7 +44,7 @@ _SIGS = {
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],
-    "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_p],
+    "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_set_variant": [c_i],
@@ -68,9 +68,9 @@ _SIGS = {
     "edge_unpack": [c_p, c_p, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
                     c_i, c_i, c_p],
     # fp32 execution mode (h3 split-fp16 GEMM operands, fp32 attention / norms / codec)
-    "edge_gemm_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p, c_f, c_f, c_p],
-    "edge_gemm_qkv_rope_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_f,
-                               c_p],
+    "edge_gemm_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p, c_f, c_f, c_p],
+    "edge_gemm_qkv_rope_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f,
+                               c_f, c_p],
     "edge_flash_attn_fwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_attn_lastrow_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_colsum_f32": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],

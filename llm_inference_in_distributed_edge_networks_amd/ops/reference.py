@@ -189,7 +189,9 @@ def head_nll(h, w, targets):
 # sums hi_a hi_b + hi_a lo_b + lo_a hi_b = s_a s_b (a b) up to the dropped lo_a lo_b (2^-22 relative) and the
 # residual rounding (2^-23): below the CPU fp32 GEMM's own error (tools/h3_error.py).  Weights are stored as B'
 # [N, 3K] fp16; activations once per plane, [hi | lo] [R, 2K] fp16 (the GEMM's A loader reads block j of A' from
-# plane H3_APLANES[j]); the epilogue multiplies by alpha = 1 / (s_a s_b).
+# plane H3_APLANES[j]); the epilogue multiplies by alpha = 1 / (s_a s_b).  A weight exact in fp16 after scaling
+# (b_lo == 0, e.g. bf16 / fp16 checkpoint values) is stored as B' = [b_hi | b_hi] [N, 2K]: the GEMM over K' = 2K
+# (A' = [a_lo | a_hi]) gives the same result, its third product being exactly zero.
 H3_APLANES = (1, 0, 0)
 H3_BPLANES = (0, 1, 0)
 H3_TOP = 15   # the scaled bound is at most 2^15: hi and lo stay below the fp16 maximum 65504 (< 2^16)
@@ -217,17 +219,28 @@ def h3_act(x: torch.Tensor, s: float) -> torch.Tensor:
     return torch.cat(split2h(x, s), -1).contiguous()
 
 
-def h3_expand(a3: torch.Tensor) -> torch.Tensor:
-    """2-plane activation [R, 2K] -> the A' K-concatenation [R, 3K] the GEMM reads (H3_APLANES)."""
+def h3_expand(a3: torch.Tensor, terms: int = 3) -> torch.Tensor:
+    """2-plane activation [R, 2K] -> the A' K-concatenation [R, terms K] the GEMM reads (H3_APLANES)."""
     K = a3.shape[-1] // 2
-    return torch.cat([a3[..., i * K:(i + 1) * K] for i in H3_APLANES], -1)
+    return torch.cat([a3[..., i * K:(i + 1) * K] for i in H3_APLANES[:terms]], -1)
 
 
-def h3_weight(w: torch.Tensor) -> tuple[torch.Tensor, float]:
-    """fp32 [N, K] nn.Linear weight -> (h3 weight [N, 3K] fp16, its scale s_w)."""
+def h3_weight(w: torch.Tensor, two_term: bool = True) -> tuple[torch.Tensor, float]:
+    """fp32 [N, K] nn.Linear weight -> (h3 weight B' [N, 3K] fp16, its scale s_w); [N, 2K] = [hi | hi] when the
+    weight is exact in fp16 after scaling and ``two_term`` (the lo plane would be all zero)."""
     s = h3_scale(_f(w).abs().max().item())
     p = split2h(w, s)
+    if two_term and not p[1].any():
+        return torch.cat([p[0], p[0]], -1).contiguous(), s
     return torch.cat([p[i] for i in H3_BPLANES], -1).contiguous(), s
+
+
+def h3_terms(a3: torch.Tensor, w3: torch.Tensor) -> int:
+    """Products of the h3 GEMM of a3 [R, 2K] and w3 [N, terms K]: 3, or 2 for a weight exact in fp16."""
+    K = a3.shape[-1] // 2
+    if w3.shape[-1] not in (2 * K, 3 * K):
+        raise ValueError(f"h3 activation width {a3.shape[-1]} does not match the weight width {w3.shape[-1]}")
+    return w3.shape[-1] // K
 
 
 def h3_to_f32(a3: torch.Tensor, s: float = 1.0) -> torch.Tensor:
@@ -236,15 +249,16 @@ def h3_to_f32(a3: torch.Tensor, s: float = 1.0) -> torch.Tensor:
     return (a3[..., :K].float() + a3[..., K:].float()) / s
 
 
-def h3w_to_f32(w3: torch.Tensor, s: float = 1.0) -> torch.Tensor:
-    """Inverse of ``h3_weight``: (hi + lo) / s."""
-    K = w3.shape[-1] // 3
+def h3w_to_f32(w3: torch.Tensor, s: float, K: int) -> torch.Tensor:
+    """Inverse of ``h3_weight`` (K = the weight's input width): (hi + lo) / s, or hi / s for a two-term weight."""
+    if w3.shape[-1] == 2 * K:
+        return w3[..., :K].float() / s
     return (w3[..., :K].float() + w3[..., K:2 * K].float()) / s
 
 
 def h3_matmul(a3: torch.Tensor, w3: torch.Tensor, alpha: float) -> torch.Tensor:
     """What the h3 GEMM computes: alpha * (A' @ B'^T), fp16 x fp16 products (exact) accumulated in fp32."""
-    return (h3_expand(a3).float() @ w3.float().t()) * alpha
+    return (h3_expand(a3, h3_terms(a3, w3)).float() @ w3.float().t()) * alpha
 
 
 # ---- fused RMSNorm (GPU fast path) semantics -------------------------------------------------------

@@ -11,6 +11,5 @@ step() {  # name timeout cmd...
 }
 TAIL=15 step pytest_f32 600 python -u -m pytest tests/test_f32_gpu.py -x -q --timeout 120 --timeout-method thread || exit $?
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-TAIL=1 step bench_h3 300 python bench.py --steps 10 --warmup 3 --no-bf16 --json-out gpurun_out/bench_h3.json || exit $?
-TAIL=20 step gemm_h3 300 python tools/gemm_bench.py --only h3_gate_up_b64,h3_down_b64,h3_o_proj_b64,h3_qkv_rope_b64,h3_big,gate_up_b64,down_b64 --rounds 3 || exit $?
+TAIL=1 step bench_h3 400 python bench.py --steps 10 --warmup 3 --json-out gpurun_out/bench_h3.json || exit $?
 exit 0

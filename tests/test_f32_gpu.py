@@ -78,16 +78,20 @@ def _f32_matmul_err(x, w):
     (300, 896, 896, "resid"), (32768, 896, 896, "resid"), (32768, 896, 4864, "resid"),   # 256x224 (w7) kernel
     (4096, 9728, 896, "swiglu"), (300, 1152, 896, "none"), (2048, 2048, 512, "gelu"),    # 256x256 / 128x128
     (700, 512, 2048, "bias_resid"), (8192, 1024, 640, "bias"), (1000, 512, 512, "bias_resid")])
-def test_linear_h3_fp32_accuracy(M, N, K, epi, slack=0):
+def test_linear_h3_fp32_accuracy(M, N, K, epi, slack=0, two_term=False):
     """h3 GEMM vs fp64; ``slack`` binades of headroom between the activation's scaled maximum and the fp16 range
-    (the model's scales come from bounds, not from the data: the planes stay accurate far below the bound)."""
+    (the model's scales come from bounds, not from the data: the planes stay accurate far below the bound).
+    ``two_term``: bf16-valued weights (checkpoint values), exact in fp16 -> the K' = 2K GEMM."""
     x = rnd(M, K, seed=10)
     w = rnd(N, K, s=1 / math.sqrt(K), seed=11)
+    if two_term:
+        w = w.to(torch.bfloat16).float()
     b = rnd(N, s=0.1, seed=12) if "bias" in epi or epi == "gelu" else None
     r = rnd(M, N, seed=13) if "resid" in epi else None
     act = {"gelu": "gelu", "swiglu": "swiglu_il"}.get(epi)
     sx = R.h3_scale(x.abs().max().item()) / 2 ** slack
     w3, sw = R.h3_weight(w)
+    assert w3.shape[1] == (2 if two_term else 3) * K
     ref = x.double() @ w.double().t()
     if b is not None:
         ref = ref + b.double()
@@ -108,6 +112,14 @@ def test_linear_h3_fp32_accuracy(M, N, K, epi, slack=0):
     # fp32-level: within a small factor of the CPU fp32 GEMM's own error (the h3 scheme drops 2^-22 terms and
     # rounds the residual plane at 2^-23; the h3 re-split of the epilogue output adds one more such rounding)
     assert err < max(4 * yard, 2e-6), (err, yard)
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(32768, 896, 896, "resid"), (32768, 896, 4864, "resid"),
+                                       (4096, 9728, 896, "swiglu"), (300, 1152, 896, "none"), (2048, 2048, 512, "gelu"),
+                                       (700, 512, 2048, "bias_resid")])
+def test_linear_h3_two_term(M, N, K, epi):
+    """Weights exact in fp16 (bf16 checkpoint values): the two-product GEMM, same fp32-level accuracy."""
+    test_linear_h3_fp32_accuracy(M, N, K, epi, two_term=True)
 
 
 @pytest.mark.parametrize("slack", [8, 14])
@@ -253,7 +265,7 @@ def test_codec_fp32_bitexact_vs_cpu(codec):
 
 
 # ---- whole models at full size: GPU fp32 mode vs the CPU fp32 model on the same random weights -----------------
-def _full_model_nll(cfg, B, S, seed=0):
+def _full_model_nll(cfg, B, S, seed=0, values=None):
     from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
     from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows, window_nll
     from llm_inference_in_distributed_edge_networks_amd.models import DecoderLM
@@ -262,7 +274,7 @@ def _full_model_nll(cfg, B, S, seed=0):
     b = next(batches(toks, wins, B))
     out = {}
     for dev in ("cpu", DEV):
-        m = DecoderLM.random_init(cfg, seed, device=dev, dtype=torch.float32)
+        m = DecoderLM.random_init(cfg, seed, device=dev, dtype=torch.float32, values=values)
         bb = b.to(dev)
         x = m.forward_hidden(bb.ids)
         out[dev] = window_nll(m.row_nll(x, bb.rows, bb.targets), bb).double().cpu()
@@ -270,12 +282,15 @@ def _full_model_nll(cfg, B, S, seed=0):
     return out["cpu"], out[DEV]
 
 
-@pytest.mark.parametrize("name,B,S", [("qwen2-0.5b", 2, 512), ("pythia-70m", 2, 2048)])
-def test_full_model_nll_matches_cpu_fp32(name, B, S):
+@pytest.mark.parametrize("name,B,S,values", [("qwen2-0.5b", 2, 512, None), ("pythia-70m", 2, 2048, None),
+                                            ("qwen2-0.5b", 2, 512, torch.bfloat16),
+                                            ("pythia-70m", 2, 2048, torch.float16)])
+def test_full_model_nll_matches_cpu_fp32(name, B, S, values):
     """Full 24-layer Qwen2-0.5B / 6-layer Pythia-70M: per-window NLL of the GPU fp32 mode within 1e-4 relative of
-    the CPU fp32 oracle (random-init weights of the exact architecture; the CPU run is itself fp32)."""
+    the CPU fp32 oracle (random-init weights of the exact architecture, full fp32 values or the checkpoints' bf16 /
+    fp16 values - the two-product GEMMs; the CPU run is itself fp32)."""
     from llm_inference_in_distributed_edge_networks_amd.models import get_config
-    cpu, gpu = _full_model_nll(get_config(name), B, S)
+    cpu, gpu = _full_model_nll(get_config(name), B, S, values=values)
     rel = ((gpu - cpu).abs() / cpu.abs()).max().item()
     assert rel < 1e-4, (rel, cpu.tolist(), gpu.tolist())
 

@@ -16,7 +16,7 @@
 extern "C" {
 int edge_gemm(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, const void* bias,
               const void* resid, int ldr, int act, const float* rscale, float* ssq_out, hipStream_t st);
-int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, int Kx, int lda, int ldb, int ldc,
+int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, int Kx, int kplane, int lda, int ldb, int ldc,
                   const float* bias, const float* resid, int ldr, int act, const float* rscale, float alpha,
                   float out_scale, hipStream_t st);
 int edge_rmsnorm_f32(const float* x, const float* w, void* y, const int* rows, int R, int H, float eps,
@@ -102,11 +102,13 @@ int main() {
     const int M = 4096, N = 512, K = 128, Kx = 3 * K;
     void *a = A((size_t)M * 2 * K * 2), *b = A((size_t)N * Kx * 2), *c = A((size_t)M * N * 4),
          *c3 = A((size_t)M * 2 * (N / 2) * 2);
-    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, 2 * K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 1.f, 1.f, st), 0);
-    EXPECT(edge_gemm_f32(a, b, c3, M, N, Kx, 2 * K, Kx, 2 * (N / 2), nullptr, nullptr, 0, 2, nullptr, 1.f, 1.f, st), 0);
-    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 1.f, 1.f, st),
+    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, K, 2 * K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 1.f, 1.f, st), 0);
+    EXPECT(edge_gemm_f32(a, b, c, M, N, 2 * K, K, 2 * K, 2 * K, N, nullptr, nullptr, 0, 0, nullptr, 1.f, 1.f, st), 0);
+    EXPECT(edge_gemm_f32(a, b, c3, M, N, Kx, K, 2 * K, Kx, 2 * (N / 2), nullptr, nullptr, 0, 2, nullptr, 1.f, 1.f, st),
+           0);
+    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, K, K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 1.f, 1.f, st),
            (int)hipErrorInvalidValue);   // lda smaller than the 2-plane row
-    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, 2 * K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 0.f, 1.f, st),
+    EXPECT(edge_gemm_f32(a, b, c, M, N, Kx, K, 2 * K, Kx, N, nullptr, nullptr, 0, 0, nullptr, 0.f, 1.f, st),
            (int)hipErrorInvalidValue);   // no product scale
     float *x = (float*)A((size_t)M * K * 4), *w = (float*)A(K * 4);
     EXPECT(edge_rmsnorm_f32(x, w, c3, nullptr, M, K, 1e-6f, 1.f, st), 0);
