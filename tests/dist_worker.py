@@ -17,7 +17,7 @@ def run(rank, world, port, pp, codec, ratio, method, out_path, split):
     from llm_inference_in_distributed_edge_networks_amd.parallel import (BoundaryConfig, DistributedPipeline, Grid,
                                                                           PipelinePlan, init_distributed, shutdown)
     env = init_distributed("cpu", timeout_s=120)
-    cfg = TINY_QWEN2
+    cfg = TINY_QWEN2.replace(num_layers=int(os.environ.get("EDGE_TEST_LAYERS", TINY_QWEN2.num_layers)))
     grid = Grid(world, pp)
     plan = PipelinePlan.from_split_layers(cfg.num_layers, split) if split else PipelinePlan.balanced(cfg, pp, 128)
     _, stage = grid.coords(rank)

@@ -23,9 +23,9 @@ def free_port():
     return p
 
 
-def local_ppl(plan, codec, ratio, method):
-    m = DecoderLM.random_init(TINY_QWEN2, 0)
-    hw = torch.linspace(-1, 2, 16).view(4, 4)
+def local_ppl(plan, codec, ratio, method, cfg=TINY_QWEN2):
+    m = DecoderLM.random_init(cfg, 0)
+    hw = torch.linspace(-1, 2, cfg.num_layers * cfg.num_heads).view(cfg.num_layers, cfg.num_heads)
     pipe = LocalPipeline(m, plan, BoundaryConfig(codec, ratio, method, hw))
     toks = synthetic_stream(1500, 512, 2)
     return pipe.evaluate(batches(toks, sliding_windows(1500, 128, 32), 3)).ppl()
@@ -46,6 +46,20 @@ def test_distributed_equals_local(tmp_path, world, pp, codec, ratio, method, spl
     plan = PipelinePlan.from_split_layers(4, split) if split else PipelinePlan.balanced(TINY_QWEN2, pp, 128)
     ref = local_ppl(plan, codec, ratio, method)
     assert abs(res["ppl"] - ref) / ref < 1e-6
+
+
+@pytest.mark.parametrize("method,codec", [("weighted_importance", "mixed_int4_int8"),
+                                          ("aggregate_till", "int4_token")])
+def test_distributed_pp8_equals_local(tmp_path, monkeypatch, method, codec):
+    """8 processes, one stage each (BASELINE config 5's 8-stage split on an 8-layer model): LRP-weighted importance
+    and the aggregate_till running-sum carry across all 7 boundaries equal the single-process pipeline."""
+    monkeypatch.setenv("EDGE_TEST_LAYERS", "8")
+    cfg = TINY_QWEN2.replace(num_layers=8)
+    split = [0, 1, 2, 3, 4, 5, 6]
+    out = tmp_path / "res.json"
+    mp.spawn(dist_worker.run, args=(8, free_port(), 8, codec, 0.5, method, str(out), split), nprocs=8, join=True)
+    ref = local_ppl(PipelinePlan.from_split_layers(8, split), codec, 0.5, method, cfg)
+    assert abs(json.loads(out.read_text())["ppl"] - ref) / ref < 1e-6
 
 
 def test_grid_and_plan():
