@@ -245,17 +245,59 @@ __device__ __forceinline__ f32x4_t x6_dot(const bf16x8_t (&a)[3], const bf16x8_t
   c = mfma_bf(a[0], b[1], c);
   return mfma_bf(a[0], b[0], c);
 }
+// h3 planes (common.h: [hi, lo] fp16 of the power-of-two scaled value, raw bits in a bf16x8_t): the three products
+// a_lo b_hi + a_hi b_lo + a_hi b_hi on the fp16 matrix cores
+__device__ __forceinline__ f32x4_t mfma_h(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                0, 0, 0);
+}
+__device__ __forceinline__ f32x4_t h3_dot(const bf16x8_t (&a)[2], const bf16x8_t (&b)[2], f32x4_t c) {
+  c = mfma_h(a[1], b[0], c);
+  c = mfma_h(a[0], b[1], c);
+  return mfma_h(a[0], b[0], c);
+}
+__device__ __forceinline__ void split_frag_h(const float (&v)[8], float s, bf16x8_t& hi, bf16x8_t& lo) {
+  float h[8], l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) split2h(v[e] * s, h[e], l[e]);
+  hi = __builtin_bit_cast(bf16x8_t, u32x4_t{pack_h2(h[0], h[1]), pack_h2(h[2], h[3]), pack_h2(h[4], h[5]),
+                                            pack_h2(h[6], h[7])});
+  lo = __builtin_bit_cast(bf16x8_t, u32x4_t{pack_h2(l[0], l[1]), pack_h2(l[2], l[3]), pack_h2(l[4], l[5]),
+                                            pack_h2(l[6], l[7])});
+}
+// NPL planes of 8 values: three bf16 planes (x6) or two scaled fp16 planes (h3)
+template <bool F16>
+__device__ __forceinline__ void split_planes(const float (&v)[8], float s, bf16x8_t (&p)[F16 ? 2 : 3]) {
+  if constexpr (F16) split_frag_h(v, s, p[0], p[1]);
+  else split_frag(v, p[0], p[1], p[2]);
+}
+template <bool F16>
+__device__ __forceinline__ f32x4_t plane_dot(const bf16x8_t (&a)[F16 ? 2 : 3], const bf16x8_t (&b)[F16 ? 2 : 3],
+                                             f32x4_t c) {
+  if constexpr (F16) return h3_dot(a, b, c);
+  else return x6_dot(a, b, c);
+}
 }  // namespace
 
-// NW waves of 16 query rows per workgroup (4: 64 rows, 8: 128 rows sharing each staged K / V^T tile)
-template <bool H3OUT, int NW>
+// NW waves of 16 query rows per workgroup (4: 64 rows, 8: 128 rows sharing each staged K / V^T tile).
+// F16: the planes are the two scaled fp16 h3 planes (three fp16 MFMAs per product instead of six bf16): q, k and
+// v are scaled by the powers of two sq, sk, sv (model bounds, so every plane stays in the fp16 range) and the
+// probabilities by 2^(15 - TAU) (p <= 2^TAU under the lazy rescale); the scores are unscaled in the exp and the
+// output in the final normalisation.
+template <bool H3OUT, int NW, bool F16>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(const float* __restrict__ q,
                                                                   const float* __restrict__ k,
                                                                   const float* __restrict__ vt, void* __restrict__ o,
                                                                   float* __restrict__ lse,
                                                                   const float* __restrict__ n_rows, int B, int Hq,
-                                                                  int Hkv, int S, int s_pad, float h3s) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];   // K planes (3 x 8 KiB), V^T planes (3 x 8 KiB)
+                                                                  int Hkv, int S, int s_pad, float h3s, float sq,
+                                                                  float sk, float sv) {
+  constexpr int NPL = F16 ? 2 : 3;
+  constexpr float SP = F16 ? 128.f : 1.f;   // probability scale 2^(15 - FTAU) of the fp16 planes
+  static_assert(FTAU == 8.f, "SP assumes p <= 2^8");
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // K planes (NPL x 8 KiB), V^T planes (NPL x 8 KiB)
+  if constexpr (!F16) sq = sk = sv = 1.f;
+  const float sc_log2 = FLOG2E / (sq * sk);   // score scale (natural log -> log2) of the scaled products
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
   constexpr int QB = 16 * NW;          // query rows per workgroup
   const int nqb = (S + QB - 1) / QB;
@@ -274,13 +316,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
   const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
   const float* vh = vt + ((size_t)b * Hkv + hk) * 64 * (size_t)s_pad;
   char* const lk = smem;
-  char* const lv = smem + 3 * XPL;
+  char* const lv = smem + NPL * XPL;
 
   const int q0 = qb * QB + wave * 16;
   const int qrow = q0 + ql;
   const int qld = qrow < S ? qrow : S - 1;
   // Q^T operand planes: lane (query ql, g) holds d = 32 ks + 8g .. +7
-  bf16x8_t qp[2][3];
+  bf16x8_t qp[2][NPL];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     float v[8];
@@ -288,7 +330,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     const f32x4_t c = *(const f32x4_t*)(qh + (size_t)qld * 64 + 32 * ks + 8 * g + 4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = c[e]; }
-    split_frag(v, qp[ks][0], qp[ks][1], qp[ks][2]);
+    split_planes<F16>(v, sq, qp[ks]);
   }
   f32x4_t oacc[4];
 #pragma unroll
@@ -316,11 +358,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
       float v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) { v[e] = kreg[2 * hc][e]; v[4 + e] = kreg[2 * hc + 1][e]; }
-      bf16x8_t p[3];
-      split_frag(v, p[0], p[1], p[2]);
+      bf16x8_t p[NPL];
+      split_planes<F16>(v, sk, p);
       const int c = scol / 8 + hc;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) *(bf16x8_t*)(lk + pl * XPL + srow * 128 + ((c ^ xsw(srow)) << 4)) = p[pl];
+      for (int pl = 0; pl < NPL; ++pl) *(bf16x8_t*)(lk + pl * XPL + srow * 128 + ((c ^ xsw(srow)) << 4)) = p[pl];
     }
     // V^T row srow (= d): keys scol .. + NF - 1 in groups of 4; the group of keys 32 s + 16 hf + 4a .. +3 goes to
     // chunk 4 s + a, half hf
@@ -328,13 +370,21 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     for (int a4 = 0; a4 < NF / 4; ++a4) {
       const int key = scol + 4 * a4;
       const int sblk = key >> 5, hf = (key >> 4) & 1, a = (key >> 2) & 3;
-      float p0[4], p1[4], p2[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) split3(vreg[a4][e], p0[e], p1[e], p2[e]);
       const int off = srow * 128 + (((4 * sblk + a) ^ xsw(srow)) << 4) + hf * 8;
-      *(u32x2_t*)(lv + 0 * XPL + off) = u32x2_t{pack_bf2(p0[0], p0[1]), pack_bf2(p0[2], p0[3])};
-      *(u32x2_t*)(lv + 1 * XPL + off) = u32x2_t{pack_bf2(p1[0], p1[1]), pack_bf2(p1[2], p1[3])};
-      *(u32x2_t*)(lv + 2 * XPL + off) = u32x2_t{pack_bf2(p2[0], p2[1]), pack_bf2(p2[2], p2[3])};
+      if constexpr (F16) {
+        float p0[4], p1[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split2h(vreg[a4][e] * sv, p0[e], p1[e]);
+        *(u32x2_t*)(lv + 0 * XPL + off) = u32x2_t{pack_h2(p0[0], p0[1]), pack_h2(p0[2], p0[3])};
+        *(u32x2_t*)(lv + 1 * XPL + off) = u32x2_t{pack_h2(p1[0], p1[1]), pack_h2(p1[2], p1[3])};
+      } else {
+        float p0[4], p1[4], p2[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split3(vreg[a4][e], p0[e], p1[e], p2[e]);
+        *(u32x2_t*)(lv + 0 * XPL + off) = u32x2_t{pack_bf2(p0[0], p0[1]), pack_bf2(p0[2], p0[3])};
+        *(u32x2_t*)(lv + 1 * XPL + off) = u32x2_t{pack_bf2(p1[0], p1[1]), pack_bf2(p1[2], p1[3])};
+        *(u32x2_t*)(lv + 2 * XPL + off) = u32x2_t{pack_bf2(p2[0], p2[1]), pack_bf2(p2[2], p2[3])};
+      }
     }
   };
 
@@ -355,9 +405,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
       st[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t kf[3] = {xfrag(lk, row, 4 * ks + g), xfrag(lk + XPL, row, 4 * ks + g),
-                                xfrag(lk + 2 * XPL, row, 4 * ks + g)};
-        st[kt] = x6_dot(kf, qp[ks], st[kt]);
+        bf16x8_t kf[NPL];
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) kf[pl] = xfrag(lk + pl * XPL, row, 4 * ks + g);
+        st[kt] = plane_dot<F16>(kf, qp[ks], st[kt]);
       }
     }
     if (kb * 64 + 63 > q0 || kb * 64 + 63 >= S) {   // causal / sequence-end mask (wave-uniform branch)
@@ -376,7 +427,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
       for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[kt][r]);
     mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float mc = mloc * FLOG2E;
+    const float mc = mloc * sc_log2;
     if (__builtin_amdgcn_ballot_w64(mc > m2 + FTAU)) {  // wave-uniform lazy rescale
       const float mn = fmaxf(m2, mc);
       const float alpha = exp2f(m2 - mn);
@@ -390,7 +441,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(fmaf(st[kt][r], FLOG2E, -m2));
+        const float pv = exp2f(fmaf(st[kt][r], sc_log2, -m2));
         st[kt][r] = pv;
         ps += pv;
       }
@@ -401,14 +452,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
       float pv8[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { pv8[r] = st[2 * sk][r]; pv8[4 + r] = st[2 * sk + 1][r]; }
-      bf16x8_t pp[3];
-      split_frag(pv8, pp[0], pp[1], pp[2]);
+      bf16x8_t pp[NPL];
+      split_planes<F16>(pv8, SP, pp);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int row = dt * 16 + ql;
-        const bf16x8_t vf[3] = {xfrag(lv, row, 4 * sk + g), xfrag(lv + XPL, row, 4 * sk + g),
-                                xfrag(lv + 2 * XPL, row, 4 * sk + g)};
-        oacc[dt] = x6_dot(vf, pp, oacc[dt]);
+        bf16x8_t vf[NPL];
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) vf[pl] = xfrag(lv + pl * XPL, row, 4 * sk + g);
+        oacc[dt] = plane_dot<F16>(vf, pp, oacc[dt]);
       }
     }
   }
@@ -416,7 +468,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
   if (qrow < S) {
-    const float inv = 1.f / l_run;
+    const float inv = 1.f / (l_run * (SP * sv));
     const int W = Hq * 64;
     if constexpr (H3OUT) {
       f16_t* orow = (f16_t*)o + ((size_t)b * S + qrow) * (size_t)(2 * W);
@@ -542,40 +594,43 @@ __global__ __launch_bounds__(256) void attn_colsum_f32_kernel(const float* __res
   }
 }
 
-static int g_attn_f32_variant = 2;   // 0: split-bf16 (x6) MFMA kernel, 64 query rows per workgroup; 2 (default): the same
+static int g_attn_f32_variant = 2;   // 0: split-plane MFMA kernel, 64 query rows per workgroup; 2 (default): the same
                                      // with 128 rows (8 waves); 1: native f32 MFMA kernel (A/B)
 EDGE_API int edge_attn_f32_set_variant(int v) {
   g_attn_f32_variant = v;
   return 0;
 }
 
+template <bool H3OUT, int NW, bool F16>
+static void launch_split_attn(dim3 grid, hipStream_t st, const float* q, const float* k, const float* vt, void* o,
+                              float* lse, const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float h3s,
+                              float sq, float sk, float sv) {
+  hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<H3OUT, NW, F16>), grid, dim3(NW * 64), (F16 ? 4 : 6) * XPL, st, q, k,
+                     vt, o, lse, n_rows, B, Hq, Hkv, S, s_pad, h3s, sq, sk, sv);
+}
+
 // out_h3_scale > 0: O as a 2-plane h3 activation [B*S, 2*Hq*64] (fp16 planes at that scale) for the O-projection;
-// 0: fp32 [B*S, Hq*64].
+// 0: fp32 [B*S, Hq*64].  sq, sk, sv > 0: the split-plane kernel runs on scaled fp16 planes (h3, three products; the
+// caller guarantees s |x| <= 2^15 for q, k and v); 0: on three bf16 planes (six products).
 EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float* vt, void* o, float* lse,
                                      const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float out_h3_scale,
-                                     hipStream_t st) {
+                                     float sq, float sk, float sv, hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
   if (Hq % Hkv || s_pad % 64 || s_pad < S || out_h3_scale < 0.f) return (int)hipErrorInvalidValue;
+  const bool f16 = sq > 0.f;
+  if (f16 && !(sk > 0.f && sv > 0.f)) return (int)hipErrorInvalidValue;
+  const bool ho = out_h3_scale > 0.f;
   const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
   const dim3 grid(8 * maxcnt * G * ((S + 63) / 64));
-  if (g_attn_f32_variant == 0 || g_attn_f32_variant == 2) {   // split-bf16 matrix cores (0: 64 query rows / WG)
+  if (g_attn_f32_variant == 0 || g_attn_f32_variant == 2) {   // split-plane matrix cores (0: 64 query rows / WG)
     const bool w8 = g_attn_f32_variant == 2;
     const dim3 gx(8 * maxcnt * G * ((S + (w8 ? 127 : 63)) / (w8 ? 128 : 64)));
-    if (w8) {
-      if (out_h3_scale > 0.f)
-        hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<true, 8>), gx, dim3(512), 6 * XPL, st, q, k, vt, o, lse, n_rows,
-                           B, Hq, Hkv, S, s_pad, out_h3_scale);
-      else
-        hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<false, 8>), gx, dim3(512), 6 * XPL, st, q, k, vt, o, lse, n_rows,
-                           B, Hq, Hkv, S, s_pad, out_h3_scale);
-    } else if (out_h3_scale > 0.f) {
-      hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<true, 4>), gx, dim3(256), 6 * XPL, st, q, k, vt, o, lse, n_rows,
-                         B, Hq, Hkv, S, s_pad, out_h3_scale);
-    } else {
-      hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<false, 4>), gx, dim3(256), 6 * XPL, st, q, k, vt, o, lse, n_rows,
-                         B, Hq, Hkv, S, s_pad, out_h3_scale);
-    }
-  } else if (out_h3_scale > 0.f) {             // f32 matrix cores
+    auto* fn = w8 ? (f16 ? (ho ? launch_split_attn<true, 8, true> : launch_split_attn<false, 8, true>)
+                         : (ho ? launch_split_attn<true, 8, false> : launch_split_attn<false, 8, false>))
+                  : (f16 ? (ho ? launch_split_attn<true, 4, true> : launch_split_attn<false, 4, true>)
+                         : (ho ? launch_split_attn<true, 4, false> : launch_split_attn<false, 4, false>));
+    fn(gx, st, q, k, vt, o, lse, n_rows, B, Hq, Hkv, S, s_pad, out_h3_scale, sq, sk, sv);
+  } else if (ho) {             // f32 matrix cores
     hipLaunchKernelGGL(flash_attn_fwd_f32_kernel<true>, grid, dim3(256), 4 * FTILE, st, q, k, vt, o, lse, n_rows, B,
                        Hq, Hkv, S, s_pad, out_h3_scale);
   } else {

@@ -70,6 +70,9 @@ def _h3_bounds(cfg: ModelConfig, L: dict) -> dict:
     * norm outputs: |x_hat_i| <= ||x_hat||_2 <= sqrt(H) for RMSNorm and LayerNorm, so |g_i x_hat_i + b_i| <=
       sqrt(H) max|g| + max|b| and ||y||_2 <= sqrt(H) max|g| + ||b||_2 =: n;
     * attention output: a convex combination of value rows, |o| <= max_j |v_j| <= max_j n ||Wv_j||_2 + |bv_j|;
+    * attention inputs (the split-plane attention kernel): v as above; q and k after RoPE, which mixes pairs of
+      components (|x1 c - x2 s| <= sqrt(2) max |x_i|), so |q| <= sqrt(2) max_j (n ||Wq_j||_2 + |bq_j|) (times the
+      1/sqrt(d) pre-scale), and the same for k;
     * SwiGLU output: |silu(g) u| <= |g| |u| <= n^2 max_j ||Wg_j||_2 ||Wu_j||_2;
     * GELU output: |gelu(f)| <= |f| <= max_j n ||Wfc_j||_2 + |bfc_j|."""
     H = cfg.hidden_size
@@ -83,15 +86,19 @@ def _h3_bounds(cfg: ModelConfig, L: dict) -> dict:
 
     qkv, n1 = norm_bound(L["ln1_w"], L.get("ln1_b"))
     mlp, n2 = norm_bound(L["ln2_w"], L.get("ln2_b"))
-    v0 = cfg.q_size + cfg.kv_size
-    wv, bv = L["wqkv"][v0:v0 + cfg.kv_size], L["bqkv"][v0:v0 + cfg.kv_size]
-    o = (n1 * _rownorm(wv) + bv.float().abs()).max().item()
+    def proj_bound(r0, r1):
+        return (n1 * _rownorm(L["wqkv"][r0:r1]) + L["bqkv"][r0:r1].float().abs()).max().item()
+
+    q0, k0, v0 = 0, cfg.q_size, cfg.q_size + cfg.kv_size
+    o = proj_bound(v0, v0 + cfg.kv_size)
+    att_q = math.sqrt(2.0) * proj_bound(q0, k0) / math.sqrt(cfg.head_dim)
+    att_k = math.sqrt(2.0) * proj_bound(k0, v0)
     if cfg.arch == "qwen2":
         g, u = ops.deinterleave_gate_up(L["wgu"].t().contiguous())
         down = n2 * n2 * (_rownorm(g.t()) * _rownorm(u.t())).max().item()
     else:
         down = (n2 * _rownorm(L["wfc"]) + L["bfc"].float().abs()).max().item()
-    return dict(qkv=qkv, o=o, mlp=mlp, down=down)
+    return dict(qkv=qkv, o=o, mlp=mlp, down=down, att_q=att_q, att_k=att_k)
 
 
 class DecoderLM:
@@ -389,7 +396,8 @@ class DecoderLM:
                                          h3=(sc["qkv"], sc["mlp"]))
         q, k, vt = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S, cfg.num_heads,
                                    cfg.num_kv_heads, cfg.head_dim, cfg.rotary_dim, self.q_scale)
-        o3, lse = ops.attention(q, k, vt, S, need_lse=need_lse, n_rows=n_rows, h3=sc["o"])
+        o3, lse = ops.attention(q, k, vt, S, need_lse=need_lse, n_rows=n_rows, h3=sc["o"],
+                                in_scales=(sc["att_q"], sc["att_k"], sc["o"]))
         return q, k, o3, lse, h23
 
     def _mlp_h3(self, i, o3, x, h23):

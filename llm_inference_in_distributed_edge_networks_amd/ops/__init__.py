@@ -300,13 +300,15 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     return q, k, vt
 
 
-def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0):
+def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scales=None):
     """Causal GQA flash attention -> (o [B*S, Hq*64], lse [B,Hq,S] or None).
 
     ``n_rows`` ([B] fp32, scored rows per window as in ``WindowBatch.n_rows``): only query rows
     >= S-1-n_rows[b] are needed (last layer of the model); other 64-row blocks may be skipped and their
     output rows are then undefined.  fp32 q/k/vt run the fp32 kernels; ``h3`` = s > 0 then writes s * o as the
-    2-plane h3 activation [B*S, 2*Hq*64] the O-projection consumes."""
+    2-plane h3 activation [B*S, 2*Hq*64] the O-projection consumes.  ``in_scales`` = (s_q, s_k, s_v), powers of two
+    with s |x| <= 2^15 for every element of q, k and v: the matrix work runs on scaled fp16 planes (three products;
+    the model derives them from weight bounds), else on three bf16 planes (six products)."""
     if not _gpu(q):
         o, lse = ref.attention(q, k, vt, S, need_lse)
         return (ref.h3_act(o, h3) if h3 else o), lse
@@ -321,8 +323,9 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0):
         _check_f32(q, k, vt)
         assert D == 64 and vt.shape[-1] % 64 == 0 and vt.shape[-1] >= S
         o = _out_f32_or_h3(B * S, Hq * D, h3, q.device)
+        sq, sk, sv = in_scales if in_scales is not None else (0.0, 0.0, 0.0)
         call("edge_flash_attn_fwd_f32", ptr(q), ptr(k), ptr(vt), ptr(o), ptr(lse), ptr(nr), B, Hq, Hkv, S,
-             vt.shape[-1], float(h3), stream())
+             vt.shape[-1], float(h3), float(sq), float(sk), float(sv), stream())
         return o, lse
     _check_bf16(q, k, vt)
     o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)

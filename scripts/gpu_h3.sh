@@ -1,4 +1,4 @@
-# fp32-mode (h3) check: fp32 kernel tests, full-model numerics, smoke, bench, GEMM shapes.
+# fp32-mode (h3) check: fp32 kernel tests, full-model numerics, smoke, bench, attention timing.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -10,6 +10,6 @@ step() {  # name timeout cmd...
   return $rc
 }
 TAIL=15 step pytest_f32 600 python -u -m pytest tests/test_f32_gpu.py -x -q --timeout 120 --timeout-method thread || exit $?
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-TAIL=1 step bench_h3 400 python bench.py --steps 10 --warmup 3 --json-out gpurun_out/bench_h3.json || exit $?
+TAIL=1 step bench_h3 400 python bench.py --steps 10 --warmup 3 --no-bf16 --no-fp32-weights --json-out gpurun_out/bench_h3.json || exit $?
+TAIL=12 step attn 300 python tools/attn_bench.py --fp32 || exit $?
 exit 0

@@ -160,19 +160,19 @@ def test_qkv_rope_h3(B, S, Hq, Hkv, rot):
 
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (3, 100, 14, 2), (1, 2048, 8, 8), (2, 64, 4, 1)])
 @pytest.mark.parametrize("h3", [False, True])
-@pytest.mark.parametrize("variant", [0, 1, 2])
-def test_attention_f32(B, S, Hq, Hkv, h3, variant):
-    """fp32 attention vs fp64: split-bf16 MFMA kernel (variant 0, 64 query rows per workgroup; 2: 128 rows) and the
-    native f32 MFMA kernel (1).  The error is dominated by the fp32 exp2 (~5e-6 relative L2 for both kernels; bf16
-    attention is ~1e-3)."""
+@pytest.mark.parametrize("variant,planes", [(0, "bf16"), (1, "bf16"), (2, "bf16"), (0, "fp16"), (2, "fp16")])
+def test_attention_f32(B, S, Hq, Hkv, h3, variant, planes):
+    """fp32 attention vs fp64: the split-plane MFMA kernel (variant 0, 64 query rows per workgroup; 2: 128 rows) on
+    three bf16 planes or two scaled fp16 planes (h3), and the native f32 MFMA kernel (1).  The error is dominated by
+    the fp32 exp2 (~5e-6 relative L2 for all; bf16 attention is ~1e-3)."""
     ops._native.lib().edge_attn_f32_set_variant(variant)
     try:
-        _attention_f32_case(B, S, Hq, Hkv, h3)
+        _attention_f32_case(B, S, Hq, Hkv, h3, planes == "fp16")
     finally:
         ops._native.lib().edge_attn_f32_set_variant(2)
 
 
-def _attention_f32_case(B, S, Hq, Hkv, h3):
+def _attention_f32_case(B, S, Hq, Hkv, h3, fp16=False, slack=0):
     q = rnd(B, Hq, S, 64, seed=40) * 0.5
     k = rnd(B, Hkv, S, 64, seed=41) * 2
     v = rnd(B, Hkv, S, 64, seed=42)
@@ -180,12 +180,18 @@ def _attention_f32_case(B, S, Hq, Hkv, h3):
     vt = torch.zeros(B, Hkv, 64, sp)
     vt[..., :S] = v.transpose(-1, -2)
     s = R.h3_scale(v.abs().max().item()) if h3 else 0.0
-    o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True, h3=s)
+    sc = tuple(R.h3_scale(t.abs().max().item()) / 2 ** slack for t in (q, k, v)) if fp16 else None
+    o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True, h3=s, in_scales=sc)
     ro, rl = R.attention(q.double(), k.double(), vt.double(), S, need_lse=True)
     if h3:
         o = R.h3_to_f32(o, s)
     assert rel_err(o, ro) < 1e-5
     assert float((lse.cpu().double() - rl).abs().max()) < 5e-5
+
+
+def test_attention_h3_loose_scales():
+    """fp16-plane attention with its input scales 10 binades below the data's (the model's bounds are loose)."""
+    _attention_f32_case(2, 512, 14, 2, True, fp16=True, slack=10)
 
 
 def test_attention_f32_scored_rows_only():

@@ -114,6 +114,8 @@ def test_h3_bounds_hold(cfg):
         assert h.abs().max() <= bd["qkv"] * (1 + 1e-5)
         q, k, vt = ops.qkv_rope(h, L["wqkv"], L["bqkv"], m.cos, m.sin, B, S, cfg.num_heads, cfg.num_kv_heads,
                                 cfg.head_dim, cfg.rotary_dim, m.q_scale)
+        assert q.abs().max() <= bd["att_q"] * (1 + 1e-5) and k.abs().max() <= bd["att_k"] * (1 + 1e-5)
+        assert vt.abs().max() <= bd["o"] * (1 + 1e-5)
         o, _ = ops.attention(q, k, vt, S)
         assert o.abs().max() <= bd["o"] * (1 + 1e-5)
         y = ops.linear(o, L["wo"], L.get("bo"), residual=x)

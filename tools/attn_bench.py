@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--Hkv", type=int, default=2)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--fp32", action="store_true", help="the fp32-mode kernels: split-bf16 (x6) vs native f32 MFMA")
+    ap.add_argument("--fp32", action="store_true", help="the fp32-mode kernels: split-plane (bf16 x6 / fp16 h3) vs native f32 MFMA")
     a = ap.parse_args()
     if a.fp32:
         return bench_fp32(a)
@@ -58,14 +58,16 @@ def bench_fp32(a):
     res = {}
     lib = ops._native.lib()
     for _ in range(a.rounds):
-        for v, name in ((0, "x6_bf16_mfma"), (2, "x6_bf16_mfma_128rows"), (1, "f32_mfma")):
+        for v, name, sc in ((0, "x6_bf16_mfma", None), (2, "x6_bf16_mfma_128rows", None), (1, "f32_mfma", None),
+                            (0, "h3_fp16_mfma", (1024.0, 1024.0, 1024.0)),
+                            (2, "h3_fp16_mfma_128rows", (1024.0, 1024.0, 1024.0))):
             lib.edge_attn_f32_set_variant(v)
             for h3 in (0.0, 1.0):
-                ops.attention(q, k, vt, S, need_lse=True, h3=h3)
+                ops.attention(q, k, vt, S, need_lse=True, h3=h3, in_scales=sc)
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 st.record()
                 for _ in range(a.iters):
-                    ops.attention(q, k, vt, S, need_lse=True, h3=h3)
+                    ops.attention(q, k, vt, S, need_lse=True, h3=h3, in_scales=sc)
                 en.record()
                 torch.cuda.synchronize()
                 res.setdefault(f"{name}{'_h3out' if h3 else ''}", []).append(st.elapsed_time(en) / a.iters * 1e3)

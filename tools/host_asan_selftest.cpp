@@ -23,7 +23,7 @@ int edge_rmsnorm_f32(const float* x, const float* w, void* y, const int* rows, i
                      float h3_scale, hipStream_t st);
 int edge_flash_attn_fwd_f32(const float* q, const float* k, const float* vt, void* o, float* lse,
                             const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float out_h3_scale,
-                            hipStream_t st);
+                            float sq, float sk, float sv, hipStream_t st);
 int edge_select(const float* imp, int B, int S, int k, void* msg, long long off_mask, int mode, float thr,
                 long long off_kvec, hipStream_t st);
 int edge_pack(const void* x, void* msg, long long om, long long os, long long oh, long long ol, long long okv,
@@ -119,8 +119,10 @@ int main() {
     float *q = (float*)A((size_t)B * Hq * S * 64 * 4), *k = (float*)A((size_t)B * Hkv * S * 64 * 4),
           *vt = (float*)A((size_t)B * Hkv * 64 * sp * 4), *o = (float*)A((size_t)B * S * Hq * 64 * 4),
           *lse = (float*)A((size_t)B * Hq * S * 4);
-    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, sp, 0.f, st), 0);
-    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, 100, 0.f, st), (int)hipErrorInvalidValue);
+    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, sp, 0.f, 0.f, 0.f, 0.f, st), 0);
+    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, sp, 0.f, 1.f, 1.f, 1.f, st), 0);
+    EXPECT(edge_flash_attn_fwd_f32(q, k, vt, o, lse, nullptr, B, Hq, Hkv, S, 100, 0.f, 0.f, 0.f, 0.f, st),
+           (int)hipErrorInvalidValue);
   }
   // codec: mixed int4 / int8 per-token message, fixed k (layout of codec/wire.py for B 2, S 64, H 256, k 32)
   {

@@ -30,11 +30,16 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--warmup-batches", type=int, default=2)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="fp32 = the reference's precision (h3 GEMMs); bf16 = the bf16 mode")
+    ap.add_argument("--weight-values", default="bf16", choices=["bf16", "fp32"],
+                    help="random weight values: bf16 as the HF checkpoint the reference upcasts, or full fp32")
     a = ap.parse_args()
     dev = "cuda" if torch.cuda.is_available() else "cpu"
-    dtype = torch.bfloat16 if dev == "cuda" else torch.float32
+    dtype = torch.bfloat16 if (dev == "cuda" and a.dtype == "bf16") else torch.float32
     cfg = get_config(a.model)
-    model, prov = build_model(cfg, dev, dtype, seed=0)
+    model, prov = build_model(cfg, dev, dtype, seed=0,
+                              values=torch.bfloat16 if a.weight_values == "bf16" else None)
     layers = [22, 18, 3, 23, 11] if cfg.num_layers == 24 else [1, 2]
     hw = torch.full((cfg.num_layers, cfg.num_heads), 1.0 / cfg.num_heads)
     sc = SweepConfig(["regular_importance", "weighted_importance", "last_row", "aggregate_till"], layers,
