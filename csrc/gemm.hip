@@ -16,6 +16,12 @@
 #include "common.h"
 #include <algorithm>
 
+// Timing ablations that produce wrong results (skipped epilogues or staging, pp-kernel variants 5-9) are compiled
+// only into a tuning build (-DEDGE_TUNING_BUILD=1, tools/gemm_bench.py); the production library cannot reach them.
+#ifndef EDGE_TUNING_BUILD
+#define EDGE_TUNING_BUILD 0
+#endif
+
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_GELU = 4, EPI_SWIGLU = 5,
        EPI_QKV_ROPE = 6, EPI_LSE = 7,
        // fp32 execution (operands in the h3 split-fp16 layout, common.h; K is the concatenated 3K; fp16 MFMAs): fp32
@@ -55,12 +61,19 @@ struct GemmArgs {
   int skip_epi;  // timing ablation only (wrong results): 1 = no epilogue (gemm_bf16 / w7 kernels); 2 = persistent
                  // 256x256 SwiGLU epilogue computed but not stored
   int h3k;       // > 0: A is a 2-plane h3 activation [M, 2 h3k] (common.h h3_acol) of the K' = 3 h3k (or 2 h3k) GEMM
+  int pairb;     // h3 two-product GEMM (K' = 2 h3k, B the single fp16 plane [N, h3k]): K-tiles interleave the planes,
+                 // t -> A plane (t odd: hi, even: lo) column 64 (t >> 1), B column 64 (t >> 1) (b_kcol)
   float alpha = 1.f;      // h3: 1 / (s_a s_b), the product's scale (applied with the row scale)
   float out_scale = 1.f;  // h3 outputs (SwiGLU / GELU): the next GEMM's input scale s_a
 };
 
 // element column of A holding GEMM column k (k a K-tile start)
-__device__ __forceinline__ int a_kcol(const GemmArgs& a, int k) { return a.h3k ? h3_acol(k, a.h3k) : k; }
+__device__ __forceinline__ int a_kcol(const GemmArgs& a, int k) {
+  if (a.pairb) return ((k >> 6) & 1 ? 0 : a.h3k) + ((k >> 7) << 6);
+  return a.h3k ? h3_acol(k, a.h3k) : k;
+}
+// element column of B holding GEMM column k (k a K-tile start): the two K-tiles of a pair share one B tile
+__device__ __forceinline__ int b_kcol(const GemmArgs& a, int k) { return a.pairb ? (k >> 7) << 6 : k; }
 
 // 16x16x32 MFMA on bf16 (bf16 mode) or fp16 (h3 planes of the fp32 mode) operands held as raw 16-bit words
 template <bool F16>
@@ -676,7 +689,7 @@ __global__ __launch_bounds__(CF::NT, CF::NT == 256 ? 2 : 1) void gemm_bf16_kerne
   };
   auto stage = [&](int k0, char* buf) {
     stage_issue<CF::A_INSTR, NW>(pa, a_kcol(a, k0), buf, wave);
-    stage_issue<CF::B_INSTR, NW>(pb, k0, buf + CF::A_BYTES, wave);
+    stage_issue<CF::B_INSTR, NW>(pb, b_kcol(a, k0), buf + CF::A_BYTES, wave);
   };
   const int nk = a.K / BK;
 
@@ -1550,8 +1563,13 @@ template <int MF, int NR>
 __device__ constexpr int slot_pos(int r) { return (r + 1) * MF / NR - 1; }
 }  // namespace w4
 
-template <int EPI, int RH, int PF, int BN>
+// PB (h3 two-product GEMMs, GemmArgs::pairb): the B tile of K-tile pair p (K-tiles 2p, 2p+1 = the two A planes
+// against the same weight columns) lives in the B region of buffer p & 1 and is staged with the pair's even K-tile
+// only - a quarter less L2 -> LDS traffic.  The K loop is unrolled by two so that every DMA / read switch stays
+// compile-time (nk is even: pairs never straddle tiles).
+template <int EPI, int RH, int PF, int BN, bool PB = false>
 __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
+  static_assert(!PB || (epi_f32(EPI) && PF == 0), "paired B: h3 GEMMs without the prefetch stream");
   using Gm = w4::Geo<BN>;
   constexpr int NJ = Gm::NJ, NB = Gm::NB, BOFF = Gm::BOFF, TB = Gm::TB, NR = Gm::NR, MF = Gm::MF;
   using CQ = Cfg<256, 256, 4, 4>;   // BN = 256 epilogue view: 64x64 slabs
@@ -1590,12 +1608,23 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   };
   int st_q = 0, st_kt = 0, st_tile = tile0;
   set_stage_tile(tile0);
-  auto dma_item = [&](int r, char* buf, int kba, int kb) {   // item r < 8: A block, else B block r - 8
-    if (r < 8) glds16(sa + kba + oa[r], buf + (r * 4 + wave) * 1024);
-    else glds16(sb + kb + ob[r - 8], buf + BOFF + ((r - 8) * 4 + wave) * 1024);
+  // item r < 8: A block, else B block r - 8 (with PB into the K-tile pair's slot; its callers skip the B items of
+  // odd K-tiles at compile time)
+  auto dma_item = [&](int r, char* buf, int kba, int kb) {
+#if EDGE_TUNING_BUILD
+    // timing ablations (wrong results): 3 = B tiles staged on even K-tiles only, 4 = no B staging
+    if (r >= 8 && ((a.skip_epi == 3 && (st_kt & 1)) || a.skip_epi == 4)) return;
+#endif
+    if (r < 8) {
+      glds16(sa + kba + oa[r], buf + (r * 4 + wave) * 1024);
+    } else {
+      char* bbuf = PB ? smem + ((st_q >> 1) & 1) * TB : buf;
+      glds16(sb + kb + ob[r - 8], bbuf + BOFF + ((r - 8) * 4 + wave) * 1024);
+    }
   };
-  int st_kba = a_kcol(a, 0) * 2;   // byte offset of the stream K-tile's A columns (2-plane h3 operands: the plane remap, computed
-                    // once per K-tile where the wave waits anyway, not on the MFMA issue path)
+  // byte offsets of the stream K-tile's A and B columns (h3 operands: the plane remap / pair mapping, computed once per
+  // K-tile where the wave waits anyway, not on the MFMA issue path)
+  int st_kba = a_kcol(a, 0) * 2, st_kb = 0;
   auto advance_stage = [&]() {   // the DMA stream stops (repeats its last K-tile) at the end
     ++st_q;
     if (st_q >= total) {
@@ -1606,12 +1635,13 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       set_stage_tile(st_tile);
     }
     st_kba = a_kcol(a, st_kt * 64) * 2;
+    st_kb = b_kcol(a, st_kt * 64) * 2;
   };
-  auto stage_all = [&]() {
+  auto stage_all = [&](auto with_b) {
     char* buf = smem + (st_q & 1) * TB;
-    const int kb = st_kt * 128, kba = st_kba;
+    const int kb = st_kb, kba = st_kba;
 #pragma unroll
-    for (int r = 0; r < NR; ++r) dma_item(r, buf, kba, kb);
+    for (int r = 0; r < (decltype(with_b)::value ? NR : 8); ++r) dma_item(r, buf, kba, kb);
     advance_stage();
   };
 
@@ -1636,7 +1666,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     if constexpr (PF > 0) {
       char* scratch = smem + 2 * TB + wave * 256;
       __builtin_amdgcn_global_load_lds(pa_ + a_kcol(a, pf_kt * 64) * 2, LDS_PTR(scratch), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds(pb_ + pf_kt * 128, LDS_PTR(scratch), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds(pb_ + b_kcol(a, pf_kt * 64) * 2, LDS_PTR(scratch), 4, 0, 0);
       ++pf_q;
       if (pf_q < total && ++pf_kt == nk) {
         pf_kt = 0;
@@ -1662,12 +1692,12 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   // glds of the stream's next K-tile spread evenly between them.  The switches are compile-time (runtime-predicated
   // asm register writes make the allocator spill the fragments); first_c: the tile's first MFMAs start from zero.
   auto mma = [&](const bf16x8_t(&FA)[8], const bf16x8_t(&FB)[NJ], bf16x8_t(&GA)[8], bf16x8_t(&GB)[NJ], uint32_t bo,
-                 int ks, auto first_c, auto dma_c, auto read_c) {
+                 uint32_t boB, int ks, auto first_c, auto dma_c, auto read_c, auto dmab_c) {
     constexpr bool first = decltype(first_c)::value, dma_on = decltype(dma_c)::value;
-    constexpr bool read_on = decltype(read_c)::value;
-    const uint32_t va = abase[ks] + bo, vb = bbase[ks] + bo;
+    constexpr bool read_on = decltype(read_c)::value, dma_b = decltype(dmab_c)::value;
+    const uint32_t va = abase[ks] + bo, vb = bbase[ks] + boB;
     char* dbuf = smem + (st_q & 1) * TB;
-    const int kb = st_kt * 128, kba = st_kba;
+    const int kb = st_kb, kba = st_kba;
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
       // MFMAs slot_pos(rr-1)+1 .. slot_pos(rr), then work item rr
@@ -1687,17 +1717,20 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
         if (rr < 8) DS_READ_B128(GA[rr], va, rr * 2048);
         else DS_READ_B128(GB[rr - 8], vb, (rr - 8) * 2048);
       }
-      if constexpr (dma_on) dma_item(rr, dbuf, kba, kb);
+      if constexpr (dma_on) {
+        if (rr < 8 || dma_b) dma_item(rr, dbuf, kba, kb);   // rr is a compile-time index of the unrolled loop
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (dma_on) advance_stage();
   };
 
   // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed and visible, its K-half 0 fragments in X
-  stage_all();
+  stage_all(std::true_type{});
   if (total > 1) {
-    stage_all();
-    if constexpr (NR == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    stage_all(std::integral_constant<bool, !PB>{});
+    if constexpr (PB) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-tile 1 staged its 8 A blocks only
+    else if constexpr (NR == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1729,13 +1762,15 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     }
   };
   load_rs(m0);
-#pragma unroll 1
-  for (int t = 0; t < total; ++t) {
+  // K-tile t of the stream; dmab_c: the DMA issued in M(t,1) (K-tile t + 2) includes the B tile; end_c: K-tile t
+  // may be its tile's last (with PB only odd K-tiles can be)
+  auto ktile = [&](int t, auto dmab_c, auto end_c) {
     const uint32_t bo = (t & 1) * TB, bn = ((t + 1) & 1) * TB;
+    const uint32_t boB = PB ? ((t >> 1) & 1) * TB : bo, bnB = PB ? (((t + 1) >> 1) & 1) * TB : bn;
     // M(t,0) on X, K-half 1 of K-tile t -> Y
     __builtin_amdgcn_sched_barrier(0);
-    if (kt == 0) mma(XA, XB, YA, YB, bo, 1, std::true_type{}, std::false_type{}, std::true_type{});
-    else mma(XA, XB, YA, YB, bo, 1, std::false_type{}, std::false_type{}, std::true_type{});
+    if (kt == 0) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, std::false_type{}, std::true_type{}, dmab_c);
+    else mma(XA, XB, YA, YB, bo, boB, 1, std::false_type{}, std::false_type{}, std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < total) {
       if constexpr (PF > 0) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
@@ -1748,14 +1783,15 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     // M(t,1) on Y, K-tile t+2 -> buffer t & 1, K-half 0 of K-tile t+1 -> X.  Unconditional: past the end of the
     // stream the DMA re-reads the last K-tile into a buffer nobody reads again and X gets values nobody consumes.
     // (A runtime switch between read / no-read copies of this loop makes the allocator spill the fragments.)
-    mma(YA, YB, XA, XB, bn, 0, std::false_type{}, std::true_type{}, std::true_type{});
+    mma(YA, YB, XA, XB, bn, bnB, 0, std::false_type{}, std::true_type{}, std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PF > 0) {
       if (pf_q < total) prefetch();
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the count rule exact at the end
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (++kt == nk) {
+    ++kt;
+    if (decltype(end_c)::value && kt == nk) {
       // all MFMAs of the tile were issued; the epilogue reads the accumulators after they drain
       MFMA_DRAIN();
       __builtin_amdgcn_sched_barrier(0);
@@ -1805,9 +1841,18 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) DS_READ_B128(XA[i], abase[0] + bn, i * 2048);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) DS_READ_B128(XB[j], bbase[0] + bn, j * 2048);
+      for (int j = 0; j < NJ; ++j) DS_READ_B128(XB[j], bbase[0] + bnB, j * 2048);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+#pragma unroll 1
+  for (int t = 0; t < total; t += PB ? 2 : 1) {
+    if constexpr (PB) {
+      ktile(t, std::true_type{}, std::false_type{});       // M(t,1) stages K-tile t+2 (even): A and the pair's B
+      ktile(t + 1, std::false_type{}, std::true_type{});   // M(t+1,1) stages K-tile t+3 (odd): A only
+    } else {
+      ktile(t, std::true_type{}, std::true_type{});
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1974,11 +2019,6 @@ __global__ __launch_bounds__(512, 1) void gemm_w7_kernel(GemmArgs a) {
   }
 }
 
-// Timing ablations that produce wrong results (skipped epilogues, pp-kernel variants 5-9) are compiled only into a
-// tuning build (-DEDGE_TUNING_BUILD=1, tools/gemm_bench.py); the production library cannot reach them.
-#ifndef EDGE_TUNING_BUILD
-#define EDGE_TUNING_BUILD 0
-#endif
 static int g_tile_override = 0;  // 0 auto, 128, 224 or 256 (tests / tuning)
 static int g_skip_epi = 0;       // timing ablation (wrong results; tuning build only)
 static int g_rs_lds = 1;         // row scales through LDS in the persistent 256x256 kernel (A/B switch)
@@ -2057,19 +2097,27 @@ static int launch_8p(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <int EPI, int RH, int PF = 0, int BN = 256>
-static int launch_4w(const GemmArgs& a, hipStream_t st) {
+template <int EPI, int RH, int PF, int BN, bool PB>
+static int launch_4w_pb(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   const int grid = std::min(tiles, num_cus());
   constexpr int lds = w4::Geo<BN>::LDS + (PF > 0 ? 1024 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, PF, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
+    (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, PF, BN, PB>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, PF, BN>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, PF, BN, PB>), dim3(grid), dim3(256), lds, st, a);
   return (int)hipGetLastError();
+}
+
+template <int EPI, int RH, int PF = 0, int BN = 256>
+static int launch_4w(const GemmArgs& a, hipStream_t st) {
+  if constexpr (epi_f32(EPI) && PF == 0) {
+    if (a.pairb) return launch_4w_pb<EPI, RH, PF, BN, true>(a, st);
+  }
+  return launch_4w_pb<EPI, RH, PF, BN, false>(a, st);
 }
 
 static int g_qkv256 = 1;  // QKV+RoPE GEMMs on the four-wave 256x256 kernel when it fills the chip (else 128x128):
@@ -2104,9 +2152,9 @@ static int launch_w7m(const GemmArgs& a, hipStream_t st) {
 
 template <int EPI>
 static int launch_w7(const GemmArgs& a, hipStream_t st) {
-  // g_w7 == 2 (or variant 11 forced), and every 2-plane h3 operand: the four-wave kernel with 256x224 tiles
-  if (g_c256_variant == 11 || (g_c256_variant < 0 && g_w7 == 2) || a.h3k) return launch_4w<EPI, 0, 0, 224>(a, st);
-  if constexpr (epi_f32(EPI)) return launch_w7m<EPI, 0>(a, st);  // the modes A/B the bf16 epilogue's traffic
+  // g_w7 == 2 (or variant 11 forced), and every h3 operand (fp32 epilogues): the four-wave kernel with 256x224 tiles
+  if constexpr (epi_f32(EPI)) return launch_4w<EPI, 0, 0, 224>(a, st);
+  if (g_c256_variant == 11 || (g_c256_variant < 0 && g_w7 == 2)) return launch_4w<EPI, 0, 0, 224>(a, st);
   switch (g_w7_mode) {
     case 1: return launch_w7m<EPI, 1>(a, st);
     case 2: return launch_w7m<EPI, 2>(a, st);
@@ -2133,6 +2181,9 @@ static int launch(const GemmArgs& args, hipStream_t st) {
     // (default for the fp32-mode h3 QKV, K' = 3K; the bf16 QKV's K = 896 loop is shorter than the 128x128 kernel's
     // tail advantage: g_qkv256 = 2 forces it there too)
     const bool on = EPI == EPI_F32_QKV_ROPE ? g_qkv256 >= 1 : g_qkv256 >= 2;
+    // the XCD-chunked tile walk: N = 1152 is 4.5 column tiles, and keeping an XCD's rounds inside one GROUP_M band
+    // re-uses its A panels from L2 (h3 QKV at M = 32768: 144 vs 159 us strided, profiles/r02h_gemm_explore.log)
+    if (g_walk == 1) a.walk = 2;
     if (on && tiles >= 256 && g_tile_override != 128) return launch_4w<EPI, RH>(a, st);
     return launch_cfg<EPI, RH, C128>(a, st);
   } else if constexpr (EPI == EPI_LSE || EPI == EPI_F32_LSE) {
@@ -2293,8 +2344,9 @@ EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, 
   }
 }
 
-// h3 operand geometry: K' = Kx = terms x kplane, terms 3 (B' = [b_hi | b_lo | b_hi]) or 2 (a weight exact in fp16,
-// b_lo = 0 - e.g. a bf16 or fp16 checkpoint: B' = [b_hi | b_hi], the A loader reads A' = [a_lo | a_hi])
+// h3 operand geometry: K' = Kx = terms x kplane, terms 3 (B' = [b_hi | b_lo | b_hi] [N, 3K]) or 2 (a weight exact in
+// fp16, b_lo = 0 - e.g. a bf16 or fp16 checkpoint: B = b_hi [N, K] once, the K-tiles interleave A' = a_lo / a_hi
+// against the same B tile, GemmArgs::pairb)
 static bool h3_geometry_ok(int Kx, int kplane) {
   return kplane > 0 && kplane % BK == 0 && (Kx == 2 * kplane || Kx == 3 * kplane);
 }
@@ -2313,7 +2365,9 @@ EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, 
   a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.biasf = bias; a.residf = resid; a.ldr = ldr;
   a.h3k = kplane;   // A: 2-plane activation rows (lda >= 2 kplane)
-  if (!h3_geometry_ok(Kx, kplane) || lda < 2 * kplane || !(alpha > 0.f) || !(out_scale > 0.f))
+  a.pairb = Kx == 2 * kplane;
+  if (!h3_geometry_ok(Kx, kplane) || lda < 2 * kplane || ldb < (a.pairb ? kplane : Kx) || !(alpha > 0.f) ||
+      !(out_scale > 0.f))
     return (int)hipErrorInvalidValue;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
@@ -2345,7 +2399,8 @@ EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* b
                                     int Hkv, int rot_dim, int s_pad, float q_scale, float alpha, hipStream_t st) {
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
-  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = 2 * kplane; a.ldb = Kx;
+  a.pairb = Kx == 2 * kplane;
+  a.M = M; a.N = (Hq + 2 * Hkv) * 64; a.K = Kx; a.lda = 2 * kplane; a.ldb = a.pairb ? kplane : Kx;
   a.h3k = kplane;   // X: 2-plane activation rows [M, 2 kplane]
   a.alpha = alpha;
   a.biasf = bias; a.qf = q; a.kf = k; a.vtf = vt;
@@ -2372,7 +2427,8 @@ EDGE_API int edge_gemm_lse(const void* X, const void* W, const int64_t* targets,
   GemmArgs a{};
   const bool h3 = alpha > 0.f;
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
-  a.M = M; a.N = N; a.K = K; a.lda = h3 ? 2 * kplane : K; a.ldb = K;
+  a.pairb = h3 && K == 2 * kplane;
+  a.M = M; a.N = N; a.K = K; a.lda = h3 ? 2 * kplane : K; a.ldb = a.pairb ? kplane : K;
   if (h3 && !h3_geometry_ok(K, kplane)) return (int)hipErrorInvalidValue;
   a.h3k = h3 ? kplane : 0;
   a.alpha = h3 ? alpha : 1.f;

@@ -45,15 +45,15 @@ def _check_f32(*ts):
 
 
 def _check_h3(a3, w3, alpha) -> int:
-    """a3: 2-plane activation [rows, 2K] (reference.h3_act), w3: h3 weight [N, 3K] or [N, 2K]
-    (reference.h3_weight).  Returns the plane width K."""
+    """a3: 2-plane activation [rows, 2K] (reference.h3_act), w3: h3 weight [N, 3K] or the single plane [N, K]
+    (reference.h3_weight).  Returns (plane width K, the GEMM's K' = 3K or 2K)."""
     for t, what in ((a3, "activations [rows, 2K] (reference.h3_act)"), (w3, "weights (reference.h3_weight)")):
         if t.dtype != torch.float16 or not t.is_contiguous():
             raise TypeError(f"h3 {what} must be contiguous fp16")
-    ref.h3_terms(a3, w3)
+    terms = ref.h3_terms(a3, w3)
     if not alpha > 0.0:
         raise ValueError(f"h3 product scale alpha must be > 0, got {alpha}")
-    return a3.shape[-1] // 2
+    return a3.shape[-1] // 2, terms * (a3.shape[-1] // 2)
 
 
 def _check_bf16(*ts):
@@ -417,7 +417,7 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
     act None -> fp32 [M, N] (``residual`` fp32, may alias ``out``); act "gelu" / "swiglu_il" -> the activation as
     the 2-plane h3 activation of ``out_scale`` * act(...) ([M, 2N] / [M, N]) for the next GEMM."""
     M = a3.shape[0]
-    N, Kx = w3.shape
+    N = w3.shape[0]
     if not _gpu(a3):
         y = ref.h3_matmul(a3, w3, alpha)
         if rscale is not None:
@@ -435,7 +435,7 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
             out.copy_(y)
             return out
         return y
-    kp = _check_h3(a3, w3, alpha)
+    kp, Kx = _check_h3(a3, w3, alpha)
     _check_f32(bias, residual, rscale)
     if act is None:
         if out is None:
@@ -459,10 +459,10 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
         y = ref.h3_matmul(a3, w3, alpha)            # x @ w.T, then the rest of the fused op on fp32
         eye = torch.eye(y.shape[1], dtype=torch.float32)
         return ref.qkv_rope(y, eye, bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
-    kp = _check_h3(a3, w3, alpha)
+    kp, Kx = _check_h3(a3, w3, alpha)
     _check_f32(bias)
     assert D == 64, "HIP attention path is specialised for head_dim 64"
-    M, Kx = a3.shape[0], w3.shape[1]
+    M = a3.shape[0]
     sp = s_pad(S)
     f32 = dict(dtype=torch.float32, device=a3.device)
     q = torch.empty(B, Hq, S, D, **f32)
@@ -478,8 +478,8 @@ def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch
     if not _gpu(a3):
         logits = ref.h3_matmul(a3, w3, alpha)
         return torch.logsumexp(logits, -1) - logits.gather(1, targets.long().view(-1, 1)).squeeze(1)
-    kp = _check_h3(a3, w3, alpha)
-    R, Kx = a3.shape[0], w3.shape[1]
+    kp, Kx = _check_h3(a3, w3, alpha)
+    R = a3.shape[0]
     V = w3.shape[0]
     nparts = V // 64
     f32 = dict(dtype=torch.float32, device=a3.device)

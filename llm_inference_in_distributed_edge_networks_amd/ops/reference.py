@@ -190,8 +190,9 @@ def head_nll(h, w, targets):
 # residual rounding (2^-23): below the CPU fp32 GEMM's own error (tools/h3_error.py).  Weights are stored as B'
 # [N, 3K] fp16; activations once per plane, [hi | lo] [R, 2K] fp16 (the GEMM's A loader reads block j of A' from
 # plane H3_APLANES[j]); the epilogue multiplies by alpha = 1 / (s_a s_b).  A weight exact in fp16 after scaling
-# (b_lo == 0, e.g. bf16 / fp16 checkpoint values) is stored as B' = [b_hi | b_hi] [N, 2K]: the GEMM over K' = 2K
-# (A' = [a_lo | a_hi]) gives the same result, its third product being exactly zero.
+# (b_lo == 0, e.g. bf16 / fp16 checkpoint values) is stored as its single plane b_hi [N, K]: the GEMM over K' = 2K
+# sums a_lo b_hi + a_hi b_hi (the kernel interleaves the two A planes against each B tile), the same result, its
+# third product being exactly zero.
 H3_APLANES = (1, 0, 0)
 H3_BPLANES = (0, 1, 0)
 H3_TOP = 15   # the scaled bound is at most 2^15: hi and lo stay below the fp16 maximum 65504 (< 2^16)
@@ -226,21 +227,21 @@ def h3_expand(a3: torch.Tensor, terms: int = 3) -> torch.Tensor:
 
 
 def h3_weight(w: torch.Tensor, two_term: bool = True) -> tuple[torch.Tensor, float]:
-    """fp32 [N, K] nn.Linear weight -> (h3 weight B' [N, 3K] fp16, its scale s_w); [N, 2K] = [hi | hi] when the
-    weight is exact in fp16 after scaling and ``two_term`` (the lo plane would be all zero)."""
+    """fp32 [N, K] nn.Linear weight -> (h3 weight B' [N, 3K] fp16, its scale s_w); the single plane hi [N, K] when
+    the weight is exact in fp16 after scaling and ``two_term`` (the lo plane would be all zero)."""
     s = h3_scale(_f(w).abs().max().item())
     p = split2h(w, s)
     if two_term and not p[1].any():
-        return torch.cat([p[0], p[0]], -1).contiguous(), s
+        return p[0].contiguous(), s
     return torch.cat([p[i] for i in H3_BPLANES], -1).contiguous(), s
 
 
 def h3_terms(a3: torch.Tensor, w3: torch.Tensor) -> int:
-    """Products of the h3 GEMM of a3 [R, 2K] and w3 [N, terms K]: 3, or 2 for a weight exact in fp16."""
+    """Products of the h3 GEMM of a3 [R, 2K] and w3: 3 for [N, 3K], 2 for a single-plane weight [N, K]."""
     K = a3.shape[-1] // 2
-    if w3.shape[-1] not in (2 * K, 3 * K):
+    if w3.shape[-1] not in (K, 3 * K):
         raise ValueError(f"h3 activation width {a3.shape[-1]} does not match the weight width {w3.shape[-1]}")
-    return w3.shape[-1] // K
+    return 3 if w3.shape[-1] == 3 * K else 2
 
 
 def h3_to_f32(a3: torch.Tensor, s: float = 1.0) -> torch.Tensor:
@@ -251,14 +252,17 @@ def h3_to_f32(a3: torch.Tensor, s: float = 1.0) -> torch.Tensor:
 
 def h3w_to_f32(w3: torch.Tensor, s: float, K: int) -> torch.Tensor:
     """Inverse of ``h3_weight`` (K = the weight's input width): (hi + lo) / s, or hi / s for a two-term weight."""
-    if w3.shape[-1] == 2 * K:
-        return w3[..., :K].float() / s
+    if w3.shape[-1] == K:
+        return w3.float() / s
     return (w3[..., :K].float() + w3[..., K:2 * K].float()) / s
 
 
 def h3_matmul(a3: torch.Tensor, w3: torch.Tensor, alpha: float) -> torch.Tensor:
     """What the h3 GEMM computes: alpha * (A' @ B'^T), fp16 x fp16 products (exact) accumulated in fp32."""
-    return (h3_expand(a3, h3_terms(a3, w3)).float() @ w3.float().t()) * alpha
+    if h3_terms(a3, w3) == 2:
+        w3 = torch.cat([w3, w3], -1)
+        return (h3_expand(a3, 2).float() @ w3.float().t()) * alpha
+    return (h3_expand(a3, 3).float() @ w3.float().t()) * alpha
 
 
 # ---- fused RMSNorm (GPU fast path) semantics -------------------------------------------------------

@@ -1,4 +1,4 @@
-# fp32-mode (h3) check: fp32 kernel tests, full-model numerics, smoke, bench, attention timing.
+# fp32-mode (h3) check: fp32 kernel tests, full-model numerics, smoke, bench, GEMM timing.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -11,5 +11,5 @@ step() {  # name timeout cmd...
 }
 TAIL=15 step pytest_f32 600 python -u -m pytest tests/test_f32_gpu.py -x -q --timeout 120 --timeout-method thread || exit $?
 TAIL=1 step bench_h3 400 python bench.py --steps 10 --warmup 3 --no-bf16 --no-fp32-weights --json-out gpurun_out/bench_h3.json || exit $?
-TAIL=12 step attn 300 python tools/attn_bench.py --fp32 || exit $?
+TAIL=30 step gemm 400 python tools/gemm_bench.py --only h3_2t_gate_up_b64,h3_2t_down_b64,h3_2t_o_proj_b64,h3_2t_qkv_rope_b64 --rounds 3 || exit $?
 exit 0

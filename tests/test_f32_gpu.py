@@ -91,7 +91,7 @@ def test_linear_h3_fp32_accuracy(M, N, K, epi, slack=0, two_term=False):
     act = {"gelu": "gelu", "swiglu": "swiglu_il"}.get(epi)
     sx = R.h3_scale(x.abs().max().item()) / 2 ** slack
     w3, sw = R.h3_weight(w)
-    assert w3.shape[1] == (2 if two_term else 3) * K
+    assert w3.shape[1] == (1 if two_term else 3) * K
     ref = x.double() @ w.double().t()
     if b is not None:
         ref = ref + b.double()

@@ -31,6 +31,11 @@ SHAPES = {  # name: (M, N, K, act, bias, resid)
     "h3_qkv_rope_b64": (32768, 1152, 3 * 896, "h3_qkv_rope", True, False),
     # epilogue-cost ablation of the h3 gate/up shape: plain fp32 output
     "h3_gate_up_f32out": (32768, 9728, 3 * 896, "h3", False, False),
+    # two-product h3 GEMMs (weights exact in fp16, the bench's checkpoint-valued weights): K' = 2K
+    "h3_2t_gate_up_b64": (32768, 9728, 2 * 896, "h3_swiglu", False, False),
+    "h3_2t_down_b64": (32768, 896, 2 * 4864, "h3", False, True),
+    "h3_2t_o_proj_b64": (32768, 896, 2 * 896, "h3", False, True),
+    "h3_2t_qkv_rope_b64": (32768, 1152, 2 * 896, "h3_qkv_rope", True, False),
 }
 
 
@@ -64,8 +69,10 @@ def main():
         h3 = act is not None and act.startswith("h3")
         # h3 shapes: K is the GEMM's K' = 3 x plane width; the activation is stored once per plane ([M, 2K'/3])
         dt = torch.float16 if h3 else torch.bfloat16
-        x = (torch.rand(M, 2 * K // 3 if h3 else K, device=dev) * 2 - 1).to(dt)
-        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(dt)
+        kp = (K // 2 if "_2t_" in name else K // 3) if h3 else K   # plane width of the h3 activation
+        x = (torch.rand(M, 2 * kp if h3 else K, device=dev) * 2 - 1).to(dt)
+        two = h3 and "_2t_" in name   # single-plane weight [N, K'/2] (the two-product GEMM)
+        w = ((torch.rand(N, K // 2 if two else K, device=dev) * 2 - 1) / K ** 0.5).to(dt)
         b = torch.randn(N, device=dev).to(torch.float32 if h3 else torch.bfloat16) if bias else None
         No = N // 2 if act in ("swiglu_il", "h3_swiglu") else N
         r = torch.randn(M, No, device=dev).to(torch.float32 if h3 else torch.bfloat16) if resid else None
@@ -75,8 +82,10 @@ def main():
         def mk(spec):  # spec may end in "/w0" = strided persistent tile walk instead of XCD chunks, or "/noepi" =
             # timing ablation of the persistent 256x256 loop without its epilogue (wrong results)
             # "/m<k>": W7 epilogue memory mode k (bit 0 nt stores, bit 1 nt residual loads)
-            noepi = 1 if spec.endswith("/noepi") else (2 if spec.endswith("/nostore") else 0)
-            spec = spec.removesuffix("/noepi").removesuffix("/nostore")
+            # "/nob1": B tiles staged on even K-tiles only, "/nob": no B staging (four-wave kernel, wrong results)
+            noepi = {"/noepi": 1, "/nostore": 2, "/nob1": 3, "/nob": 4}.get("/" + spec.rpartition("/")[2], 0)
+            if noepi:
+                spec = spec.rpartition("/")[0]
             mode = int(spec.partition("/m")[2] or 0)
             cfg, _, walk = spec.partition("/m")[0].partition("/w")
 
@@ -102,8 +111,9 @@ def main():
             cos, sin = (t.to(dev) for t in ops.rope_tables(512, 64, 1e6))
         variants = {t: mk(t) for t in tiles}
         ours = variants[tiles[0]]
-        xl = torch.cat([x, x[:, :K // 3]], 1) if h3 else x   # hipBLASLt reference: the same K' GEMM, plain operands
-        lib = lambda: torch.matmul(xl, w.t())  # noqa: E731
+        xl = torch.cat([x, x[:, :K - 2 * kp]], 1) if h3 else x   # hipBLASLt reference: the same K' GEMM, plain operands
+        wl = torch.cat([w, w], 1) if two else w
+        lib = lambda: torch.matmul(xl, wl.t())  # noqa: E731
         if resid and not h3:  # hipBLASLt with the residual as beta*C (what a library route for RESID GEMMs would run)
             variants["libr"] = lambda: torch.addmm(r, x, w.t())
         for _ in range(3):
