@@ -1563,6 +1563,65 @@ template <int MF, int NR>
 __device__ constexpr int slot_pos(int r) { return (r + 1) * MF / NR - 1; }
 }  // namespace w4
 
+// ---- 256 x 192 QKV tiles (fp32 mode, N = 1152 = 6 x 192: 768 tiles = exactly 3 rounds of the 256 CUs, where 256-wide
+// tiles give 4.5 column tiles, a half-empty fifth and 2.5 rounds).  A wave's 96-column slab is 1.5 heads, so the
+// tile's weight rows are loaded permuted: 16-row blocks 1 and 2 of every head swapped (q192_feat), which puts each
+// RoPE pair of blocks - dims [0,16) with [32,48), [16,32) with [48,64) - into adjacent MFMA column groups (2p, 2p+1):
+// the rotation partner of a lane's value is in the same lane, and no pair straddles the two waves.
+__device__ __forceinline__ int q192_feat(int col) {   // tile column (permuted order) -> weight output feature
+  const int q = (col >> 4) & 3;
+  return (col & ~63) | ((q == 1 ? 2 : q == 2 ? 1 : q) << 4) | (col & 15);
+}
+
+// c: the virtual wave vw's 64 x 96 slab (rows m0 + vw 64 + i 16 + (lane & 15), columns nw + j 16 + 4 g + r); RH = 32
+// (full 64-dim rotary: pair offset 32) or 0 (no rotary)
+template <int RH>
+__device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[4][6], int m0, int n0, int lane,
+                                                int vw, int wn) {
+  static_assert(RH == 0 || RH == 32, "192-wide QKV tiles: full rotary or none");
+  const int g = lane >> 4;
+  const int nw = n0 + wn * 96;
+  f32x4_t bw[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) bw[j] = *(const f32x4_t*)(a.biasf + q192_feat(nw + j * 16) + g * 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + vw * 64 + i * 16 + (lane & 15);
+    if (m >= a.M) continue;
+    const int b = m / a.S, pos = m - b * a.S;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int col = nw + 32 * p;                       // block 2p: q = 0 or 2 of its head
+      const int head = col >> 6;                         // wave-uniform
+      const int d = (((col >> 4) & 3) ? 16 : 0) + g * 4; // low-half dims d .. d+3, partners d+32 ..
+      f32x4_t lo = c[i][2 * p] * a.alpha + bw[2 * p];
+      f32x4_t hi = c[i][2 * p + 1] * a.alpha + bw[2 * p + 1];
+      const bool is_v = head >= a.Hq + a.Hkv;
+      if (!is_v) {
+        if constexpr (RH == 32) {
+          const f32x4_t cs = *(const f32x4_t*)(a.cosT + pos * 32 + d);
+          const f32x4_t sn = *(const f32x4_t*)(a.sinT + pos * 32 + d);
+          const f32x4_t l2 = lo * cs - hi * sn;
+          hi = hi * cs + lo * sn;
+          lo = l2;
+        }
+        const float sc = head < a.Hq ? a.q_scale : 1.f;
+        float* dst = head < a.Hq ? a.qf + (((size_t)b * a.Hq + head) * a.S + pos) * 64
+                                 : a.kf + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
+        *(f32x4_t*)(dst + d) = lo * sc;
+        *(f32x4_t*)(dst + d + 32) = hi * sc;
+      } else {
+        float* dst = a.vtf + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dst[(size_t)(d + r) * a.s_pad] = lo[r];
+          dst[(size_t)(d + 32 + r) * a.s_pad] = hi[r];
+        }
+      }
+    }
+  }
+}
+
 // PB (h3 two-product GEMMs, GemmArgs::pairb): the B tile of K-tile pair p (K-tiles 2p, 2p+1 = the two A planes
 // against the same weight columns) lives in the B region of buffer p & 1 and is staged with the pair's even K-tile
 // only - a quarter less L2 -> LDS traffic.  The K loop is unrolled by two so that every DMA / read switch stays
@@ -1570,6 +1629,8 @@ __device__ constexpr int slot_pos(int r) { return (r + 1) * MF / NR - 1; }
 template <int EPI, int RH, int PF, int BN, bool PB = false>
 __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   static_assert(!PB || (epi_f32(EPI) && PF == 0), "paired B: h3 GEMMs without the prefetch stream");
+  static_assert(BN != 192 || (EPI == EPI_F32_QKV_ROPE && (RH == 0 || RH == 32)), "192-wide tiles: fp32 QKV only");
+  static_assert(BN == 192 || BN == 224 || BN == 256, "tile width");
   using Gm = w4::Geo<BN>;
   constexpr int NJ = Gm::NJ, NB = Gm::NB, BOFF = Gm::BOFF, TB = Gm::TB, NR = Gm::NR, MF = Gm::MF;
   using CQ = Cfg<256, 256, 4, 4>;   // BN = 256 epilogue view: 64x64 slabs
@@ -1603,7 +1664,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int r = (i * 4 + wave) * 8 + (lane >> 3);
-      ob[i] = (uint32_t)(min(r, a.N - 1 - n0) * a.ldb + ((lane & 7) ^ swz(r)) * 8) * 2u;
+      // 192-wide QKV tiles (head-aligned n0): LDS row r holds weight row q192_feat(n0 + r)
+      const int rb = BN == 192 ? q192_feat(n0 + r) - n0 : r;
+      ob[i] = (uint32_t)(min(rb, a.N - 1 - n0) * a.ldb + ((lane & 7) ^ swz(r)) * 8) * 2u;
     }
   };
   int st_q = 0, st_kt = 0, st_tile = tile0;
@@ -1731,7 +1794,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     stage_all(std::integral_constant<bool, !PB>{});
     if constexpr (PB) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-tile 1 staged its 8 A blocks only
     else if constexpr (NR == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    else if constexpr (NR == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -1813,6 +1877,20 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
             }
           }
           if (n0 + wn * 128 + h * 64 < a.N) gemm_epilogue<EPI, RH, CQ>(a, c, m0, n0, lane, wm * 2 + ih, wn * 2 + h, rq);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else if constexpr (BN == 192) {
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih) {   // 64 x 96 halves
+          f32x4_t c[4][6];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+              c[i][j] = acc[ih * 4 + i][j];
+              asm volatile("" : "+v"(c[i][j]));
+            }
+          qkv192_epilogue<RH>(a, c, m0, n0, lane, wm * 2 + ih, wn);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
@@ -2122,6 +2200,7 @@ static int launch_4w(const GemmArgs& a, hipStream_t st) {
 
 static int g_qkv256 = 1;  // QKV+RoPE GEMMs on the four-wave 256x256 kernel when it fills the chip (else 128x128):
                           // 0 never, 1 the fp32-mode QKV, 2 both
+static int g_qkv192 = 1;  // fp32-mode QKV on 256x192 tiles when 192 divides N and 256 does not (A/B: 0 = 256x256)
 static int g_w7 = 2;  // 256x224 tiles for N % 224 == 0 shapes that 256 does not divide (N = 896): 1 eight-wave
                       // 64x112 wave tiles, 2 four-wave 128x112 wave tiles (default: 10-17 % faster on N = 896)
 
@@ -2184,6 +2263,14 @@ static int launch(const GemmArgs& args, hipStream_t st) {
     // the XCD-chunked tile walk: N = 1152 is 4.5 column tiles, and keeping an XCD's rounds inside one GROUP_M band
     // re-uses its A panels from L2 (h3 QKV at M = 32768: 144 vs 159 us strided, profiles/r02h_gemm_explore.log)
     if (g_walk == 1) a.walk = 2;
+    if constexpr (EPI == EPI_F32_QKV_ROPE && (RH == 0 || RH == 32)) {
+      // 256x192 tiles when 192 divides N and 256 does not (N = 1152: 768 tiles, 3 full rounds)
+      const long long t192 = (long long)((a.M + 255) / 256) * (a.N / 192);
+      // (tile override 192 forces it at any M, for tests)
+      if (a.N % 192 == 0 && a.N % 256 &&
+          (g_tile_override == 192 || (on && g_qkv192 && t192 >= 256 && !g_tile_override)))
+        return launch_4w<EPI, RH, 0, 192>(a, st);
+    }
     if (on && tiles >= 256 && g_tile_override != 128) return launch_4w<EPI, RH>(a, st);
     return launch_cfg<EPI, RH, C128>(a, st);
   } else if constexpr (EPI == EPI_LSE || EPI == EPI_F32_LSE) {
@@ -2260,6 +2347,11 @@ EDGE_API int edge_gemm_set_skip_epi(int on) {
 
 EDGE_API int edge_gemm_set_qkv256(int on) {
   g_qkv256 = on;
+  return 0;
+}
+
+EDGE_API int edge_gemm_set_qkv192(int on) {
+  g_qkv192 = on;
   return 0;
 }
 

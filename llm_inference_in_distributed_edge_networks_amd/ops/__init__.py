@@ -149,8 +149,9 @@ def layernorm_dual(x, w1, b1, w2, b2, eps, h3: tuple[float, float] = (0.0, 0.0))
 
 
 def set_gemm_tile(tile: int) -> None:
-    """Force the GEMM block tile (128, 224 or 256; 0 = automatic by shape).  Tuning / tests only.  224 is the
-    256x224 kernel for N % 224 == 0 shapes that 256 does not divide (the Qwen2 hidden size 896)."""
+    """Force the GEMM block tile (128, 192, 224 or 256; 0 = automatic by shape).  Tuning / tests only.  224 is the
+    256x224 kernel for N % 224 == 0 shapes that 256 does not divide (the Qwen2 hidden size 896); 192 the fp32-mode
+    QKV kernel for N % 192 == 0 (N = 1152)."""
     call("edge_gemm_set_tile", int(tile))
 
 
@@ -182,6 +183,12 @@ def set_gemm_qkv256(mode: int) -> None:
     """QKV+RoPE GEMMs on the four-wave 256x256 kernel when the shape fills the chip: 0 never, 1 the fp32-mode (h3)
     QKV (default), 2 the bf16 QKV too."""
     call("edge_gemm_set_qkv256", int(mode))
+
+
+def set_gemm_qkv192(on) -> None:
+    """fp32-mode QKV+RoPE GEMMs on 256x192 tiles when 192 divides N and 256 does not (N = 1152: 768 tiles, three
+    full rounds of the chip; default on).  A/B only."""
+    call("edge_gemm_set_qkv192", int(on))
 
 
 def set_gemm_walk(chunked) -> None:

@@ -37,6 +37,7 @@ _SIGS = {
     "edge_gemm_set_walk": [c_i],
     "edge_gemm_set_w7": [c_i],
     "edge_gemm_set_qkv256": [c_i],
+    "edge_gemm_set_qkv192": [c_i],
     "edge_gemm_set_skip_epi": [c_i],
     "edge_gemm_set_rs_lds": [c_i],
     "edge_gemm_set_lse256": [c_i],

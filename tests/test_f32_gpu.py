@@ -140,19 +140,36 @@ def test_linear_h3_inplace_residual():
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv,rot", [(2, 512, 14, 2, 64), (2, 100, 14, 2, 64), (1, 2048, 8, 8, 16),
-                                             (64, 512, 14, 2, 64), (24, 2048, 8, 8, 16)])
-def test_qkv_rope_h3(B, S, Hq, Hkv, rot):
-    """fp32 QKV+RoPE from h3 operands: 128x128 tiles (small M) and the four-wave 256x256 kernel (production M)."""
+                                             (64, 512, 14, 2, 64), (24, 2048, 8, 8, 16), (2, 512, 14, 2, 0)])
+@pytest.mark.parametrize("tile", ["auto", "192", "256"])
+@pytest.mark.parametrize("two_term", [False, True])
+def test_qkv_rope_h3(B, S, Hq, Hkv, rot, tile, two_term):
+    """fp32 QKV+RoPE from h3 operands: 128x128 tiles (small M), the four-wave 256x192 kernel with permuted weight rows
+    (N = 1152, production M; forced at small M with tile 192) and the 256x256 kernel (tile 256), three- and
+    two-product weights."""
     H = 896 if Hq == 14 else 512
     Nq = (Hq + 2 * Hkv) * 64
+    if tile == "192" and Nq % 192:
+        pytest.skip("192-wide tiles need N % 192 == 0")
     x = rnd(B * S, H, seed=30)
     w = rnd(Nq, H, s=1 / math.sqrt(H), seed=31)
+    if two_term:
+        w = w.to(torch.bfloat16).float()
     b = rnd(Nq, s=0.1, seed=32)
-    cos, sin = R.rope_tables(4096, rot, 1e6 if rot == 64 else 1e4)
+    cos, sin = R.rope_tables(4096, max(rot, 2), 1e6 if rot == 64 else 1e4)
     sx = R.h3_scale(x.abs().max().item())
     w3, sw = R.h3_weight(w)
-    q, k, vt = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV), cos.to(DEV),
-                               sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125)
+    try:
+        if tile == "192":
+            ops.set_gemm_tile(192)
+        elif tile == "256":
+            ops.set_gemm_qkv192(0)
+        q, k, vt = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV), cos.to(DEV),
+                                   sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_gemm_tile(0)
+        ops.set_gemm_qkv192(1)
     rq, rk, rv = R.qkv_rope(x.double(), w.double(), b.double(), cos.double(), sin.double(), B, S, Hq, Hkv, 64, rot,
                             0.125)
     assert rel_err(q, rq) < 4e-6 and rel_err(k, rk) < 4e-6 and rel_err(vt, rv) < 4e-6
