@@ -467,15 +467,34 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
 
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
-  if (qrow < S) {
-    const float inv = 1.f / (l_run * (SP * sv));
-    const int W = Hq * 64;
-    if constexpr (H3OUT) {
-      f16_t* orow = (f16_t*)o + ((size_t)b * S + qrow) * (size_t)(2 * W);
+  const float inv = 1.f / (l_run * (SP * sv));
+  const int W = Hq * 64;
+  u32x4_t oh[2], ol[2];
+  if constexpr (H3OUT) {
+    // h3 planes of O: the d-groups (0,1) and (2,3) pair-swapped (permlane16, partners share the query row) into 8
+    // consecutive values per lane, one 16-byte store per plane and pair instead of two 8-byte ones
+    u32x2_t hw[4], lw[4];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
-        store_h3_4(orow, W, h * 64 + dt * 16 + 4 * g, v, h3s);
+    for (int dt = 0; dt < 4; ++dt) {
+      float hi[4], lo[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) split2h(oacc[dt][r] * inv * h3s, hi[r], lo[r]);
+      hw[dt] = u32x2_t{pack_h2(hi[0], hi[1]), pack_h2(hi[2], hi[3])};
+      lw[dt] = u32x2_t{pack_h2(lo[0], lo[1]), pack_h2(lo[2], lo[3])};
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 2; ++q2) {
+      oh[q2] = pair_swap16(hw[2 * q2], hw[2 * q2 + 1]);
+      ol[q2] = pair_swap16(lw[2 * q2], lw[2 * q2 + 1]);
+    }
+  }
+  if (qrow < S) {
+    if constexpr (H3OUT) {
+      f16_t* orow = (f16_t*)o + ((size_t)b * S + qrow) * (size_t)(2 * W) + h * 64;
+#pragma unroll
+      for (int q2 = 0; q2 < 2; ++q2) {
+        *(u32x4_t*)(orow + q2 * 32 + pair_col(g)) = oh[q2];
+        *(u32x4_t*)(orow + W + q2 * 32 + pair_col(g)) = ol[q2];
       }
     } else {
       float* orow = (float*)o + ((size_t)b * S + qrow) * (size_t)W + h * 64;

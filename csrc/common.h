@@ -86,6 +86,17 @@ __device__ __forceinline__ void store_h3_8(f16_t* __restrict__ row, int K, int c
   *(u32x4_t*)(row + (size_t)K + col) = wl;
 }
 
+// T21-style store widening for the swapped 16x16 MFMA layout: lane group g = lane>>4 holds 4 consecutive
+// columns g*4.. of a 16-column group.  v_permlane16_swap exchanges rows 1,3 of `lo` with rows 0,2 of `hi`,
+// so for two groups (lo, hi) lanes g=0/2 end with 8 consecutive columns of `lo` and lanes g=1/3 with 8 of `hi`:
+// one 16-byte store per lane at column offset (g&1)*16 + (g>>1)*8 of the 32-column pair (was two 8-byte stores).
+__device__ __forceinline__ u32x4_t pair_swap16(u32x2_t lo, u32x2_t hi) {
+  const auto r0 = __builtin_amdgcn_permlane16_swap(lo[0], hi[0], false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(lo[1], hi[1], false, false);
+  return u32x4_t{r0[0], r1[0], r0[1], r1[1]};
+}
+__device__ __forceinline__ int pair_col(int g) { return (g & 1) * 16 + (g >> 1) * 8; }
+
 // silu(x) = x / (1 + e^-x) on the hardware transcendentals (v_exp_f32, v_rcp_f32, ~1 ulp): a plain '/' compiles
 // to the IEEE division sequence (2 v_div_scale + v_div_fmas + v_div_fixup + v_rcp + FMAs), which made the
 // SwiGLU epilogue of the gate/up GEMM cost ~20 VALU per output.  Saturates correctly: e^-x = inf -> 0.

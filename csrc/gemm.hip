@@ -108,16 +108,6 @@ using C256 = Cfg<256, 256, 2, 4>;   // 8 waves, 128 KiB LDS, 1 block/CU
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
-// T21-style store widening for the swapped 16x16 MFMA layout: lane group g = lane>>4 holds 4 consecutive
-// columns g*4.. of a 16-column group.  v_permlane16_swap exchanges rows 1,3 of `lo` with rows 0,2 of `hi`,
-// so for two groups (lo, hi) lanes g=0/2 end with 8 consecutive columns of `lo` and lanes g=1/3 with 8 of `hi`:
-// one 16-byte store per lane at column offset (g&1)*16 + (g>>1)*8 of the 32-column pair (was two 8-byte stores).
-__device__ __forceinline__ u32x4_t pair_swap16(u32x2_t lo, u32x2_t hi) {
-  const auto r0 = __builtin_amdgcn_permlane16_swap(lo[0], hi[0], false, false);
-  const auto r1 = __builtin_amdgcn_permlane16_swap(lo[1], hi[1], false, false);
-  return u32x4_t{r0[0], r1[0], r0[1], r1[1]};
-}
-__device__ __forceinline__ int pair_col(int g) { return (g & 1) * 16 + (g >> 1) * 8; }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float silu(float x) { return fast_silu(x); }
@@ -231,44 +221,72 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
-    if (m >= a.M) continue;
     if constexpr (EPI == EPI_H3_SWIGLU) {
       // gate/up interleaved in 16-column blocks: acc[i][2p] gate, acc[i][2p+1] up of output columns
       // nw/2 + 16p + 4g + r; silu via v_exp_f32 / v_rcp_f32 (about 1 ulp each: fp32-level, as the h3 products; the
-      // IEEE-exact expf and division were a third of this epilogue's VALU time)
-      f16_t* row = a.C + (size_t)m * a.ldc;
+      // IEEE-exact expf and division were a third of this epilogue's VALU time).  Each plane's two 4-column groups
+      // are pair-swapped (permlane16) into 8 consecutive columns per lane: one 16-byte store per plane and row
+      // group instead of two 8-byte ones - the store issue, not the arithmetic, bounded this epilogue (the h3
+      // gate/up ran 21 % faster without it).  Every lane swaps (partners share m); only the stores are guarded.
+      u32x2_t hw[2], lw[2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
-        float o[4];
+        float hi[4], lo[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float gg = acc[i][2 * p][r], uu = acc[i][2 * p + 1][r];
-          o[r] = gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * uu;
+          split2h(gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * uu * a.out_scale, hi[r], lo[r]);
         }
-        store_h3_4(row, a.N / 2, nw / 2 + p * 16 + g * 4, o, a.out_scale);
+        hw[p] = u32x2_t{pack_h2(hi[0], hi[1]), pack_h2(hi[2], hi[3])};
+        lw[p] = u32x2_t{pack_h2(lo[0], lo[1]), pack_h2(lo[2], lo[3])};
       }
-    } else {
+      const u32x4_t H = pair_swap16(hw[0], hw[1]), Lw = pair_swap16(lw[0], lw[1]);
+      if (m < a.M) {
+        f16_t* dst = a.C + (size_t)m * a.ldc + nw / 2 + pair_col(g);
+        *(u32x4_t*)dst = H;
+        *(u32x4_t*)(dst + a.N / 2) = Lw;
+      }
+      continue;
+    }
+    if constexpr (EPI == EPI_H3_BIAS_GELU) {   // same 16-byte plane stores for the column-group pairs (0,1) (2,3)
+      u32x2_t hw[4], lw[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4_t bw = *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
+        float hi[4], lo[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) split2h(gelu_erf(acc[i][j][r] + bw[r]) * a.out_scale, hi[r], lo[r]);
+        hw[j] = u32x2_t{pack_h2(hi[0], hi[1]), pack_h2(hi[2], hi[3])};
+        lw[j] = u32x2_t{pack_h2(lo[0], lo[1]), pack_h2(lo[2], lo[3])};
+      }
+#pragma unroll
+      for (int q2 = 0; q2 < 2; ++q2) {
+        const u32x4_t H = pair_swap16(hw[2 * q2], hw[2 * q2 + 1]), Lw = pair_swap16(lw[2 * q2], lw[2 * q2 + 1]);
+        if (m < a.M) {
+          f16_t* dst = a.C + (size_t)m * a.ldc + nw + q2 * 32 + pair_col(g);
+          *(u32x4_t*)dst = H;
+          *(u32x4_t*)(dst + a.N) = Lw;
+        }
+      }
+      continue;
+    }
+    if (m >= a.M) continue;
+    {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = nw + j * 16 + g * 4;
         float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID || EPI == EPI_H3_BIAS_GELU) {
+        if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID) {
           const f32x4_t bw = *(const f32x4_t*)(a.biasf + n);
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] += bw[r];
         }
-        if constexpr (EPI == EPI_H3_BIAS_GELU) {
+        if constexpr (EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID) {
+          const f32x4_t rw = *(const f32x4_t*)(a.residf + (size_t)m * a.ldr + n);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
-          store_h3_4(a.C + (size_t)m * a.ldc, a.N, n, o, a.out_scale);
-        } else {
-          if constexpr (EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID) {
-            const f32x4_t rw = *(const f32x4_t*)(a.residf + (size_t)m * a.ldr + n);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] += rw[r];
-          }
-          *(f32x4_t*)(a.Cf + (size_t)m * a.ldc + n) = f32x4_t{o[0], o[1], o[2], o[3]};
+          for (int r = 0; r < 4; ++r) o[r] += rw[r];
         }
+        *(f32x4_t*)(a.Cf + (size_t)m * a.ldc + n) = f32x4_t{o[0], o[1], o[2], o[3]};
       }
     }
   }
@@ -1865,6 +1883,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
           // one 64x64 slab at a time (row half ih, column half h), as virtual wave (2 wm + ih, 2 wn + h) of a 4x4
           // layout: its accumulators are copied to VGPRs here (the scheduler would otherwise hoist all the reads)
           const int ih = qd >> 1, h = qd & 1;
+#if EDGE_TUNING_BUILD
+          if (a.skip_epi == 1) continue;   // timing ablation: no epilogue (wrong results)
+#endif
           f32x4_t c[4][4];
           float rq[4];
 #pragma unroll
