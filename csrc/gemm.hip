@@ -235,12 +235,24 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float gg = acc[i][2 * p][r], uu = acc[i][2 * p + 1][r];
+#if EDGE_TUNING_BUILD
+          if (a.skip_epi == 5) {   // timing ablation: no transcendentals (wrong results)
+            split2h(gg * uu * a.out_scale, hi[r], lo[r]);
+            continue;
+          }
+#endif
           split2h(gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * uu * a.out_scale, hi[r], lo[r]);
         }
         hw[p] = u32x2_t{pack_h2(hi[0], hi[1]), pack_h2(hi[2], hi[3])};
         lw[p] = u32x2_t{pack_h2(lo[0], lo[1]), pack_h2(lo[2], lo[3])};
       }
       const u32x4_t H = pair_swap16(hw[0], hw[1]), Lw = pair_swap16(lw[0], lw[1]);
+#if EDGE_TUNING_BUILD
+      if (a.skip_epi == 2) {   // timing ablation: epilogue computed, not stored (wrong results)
+        if (H[0] == 0x7fff1234u) a.C[0] = 0;   // keeps the arithmetic live
+        continue;
+      }
+#endif
       if (m < a.M) {
         f16_t* dst = a.C + (size_t)m * a.ldc + nw / 2 + pair_col(g);
         *(u32x4_t*)dst = H;
@@ -1599,28 +1611,46 @@ __device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[
   static_assert(RH == 0 || RH == 32, "192-wide QKV tiles: full rotary or none");
   const int g = lane >> 4;
   const int nw = n0 + wn * 96;
+  // every global load of the epilogue (bias, the RoPE tables of all four row groups for both low-half dim groups
+  // 4g and 16 + 4g) is issued before the first store: vmcnt counts stores too, so a load waited between two
+  // groups' stores would drain them
   f32x4_t bw[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) bw[j] = *(const f32x4_t*)(a.biasf + q192_feat(nw + j * 16) + g * 4);
+  int bi[4], pi[4];
+  f32x4_t cs[4][2], sn[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = min(m0 + vw * 64 + i * 16 + (lane & 15), a.M - 1);
+    bi[i] = m / a.S;
+    pi[i] = m - bi[i] * a.S;
+    if constexpr (RH == 32) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        cs[i][hf] = *(const f32x4_t*)(a.cosT + pi[i] * 32 + hf * 16 + g * 4);
+        sn[i][hf] = *(const f32x4_t*)(a.sinT + pi[i] * 32 + hf * 16 + g * 4);
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + vw * 64 + i * 16 + (lane & 15);
     if (m >= a.M) continue;
-    const int b = m / a.S, pos = m - b * a.S;
+    const int b = bi[i], pos = pi[i];
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       const int col = nw + 32 * p;                       // block 2p: q = 0 or 2 of its head
       const int head = col >> 6;                         // wave-uniform
-      const int d = (((col >> 4) & 3) ? 16 : 0) + g * 4; // low-half dims d .. d+3, partners d+32 ..
+      const int hf = ((col >> 4) & 3) ? 1 : 0;           // low-half dims d .. d+3 (d = 16 hf + 4g), partners d+32
+      const int d = hf * 16 + g * 4;
       f32x4_t lo = c[i][2 * p] * a.alpha + bw[2 * p];
       f32x4_t hi = c[i][2 * p + 1] * a.alpha + bw[2 * p + 1];
       const bool is_v = head >= a.Hq + a.Hkv;
       if (!is_v) {
         if constexpr (RH == 32) {
-          const f32x4_t cs = *(const f32x4_t*)(a.cosT + pos * 32 + d);
-          const f32x4_t sn = *(const f32x4_t*)(a.sinT + pos * 32 + d);
-          const f32x4_t l2 = lo * cs - hi * sn;
-          hi = hi * cs + lo * sn;
+          const f32x4_t cv = hf ? cs[i][1] : cs[i][0], sv = hf ? sn[i][1] : sn[i][0];
+          const f32x4_t l2 = lo * cv - hi * sv;
+          hi = hi * cv + lo * sv;
           lo = l2;
         }
         const float sc = head < a.Hq ? a.q_scale : 1.f;
@@ -1637,6 +1667,70 @@ __device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[
         }
       }
     }
+  }
+}
+
+// fp32-output epilogue of the four-wave 256x224 kernel (O-projection / down + fp32 residual): the wave's 128 x 112
+// block in four pairs of 16-row groups, the residual (and row-scale) loads running two pairs ahead of the stores.
+// (vmcnt counts stores too: with each pair's loads issued after the previous pair's stores, every wait drained those
+// stores and the epilogue was four serial memory round trips per tile - 37 % of the O-projection's time.)
+// Reads the accumulators in place (C may alias the residual: a pair's loads are rows no earlier store wrote).
+template <int EPI>
+__device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (&acc)[8][7], int m0, int n0,
+                                                    int lane, int wm, int wn) {
+  constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID;
+  constexpr bool BIAS = EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID;
+  const int g = lane >> 4;
+  const int nw = n0 + wn * 112;
+  const int rbase = m0 + wm * 128 + (lane & 15);
+  f32x4_t bw[BIAS ? 7 : 1];
+  if constexpr (BIAS) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) bw[j] = *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
+  }
+  f32x4_t rv[2][2][RESF ? 7 : 1];
+  float rsv[2][2];
+  auto load = [&](int pr, int buf) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) {
+      const int mr = min(rbase + (2 * pr + i2) * 16, a.M - 1);
+      rsv[buf][i2] = (a.rscale ? a.rscale[mr] : 1.f) * a.alpha;
+      if constexpr (RESF) {
+        const float* rrow = a.residf + (size_t)mr * a.ldr + nw + g * 4;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) rv[buf][i2][j] = *(const f32x4_t*)(rrow + j * 16);
+      }
+    }
+  };
+  load(0, 0);
+  load(1, 1);
+#pragma unroll
+  for (int pr = 0; pr < 4; ++pr) {
+    const int buf = pr & 1;
+    f32x4_t c[2][7];
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        c[i2][j] = acc[2 * pr + i2][j];
+        asm volatile("" : "+v"(c[i2][j]));
+      }
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) {
+      const int m = rbase + (2 * pr + i2) * 16;
+      if (m < a.M) {
+        float* row = a.Cf + (size_t)m * a.ldc + nw + g * 4;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+          f32x4_t o = c[i2][j] * rsv[buf][i2];
+          if constexpr (BIAS) o += bw[j];
+          if constexpr (RESF) o += rv[buf][i2][j];
+          *(f32x4_t*)(row + j * 16) = o;
+        }
+      }
+    }
+    if (pr + 2 < 4) load(pr + 2, buf);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -1660,6 +1754,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   // strided walk: at any time the whole chip works on ~256 consecutive grouped-M tiles, so every XCD shares the same
   // 8 A panels through the Infinity Cache (the per-XCD chunked walk was 3-8 % slower on the M = 32768 shapes)
   const TileWalk walk = tile_walk(blockIdx.x, gridDim.x, ntiles, a.walk == 2 ? 1 : 0);
+
   const int tile0 = walk.first, G = walk.stride;
   if (tile0 >= walk.end) return;
   const int nk = a.K / 64;
@@ -1903,6 +1998,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       } else if constexpr (BN == 192) {
 #pragma unroll
         for (int ih = 0; ih < 2; ++ih) {   // 64 x 96 halves
+#if EDGE_TUNING_BUILD
+          if (a.skip_epi == 1) continue;   // timing ablation: no epilogue (wrong results)
+#endif
           f32x4_t c[4][6];
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -1914,9 +2012,18 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
           qkv192_epilogue<RH>(a, c, m0, n0, lane, wm * 2 + ih, wn);
           __builtin_amdgcn_sched_barrier(0);
         }
+      } else if constexpr (epi_f32(EPI)) {
+#if EDGE_TUNING_BUILD
+        if (a.skip_epi != 1)   // timing ablation: no epilogue (wrong results)
+#endif
+          w4_f32_epilogue_224<EPI>(a, acc, m0, n0, lane, wm, wn);
+        __builtin_amdgcn_sched_barrier(0);
       } else {
 #pragma unroll
         for (int ih = 0; ih < 2; ++ih) {   // 64 x 112 halves as virtual waves (2 wm + ih, wn) of the W7 layout
+#if EDGE_TUNING_BUILD
+          if (a.skip_epi == 1) continue;   // timing ablation: no epilogue (wrong results)
+#endif
           f32x4_t c[4][NJ];
 #pragma unroll
           for (int i = 0; i < 4; ++i)

@@ -83,7 +83,8 @@ def main():
             # timing ablation of the persistent 256x256 loop without its epilogue (wrong results)
             # "/m<k>": W7 epilogue memory mode k (bit 0 nt stores, bit 1 nt residual loads)
             # "/nob1": B tiles staged on even K-tiles only, "/nob": no B staging (four-wave kernel, wrong results)
-            noepi = {"/noepi": 1, "/nostore": 2, "/nob1": 3, "/nob": 4}.get("/" + spec.rpartition("/")[2], 0)
+            # "/notrans": SwiGLU h3 epilogue without its two transcendentals (four-wave kernel, wrong results)
+            noepi = {"/noepi": 1, "/nostore": 2, "/nob1": 3, "/nob": 4, "/notrans": 5}.get("/" + spec.rpartition("/")[2], 0)
             if noepi:
                 spec = spec.rpartition("/")[0]
             mode = int(spec.partition("/m")[2] or 0)
