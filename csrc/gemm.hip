@@ -143,7 +143,7 @@ __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
 // output is 4 consecutive fp32 values (one 16-byte store) or 4 consecutive values of each of the two h3 planes.
 template <int EPI, int RH, class CF>
 __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&acc)[CF::MI][4], int m0, int nw,
-                                                  int lane, int wm) {
+                                                  int lane, int wm, const float (&rs)[CF::MI]) {
   constexpr int MI = CF::MI;
   const int g = lane >> 4;
   if constexpr (EPI == EPI_F32_QKV_ROPE) {
@@ -228,23 +228,36 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
       // are pair-swapped (permlane16) into 8 consecutive columns per lane: one 16-byte store per plane and row
       // group instead of two 8-byte ones - the store issue, not the arithmetic, bounded this epilogue (the h3
       // gate/up ran 21 % faster without it).  Every lane swaps (partners share m); only the stores are guarded.
+      // The accumulators arrive unscaled (product scale f = row scale x alpha): the gate's f folds into the exp2
+      // argument and f^2 s into one output multiply, on packed-f32 pairs: o = (g u) (1 / (1 + 2^(-f log2e g))) f^2 s
+      const float f = rs[i] * a.alpha;
+      const f32x2_t c1 = {-1.4426950408889634f * f, -1.4426950408889634f * f};
+      const f32x2_t k2 = {f * f * a.out_scale, f * f * a.out_scale};
       u32x2_t hw[2], lw[2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
-        float hi[4], lo[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gg = acc[i][2 * p][r], uu = acc[i][2 * p + 1][r];
+        for (int h = 0; h < 2; ++h) {
+          const f32x2_t gg = {acc[i][2 * p][2 * h], acc[i][2 * p][2 * h + 1]};
+          const f32x2_t uu = {acc[i][2 * p + 1][2 * h], acc[i][2 * p + 1][2 * h + 1]};
+          f32x2_t o = gg * uu;
 #if EDGE_TUNING_BUILD
-          if (a.skip_epi == 5) {   // timing ablation: no transcendentals (wrong results)
-            split2h(gg * uu * a.out_scale, hi[r], lo[r]);
-            continue;
+          if (a.skip_epi != 5) {   // 5: timing ablation without the transcendentals (wrong results)
+#endif
+          const f32x2_t t = gg * c1;
+          f32x2_t e = {__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+          e = e + f32x2_t{1.f, 1.f};
+          o = o * f32x2_t{__builtin_amdgcn_rcpf(e[0]), __builtin_amdgcn_rcpf(e[1])};
+#if EDGE_TUNING_BUILD
           }
 #endif
-          split2h(gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * uu * a.out_scale, hi[r], lo[r]);
+          o = o * k2;
+          float hi0, lo0, hi1, lo1;
+          split2h(o[0], hi0, lo0);
+          split2h(o[1], hi1, lo1);
+          hw[p][h] = pack_h2(hi0, hi1);
+          lw[p][h] = pack_h2(lo0, lo1);
         }
-        hw[p] = u32x2_t{pack_h2(hi[0], hi[1]), pack_h2(hi[2], hi[3])};
-        lw[p] = u32x2_t{pack_h2(lo[0], lo[1]), pack_h2(lo[2], lo[3])};
       }
       const u32x4_t H = pair_swap16(hw[0], hw[1]), Lw = pair_swap16(lw[0], lw[1]);
 #if EDGE_TUNING_BUILD
@@ -315,13 +328,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
   if (nw >= a.N) return;        // slab beyond N in a partial last column tile (wave-uniform)
 
   if constexpr (epi_f32(EPI)) {  // h3 operands: the product's scale alpha with the optional row scale
+    if constexpr (EPI != EPI_H3_SWIGLU) {   // (the SwiGLU epilogue folds it into its constants)
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const float f = rs[i] * a.alpha;
+      for (int i = 0; i < MI; ++i) {
+        const float f = rs[i] * a.alpha;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] *= f;
+        for (int j = 0; j < 4; ++j) acc[i][j] *= f;
+      }
     }
-    if constexpr (EPI != EPI_F32_LSE) return gemm_epilogue_f32<EPI, RH, CF>(a, acc, m0, nw, lane, wm);
+    if constexpr (EPI != EPI_F32_LSE) return gemm_epilogue_f32<EPI, RH, CF>(a, acc, m0, nw, lane, wm, rs);
   } else if (a.rscale || a.ssq_in) {  // fused RMSNorm of the A operand: per-row scale (prefetched at tile start)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
