@@ -138,6 +138,107 @@ __device__ __forceinline__ bf16x8_t read_frag(const char* lds, int r, int c) {
   return *(const bf16x8_t*)(lds + r * 128 + ((c ^ swz(r)) << 4));
 }
 
+// SwiGLU h3 epilogue of one 16-row group of a 64-column slab: gate/up interleaved in 16-column blocks (acc4[2p] gate,
+// acc4[2p+1] up of output columns 16p + 4g + r) -> the 8 output columns pair_col(g) .. + 7 of the lane's row as the
+// two h3 planes H, L (16 bytes each).  silu via v_exp_f32 / v_rcp_f32 (about 1 ulp each: fp32-level, as the h3
+// products; the IEEE-exact expf and division were a third of this epilogue's VALU time).  The accumulators arrive
+// unscaled (product scale f = row scale x alpha): the gate's f folds into the exp2 argument and f^2 s into one output
+// multiply, on packed-f32 pairs: o = (g u) (1 / (1 + 2^(-f log2e g))) f^2 s.  The two 4-column groups of a plane are
+// pair-swapped (permlane16: every lane must execute it, partners share the row) into 8 consecutive columns.
+__device__ __forceinline__ void swiglu_h3_rowgroup(const GemmArgs& a, const f32x4_t (&acc4)[4], float f, u32x4_t& H,
+                                                   u32x4_t& L) {
+  const f32x2_t c1 = {-1.4426950408889634f * f, -1.4426950408889634f * f};
+  const f32x2_t k2 = {f * f * a.out_scale, f * f * a.out_scale};
+  u32x2_t hw[2], lw[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2_t gg = {acc4[2 * p][2 * h], acc4[2 * p][2 * h + 1]};
+      const f32x2_t uu = {acc4[2 * p + 1][2 * h], acc4[2 * p + 1][2 * h + 1]};
+      f32x2_t o = gg * uu;
+#if EDGE_TUNING_BUILD
+      if (a.skip_epi != 5) {   // 5: timing ablation without the transcendentals (wrong results)
+#endif
+      const f32x2_t t = gg * c1;
+      f32x2_t e = {__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+      e = e + f32x2_t{1.f, 1.f};
+      o = o * f32x2_t{__builtin_amdgcn_rcpf(e[0]), __builtin_amdgcn_rcpf(e[1])};
+#if EDGE_TUNING_BUILD
+      }
+#endif
+      o = o * k2;
+      float hi0, lo0, hi1, lo1;
+      split2h(o[0], hi0, lo0);
+      split2h(o[1], hi1, lo1);
+      hw[p][h] = pack_h2(hi0, hi1);
+      lw[p][h] = pack_h2(lo0, lo1);
+    }
+  }
+  H = pair_swap16(hw[0], hw[1]);
+  L = pair_swap16(lw[0], lw[1]);
+}
+
+// Exchange of two 16-byte chunks between lanes r and r ^ 8 of each 16-lane row (DPP row_ror:8): lanes r < 8 keep X
+// and get the X of lane r + 8 in B; lanes r >= 8 get the Y of lane r - 8 in A and keep Y in B.  For X / Y = the
+// chunks of row r in the left / right 64-byte half of a 128-byte line, A then holds rows 0-7 and B rows 8-15 of the
+// 16-row group as full lines (8 lanes per row).
+__device__ __forceinline__ void line_exchange8(const u32x4_t& X, const u32x4_t& Y, bool lo8, u32x4_t& A, u32x4_t& B) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t t = lo8 ? Y[d] : X[d];
+    const uint32_t u = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x128, 0xF, 0xF, false);   // row_ror:8
+    A[d] = lo8 ? X[d] : u;
+    B[d] = lo8 ? u : Y[d];
+  }
+}
+
+// SwiGLU h3 epilogue of the four-wave 256x256 kernel with full-line stores: the wave's 128 accumulator columns are 64
+// output columns = one 128-byte line per plane and row, written 8 rows x 128 bytes per store instruction (the two
+// 64-column slabs of a row group exchanged between lanes r and r ^ 8) instead of 16 rows x 64 bytes - half the
+// store cost of the per-slab layout (ablation: 1 KiB-contiguous stores, profiles/r02k_gemm_epilogue_ablations.log).
+template <int MI8>
+__device__ __forceinline__ void swiglu_h3_lines_4w(const GemmArgs& a, f32x4_t (&acc)[MI8][8], const float (&rs)[MI8],
+                                                   int m0, int n0, int lane, int wm, int wn) {
+  const int r = lane & 15, g = lane >> 4;
+  const bool lo8 = r < 8;
+  const int col = n0 / 2 + wn * 64 + (lo8 ? 0 : 32) + pair_col(g);   // output column of the lane's chunk in A and B
+  f16_t* const base = a.C + col;
+#pragma unroll
+  for (int i = 0; i < MI8; ++i) {
+    f32x4_t c0[4], c1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c0[j] = acc[i][j];
+      c1[j] = acc[i][4 + j];
+      asm volatile("" : "+v"(c0[j]), "+v"(c1[j]));
+    }
+    const float f = rs[i] * a.alpha;
+    u32x4_t H0, L0, H1, L1;
+    swiglu_h3_rowgroup(a, c0, f, H0, L0);
+    swiglu_h3_rowgroup(a, c1, f, H1, L1);
+    u32x4_t HA, HB, LA, LB;
+    line_exchange8(H0, H1, lo8, HA, HB);
+    line_exchange8(L0, L1, lo8, LA, LB);
+    const int ma = m0 + wm * 128 + i * 16 + (r & 7), mb = ma + 8;
+#if EDGE_TUNING_BUILD
+    if (a.skip_epi == 2) {   // timing ablation: epilogue computed, not stored (wrong results)
+      if (HA[0] == 0x7fff1234u || HB[0] == 0x7fff1234u || LA[0] == LB[1]) a.C[0] = 0;
+      continue;
+    }
+#endif
+    if (ma < a.M) {
+      *(u32x4_t*)(base + (size_t)ma * a.ldc) = HA;
+      *(u32x4_t*)(base + (size_t)ma * a.ldc + a.N / 2) = LA;
+    }
+    if (mb < a.M) {
+      *(u32x4_t*)(base + (size_t)mb * a.ldc) = HB;
+      *(u32x4_t*)(base + (size_t)mb * a.ldc + a.N / 2) = LB;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // ---- fp32-execution epilogues (EPI >= EPI_F32).  Same ownership as gemm_epilogue below: lane owns rows
 // m0 + wm*WTM + i*16 + (lane&15) and columns nw + j*16 + 4*(lane>>4) + r of the wave's 64-column slab, so every
 // output is 4 consecutive fp32 values (one 16-byte store) or 4 consecutive values of each of the two h3 planes.
@@ -222,44 +323,8 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
     if constexpr (EPI == EPI_H3_SWIGLU) {
-      // gate/up interleaved in 16-column blocks: acc[i][2p] gate, acc[i][2p+1] up of output columns
-      // nw/2 + 16p + 4g + r; silu via v_exp_f32 / v_rcp_f32 (about 1 ulp each: fp32-level, as the h3 products; the
-      // IEEE-exact expf and division were a third of this epilogue's VALU time).  Each plane's two 4-column groups
-      // are pair-swapped (permlane16) into 8 consecutive columns per lane: one 16-byte store per plane and row
-      // group instead of two 8-byte ones - the store issue, not the arithmetic, bounded this epilogue (the h3
-      // gate/up ran 21 % faster without it).  Every lane swaps (partners share m); only the stores are guarded.
-      // The accumulators arrive unscaled (product scale f = row scale x alpha): the gate's f folds into the exp2
-      // argument and f^2 s into one output multiply, on packed-f32 pairs: o = (g u) (1 / (1 + 2^(-f log2e g))) f^2 s
-      const float f = rs[i] * a.alpha;
-      const f32x2_t c1 = {-1.4426950408889634f * f, -1.4426950408889634f * f};
-      const f32x2_t k2 = {f * f * a.out_scale, f * f * a.out_scale};
-      u32x2_t hw[2], lw[2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f32x2_t gg = {acc[i][2 * p][2 * h], acc[i][2 * p][2 * h + 1]};
-          const f32x2_t uu = {acc[i][2 * p + 1][2 * h], acc[i][2 * p + 1][2 * h + 1]};
-          f32x2_t o = gg * uu;
-#if EDGE_TUNING_BUILD
-          if (a.skip_epi != 5) {   // 5: timing ablation without the transcendentals (wrong results)
-#endif
-          const f32x2_t t = gg * c1;
-          f32x2_t e = {__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
-          e = e + f32x2_t{1.f, 1.f};
-          o = o * f32x2_t{__builtin_amdgcn_rcpf(e[0]), __builtin_amdgcn_rcpf(e[1])};
-#if EDGE_TUNING_BUILD
-          }
-#endif
-          o = o * k2;
-          float hi0, lo0, hi1, lo1;
-          split2h(o[0], hi0, lo0);
-          split2h(o[1], hi1, lo1);
-          hw[p][h] = pack_h2(hi0, hi1);
-          lw[p][h] = pack_h2(lo0, lo1);
-        }
-      }
-      const u32x4_t H = pair_swap16(hw[0], hw[1]), Lw = pair_swap16(lw[0], lw[1]);
+      u32x4_t H, Lw;
+      swiglu_h3_rowgroup(a, acc[i], rs[i] * a.alpha, H, Lw);
 #if EDGE_TUNING_BUILD
       if (a.skip_epi == 2) {   // timing ablation: epilogue computed, not stored (wrong results)
         if (H[0] == 0x7fff1234u) a.C[0] = 0;   // keeps the arithmetic live
@@ -1987,7 +2052,13 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       // all MFMAs of the tile were issued; the epilogue reads the accumulators after they drain
       MFMA_DRAIN();
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (BN == 256) {
+      if constexpr (BN == 256 && EPI == EPI_H3_SWIGLU) {
+#if EDGE_TUNING_BUILD
+        if (a.skip_epi != 1)   // timing ablation: no epilogue (wrong results)
+#endif
+          swiglu_h3_lines_4w<8>(a, acc, rs, m0, n0, lane, wm, wn);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (BN == 256) {
 #pragma unroll
         for (int qd = 0; qd < 4; ++qd) {
           // one 64x64 slab at a time (row half ih, column half h), as virtual wave (2 wm + ih, 2 wn + h) of a 4x4
