@@ -23,7 +23,7 @@ import time
 import torch
 
 from .. import codec as C
-from ..config import Params, dump_json, resolve_device, resolve_dtype
+from ..config import Params, dump_json, resolve_device, resolve_dtype, resolve_window_batch
 from ..importance import canonical, load_head_weights
 from ..models import build_model, get_config
 from ..parallel.dist import all_reduce_sum, get_env, init_distributed
@@ -40,6 +40,7 @@ def _setup(p: Params, default_model: str):
     env = init_distributed(p.device)
     device = str(env.device) if env.device.type == "cuda" else resolve_device(p)
     dtype = resolve_dtype(p, device)
+    resolve_window_batch(p, device)
     cfg = get_config(p.model or default_model)
     model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed)
     ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed,
@@ -233,6 +234,7 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
     env = init_distributed(p.device)
     device = str(env.device) if env.device.type == "cuda" else resolve_device(p)
     dtype = resolve_dtype(p, device)
+    resolve_window_batch(p, device)
     cfg = get_config(p.model or default_model)
     max_len = p.max_length or cfg.max_position
     pp = len(p.split_layers) + 1 if p.split_layers else p.num_stages

@@ -229,6 +229,8 @@ def relevance_main(p) -> list:
     # (head_relevance_batched); dtype "bf16" on the GPU runs the explicit-backward HIP engine (csrc/lrp.hip, ~10x
     # faster, bf16 storage: head table within ~10 % of the fp32 one, tests/test_lrp_gpu.py)
     dtype = resolve_dtype(p, device) if p.dtype != "auto" else torch.float32
+    if p.window_batch <= 0:   # auto: 8 windows per relevance batch (forward + AttnLRP backward)
+        p.window_batch = 8
     fast = device.startswith("cuda") and dtype == torch.bfloat16
     model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed)
     ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed,

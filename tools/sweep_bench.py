@@ -27,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="qwen2-0.5b")
     ap.add_argument("--windows", type=int, default=256)
-    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--warmup-batches", type=int, default=2)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
