@@ -293,8 +293,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
                                                                   int Hkv, int S, int s_pad, float h3s, float sq,
                                                                   float sk, float sv) {
   constexpr int NPL = F16 ? 2 : 3;
-  constexpr float SP = F16 ? 128.f : 1.f;   // probability scale 2^(15 - FTAU) of the fp16 planes
-  static_assert(FTAU == 8.f, "SP assumes p <= 2^8");
+  // probability scale 2^(15 - FTAU) of the fp16 planes, applied in the exp2 argument (the row sum l_run and the
+  // probabilities carry it; the normalisation and the LSE take it out)
+  constexpr float LSP = F16 ? 7.f : 0.f;
+  static_assert(FTAU == 8.f, "LSP assumes p <= 2^8");
   extern __shared__ __attribute__((aligned(16))) char smem[];   // K planes (NPL x 8 KiB), V^T planes (NPL x 8 KiB)
   if constexpr (!F16) sq = sk = sv = 1.f;
   const float sc_log2 = FLOG2E / (sq * sk);   // score scale (natural log -> log2) of the scaled products
@@ -441,7 +443,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(fmaf(st[kt][r], sc_log2, -m2));
+        const float pv = exp2f(fmaf(st[kt][r], sc_log2, LSP - m2));
         st[kt][r] = pv;
         ps += pv;
       }
@@ -453,7 +455,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
 #pragma unroll
       for (int r = 0; r < 4; ++r) { pv8[r] = st[2 * sk][r]; pv8[4 + r] = st[2 * sk + 1][r]; }
       bf16x8_t pp[NPL];
-      split_planes<F16>(pv8, SP, pp);
+      split_planes<F16>(pv8, 1.f, pp);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int row = dt * 16 + ql;
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
 
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
-  const float inv = 1.f / (l_run * (SP * sv));
+  const float inv = 1.f / (l_run * sv);
   const int W = Hq * 64;
   u32x4_t oh[2], ol[2];
   if constexpr (H3OUT) {
@@ -501,7 +503,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(orow + dt * 16 + 4 * g) = oacc[dt] * inv;
     }
-    if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = m2 * 0.6931471805599453f + logf(l_run);
+    if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = (m2 - LSP) * 0.6931471805599453f + logf(l_run);
   }
 }
 
