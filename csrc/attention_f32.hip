@@ -256,14 +256,19 @@ __device__ __forceinline__ f32x4_t h3_dot(const bf16x8_t (&a)[2], const bf16x8_t
   c = mfma_h(a[0], b[1], c);
   return mfma_h(a[0], b[0], c);
 }
+// on value pairs: v_cvt_pk_f16_f32 for both planes, the residual on packed f32 (the same RNE splits as split2h)
 __device__ __forceinline__ void split_frag_h(const float (&v)[8], float s, bf16x8_t& hi, bf16x8_t& lo) {
-  float h[8], l[8];
+  u32x4_t H, L;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) split2h(v[e] * s, h[e], l[e]);
-  hi = __builtin_bit_cast(bf16x8_t, u32x4_t{pack_h2(h[0], h[1]), pack_h2(h[2], h[3]), pack_h2(h[4], h[5]),
-                                            pack_h2(h[6], h[7])});
-  lo = __builtin_bit_cast(bf16x8_t, u32x4_t{pack_h2(l[0], l[1]), pack_h2(l[2], l[3]), pack_h2(l[4], l[5]),
-                                            pack_h2(l[6], l[7])});
+  for (int e = 0; e < 4; ++e) {
+    const f32x2_t x = f32x2_t{v[2 * e], v[2 * e + 1]} * f32x2_t{s, s};
+    const f16x2_t h = __builtin_convertvector(x, f16x2_t);
+    const f32x2_t r = x - __builtin_convertvector(h, f32x2_t);
+    H[e] = __builtin_bit_cast(uint32_t, h);
+    L[e] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2_t));
+  }
+  hi = __builtin_bit_cast(bf16x8_t, H);
+  lo = __builtin_bit_cast(bf16x8_t, L);
 }
 // NPL planes of 8 values: three bf16 planes (x6) or two scaled fp16 planes (h3)
 template <bool F16>
@@ -300,7 +305,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
   extern __shared__ __attribute__((aligned(16))) char smem[];   // K planes (NPL x 8 KiB), V^T planes (NPL x 8 KiB)
   if constexpr (!F16) sq = sk = sv = 1.f;
   const float sc_log2 = FLOG2E / (sq * sk);   // score scale (natural log -> log2) of the scaled products
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
+  // wave index in an SGPR: q0, kmax and the diagonal-tile test are wave-uniform scalars (scalar branches; with a VGPR
+  // wave index the compiler if-converted the causal mask into every key tile)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            ql = lane & 15;
   constexpr int QB = 16 * NW;          // query rows per workgroup
   const int nqb = (S + QB - 1) / QB;
   const int G = Hq / Hkv, NG = B * Hkv;
@@ -413,14 +421,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
         st[kt] = plane_dot<F16>(kf, qp[ks], st[kt]);
       }
     }
-    if (kb * 64 + 63 > q0 || kb * 64 + 63 >= S) {   // causal / sequence-end mask (wave-uniform branch)
+    if (__builtin_expect(kb * 64 + 63 > q0 || kb * 64 + 63 >= S, 0)) {   // causal / sequence-end mask (scalar branch)
+      // key kb 64 + 16 kt + 4 g + r is masked when 16 kt + r exceeds the lane's limit (one compare per value)
+      const int lim = min(qrow, S - 1) - kb * 64 - 4 * g;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kb * 64 + kt * 16 + 4 * g + r;
-          if (key > qrow || key >= S) st[kt][r] = -INFINITY;
-        }
+        for (int r = 0; r < 4; ++r)
+          if (kt * 16 + r > lim) st[kt][r] = -INFINITY;
     }
     float mloc = -INFINITY;
 #pragma unroll
@@ -432,7 +440,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     const float mc = mloc * sc_log2;
     if (__builtin_amdgcn_ballot_w64(mc > m2 + FTAU)) {  // wave-uniform lazy rescale
       const float mn = fmaxf(m2, mc);
-      const float alpha = exp2f(m2 - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m2 - mn);   // v_exp_f32 (m2 = -inf -> 0)
       m2 = mn;
       l_run *= alpha;
 #pragma unroll
@@ -443,7 +451,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(fmaf(st[kt][r], sc_log2, LSP - m2));
+        // v_exp_f32 without exp2f's denormal range reduction: p < 2^-126 of the row max does not matter
+        const float pv = __builtin_amdgcn_exp2f(fmaf(st[kt][r], sc_log2, LSP - m2));
         st[kt][r] = pv;
         ps += pv;
       }
