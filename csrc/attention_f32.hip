@@ -435,8 +435,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[kt][r]);
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    mloc = xor_max32(xor_max16(mloc));
     const float mc = mloc * sc_log2;
     if (__builtin_amdgcn_ballot_w64(mc > m2 + FTAU)) {  // wave-uniform lazy rescale
       const float mn = fmaxf(m2, mc);

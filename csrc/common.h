@@ -96,6 +96,16 @@ __device__ __forceinline__ u32x4_t pair_swap16(u32x2_t lo, u32x2_t hi) {
   return u32x4_t{r0[0], r1[0], r0[1], r1[1]};
 }
 __device__ __forceinline__ int pair_col(int g) { return (g & 1) * 16 + (g >> 1) * 8; }
+// max over lanes l, l ^ 16 and l ^ 32 without LDS: v_permlane16_swap / v_permlane32_swap of a value with itself give
+// every lane the pair (x_l, x_partner) in some order (a __shfl_xor is a ds_bpermute plus index arithmetic)
+__device__ __forceinline__ float xor_max16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor_max32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 
 // silu(x) = x / (1 + e^-x) on the hardware transcendentals (v_exp_f32, v_rcp_f32, ~1 ulp): a plain '/' compiles
 // to the IEEE division sequence (2 v_div_scale + v_div_fmas + v_div_fixup + v_rcp + FMAs), which made the
