@@ -122,6 +122,18 @@ def test_linear_h3_two_term(M, N, K, epi):
     test_linear_h3_fp32_accuracy(M, N, K, epi, two_term=True)
 
 
+@pytest.mark.parametrize("M", [1000, 257])
+@pytest.mark.parametrize("two_term", [False, True])
+def test_linear_h3_swiglu_partial_tiles(M, two_term):
+    """SwiGLU h3 epilogue of the four-wave 256x256 kernel (full-line stores: rows r and r ^ 8 of a 16-row group
+    exchange chunks) forced at M not a multiple of 256: the guarded rows of the partial last tile."""
+    ops.set_gemm_tile(256)
+    try:
+        test_linear_h3_fp32_accuracy(M, 9728, 896, "swiglu", two_term=two_term)
+    finally:
+        ops.set_gemm_tile(0)
+
+
 @pytest.mark.parametrize("slack", [8, 14])
 def test_linear_h3_loose_scale(slack):
     """Scales 2^8 / 2^14 below the data's own (the model's bounds are loose): still fp32-level."""
