@@ -381,12 +381,17 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
       const int key = scol + 4 * a4;
       const int sblk = key >> 5, hf = (key >> 4) & 1, a = (key >> 2) & 3;
       const int off = srow * 128 + (((4 * sblk + a) ^ xsw(srow)) << 4) + hf * 8;
-      if constexpr (F16) {
-        float p0[4], p1[4];
+      if constexpr (F16) {   // value pairs: v_cvt_pk_f16_f32 for both planes, the residual on packed f32
+        u32x2_t H, L;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) split2h(vreg[a4][e] * sv, p0[e], p1[e]);
-        *(u32x2_t*)(lv + 0 * XPL + off) = u32x2_t{pack_h2(p0[0], p0[1]), pack_h2(p0[2], p0[3])};
-        *(u32x2_t*)(lv + 1 * XPL + off) = u32x2_t{pack_h2(p1[0], p1[1]), pack_h2(p1[2], p1[3])};
+        for (int e = 0; e < 2; ++e) {
+          const f32x2_t x = f32x2_t{vreg[a4][2 * e], vreg[a4][2 * e + 1]} * f32x2_t{sv, sv};
+          const f16x2_t h = __builtin_convertvector(x, f16x2_t);
+          H[e] = __builtin_bit_cast(uint32_t, h);
+          L[e] = __builtin_bit_cast(uint32_t, __builtin_convertvector(x - __builtin_convertvector(h, f32x2_t), f16x2_t));
+        }
+        *(u32x2_t*)(lv + 0 * XPL + off) = H;
+        *(u32x2_t*)(lv + 1 * XPL + off) = L;
       } else {
         float p0[4], p1[4], p2[4];
 #pragma unroll
