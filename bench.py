@@ -13,6 +13,11 @@ N GPUs -> pp stages x dp = N/pp replicas, one process per GPU (``--pp`` 2 by def
 split after layer ``--split``; ``--pp 4`` / ``--pp 8`` are BASELINE configs 4-5, cost-balanced stages).  N = 1 runs
 the same stages in one process on the one GPU (the boundary is still encoded and decoded).
 
+Launch: under ``torch.distributed.run`` the ranks come from the env (``--gpus`` must equal WORLD_SIZE, or the run
+stops).  ``python bench.py --gpus N`` with N > 1 and no launcher env starts the N ranks itself: this process runs
+``torch.distributed.run --nproc-per-node N`` as a child before it makes any GPU call, and exits with its code.  The
+JSON line records the world size, the process-group backend and every rank's device.
+
 Precision: ``--dtype fp32`` (default) is the reference's precision (it loads its models without a torch_dtype,
 ``Experiments/Qwen2-0.5B/qwen_layer_wise.py:17``): fp32 residual stream, norms, softmax, attention (split-bf16
 matrix-core products) and codec, GEMMs on h3 split-fp16 operands (fp32-accurate, see ``ops.reference.h3_act``).
@@ -91,6 +96,61 @@ def parse():
     return p.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_mode(a) -> str:
+    """"torchrun" (rank env present), "self" (--gpus N > 1 without it: spawn the ranks) or "single".
+
+    Called before any GPU call: ``torch.cuda.device_count()`` does not initialise the HIP runtime."""
+    if "WORLD_SIZE" in os.environ and "RANK" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks; "
+                             f"refusing to report a run of a different size")
+        return "torchrun" if world > 1 else "single"
+    if a.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {a.gpus})")
+    if a.gpus == 1:
+        return "single"
+    ndev = torch.cuda.device_count()
+    shared = os.environ.get("EDGE_SHARED_GPU", "0") not in ("", "0")
+    if 0 < ndev < a.gpus and not shared:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but only {ndev} GPU(s) are visible")
+    return "self"
+
+
+def self_launch(a) -> int:
+    """Run this script as ``a.gpus`` ranks under torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1) and return the launcher's exit code.  Rank 0 prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, EDGE_BENCH_LAUNCH="self")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC (RCCL peer mappings on this host driver)
+    return subprocess.call(cmd, env=env)
+
+
+def rank_devices(env) -> list:
+    """[{rank, local_rank, device, pci}] of every rank (collective)."""
+    me = {"rank": env.rank, "local_rank": env.local_rank, "device": str(env.device)}
+    if env.device.type == "cuda":
+        pr = torch.cuda.get_device_properties(env.device)
+        me["pci"] = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+        me["name"] = pr.gcnArchName
+    if not env.is_dist:
+        return [me]
+    out = [None] * env.world_size
+    torch.distributed.all_gather_object(out, me)
+    return out
+
+
 def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None):
     """Build the model/pipeline for ``dtype`` (random weights with ``values`` precision) and time ``timed_steps``
     steps after ``warmup``.  Returns a dict."""
@@ -165,6 +225,8 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
         gathered = [None] * world
         torch.distributed.all_gather_object(gathered, reports[-1] if reports else {})
         stage_reports = [dict(r, rank=i) for i, r in enumerate(gathered)]
+    if dist_pp:
+        runner.close()
     del runner, model
     gc.collect()
     if dev.type == "cuda":
@@ -174,7 +236,11 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
 
 def main():
     a = parse()
+    mode = launch_mode(a)
+    if mode == "self":
+        sys.exit(self_launch(a))
     env = init_distributed("auto")
+    devices = rank_devices(env)
     cfg = get_config(a.model)
     world = env.world_size
     pp = a.pp
@@ -223,6 +289,8 @@ def main():
         "wire_bits_per_element": [round(8 * w / cfg.hidden_size, 3) for w in wires],
         "wire_compression_vs_fp32_reference": [round(4 * cfg.hidden_size / w, 3) for w in wires],
         "ppl_random_weights": main_run["ppl"], "weights": main_run["prov"],
+        "world_size": world, "backend": env.backend,
+        "launch": os.environ.get("EDGE_BENCH_LAUNCH", mode), "rank_devices": devices,
     }
     if main_run["stages"]:
         out["stages"] = main_run["stages"]

@@ -1,15 +1,17 @@
 // Native RCCL point-to-point transport for pipeline-stage boundaries.
 //
 // The boundary message is one contiguous byte buffer, so a stage hand-off is a single ncclSend /
-// ncclRecv pair over xGMI.  This layer owns its own communicator (bootstrapped from a unique id the
-// Python side distributes through the torch.distributed store) and a dedicated, non-blocking comm
-// stream per communicator; ordering with the compute stream is expressed with HIP events only:
+// ncclRecv pair over xGMI.  A handle here is one *channel*: a communicator (for a pipeline edge: the
+// two ranks of the edge, bootstrapped from a unique id the Python side hands over through the
+// torch.distributed store) plus its own non-blocking stream.  A middle stage therefore owns two
+// channels - the receive edge from its upstream and the send edge to its downstream - on two
+// streams, so a receive posted ahead for the next micro-batch never sits in front of the send of the
+// current one.  Ordering with the compute stream is expressed with HIP events only:
 //
-//   send: compute stream --event--> comm stream: ncclSend
-//   recv: comm stream: ncclRecv --event--> compute stream (waits before the decode kernel)
+//   send: compute stream --event--> channel stream: ncclSend --event (per op, Python side)--> waiter
+//   recv: channel stream: ncclRecv --event (per op)--> compute stream (waits before the decode kernel)
 //
-// so neither stream ever blocks the host, and a receive can be posted ahead of the compute that
-// will consume it (the pipeline prefetches the next micro-batch's boundary while computing).
+// so no stream ever blocks the host.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>

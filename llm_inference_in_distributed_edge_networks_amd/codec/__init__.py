@@ -22,7 +22,18 @@ mixed_int2_int8        int8            int2 ternary    per token    extra compre
 channel_8 / channel_4  int8 / int4     --              per channel  Q5
 channel_1_mean/_max    int2 ternary    --              per channel  Q6
 int8_token_keep        native dtype    int8            per token    Q2/Q4 (Pythia 'initial', intended semantics)
+mxfp4 / mxfp8          MXFP4 / MXFP8   --              E8M0 / 32ch  OCP microscaling, every token (gfx950
+                                                                    scaled converts)
+mixed_mxfp4_mxfp8      MXFP8 (E4M3)    MXFP4 (E2M1)    E8M0 / 32ch  configs 3-5 at microscaling widths
+mxfp4_keep             native dtype    MXFP4           E8M0 / 32ch  Q1 with MX blocks instead of one scale
+rgroup                 head groups     --              per group    every 64-channel group (one head) its
+                                                                    own max-abs scale and 2/4/8-bit width
+mixed_rgroup_int8      int8            head groups     token/group  config 5 (relevance-allocated widths
+                                                                    from channel_group_relevance.json)
 =====================  ==============  ==============  ===========  ==================================
+
+Head-group codecs carry their group bit plan in the message; a boundary's plan comes from
+``wire.allocate_group_bits`` over the LRP relevance of its 64-channel groups (uniform without a table).
 
 "hi"/"lo" classes: the ``k = int(ratio * S)`` least important tokens of a
 window (ascending importance, ties broken by position) are the lo class.

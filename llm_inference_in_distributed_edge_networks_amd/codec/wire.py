@@ -638,10 +638,13 @@ def encode(x: torch.Tensor, spec: CodecSpec, B: int, S: int, ratio: float = 0.0,
     ``1 - ratio`` and quantizes the rest (per-window k, variable-k message)."""
     H = x.shape[-1]
     if uses_kvar(spec, selection):
-        if importance is None:
-            raise ValueError("top-rho selection needs token importance")
-        L = layout(spec, B, S, H, -1, x.dtype, kvar=True)
         mass = 1.0 - float(ratio)
+        if importance is None:
+            if mass > 0:
+                raise ValueError("top-rho selection needs token importance")
+            # ratio >= 1: keep mass <= 0 keeps nothing for any importance (every window all lo, k = S)
+            importance = torch.zeros(B, S, dtype=torch.float32, device=x.device)
+        L = layout(spec, B, S, H, -1, x.dtype, kvar=True)
         if x.is_cuda:
             if out is None:
                 out = torch.zeros(L.total, dtype=torch.uint8, device=x.device)

@@ -63,6 +63,7 @@ def _shard(batch_iter, env):
 
 def _reduce(engine: SweepEngine):
     env = get_env()
+    engine._flush()
     if not env.is_dist:
         return
     dev = env.device if env.backend == "nccl" else torch.device("cpu")
@@ -90,7 +91,8 @@ def importance_sweep(p: Params, default_model: str, out_name: str) -> dict:
             raise FileNotFoundError("weighted_importance needs attention_head_weights.json "
                                     "(run Experiments/Relevance/main.py or set params['head_weights'])")
     rows = [SweepMethod(m, m, selection=p.selection) for m in methods]
-    sc = SweepConfig(rows, p.layers_of_interest, p.ratios, p.codec, hw)
+    sc = SweepConfig(rows, p.layers_of_interest, p.ratios, p.codec, hw, group_relevance=_group_relevance(p),
+                     group_avg_bits=p.group_avg_bits)
     eng = SweepEngine(model, sc)
     state = _state(p, env, out_name)
     pb = progress_bar(len(wins), env.is_main)
@@ -195,6 +197,21 @@ def initial_experiment(p: Params) -> dict:
     return out
 
 
+def _group_relevance(p: Params):
+    """Channel-group relevance table [layers][H / 64] for the head-group codecs (None: uniform plans), loaded the
+    same way by the sweep and the pipeline drivers so both quantize a boundary identically."""
+    if not C.wire.needs_plan(C.get_codec(p.codec)):
+        return None
+    path = p.group_relevance or _default_group_relevance()
+    if p.group_relevance and not os.path.exists(path):
+        raise FileNotFoundError(f"group_relevance {path} not found (run Experiments/Relevance/main.py)")
+    if path and os.path.exists(path):
+        with open(path) as f:
+            return torch.tensor(json.load(f), dtype=torch.float32)
+    log("head-group codec without channel_group_relevance.json: every group gets the same width")
+    return None
+
+
 def _default_group_relevance() -> str | None:
     for c in ("channel_group_relevance.json", "../Relevance/channel_group_relevance.json",
               os.path.join(os.path.dirname(__file__), "..", "..", "Experiments", "Relevance",
@@ -263,47 +280,70 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
             raise FileNotFoundError("weighted_importance needs attention_head_weights.json "
                                     "(run Experiments/Relevance/main.py or set params['head_weights'])")
         hw = load_head_weights(path)
-    grel = None
-    if C.wire.needs_plan(C.get_codec(p.codec)):
-        path = p.group_relevance or _default_group_relevance()
-        if p.group_relevance and not os.path.exists(path):
-            raise FileNotFoundError(f"group_relevance {path} not found (run Experiments/Relevance/main.py)")
-        if path and os.path.exists(path):
-            with open(path) as f:
-                grel = torch.tensor(json.load(f), dtype=torch.float32)
-        else:
-            log("head-group codec without channel_group_relevance.json: every group gets the same width")
+    grel = _group_relevance(p)
     log(f"pipeline: model={cfg.name} weights={prov} data={data_prov} stages={plan.num_stages} "
         f"boundaries={plan.boundary_layers()} world={env.world_size} codec={p.codec} windows={len(wins)}")
     results: dict = {}
+    state = SweepState(os.path.join(p.output_dir, f"pipeline_results.rank{env.rank}.ckpt.json"), p.config_hash(),
+                       enabled=p.resume, shard=(env.rank, env.world_size, f"pipeline/{p.window_batch}"))
+    saved = state.load() or {}
+    results.update(saved.get("results", {}))
+    bl = list(batches(ids, wins, p.window_batch))
+    toks = sum(w.end - w.begin for w in wins)
+    runner = None
+    # windows per resumable chunk (the reference dumps its running sums every 1000 windows, main.py:184-192)
+    chunk = max(1, p.checkpoint_every // max(1, p.window_batch))
     for m in methods:
         for r in p.ratios:
+            if str(r) in results.get(m, {}):
+                log(f"{m} ratio={r}: resumed from checkpoint")
+                continue
             bcfg = BoundaryConfig(p.codec, float(r), m, hw, selection=p.selection, group_relevance=grel,
                                   group_avg_bits=p.group_avg_bits)
-            bl = list(batches(ids, wins, p.window_batch))
-            t0 = time.perf_counter()
-            if distributed:
-                runner = DistributedPipeline(model, plan, bcfg, grid, env.rank)
-                acc, info = runner.evaluate(bl)
-                wire = torch.tensor([info["wire_bytes_per_token"] if stage < pp - 1 else 0.0], dtype=torch.float64,
-                                    device=env.device if env.backend == "nccl" else "cpu")
-                all_reduce_sum(wire)
-                wire_pt = float(wire) / (grid.dp * max(1, pp - 1))
+            # one runtime for the whole sweep: the transport (RCCL channels / IPC slot rings) is set up once, only
+            # the boundary codec changes between (method, ratio)
+            if runner is None:
+                runner = (DistributedPipeline(model, plan, bcfg, grid, env.rank) if distributed
+                          else LocalPipeline(model, plan, bcfg))
             else:
-                runner = LocalPipeline(model, plan, bcfg)
-                acc = runner.evaluate(bl)
-                wb = runner.wire_bytes_per_token()
-                wire_pt = sum(wb) / len(wb) if wb else 0.0
-            if device.startswith("cuda"):
-                torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            toks = sum(w.end - w.begin for w in wins)
-            results.setdefault(m, {})[str(r)] = {"ppl": acc.ppl(), "total_nll": acc.total_nll,
-                                                 "n_tokens": acc.n_tokens, "wire_bytes_per_token": wire_pt,
-                                                 "tokens_per_s": toks / max(dt, 1e-9), "seconds": dt}
+                runner.set_boundary(bcfg)
+            part = saved.get("partial") if saved.get("partial", {}).get("key") == [m, str(r)] else None
+            tot, ntok, sec = (part["total_nll"], part["n_tokens"], part["seconds"]) if part else (0.0, 0.0, 0.0)
+            wsum, wcnt = (part["wire_sum"], part["wire_n"]) if part else (0.0, 0)
+            start = part["next_batch"] if part else 0
+            for c0 in range(start, len(bl), chunk):
+                t0 = time.perf_counter()
+                piece = bl[c0:c0 + chunk]
+                if distributed:
+                    acc, info = runner.evaluate(piece)
+                    wire = torch.tensor([info["wire_bytes_per_token"] if stage < pp - 1 else 0.0],
+                                        dtype=torch.float64, device=env.device if env.backend == "nccl" else "cpu")
+                    all_reduce_sum(wire)
+                    wire_pt = float(wire) / (grid.dp * max(1, pp - 1))
+                else:
+                    acc = runner.evaluate(piece)
+                    wb = runner.wire_bytes_per_token()
+                    wire_pt = sum(wb) / len(wb) if wb else 0.0
+                if device.startswith("cuda"):
+                    torch.cuda.synchronize()
+                sec += time.perf_counter() - t0
+                tot += acc.total_nll
+                ntok += acc.n_tokens
+                wsum, wcnt = wire_pt, 1          # the stage byte counters are cumulative over the run
+                if c0 + chunk < len(bl):
+                    state.save({"results": results, "partial": {
+                        "key": [m, str(r)], "next_batch": c0 + chunk, "total_nll": tot, "n_tokens": ntok,
+                        "seconds": sec, "wire_sum": wsum, "wire_n": wcnt}})
+            ppl = math.exp(tot / ntok) if ntok else float("nan")
+            results.setdefault(m, {})[str(r)] = {"ppl": ppl, "total_nll": tot, "n_tokens": ntok,
+                                                 "wire_bytes_per_token": wsum / max(1, wcnt),
+                                                 "tokens_per_s": toks / max(sec, 1e-9), "seconds": sec}
+            state.save({"results": results})
             if env.is_main:
-                log(f"{m:20s} ratio={r:<5} ppl={acc.ppl():.4f} wire={wire_pt:.1f} B/token "
-                    f"({toks / max(dt, 1e-9):,.0f} tok/s)")
+                log(f"{m:20s} ratio={r:<5} ppl={ppl:.4f} wire={wsum / max(1, wcnt):.1f} B/token "
+                    f"({toks / max(sec, 1e-9):,.0f} tok/s)")
+    if runner is not None and distributed:
+        runner.close()
     out = {"results": results, "stages": plan.num_stages, "boundaries": plan.boundary_layers(),
            "stage_layers": [list(plan.stage_layers(s)) for s in range(plan.num_stages)], "codec": p.codec,
            "world_size": env.world_size, "weights": prov, "data": data_prov, "device": device, "dtype": str(dtype),

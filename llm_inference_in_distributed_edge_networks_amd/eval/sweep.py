@@ -92,6 +92,7 @@ class SweepEngine:
         self.tokens_done = 0
         # the model's last layer only at the scored rows (see DecoderLM.layer_rows)
         self.rows_only = os.environ.get("EDGE_LAST_LAYER_ALL_ROWS", "0") in ("", "0")
+        self._dev = None               # [total_nll, sum_window_nll] increments on the model's device
         hw = sc.head_weights  # LRP head table on the model's device once
         self.head_weights = None if hw is None else torch.as_tensor(hw).to(self.m.device, torch.float32).contiguous()
 
@@ -214,20 +215,31 @@ class SweepEngine:
                 for vi, key in enumerate(chunk):
                     for (mi, ri) in variants[key]:
                         out[mi, li, ri] = wn[vi]
-        w = batch.weights.to(out.device)
+        w = batch.weights.to(out.device, non_blocking=True)
         od = out.double()
-        self.total_nll += (od * w).sum(-1).cpu()
-        self.sum_window_nll += od.sum(-1).cpu()
+        if self._dev is None:          # device-side running sums: no host sync per batch (flushed by _flush)
+            self._dev = [torch.zeros_like(self.total_nll, device=out.device) for _ in range(2)]
+        self._dev[0] += (od * w).sum(-1)
+        self._dev[1] += od.sum(-1)
         self.n_tokens += float(batch.weights.sum())
         self.windows_done += B
         self.tokens_done += B * S
         return out
 
     # -------------------------------------------------------------- results
+    def _flush(self) -> None:
+        """Move the device-side NLL sums into the host accumulators (one sync)."""
+        if self._dev is not None:
+            self.total_nll += self._dev[0].cpu()
+            self.sum_window_nll += self._dev[1].cpu()
+            self._dev = None
+
     def ppl(self) -> torch.Tensor:
+        self._flush()
         return torch.exp(self.total_nll / self.n_tokens)
 
     def results(self) -> dict:
+        self._flush()
         p = self.ppl()
         return {
             "methods": self.methods, "layers_of_interest": self.layers, "ratios": self.ratios, "codec": self.sc.codec,
@@ -239,11 +251,13 @@ class SweepEngine:
         }
 
     def state(self) -> dict:
+        self._flush()
         return {"total_nll": self.total_nll.tolist(), "n_tokens": self.n_tokens, "windows_done": self.windows_done,
                 "wire_bytes": self.wire_bytes.tolist(), "tokens_done": self.tokens_done,
                 "sum_window_nll": self.sum_window_nll.tolist()}
 
     def load_state(self, st: dict) -> None:
+        self._dev = None
         self.total_nll = torch.tensor(st["total_nll"], dtype=torch.float64)
         self.sum_window_nll = torch.tensor(st["sum_window_nll"], dtype=torch.float64)
         self.n_tokens = float(st["n_tokens"])

@@ -132,16 +132,33 @@ def window_nll(row_nll: torch.Tensor, batch: WindowBatch) -> torch.Tensor:
 
 
 class PPLAccumulator:
-    """Token-weighted NLL accumulation, exactly the reference's ``total_nll``/``n_tokens``."""
+    """Token-weighted NLL accumulation, exactly the reference's ``total_nll``/``n_tokens``.
+
+    ``add`` keeps the running NLL sum on the device of the per-window NLLs (fp64, no host sync per batch); reading
+    ``total_nll`` synchronises once."""
 
     def __init__(self):
-        self.total_nll = 0.0
+        self._host_nll = 0.0
+        self._dev_nll = None
         self.n_tokens = 0.0
 
     def add(self, wnll: torch.Tensor, batch: WindowBatch) -> None:
         w = batch.weights
-        self.total_nll += float((wnll.double().cpu() * w).sum())
+        contrib = (wnll.double() * w.to(wnll.device, non_blocking=True)).sum()
+        self._dev_nll = contrib if self._dev_nll is None else self._dev_nll + contrib
         self.n_tokens += float(w.sum())
+
+    @property
+    def total_nll(self) -> float:
+        if self._dev_nll is not None:
+            self._host_nll += float(self._dev_nll)
+            self._dev_nll = None
+        return self._host_nll
+
+    @total_nll.setter
+    def total_nll(self, v: float) -> None:
+        self._dev_nll = None
+        self._host_nll = float(v)
 
     def ppl(self) -> float:
         return math.exp(self.total_nll / self.n_tokens) if self.n_tokens else float("nan")

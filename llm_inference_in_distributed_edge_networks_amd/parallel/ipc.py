@@ -5,19 +5,19 @@ receiving stage allocates a ring of ``slots`` receive buffers once and hands the
 neighbour (``torch.multiprocessing`` CUDA IPC = hipIpcGetMemHandle on dmabuf; /dev/shm mappings for CPU tensors).
 A message then moves as
 
-  sender   : [wait credit for the slot's previous message] -> copy into the peer's slot (copy engine over xGMI,
-             no CUs, stream-ordered) -> flag (seq, bytes) via the process group
+  sender   : [wait for the credit of the slot's previous message] -> copy into the peer's slot (copy engine over
+             xGMI, no CUs, stream-ordered) -> flag (seq, bytes) via the process group
   receiver : flag -> local copy out of the slot into the stage's buffer -> credit back
 
-so RCCL (or gloo) carries only 16-byte flags.  Slot reuse: message m goes into slot m % slots, which held message
-m - slots.  With RCCL the receiver posts its receive for flag m' only after it enqueued the copy-out of message
-m' - RECV_AHEAD (RCCL's stream waits for that), so the completion of the send of flag m - slots + RECV_AHEAD proves
-the slot is free: the
-sender's stream waits for it (``Work.wait``, no host blocking) - no backward messages, which would serialize
-against the flags on RCCL's one stream per peer pair and deadlock.  With gloo (CPU runs, the one-GPU rehearsal,
-asynchronous host-side sends) the receiver returns explicit credits instead, and the copies are synchronized on the
-host before a flag or credit goes out.  A message larger than the
-slot capacity falls back to a plain process-group send/recv (both sides decide the same way from the byte count).
+so the process group carries only 16-byte flags and credits.  Slot reuse: message m goes into slot m % slots, which
+held message m - slots; the sender copies it only after the receiver's credit for m - slots arrived, and the
+receiver sends that credit only after its copy-out of m - slots (stream order on RCCL: the credit send waits for
+the copy-out on the GPU, and the sender's stream waits for the credit receive before its copy - no host blocking;
+host-synchronous on gloo).  Credits travel on their own process group: with RCCL a group is one communicator and one
+stream per rank pair, and credits queued on the flags' stream would sit behind receives posted ahead and deadlock.
+A completed flag *send* proves nothing about the receiver (RCCL may finish a small send into the peer's FIFO before
+the matching receive runs), so it is never used as a slot-free signal.  A message larger than the slot capacity
+falls back to a plain process-group send/recv (both sides decide the same way from the byte count).
 """
 from __future__ import annotations
 
@@ -30,7 +30,8 @@ import torch.distributed as dist
 DEFAULT_CAPACITY = int(os.environ.get("EDGE_IPC_SLOT_BYTES", str(64 << 20)))
 DEFAULT_SLOTS = 8
 # receives a stage posts ahead of consuming (boundary message + aggregate carry, each with a checked-transport
-# fingerprint): the completion of flag m proves the copy-out of message m - RECV_AHEAD
+# fingerprint); the ring needs more slots than that so the sender never waits on a credit the receiver can only
+# send after a receive the sender has not fed yet
 RECV_AHEAD = 4
 
 
@@ -48,12 +49,17 @@ class _Done:
 
 
 class _Work:
+    """Idempotent wait: a gloo send's ``wait()`` consumes one completion of its buffer, so waiting the same work
+    twice (the pipeline and the transport's own bookkeeping) would block for a completion that never comes."""
+
     def __init__(self, works, keep=None):
-        self.works, self.keep = works, keep
+        self.works, self.keep, self.done = works, keep, False
 
     def wait(self):
-        for w in self.works:
-            w.wait()
+        if not self.done:
+            for w in self.works:
+                w.wait()
+            self.done = True
 
 
 class _IpcRecv:
@@ -71,8 +77,7 @@ class _IpcRecv:
                                    f"got {seq} ({nb} B)")
         slot = tr.rx_slots[self.peer][self.seq % tr.slots]
         _bytes_view(self.t).copy_(slot[:n], non_blocking=True)
-        if not tr.nccl:
-            tr._credit(self.peer, self.seq)
+        tr._credit(self.peer, self.seq)
 
 
 class IpcP2P:
@@ -91,9 +96,10 @@ class IpcP2P:
         self.tx_seq: dict = {}       # messages sent to a peer
         self.cred_seen: dict = {}    # credits received from it (= messages it has copied out of its slots)
         self.rx_seq: dict = {}
-        self._credits: dict = {}     # peer -> pending credit sends (gloo; kept alive)
-        self._flags: dict = {}       # peer -> {seq: flag send work} (RCCL: slot-free proof)
+        self._credits: dict = {}     # peer -> pending credit sends (kept alive until done)
+        self._flags: dict = {}       # peer -> pending flag sends
         self._files: list = []
+        self.credit_pg = None        # process group of the credits (set up collectively in ``setup``)
 
     # ---- setup -----------------------------------------------------------------------------------------------
     def _alloc_slots(self):
@@ -127,6 +133,7 @@ class IpcP2P:
             self.rx_seq[prev] = 0
         gathered = [None] * dist.get_world_size()
         dist.all_gather_object(gathered, (prev, desc))
+        self.credit_pg = dist.new_group(backend="nccl" if self.nccl else "gloo")
         if next_ is not None:
             nprev, ndesc = gathered[next_]
             if nprev != rank or ndesc is None:
@@ -146,23 +153,18 @@ class IpcP2P:
             return dist.isend(t if (self.nccl or not t.is_cuda) else t.cpu(), peer)
         seq = self.tx_seq[peer]
         self.tx_seq[peer] = seq + 1
-        flags = self._flags.setdefault(peer, {})
-        if self.nccl:
-            # its completion: the receiver copied message seq - slots out of the slot
-            w = flags.pop(seq - self.slots + RECV_AHEAD, None)
-            if w is not None:
-                w.wait()
-        else:
-            self._take_credits(peer, seq - self.slots + 1)
+        self._take_credits(peer, seq - self.slots + 1)       # the slot's previous message was copied out
         slot = self.tx_slots[peer][seq % self.slots]
         slot[:n].copy_(_bytes_view(t), non_blocking=True)     # peer copy (same device: D2D; CPU: shared memory)
         if t.is_cuda and not self.nccl:
             torch.cuda.current_stream().synchronize()           # gloo flags are host-ordered
         flag = self._sig(seq, n)
-        work = dist.isend(flag, peer)
-        if self.nccl:
-            flags[seq] = work
-        return _Work([work], keep=(flag, t))
+        work = _Work([dist.isend(flag, peer)], keep=(flag, t))
+        pend = self._flags.setdefault(peer, [])
+        pend.append(work)
+        while len(pend) > 2 * self.slots:
+            pend.pop(0).wait()
+        return work
 
     def recv(self, t: torch.Tensor, peer: int):
         n = _nbytes(t)
@@ -178,35 +180,29 @@ class IpcP2P:
         return _IpcRecv(self, peer, t, seq, flag, dist.irecv(flag, peer))
 
     def _take_credits(self, peer: int, upto: int):
-        """Receive credits until ``upto`` messages are known to be copied out of ``peer``'s slots."""
+        """Receive credits until ``upto`` messages are known to be copied out of ``peer``'s slots (RCCL: the
+        current stream waits for each credit on the GPU; gloo: the host waits)."""
         while self.cred_seen[peer] < upto:
             credit = torch.empty(2, dtype=torch.int64, device=self.sig_dev)
-            dist.irecv(credit, peer).wait()
+            dist.irecv(credit, peer, group=self.credit_pg).wait()
             self.cred_seen[peer] += 1
 
     def _credit(self, peer: int, seq: int):
         if self.device.type == "cuda" and not self.nccl:
             torch.cuda.current_stream().synchronize()           # the copy-out is done before the slot is freed
-        c = self._sig(seq, 0)
+        c = self._sig(seq, 0)          # RCCL: the credit send is stream-ordered after the copy-out
         pend = self._credits.setdefault(peer, [])
-        pend.append((dist.isend(c, peer), c))
+        pend.append(_Work([dist.isend(c, peer, group=self.credit_pg)], keep=c))
         while len(pend) > 2 * self.slots:
-            w, _ = pend.pop(0)
-            w.wait()
+            pend.pop(0).wait()
 
     def quiesce(self):
-        """gloo: consume every outstanding credit and finish the credit sends (end of an evaluation run: both
-        neighbours call it, so no credit is left unmatched).  RCCL: nothing is outstanding but flag sends."""
-        if self.nccl:
-            for flags in self._flags.values():
-                for w in flags.values():
-                    w.wait()
-                flags.clear()
-            return
+        """Consume every outstanding credit and finish the flag and credit sends (end of an evaluation run: both
+        neighbours call it, so no credit is left unmatched)."""
         for peer in self.tx_seq:
             self._take_credits(peer, self.tx_seq[peer])
-        for pend in self._credits.values():
-            for w, _ in pend:
+        for pend in list(self._credits.values()) + list(self._flags.values()):
+            for w in pend:
                 w.wait()
             pend.clear()
 

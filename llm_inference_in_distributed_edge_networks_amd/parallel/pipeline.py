@@ -203,6 +203,13 @@ class LocalPipeline:
         self.stages = [StageRunner(model, plan, s, bcfg) for s in range(plan.num_stages)]
         self.graphs = GraphCache(self._step, enabled=use_graphs and model.device.type == "cuda")
 
+    def set_boundary(self, bcfg: BoundaryConfig) -> None:
+        """Switch the boundary codec / importance / ratio (fresh stage runners and byte counters; graphs of the old
+        configuration are dropped)."""
+        self.bcfg = bcfg
+        self.stages = [StageRunner(self.model, self.plan, s, bcfg) for s in range(self.plan.num_stages)]
+        self.graphs.clear()
+
     def _step(self, ids, rows, targets, row_window, n_rows):
         msg = carry = None
         for st in self.stages:
@@ -236,7 +243,7 @@ class DistributedPipeline:
     """One pipeline stage per rank; ``grid.dp`` replicas share the window batches round-robin."""
 
     def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig, grid: Grid, rank: int,
-                 use_graphs: bool = True, transport: str = "torch", check: bool | None = None):
+                 use_graphs: bool = True, transport="torch", check: bool | None = None):
         self.model, self.plan, self.bcfg, self.grid, self.rank = model, plan, bcfg, grid, rank
         self.dp_idx, self.stage = grid.coords(rank)
         if plan.num_stages != grid.pp:
@@ -246,9 +253,11 @@ class DistributedPipeline:
         self.next = grid.rank_of(self.dp_idx, self.stage + 1) if self.stage < grid.pp - 1 else None
         self.device = model.device
         self.graphs = GraphCache(self._stage_step, enabled=use_graphs and model.device.type == "cuda")
-        if transport == "rccl":
+        if not isinstance(transport, str):       # a transport object with send(t, peer) / recv(t, peer)
+            self.tr = transport
+        elif transport == "rccl":
             from .rccl import RcclComm
-            self.tr = RcclComm(rank, grid.world, model.device.index or 0)
+            self.tr = RcclComm(rank, grid.world, model.device.index or 0, peers=[self.prev, self.next])
         elif transport == "torch":
             from .rccl import TorchP2P
             self.tr = TorchP2P()
@@ -263,6 +272,13 @@ class DistributedPipeline:
         if check:
             from .rccl import CheckedTransport
             self.tr = CheckedTransport(self.tr)
+
+    def set_boundary(self, bcfg: BoundaryConfig) -> None:
+        """Switch the boundary configuration, keeping the transport (RCCL channels, IPC slot rings) and process
+        layout.  Every rank must switch to the same configuration before its next ``evaluate``."""
+        self.bcfg = bcfg
+        self.runner = StageRunner(self.model, self.plan, self.stage, bcfg)
+        self.graphs.clear()
 
     def _stage_step(self, ids, rows, targets, row_window, n_rows, msg_in=None, carry_in=None):
         return self.runner.forward(ids, rows, targets, row_window, n_rows, msg_in, carry_in)
@@ -320,6 +336,12 @@ class DistributedPipeline:
             if timing:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
+            # the send that still reads this slot's message buffer (micro-batch i - 2) must be done before the slot
+            # is replayed; waited for before the next receive is posted, so the wait can never cover that receive
+            if in_flight[slot] is not None:
+                for r in in_flight[slot]:
+                    r.wait()
+                in_flight[slot] = None
             if self.prev is not None:
                 msg_in, carry_in, reqs = recv_next
                 with trace.range(f"{tag}/recv_wait"):
@@ -327,10 +349,6 @@ class DistributedPipeline:
                         r.wait()
                 if i + 1 < len(mine):
                     recv_next = self._post_recv(mine[i + 1])  # prefetch: overlap next transfer with compute
-            if in_flight[slot] is not None:
-                for r in in_flight[slot]:
-                    r.wait()
-                in_flight[slot] = None
             if timing:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
@@ -388,3 +406,17 @@ class DistributedPipeline:
         acc.total_nll, acc.n_tokens = float(acc_local[0]), float(acc_local[1])
         report["wire_bytes_per_token"] = self.runner.stats.bytes_per_token
         return acc, report
+
+    def close(self) -> None:
+        """Release the transport (IPC slot rings and their /dev/shm files, RCCL channels).  Idempotent."""
+        tr = getattr(self, "tr", None)
+        inner = getattr(tr, "inner", tr)
+        if inner is not None and hasattr(inner, "close"):
+            inner.close()
+        self.tr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -1,11 +1,13 @@
 """Native RCCL transport for boundary messages (``csrc/comm/rccl_comm.cpp``).
 
-An alternative to ``torch.distributed`` p2p for the stage hand-off: one communicator over all ranks
-(bootstrapped with a unique id broadcast through the default process group), a dedicated
-non-blocking HIP comm stream, and event-only ordering with the compute stream.  ``send``/``recv``
-return handles whose ``wait()`` makes the *current* stream wait on the GPU (no host blocking),
-mirroring ``torch.distributed.Work.wait`` for NCCL.  Buffers are tied to the comm stream with
-``record_stream`` so the caching allocator never recycles them while RCCL still uses them.
+An alternative to ``torch.distributed`` p2p for the stage hand-off: one 2-rank communicator per pipeline edge
+(its unique id handed over through the process group's store), each with its own non-blocking HIP stream, and
+event-only ordering with the compute stream.  ``send``/``recv`` return handles holding an event recorded right
+after that operation; ``wait()`` makes the *current* stream wait for that operation only (no host blocking),
+mirroring ``torch.distributed.Work.wait`` for NCCL.  Because a middle stage's receive from ``prev`` and its send
+to ``next`` live on different streams, the receive it posts ahead for micro-batch i+1 never delays the send of
+micro-batch i.  Buffers are tied to the channel stream with ``record_stream`` so the caching allocator never
+recycles them while RCCL still uses them.
 """
 from __future__ import annotations
 
@@ -46,24 +48,87 @@ def _ok(rc, what):
 
 
 class _Handle:
-    def __init__(self, comm, is_recv):
-        self.comm, self.is_recv = comm, is_recv
+    """One RCCL operation: an event recorded on its channel's stream right after the operation was enqueued.
+
+    ``wait()`` makes the *current* stream wait (GPU-side) for exactly that operation: a receive's data is
+    visible, or a send has finished reading its buffer.  Later operations queued on the same or other channels
+    are not waited for."""
+
+    def __init__(self, stream, keep=()):
+        self.ev = torch.cuda.Event()
+        self.ev.record(stream)
+        self.keep = keep
 
     def wait(self):
-        # the current stream waits (GPU-side) for the comm stream's work so far: a receive's data is visible, or
-        # a send has finished reading its buffer (the pipeline reuses graph output buffers after this)
-        _ok(lib().edge_rccl_signal_to(self.comm.h, torch.cuda.current_stream().cuda_stream), "signal_to")
+        torch.cuda.current_stream().wait_event(self.ev)
+
+    def query(self) -> bool:
+        return self.ev.query()
+
+
+class _Channel:
+    """A communicator over a rank set (a pipeline edge = 2 ranks, or this rank alone for loopback) and its
+    own non-blocking HIP stream."""
+
+    def __init__(self, ranks: tuple, me: int, device: int, unique_id: bytes):
+        L = lib()
+        h = ctypes.c_void_p()
+        _ok(L.edge_rccl_init(ctypes.byref(h), len(ranks), unique_id, ranks.index(me), device), "ncclCommInitRank")
+        self.h, self.ranks = h, ranks
+        self.stream = torch.cuda.ExternalStream(L.edge_rccl_stream(h), device=torch.device("cuda", device))
+
+    def peer_index(self, peer: int) -> int:
+        return self.ranks.index(peer)
+
+    def after_compute(self):
+        _ok(lib().edge_rccl_wait_for(self.h, torch.cuda.current_stream().cuda_stream), "wait_for")
+
+    def close(self):
+        if self.h:
+            lib().edge_rccl_destroy(self.h)
+            self.h = None
+
+
+def channel_key(rank: int, peer: int) -> tuple:
+    """The channel an operation between ``rank`` and ``peer`` runs on: one per unordered rank pair.  A pipeline
+    stage receives from ``prev`` and sends to ``next`` on two different channels (two streams), so a send never
+    queues behind a receive posted ahead of it (and vice versa)."""
+    return (min(rank, peer), max(rank, peer))
 
 
 class RcclComm:
-    def __init__(self, rank: int, world: int, device: int, unique_id: bytes | None = None):
-        L = lib()
-        if unique_id is None:
-            unique_id = self.make_unique_id() if world == 1 else self._bootstrap_id(rank)
-        h = ctypes.c_void_p()
-        _ok(L.edge_rccl_init(ctypes.byref(h), world, unique_id, rank, device), "ncclCommInitRank")
-        self.h, self.rank, self.world = h, rank, world
-        self.stream = torch.cuda.ExternalStream(L.edge_rccl_stream(h), device=torch.device("cuda", device))
+    """Native RCCL transport with one 2-rank communicator and one stream per pipeline edge.
+
+    ``peers``: the ranks this rank exchanges messages with (its pipeline neighbours).  Every edge's unique id is
+    created by its lower rank and handed to the other through the process group's key-value store (no
+    collective), and the edges are initialised in one global order (sorted rank pairs), so the blocking
+    ``ncclCommInitRank`` calls of a chain of stages cannot wait on each other in a cycle.  ``peers=None`` with
+    ``world == 1`` is the single-GPU loopback (``sendrecv`` to itself, ``all_reduce_sum_f64``)."""
+
+    _generation = 0
+
+    def __init__(self, rank: int, world: int, device: int, unique_id: bytes | None = None, peers=None):
+        self.rank, self.world, self.device = rank, world, device
+        self.channels: dict = {}
+        if peers is None:
+            if world != 1:
+                raise ValueError("RcclComm over several ranks needs its peers (the pipeline neighbours)")
+            peers = [rank]
+        RcclComm._generation += 1
+        gen = RcclComm._generation
+        for key in sorted({channel_key(rank, p) for p in peers if p is not None}):
+            ranks = tuple(sorted(set(key)))
+            if len(ranks) == 1:
+                uid = unique_id if unique_id is not None else self.make_unique_id()
+            else:
+                uid = self._exchange_id(gen, ranks)
+            self.channels[key] = _Channel(ranks, rank, device, uid)
+        # the loopback/all-reduce channel (world == 1), or the first edge: what ``stream`` / ``h`` refer to
+        self.h = next(iter(self.channels.values())).h if self.channels else None
+
+    @property
+    def stream(self):
+        return next(iter(self.channels.values())).stream
 
     @staticmethod
     def make_unique_id() -> bytes:
@@ -72,49 +137,64 @@ class RcclComm:
         _ok(L.edge_rccl_unique_id(buf), "ncclGetUniqueId")
         return buf.raw
 
-    @staticmethod
-    def _bootstrap_id(rank: int) -> bytes:
-        from .dist import broadcast_object
-        return broadcast_object(RcclComm.make_unique_id() if rank == 0 else None, src=0)
+    def _exchange_id(self, gen: int, ranks: tuple) -> bytes:
+        import torch.distributed as dist
+        store = dist.distributed_c10d._get_default_store()
+        k = f"edge_rccl/{gen}/{ranks[0]}-{ranks[1]}"
+        if self.rank == ranks[0]:
+            uid = self.make_unique_id()
+            store.set(k, uid)
+            return uid
+        return bytes(store.get(k))
 
-    def _after_compute(self):
-        _ok(lib().edge_rccl_wait_for(self.h, torch.cuda.current_stream().cuda_stream), "wait_for")
+    def _channel(self, peer: int) -> _Channel:
+        try:
+            return self.channels[channel_key(self.rank, peer)]
+        except KeyError:
+            raise ValueError(f"rank {self.rank} has no RCCL channel to rank {peer}") from None
 
     def send(self, t: torch.Tensor, peer: int) -> _Handle:
-        self._after_compute()
-        t.record_stream(self.stream)
-        _ok(lib().edge_rccl_send(self.h, t.data_ptr(), t.numel() * t.element_size(), peer), "ncclSend")
-        return _Handle(self, False)
+        ch = self._channel(peer)
+        ch.after_compute()
+        t.record_stream(ch.stream)
+        _ok(lib().edge_rccl_send(ch.h, t.data_ptr(), t.numel() * t.element_size(), ch.peer_index(peer)), "ncclSend")
+        return _Handle(ch.stream, (t,))
 
     def recv(self, t: torch.Tensor, peer: int) -> _Handle:
-        self._after_compute()
-        t.record_stream(self.stream)
-        _ok(lib().edge_rccl_recv(self.h, t.data_ptr(), t.numel() * t.element_size(), peer), "ncclRecv")
-        return _Handle(self, True)
+        ch = self._channel(peer)
+        ch.after_compute()
+        t.record_stream(ch.stream)
+        _ok(lib().edge_rccl_recv(ch.h, t.data_ptr(), t.numel() * t.element_size(), ch.peer_index(peer)), "ncclRecv")
+        return _Handle(ch.stream, (t,))
 
     def sendrecv(self, send_t, recv_t, peer):
         """Grouped send+recv with one peer (self-loopback when peer == rank)."""
         L = lib()
-        self._after_compute()
-        send_t.record_stream(self.stream)
-        recv_t.record_stream(self.stream)
+        ch = self._channel(peer)
+        ch.after_compute()
+        send_t.record_stream(ch.stream)
+        recv_t.record_stream(ch.stream)
+        p = ch.peer_index(peer)
         _ok(L.edge_rccl_group_start(), "group_start")
-        _ok(L.edge_rccl_send(self.h, send_t.data_ptr(), send_t.numel() * send_t.element_size(), peer), "send")
-        _ok(L.edge_rccl_recv(self.h, recv_t.data_ptr(), recv_t.numel() * recv_t.element_size(), peer), "recv")
+        _ok(L.edge_rccl_send(ch.h, send_t.data_ptr(), send_t.numel() * send_t.element_size(), p), "send")
+        _ok(L.edge_rccl_recv(ch.h, recv_t.data_ptr(), recv_t.numel() * recv_t.element_size(), p), "recv")
         _ok(L.edge_rccl_group_end(), "group_end")
-        return _Handle(self, True)
+        return _Handle(ch.stream, (send_t, recv_t))
 
     def all_reduce_sum_f64(self, t: torch.Tensor):
+        """In-place sum over the loopback channel's ranks (world == 1 self-test)."""
         assert t.dtype == torch.float64
-        self._after_compute()
-        _ok(lib().edge_rccl_allreduce_sum_f64(self.h, t.data_ptr(), t.numel()), "allreduce")
-        _Handle(self, True).wait()
+        ch = self.channels[channel_key(self.rank, self.rank)]
+        ch.after_compute()
+        _ok(lib().edge_rccl_allreduce_sum_f64(ch.h, t.data_ptr(), t.numel()), "allreduce")
+        _Handle(ch.stream).wait()
         return t
 
     def close(self):
-        if self.h:
-            lib().edge_rccl_destroy(self.h)
-            self.h = None
+        for ch in self.channels.values():
+            ch.close()
+        self.channels.clear()
+        self.h = None
 
 
 class _HostSend:

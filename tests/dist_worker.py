@@ -76,3 +76,116 @@ def run_checked(rank, world, port, out_path, corrupt):
         with open(out_path, "w") as f:
             json.dump(res, f)
     shutdown()
+
+
+class LaneP2P:
+    """Host model of a stream-ordered transport (the native RCCL layer's semantics on gloo): every operation runs
+    on a *lane* - a worker thread executing its lane's operations strictly in posting order, like a HIP stream
+    running ncclSend / ncclRecv kernels that block until matched.  ``lanes="per_peer"`` puts each peer on its own
+    lane (``RcclComm``: one channel and stream per pipeline edge, ``rccl.channel_key``); ``lanes="single"`` is the
+    round-2 layout (every operation on one comm stream)."""
+
+    def __init__(self, rank, lanes, on_recv=None, before_send=None):
+        import queue
+        import threading
+        from llm_inference_in_distributed_edge_networks_amd.parallel.rccl import channel_key
+        self.rank, self.lanes, self.on_recv, self.before_send = rank, lanes, on_recv, before_send
+        self.key = (lambda peer: channel_key(rank, peer)) if lanes == "per_peer" else (lambda peer: 0)
+        self.queues, self.threads, self.sent, self.recvd = {}, [], {}, {}
+        self._queue, self._threading = queue, threading
+
+    def _lane(self, peer):
+        k = self.key(peer)
+        if k not in self.queues:
+            q = self._queue.Queue()
+
+            def loop():
+                while True:
+                    item = q.get()
+                    if item is None:
+                        return
+                    fn, done = item
+                    fn()
+                    done.set()
+            th = self._threading.Thread(target=loop, daemon=True)
+            th.start()
+            self.queues[k] = q
+            self.threads.append(th)
+        return self.queues[k]
+
+    def _post(self, peer, fn):
+        done = self._threading.Event()
+        self._lane(peer).put((fn, done))
+
+        class H:
+            def wait(self_inner):
+                if not done.wait(60):
+                    raise TimeoutError("lane operation did not complete")
+        return H()
+
+    def send(self, t, peer):
+        seq = self.sent.get(peer, 0)
+        self.sent[peer] = seq + 1
+        t = t.clone()
+
+        def fn():
+            if self.before_send:
+                self.before_send(peer, seq)
+            dist.send(t, peer)
+        return self._post(peer, fn)
+
+    def recv(self, t, peer):
+        seq = self.recvd.get(peer, 0)
+        self.recvd[peer] = seq + 1
+
+        def fn():
+            dist.recv(t, peer)
+            if self.on_recv:
+                self.on_recv(peer, seq)
+        return self._post(peer, fn)
+
+    def close(self):
+        for q in self.queues.values():
+            q.put(None)
+
+
+def run_lanes(rank, world, port, lanes, out_path):
+    """3 stages; stage 0 holds micro-batch i >= 1 back until the LAST stage has received micro-batch i - 1.  The
+    middle stage therefore has to get send(i - 1) out while its receive of micro-batch i (posted ahead) is still
+    pending: with one lane for both (``lanes="single"``) this deadlocks, with a lane per edge it completes."""
+    import datetime
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
+    from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows
+    from llm_inference_in_distributed_edge_networks_amd.models import TINY_QWEN2, build_model
+    from llm_inference_in_distributed_edge_networks_amd.parallel import (BoundaryConfig, DistributedPipeline, Grid,
+                                                                          PipelinePlan, init_distributed, shutdown)
+    init_distributed("cpu", timeout_s=30)
+    store = dist.distributed_c10d._get_default_store()
+    cfg = TINY_QWEN2
+    grid = Grid(world, 3)
+    plan = PipelinePlan.from_split_layers(cfg.num_layers, [0, 2])
+    stage = rank
+    model, _ = build_model(cfg, "cpu", torch.float32, seed=0, layers=plan.stage_layers(stage),
+                           with_embed=stage == 0, with_head=stage == 2)
+
+    def gate(peer, seq):          # stage 0: micro-batch seq waits until the last stage got seq - 1
+        if seq >= 1:
+            store.wait([f"got/{seq - 1}"], datetime.timedelta(seconds=15))
+
+    def got(peer, seq):
+        store.set(f"got/{seq}", "1")
+
+    tr = LaneP2P(rank, lanes, on_recv=got if stage == 2 else None, before_send=gate if stage == 0 else None)
+    pipe = DistributedPipeline(model, plan, BoundaryConfig("mixed_int4_int8", 0.5, "regular_importance"), grid,
+                               rank, transport=tr)
+    toks = synthetic_stream(1500, cfg.vocab_size, 2)
+    bl = list(batches(toks, sliding_windows(1500, 128, 32), 3))[:5]
+    acc, _ = pipe.evaluate(bl)
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump({"ppl": acc.ppl()}, f)
+    tr.close()
+    shutdown()

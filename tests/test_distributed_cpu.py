@@ -112,3 +112,26 @@ def test_distributed_peer_copy_transport(tmp_path, monkeypatch, world, pp, metho
              nprocs=world, join=True)
     ref = local_ppl(PipelinePlan.from_split_layers(4, split), "mixed_int4_int8", 0.5, method)
     assert abs(json.loads(out.read_text())["ppl"] - ref) / ref < 1e-6
+
+
+def test_middle_stage_send_does_not_wait_for_next_recv(tmp_path):
+    """The native RCCL layer's stream layout (one channel + stream per pipeline edge, per-op events), modelled on
+    gloo with in-order worker lanes: a middle stage's send(i) completes while its posted-ahead recv(i+1) cannot
+    complete until that send has arrived downstream.  Equal to the local pipeline."""
+    out = tmp_path / "res.json"
+    mp.spawn(dist_worker.run_lanes, args=(3, free_port(), "per_peer", str(out)), nprocs=3, join=True)
+    toks = synthetic_stream(1500, 512, 2)
+    m = DecoderLM.random_init(TINY_QWEN2, 0)
+    pipe = LocalPipeline(m, PipelinePlan.from_split_layers(4, [0, 2]),
+                         BoundaryConfig("mixed_int4_int8", 0.5, "regular_importance"))
+    ref = pipe.evaluate(list(batches(toks, sliding_windows(1500, 128, 32), 3))[:5]).ppl()
+    assert abs(json.loads(out.read_text())["ppl"] - ref) / ref < 1e-6
+
+
+def test_single_comm_stream_layout_deadlocks(tmp_path):
+    """Control for the test above: the round-2 layout (sends and receives on one in-order comm stream) cannot
+    deliver send(i) before recv(i+1) completes, so the gated run times out."""
+    out = tmp_path / "res.json"
+    with pytest.raises(Exception):
+        mp.spawn(dist_worker.run_lanes, args=(3, free_port(), "single", str(out)), nprocs=3, join=True)
+    assert not out.exists()

@@ -98,3 +98,62 @@ def test_top_rho_selection_from_params(tmp_path):
                  tmp_path)
     res = json.loads((p / "pipeline_results.json").read_text())["results"]["last_row"]["0.5"]
     assert abs(res["ppl"] - sw["avg_ppl_results"][0][0][0]) / res["ppl"] < 1e-6
+
+
+def test_rgroup_sweep_equals_pipeline_with_relevance_table(tmp_path):
+    """The Qwen2 sweep driver and the pipeline driver load params['group_relevance'] the same way: with a skewed
+    channel-group relevance table the mixed_rgroup_int8 boundary (relevance-allocated group widths) gives the same
+    PPL and wire bytes through both."""
+    from llm_inference_in_distributed_edge_networks_amd.models import TINY_QWEN2
+    G = TINY_QWEN2.hidden_size // 64
+    rel = [[(10.0 if g == G - 1 else 0.05) * (1 + l) for g in range(G)] for l in range(TINY_QWEN2.num_layers + 1)]
+    from llm_inference_in_distributed_edge_networks_amd.codec import wire
+    assert wire.allocate_group_bits(rel[2], 4.0) != wire.allocate_group_bits([1.0] * G, 4.0)   # the table matters
+    tab = tmp_path / "grel.json"
+    tab.write_text(json.dumps(rel))
+    common = {"model": "tiny-qwen2", "max_length": 128, "ratios": [0.5, 1.0], "methods": ["last_row"],
+              "codec": "mixed_rgroup_int8", "group_relevance": str(tab), "group_avg_bits": 4.0}
+    sw = json.loads((run_main("Qwen2-0.5B", dict(common, layers_of_interest=[1]), tmp_path)
+                     / "avg_ppl_results.json").read_text())
+    pr = json.loads((run_main("Pipeline", dict(common, split_layers=[1]), tmp_path)
+                     / "pipeline_results.json").read_text())["results"]["last_row"]
+    for ri, r in enumerate(("0.5", "1.0")):
+        assert abs(pr[r]["ppl"] - sw["avg_ppl_results"][0][0][ri]) / pr[r]["ppl"] < 1e-6
+        assert pr[r]["wire_bytes_per_token"] == pytest.approx(sw["wire_bytes_per_token"][0][0][ri], rel=1e-6)
+
+
+def test_pipeline_driver_resumes_mid_run(tmp_path, monkeypatch):
+    """pipeline_experiment checkpoints after every chunk of checkpoint_every windows and after every (method,
+    ratio); a run killed in the middle of its second configuration resumes to the uninterrupted result."""
+    import sys as _sys
+    _sys.path.insert(0, ROOT)
+    from llm_inference_in_distributed_edge_networks_amd.config import Params
+    from llm_inference_in_distributed_edge_networks_amd.eval import experiments as E
+    from llm_inference_in_distributed_edge_networks_amd.parallel import pipeline as P
+
+    def params(d):
+        d.mkdir()
+        return Params.from_dict({"model": "tiny-qwen2", "split_layers": [1], "codec": "mixed_int4_int8",
+                                 "methods": ["last_row"], "ratios": [0.25, 0.75], "max_length": 128, "stride": 32,
+                                 "window_batch": 2, "dataset": "synthetic", "synthetic_tokens": 1200,
+                                 "device": "cpu", "checkpoint_every": 4, "output_dir": str(d)})
+    full = E.pipeline_experiment(params(tmp_path / "full"), "qwen2-0.5b")["results"]
+    calls = {"n": 0}
+    orig = P.LocalPipeline.evaluate
+
+    def flaky(self, *a, **k):
+        calls["n"] += 1
+        if calls["n"] == 14:                 # inside the second ratio's run
+            raise KeyboardInterrupt("simulated crash")
+        return orig(self, *a, **k)
+    p = params(tmp_path / "crash")
+    monkeypatch.setattr(P.LocalPipeline, "evaluate", flaky)
+    with pytest.raises(KeyboardInterrupt):
+        E.pipeline_experiment(p, "qwen2-0.5b")
+    ck = json.loads((tmp_path / "crash" / "pipeline_results.rank0.ckpt.json").read_text())
+    assert "0.25" in ck["results"]["last_row"] and ck["partial"]["key"] == ["last_row", "0.75"]
+    monkeypatch.setattr(P.LocalPipeline, "evaluate", orig)
+    res = E.pipeline_experiment(p, "qwen2-0.5b")["results"]
+    for r in ("0.25", "0.75"):
+        assert res["last_row"][r]["ppl"] == pytest.approx(full["last_row"][r]["ppl"], rel=1e-9)
+        assert res["last_row"][r]["n_tokens"] == full["last_row"][r]["n_tokens"]

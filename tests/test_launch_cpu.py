@@ -111,3 +111,29 @@ def test_baseline_config_files_load():
         p = Params.load(os.path.join(d, n))
         get_codec(p.codec)
         assert p.num_stages > 1 or p.split_layers
+
+
+def test_bench_self_launch_equals_local():
+    """``python bench.py --gpus 4`` without a launcher starts the 4 ranks itself (pp2 x dp2 over gloo here) and
+    reports them; its PPL equals the single-process run over the same windows (--microbatches doubled at N=1:
+    both process batches 0..2m-1 of the pool per step)."""
+    base = BENCH[:4] + BENCH[6:]          # without "--microbatches 2"
+    r4 = subprocess.run([sys.executable] + base + ["--microbatches", "2", "--gpus", "4", "--pp", "2"], cwd=ROOT,
+                        env=_env(), capture_output=True, text=True, timeout=600)
+    assert r4.returncode == 0, r4.stderr[-3000:]
+    d4 = _json_line(r4.stdout)
+    assert d4["n_gpus"] == 4 and d4["world_size"] == 4 and d4["launch"] == "self" and d4["backend"] == "gloo"
+    assert [x["rank"] for x in d4["rank_devices"]] == [0, 1, 2, 3]
+    assert d4["config"]["parallelism"] == "pp2xdp2"
+    r1 = subprocess.run([sys.executable] + base + ["--microbatches", "4", "--gpus", "1"], cwd=ROOT, env=_env(),
+                        capture_output=True, text=True, timeout=600)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    d1 = _json_line(r1.stdout)
+    assert d1["launch"] == "single" and d1["config"]["global_batch"] == d4["config"]["global_batch"]
+    assert d4["ppl_random_weights"] == pytest.approx(d1["ppl_random_weights"], rel=1e-9)
+
+
+def test_bench_refuses_gpus_world_size_mismatch():
+    r = _torchrun(2, BENCH + ["--gpus", "4"])
+    assert r.returncode != 0
+    assert "--gpus 4 but the launcher started WORLD_SIZE=2" in r.stderr

@@ -23,10 +23,10 @@ def _port():
     return p
 
 
-def _run(n, extra=(), env_extra=None):
+def _run(n, extra=(), env_extra=None, self_launch=False):
     env = dict(os.environ, EDGE_SHARED_GPU="1", **(env_extra or {}))
-    if n == 1:
-        cmd = [sys.executable] + ARGS + list(extra)
+    if n == 1 or self_launch:
+        cmd = [sys.executable] + ARGS + list(extra) + (["--gpus", str(n)] if self_launch else [])
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
                "127.0.0.1", "--master-port", str(_port())] + ARGS + ["--gpus", str(n)] + list(extra)
@@ -42,6 +42,16 @@ def test_two_ranks_one_gpu_equals_single_process():
     assert two["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
     chk = _run(2, ["--no-graphs"], {"EDGE_P2P_CHECK": "1"})
     assert chk["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
+
+
+def test_self_launch_one_gpu_equals_single_process():
+    """``bench.py --gpus 2`` with no launcher env spawns its two ranks itself (the path the driver takes if it runs
+    ``bench.py --gpus N`` directly); same PPL as one process, n_gpus and the rank -> device map reported."""
+    one = _run(1, ["--no-bf16", "--no-fp32-weights"])
+    two = _run(2, ["--no-bf16", "--no-fp32-weights"], self_launch=True)
+    assert two["n_gpus"] == 2 and two["launch"] == "self" and two["world_size"] == 2
+    assert [d["device"] for d in two["rank_devices"]] == ["cuda:0", "cuda:0"]
+    assert two["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
 
 
 def test_four_stage_pipeline_one_gpu_equals_local():

@@ -57,10 +57,10 @@ def test_sweep_top_rho_equals_split_runner():
     from llm_inference_in_distributed_edge_networks_amd.eval.sweep import SweepMethod
     rows = [SweepMethod("rho", "regular_importance", selection="top_rho"),
             SweepMethod("rho_last", "last_row", selection="top_rho")]
-    sc = SweepConfig(rows, [1], [0.25, 0.75], codec="mixed_int4_int8")
+    sc = SweepConfig(rows, [1], [0.25, 0.75, 1.0], codec="mixed_int4_int8")
     res = run_sweep(SweepEngine(M, sc), batches(TOK, WINS, 4))
     for mi, meth in enumerate(["regular_importance", "last_row"]):
-        for ri, r in enumerate([0.25, 0.75]):
+        for ri, r in enumerate([0.25, 0.75, 1.0]):   # 1.0: keep mass 0, no importance tracked
             pipe = LocalPipeline(M, PipelinePlan.from_split_layers(4, [1]),
                                  BoundaryConfig("mixed_int4_int8", r, meth, selection="top_rho"))
             ppl = pipe.evaluate(batches(TOK, WINS, 4)).ppl()
