@@ -1,0 +1,610 @@
+// AttnLRP relevance backward at the reference's precision (fp32; SURVEY §2.4 K17, reference C8:
+// Experiments/Relevance/main.py:84-103, normalisation :111-118).
+//
+// The bf16 engine (lrp.hip) stores every operand in bf16.  This file is its fp32 counterpart, built around the
+// fp32 execution mode of the forward (csrc/common.h "h3"): every GEMM of the backward pass - the input gradients
+// through the frozen projections, with the transposed weights - runs on the same split-fp16 matrix-core GEMM as
+// the forward (csrc/gemm.hip EPI_F32*), and the non-GEMM parts are here, in fp32:
+//
+//   lrp_attn_delta_f32  D[b,h,i] = 0.5 dO_i . O_i (uniform rule on A V) and the per-(window, head) relevance
+//                       rel[b,h] = sum_i D[b,h,i] = sum_{ij} A_ij dA_ij - the reference hook's quantity.
+//   lrp_attn_dkdv_f32   dK, dV partials per (window, q head, 64-key block): P recomputed from Q K^T and the forward
+//                       LSE, dA = 0.5 dO V^T, dS = P (dA - D), dV = 0.5 P^T dO, dK = 0.5 dS^T Q.
+//   lrp_attn_dq_f32     dQ = 0.5 dS K per (window, q head, 64-query block).  Separate sweeps: no atomics.
+//                       All products on v_mfma_f32_16x16x4_f32 (full fp32 operands, no operand rounding).
+//   *_h3 rule kernels   the LRP rules whose output feeds a backward GEMM (SwiGLU / GELU identity rule with the
+//                       uniform product rule, inverse RoPE + GQA sum) write it directly as an h3 activation with a
+//                       per-row power-of-two scale: gradients have no a-priori bound, so each row is scaled to put
+//                       its own max |value| just below 2^15 (fp16 planes can never overflow) and the GEMM's
+//                       per-row epilogue scale multiplies by the inverse (exact: powers of two), times an optional
+//                       per-row factor (the detached norm's rstd).
+//   split_h3_dyn        the same per-row-scaled split for a plain fp32 gradient (the residual stream).
+//   swiglu_h3 / gelu_h3 forward activations from the saved fp32 pre-activations to the down / proj GEMM input.
+//   row_rstd_f32, lrp_ln_bwd_f32, group_absprod   detached-norm statistics, the LayerNorm rule, and the
+//                       channel-group relevance sum |x dx| of the boundary codec's bit allocation.
+//
+// f32 MFMA 16x16x4: lane l holds A[row = l&15][k = l>>4], B[k = l>>4][col = l&15], C[row = 4(l>>4)+r][col = l&15].
+// The 64-wide reductions over the head dimension use the order d(s, g) = 16(s>>2) + 4g + (s&3) for step s and
+// k-slot g, so a lane's four consecutive steps read four consecutive floats (one 16-byte LDS read); the reductions
+// over tokens use the lane-local probabilities with k-slot g <-> token 4g + kk (the bf16 kernels' trick).
+#include "common.h"
+
+namespace {
+constexpr int LDF = 68;   // LDS row stride (floats) of the staged 64-wide tiles
+
+__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Stage 64 rows x 64 floats (row stride `ld` floats; rows >= nrows zero-filled) into an LDS tile [64][LDF].
+__device__ __forceinline__ void stage64(const float* __restrict__ src, size_t ld, int row0, int nrows, float* t) {
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = threadIdx.x + it * 256, r = idx >> 4, c = (idx & 15) * 4;
+    const int gr = row0 + r;
+    f32x4_t v = {0.f, 0.f, 0.f, 0.f};
+    if (gr < nrows) v = *(const f32x4_t*)(src + (size_t)gr * ld + c);
+    *(f32x4_t*)(t + r * LDF + c) = v;
+  }
+}
+
+// Power-of-two row scale: s = 2^(15 - E) with max = m 2^E, m in [0.5, 1): s * max < 2^15.  Returns s, sets inv = 1/s.
+__device__ __forceinline__ float row_pow2_scale(float mx, float& inv) {
+  if (!(mx > 0.f) || !isfinite(mx)) {
+    inv = 1.f;
+    return 1.f;
+  }
+  int e;
+  (void)frexpf(mx, &e);
+  const int sh = 15 - e;
+  inv = ldexpf(1.f, -sh);
+  return ldexpf(1.f, sh);
+}
+
+__device__ __forceinline__ float sigmoid_f32(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float gelu_f32(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_ratio(float x) { return fabsf(x) > 1e-6f ? gelu_f32(x) / x : 0.5f; }
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// D and per-(window, head) relevance.  o, dO token-major fp32 [B*S, Hq*64]; D [B,Hq,S]; rel [B,Hq].
+__global__ __launch_bounds__(256) void lrp_attn_delta_f32_kernel(const float* __restrict__ o,
+                                                                 const float* __restrict__ dO, float* __restrict__ D,
+                                                                 float* __restrict__ rel, int Hq, int S) {
+  __shared__ float red[4];
+  const int bh = blockIdx.x, b = bh / Hq, h = bh - b * Hq;
+  float tot = 0.f;
+  for (int i = threadIdx.x; i < S; i += 256) {
+    const size_t off = ((size_t)b * S + i) * (size_t)(Hq * 64) + h * 64;
+    const f32x4_t* po = (const f32x4_t*)(o + off);
+    const f32x4_t* pd = (const f32x4_t*)(dO + off);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const f32x4_t a = po[c], d = pd[c];
+      s = fmaf(a[0], d[0], fmaf(a[1], d[1], fmaf(a[2], d[2], fmaf(a[3], d[3], s))));
+    }
+    s *= 0.5f;
+    D[(size_t)bh * S + i] = s;
+    tot += s;
+  }
+  tot = block_sum<256>(tot, red);
+  if (threadIdx.x == 0) rel[bh] = tot;
+}
+
+// ---------------------------------------------------------------------------------------------
+// dK, dV partials per q head.  q [B,Hq,S,64] (pre-scaled), k, v [B,Hkv,S,64], dO token-major [B*S, Hq*64],
+// lse/D [B,Hq,S] -> dk, dv [B,Hq,S,64] (the GQA group sum happens in the rope/pack kernel).
+// Workgroup = (b, q head, 64-key block), heaviest key blocks (first keys: most causal queries) first; wave w owns keys
+// kb*64 + 16w .. +15 (lane column cl); query tiles of 64 rows staged in LDS, processed as four 16-row sub-tiles.
+__global__ __launch_bounds__(256) void lrp_attn_dkdv_f32_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                                const float* __restrict__ v,
+                                                                const float* __restrict__ dO,
+                                                                const float* __restrict__ lse,
+                                                                const float* __restrict__ D, float* __restrict__ dk,
+                                                                float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
+  __shared__ __attribute__((aligned(16))) float sQ[64 * LDF];
+  __shared__ __attribute__((aligned(16))) float sO[64 * LDF];
+  __shared__ float sL[64], sD[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int kb = blockIdx.x / (B * Hq);
+  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
+  const int key = kb * 64 + wave * 16 + cl;
+  const int keyc = key < S ? key : S - 1;
+  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const float* vh = v + ((size_t)b * Hkv + hk) * S * 64;
+  float kB[16], vB[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x4_t kv = *(const f32x4_t*)(kh + (size_t)keyc * 64 + 16 * j + 4 * g);
+    const f32x4_t vv = *(const f32x4_t*)(vh + (size_t)keyc * 64 + 16 * j + 4 * g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      kB[4 * j + e] = kv[e];
+      vB[4 * j + e] = vv[e];
+    }
+  }
+  f32x4_t dka[4], dva[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
+  const float* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
+  const float* lh = lse + ((size_t)b * Hq + h) * S;
+  const float* dh = D + ((size_t)b * Hq + h) * S;
+  for (int q0 = kb * 64; q0 < S; q0 += 64) {
+    __syncthreads();
+    stage64(qh, 64, q0, S, sQ);
+    stage64(doh, (size_t)Hq * 64, q0, S, sO);
+    if (tid < 64) {
+      const int qi = q0 + tid;
+      sL[tid] = qi < S ? lh[qi] : INFINITY;
+      sD[tid] = qi < S ? dh[qi] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      // scores and dA for queries q0 + sub*16 + 4g + r (C rows) x this lane's key (C column)
+      f32x4_t s = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
+      const float* qa = sQ + (sub * 16 + cl) * LDF + 4 * g;
+      const float* oa = sO + (sub * 16 + cl) * LDF + 4 * g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4_t qv = *(const f32x4_t*)(qa + 16 * j);
+        const f32x4_t ov = *(const f32x4_t*)(oa + 16 * j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s = mfma4(qv[e], kB[4 * j + e], s);
+          da = mfma4(ov[e], vB[4 * j + e], da);
+        }
+      }
+      float p[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = sub * 16 + g * 4 + r;
+        const int qi = q0 + ql;
+        const bool ok = qi < S && key <= qi && key < S;
+        const float pr = ok ? expf(s[r] - sL[ql]) : 0.f;
+        p[r] = pr;
+        ds[r] = pr * (0.5f * da[r] - sD[ql]);
+      }
+      // dV[key][d] += P^T dO, dK[key][d] += dS^T Q over the 16 queries: MFMA kk takes query 4g + kk of k-slot g
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int row = (sub * 16 + 4 * g + kk) * LDF;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dva[dt] = mfma4(p[kk], sO[row + dt * 16 + cl], dva[dt]);
+          dka[dt] = mfma4(ds[kk], sQ[row + dt * 16 + cl], dka[dt]);
+        }
+      }
+    }
+  }
+  // C[row = key 16w + 4g + r][col = d 16dt + cl]
+  float* dkh = dk + ((size_t)b * Hq + h) * S * 64;
+  float* dvh = dv + ((size_t)b * Hq + h) * S * 64;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int kr = kb * 64 + wave * 16 + g * 4 + r;
+    if (kr < S) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dkh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dka[dt][r];
+        dvh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dva[dt][r];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dQ.  Workgroup = (b, h, 64-query block), heaviest (last) query blocks first; wave w owns queries qb*64 + 16w + cl.
+// S^T = K Q^T and dA^T = V dO^T keep the query on the lane column, so dQ^T = K^T dS^T takes dS^T lane-locally.
+__global__ __launch_bounds__(256) void lrp_attn_dq_f32_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                              const float* __restrict__ v, const float* __restrict__ dO,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ D, float* __restrict__ dq,
+                                                              int B, int Hq, int Hkv, int S) {
+  __shared__ __attribute__((aligned(16))) float sK[64 * LDF];
+  __shared__ __attribute__((aligned(16))) float sV[64 * LDF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int nqb = (S + 63) / 64;
+  const int qb = nqb - 1 - blockIdx.x / (B * Hq);
+  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
+  const int qi = qb * 64 + wave * 16 + cl;
+  const int qic = qi < S ? qi : S - 1;
+  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
+  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const float* vh = v + ((size_t)b * Hkv + hk) * S * 64;
+  const float* dorow = dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64;
+  float qB[16], oB[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x4_t qv = *(const f32x4_t*)(qh + (size_t)qic * 64 + 16 * j + 4 * g);
+    const f32x4_t ov = *(const f32x4_t*)(dorow + 16 * j + 4 * g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      qB[4 * j + e] = qv[e];
+      oB[4 * j + e] = ov[e];
+    }
+  }
+  const float lq = lse[((size_t)b * Hq + h) * S + qic];
+  const float dq_ = D[((size_t)b * Hq + h) * S + qic];
+  f32x4_t acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int kend = min(S, qb * 64 + 64);
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    __syncthreads();
+    stage64(kh, 64, k0, S, sK);
+    stage64(vh, 64, k0, S, sV);
+    __syncthreads();
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      f32x4_t s = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
+      const float* ka = sK + (sub * 16 + cl) * LDF + 4 * g;
+      const float* va = sV + (sub * 16 + cl) * LDF + 4 * g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4_t kv = *(const f32x4_t*)(ka + 16 * j);
+        const f32x4_t vv = *(const f32x4_t*)(va + 16 * j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s = mfma4(kv[e], qB[4 * j + e], s);
+          da = mfma4(vv[e], oB[4 * j + e], da);
+        }
+      }
+      // s[r] = score(key = k0 + sub*16 + 4g + r, query = qi)
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + sub * 16 + g * 4 + r;
+        const bool ok = qi < S && kj <= qi;
+        const float pr = ok ? expf(s[r] - lq) : 0.f;
+        ds[r] = pr * (0.5f * da[r] - dq_);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int row = (sub * 16 + 4 * g + kk) * LDF;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma4(sK[row + dt * 16 + cl], ds[kk], acc[dt]);
+      }
+    }
+  }
+  // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
+  if (qi < S) {
+    float* o = dq + (((size_t)b * Hq + h) * S + qi) * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = 0.5f * acc[dt];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-row power-of-two h3 split of rule outputs.  Every kernel below computes its row twice: a max pass and a
+// store pass (the recomputation is a handful of L1/L2 hits, and no register array of a model-dependent width).
+
+// Inverse RoPE + q scale + GQA group sum of the dK/dV partials + scatter into the token-major d[q|k|v] row,
+// as a per-row-scaled h3 activation out3 [B*S, 2W] (W = (Hq + 2Hkv) 64), rinv[row] = 1/s * post[row].
+__device__ __forceinline__ float rope_pack_value(const float* __restrict__ dq, const float* __restrict__ dk,
+                                                 const float* __restrict__ dv, const float* __restrict__ cosT,
+                                                 const float* __restrict__ sinT, int b, int s, int c, int S, int Hq,
+                                                 int Hkv, int rot_dim, float q_scale) {
+  const int hh = c >> 6, d = c & 63, G = Hq / Hkv;
+  const float* src;
+  float scale = 1.f;
+  bool rope = true;
+  int ng = 1;
+  if (hh < Hq) {
+    src = dq + (((size_t)b * Hq + hh) * S + s) * 64;
+    scale = q_scale;
+  } else if (hh < Hq + Hkv) {
+    src = dk + (((size_t)b * Hq + (hh - Hq) * G) * S + s) * 64;
+    ng = G;
+  } else {
+    src = dv + (((size_t)b * Hq + (hh - Hq - Hkv) * G) * S + s) * 64;
+    ng = G;
+    rope = false;
+  }
+  const int half = rot_dim >> 1;
+  const bool rot = rope && d < rot_dim;
+  const int dp = !rot ? d : (d < half ? d + half : d - half);
+  float x0 = 0.f, xp = 0.f;
+  for (int gi = 0; gi < ng; ++gi) {
+    x0 += src[(size_t)gi * S * 64 + d];
+    if (rot) xp += src[(size_t)gi * S * 64 + dp];
+  }
+  float val = x0;
+  if (rot) {
+    const int j = d < half ? d : d - half;
+    const float cs = cosT[(size_t)s * half + j], sn = sinT[(size_t)s * half + j];
+    val = d < half ? x0 * cs + xp * sn : x0 * cs - xp * sn;
+  }
+  return val * scale;
+}
+
+__global__ __launch_bounds__(256) void lrp_rope_pack_h3_kernel(const float* __restrict__ dq, const float* __restrict__ dk,
+                                                               const float* __restrict__ dv,
+                                                               const float* __restrict__ cosT,
+                                                               const float* __restrict__ sinT, f16_t* __restrict__ out,
+                                                               float* __restrict__ rinv,
+                                                               const float* __restrict__ post, int B, int S, int Hq,
+                                                               int Hkv, int rot_dim, float q_scale) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B * S) return;
+  const int b = row / S, s = row - b * S, W = (Hq + 2 * Hkv) * 64;
+  float mx = 0.f;
+  for (int c = lane; c < W; c += 64)
+    mx = fmaxf(mx, fabsf(rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale)));
+  mx = wave_max(mx);
+  float inv;
+  const float sc = row_pow2_scale(mx, inv);
+  f16_t* o = out + (size_t)row * (2 * W);
+  for (int c = lane; c < W; c += 64) {
+    float hi, lo;
+    split2h(sc * rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale), hi, lo);
+    o[c] = __builtin_bit_cast(f16_t, (_Float16)hi);
+    o[W + c] = __builtin_bit_cast(f16_t, (_Float16)lo);
+  }
+  if (lane == 0) rinv[row] = inv * (post ? post[row] : 1.f);
+}
+
+// Plain fp32 rows [R, K] -> per-row-scaled h3 activation [R, 2K] + rinv.  One wave per row, 4 values per access.
+__global__ __launch_bounds__(256) void split_h3_dyn_kernel(const float* __restrict__ x, f16_t* __restrict__ out,
+                                                           float* __restrict__ rinv, const float* __restrict__ post,
+                                                           int R, int K) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const float* xr = x + (size_t)row * K;
+  float mx = 0.f;
+  for (int c = lane * 4; c < K; c += 256) {
+    const f32x4_t v = *(const f32x4_t*)(xr + c);
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  mx = wave_max(mx);
+  float inv;
+  const float sc = row_pow2_scale(mx, inv);
+  f16_t* o = out + (size_t)row * (2 * K);
+  for (int c = lane * 4; c < K; c += 256) {
+    const f32x4_t v = *(const f32x4_t*)(xr + c);
+    const float vv[4] = {v[0], v[1], v[2], v[3]};
+    store_h3_4(o, K, c, vv, sc);
+  }
+  if (lane == 0) rinv[row] = inv * (post ? post[row] : 1.f);
+}
+
+// SwiGLU rule on the interleaved gate|up layout (blocks of 16 columns): dg = 0.5 dm u sigmoid(g) (uniform rule on g*u,
+// identity rule on SiLU), du = 0.5 dm silu(g); output the interleaved d[gate|up] row [2I] as a per-row-scaled h3
+// activation [T, 4I].  One workgroup per row, 8 columns of one 16-column block per thread and step.
+__device__ __forceinline__ void swiglu_bwd8(const float* __restrict__ dmr, const float* __restrict__ gur, int c,
+                                            float (&dg)[8], float (&du)[8]) {
+  const int blk = c >> 4, e = c & 15;
+  const float* gp = gur + blk * 32 + e;
+#pragma unroll
+  for (int i = 0; i < 8; i += 4) {
+    const f32x4_t gv = *(const f32x4_t*)(gp + i), uv = *(const f32x4_t*)(gp + 16 + i);
+    const f32x4_t mv = *(const f32x4_t*)(dmr + c + i);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float sg = sigmoid_f32(gv[t]), m = 0.5f * mv[t];
+      dg[i + t] = m * uv[t] * sg;
+      du[i + t] = m * gv[t] * sg;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void lrp_swiglu_bwd_h3_kernel(const float* __restrict__ dm,
+                                                                const float* __restrict__ gu, f16_t* __restrict__ out,
+                                                                float* __restrict__ rinv,
+                                                                const float* __restrict__ post, int I) {
+  __shared__ float red[4];
+  const int t = blockIdx.x;
+  const float* dmr = dm + (size_t)t * I;
+  const float* gur = gu + (size_t)t * (2 * I);
+  float mx = 0.f;
+  for (int c = threadIdx.x * 8; c < I; c += 256 * 8) {
+    float dg[8], du[8];
+    swiglu_bwd8(dmr, gur, c, dg, du);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mx = fmaxf(mx, fmaxf(fabsf(dg[i]), fabsf(du[i])));
+  }
+  mx = block_max<256>(mx, red);
+  float inv;
+  const float sc = row_pow2_scale(mx, inv);
+  const int W = 2 * I;
+  f16_t* o = out + (size_t)t * (2 * W);
+  for (int c = threadIdx.x * 8; c < I; c += 256 * 8) {
+    float dg[8], du[8];
+    swiglu_bwd8(dmr, gur, c, dg, du);
+    const int col = (c >> 4) * 32 + (c & 15);
+    store_h3_8(o, W, col, dg, sc);
+    store_h3_8(o, W, col + 16, du, sc);
+  }
+  if (threadIdx.x == 0) rinv[t] = inv * (post ? post[t] : 1.f);
+}
+
+// GELU identity rule on the fc output gradient (GPT-NeoX): dx = dy gelu(a)/a, as a per-row-scaled h3 activation.
+__global__ __launch_bounds__(256) void lrp_gelu_bwd_h3_kernel(const float* __restrict__ dy, const float* __restrict__ a,
+                                                              f16_t* __restrict__ out, float* __restrict__ rinv,
+                                                              int I) {
+  __shared__ float red[4];
+  const int t = blockIdx.x;
+  const float* dr = dy + (size_t)t * I;
+  const float* ar = a + (size_t)t * I;
+  float mx = 0.f;
+  for (int c = threadIdx.x; c < I; c += 256) mx = fmaxf(mx, fabsf(dr[c] * gelu_ratio(ar[c])));
+  mx = block_max<256>(mx, red);
+  float inv;
+  const float sc = row_pow2_scale(mx, inv);
+  f16_t* o = out + (size_t)t * (2 * I);
+  for (int c = threadIdx.x; c < I; c += 256) {
+    float hi, lo;
+    split2h(sc * (dr[c] * gelu_ratio(ar[c])), hi, lo);
+    o[c] = __builtin_bit_cast(f16_t, (_Float16)hi);
+    o[I + c] = __builtin_bit_cast(f16_t, (_Float16)lo);
+  }
+  if (threadIdx.x == 0) rinv[t] = inv;
+}
+
+// Forward activations from saved fp32 pre-activations to the next GEMM's h3 input at the model's scale s:
+// SwiGLU on the interleaved gate|up row [2I] -> [I] (act 0), GELU [I] -> [I] (act 1).
+__global__ __launch_bounds__(256) void act_h3_kernel(const float* __restrict__ x, f16_t* __restrict__ out, size_t n4,
+                                                     int I, int act, float s) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n4) return;
+  const int I4 = I >> 2;
+  const size_t t = idx / I4;
+  const int c = (int)(idx - t * I4) * 4;
+  float v[4];
+  if (act == 0) {
+    const float* gp = x + t * (size_t)(2 * I) + (c >> 4) * 32 + (c & 15);
+    const f32x4_t gv = *(const f32x4_t*)gp, uv = *(const f32x4_t*)(gp + 16);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gv[e] * sigmoid_f32(gv[e]) * uv[e];
+  } else {
+    const f32x4_t xv = *(const f32x4_t*)(x + t * (size_t)I + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gelu_f32(xv[e]);
+  }
+  store_h3_4(out + t * (size_t)(2 * I), I, c, v, s);
+}
+
+// rstd per row: rsqrt(mean(x^2) + eps) (RMSNorm), or of the centred row (LayerNorm, center = 1).  One wave per row.
+__global__ __launch_bounds__(256) void row_rstd_f32_kernel(const float* __restrict__ x, float* __restrict__ rstd, int R,
+                                                           int H, float eps, int center) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const float* xr = x + (size_t)row * H;
+  float mu = 0.f;
+  if (center) {
+    float s = 0.f;
+    for (int c = lane; c < H; c += 64) s += xr[c];
+    mu = wave_sum(s) / H;
+  }
+  float v = 0.f;
+  for (int c = lane; c < H; c += 64) {
+    const float d = xr[c] - mu;
+    v = fmaf(d, d, v);
+  }
+  v = wave_sum(v) / H;
+  if (lane == 0) rstd[row] = 1.f / sqrtf(v + eps);
+}
+
+// LayerNorm rule with detached variance (mean not detached), dual norm of one input (GPT-NeoX parallel residual):
+// out = resid + (gc1 - mean gc1) + (gc2 - mean gc2), gc = dy * rstd * w.  fp32, one wave per row.
+__global__ __launch_bounds__(256) void lrp_ln_bwd_f32_kernel(const float* __restrict__ dy1, const float* __restrict__ rs,
+                                                             const float* __restrict__ w1,
+                                                             const float* __restrict__ dy2,
+                                                             const float* __restrict__ w2,
+                                                             const float* __restrict__ resid, float* __restrict__ out,
+                                                             int R, int H) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const size_t base = (size_t)row * H;
+  const float r = rs[row];
+  float m1 = 0.f, m2 = 0.f;
+  for (int c = lane; c < H; c += 64) {
+    m1 += dy1[base + c] * r * w1[c];
+    if (dy2) m2 += dy2[base + c] * r * w2[c];
+  }
+  m1 = wave_sum(m1) / H;
+  m2 = wave_sum(m2) / H;
+  for (int c = lane; c < H; c += 64) {
+    float val = resid[base + c] + (dy1[base + c] * r * w1[c] - m1);
+    if (dy2) val += dy2[base + c] * r * w2[c] - m2;
+    out[base + c] = val;
+  }
+}
+
+// Channel-group relevance of the residual stream: out[b * ob + g] = sum over the window's S tokens and the group's
+// 64 channels of |x dx|.  One workgroup per (window, group); deterministic (no atomics).
+__global__ __launch_bounds__(256) void group_absprod_kernel(const float* __restrict__ x, const float* __restrict__ dx,
+                                                            float* __restrict__ out, int S, int H, int G, int ob) {
+  __shared__ float red[4];
+  const int b = blockIdx.x / G, gi = blockIdx.x - b * G;
+  const int c = threadIdx.x & 63;
+  float acc = 0.f;
+  for (int s = threadIdx.x >> 6; s < S; s += 4) {
+    const size_t off = ((size_t)b * S + s) * H + gi * 64 + c;
+    acc += fabsf(x[off] * dx[off]);
+  }
+  acc = block_sum<256>(acc, red);
+  if (threadIdx.x == 0) out[(size_t)b * ob + gi] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+static inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
+
+EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* v, const float* o, const float* dO,
+                                   const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, int B,
+                                   int Hq, int Hkv, int S, hipStream_t st) {
+  if (B <= 0 || S <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
+  const int nb = (S + 63) / 64;
+  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
+  lrp_attn_dkdv_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+  lrp_attn_dq_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_lrp_rope_pack_h3(const float* dq, const float* dk, const float* dv, const float* cosT,
+                                   const float* sinT, void* out, float* rinv, const float* post, int B, int S, int Hq,
+                                   int Hkv, int rot_dim, float q_scale, hipStream_t st) {
+  const int R = B * S;
+  if (R <= 0) return 0;
+  if (rot_dim > 64 || rot_dim % 2 || Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
+  lrp_rope_pack_h3_kernel<<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S, Hq, Hkv,
+                                                        rot_dim, q_scale);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_split_h3_dyn(const float* x, void* out, float* rinv, const float* post, int R, int K, hipStream_t st) {
+  if (R <= 0) return 0;
+  if (K % 4) return (int)hipErrorInvalidValue;
+  split_h3_dyn_kernel<<<(R + 3) / 4, 256, 0, st>>>(x, (f16_t*)out, rinv, post, R, K);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_lrp_swiglu_bwd_h3(const float* dm, const float* gu, void* out, float* rinv, const float* post,
+                                    int T, int I, hipStream_t st) {
+  if (T <= 0) return 0;
+  if (I % 16) return (int)hipErrorInvalidValue;
+  lrp_swiglu_bwd_h3_kernel<<<T, 256, 0, st>>>(dm, gu, (f16_t*)out, rinv, post, I);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_lrp_gelu_bwd_h3(const float* dy, const float* a, void* out, float* rinv, int T, int I,
+                                  hipStream_t st) {
+  if (T <= 0) return 0;
+  lrp_gelu_bwd_h3_kernel<<<T, 256, 0, st>>>(dy, a, (f16_t*)out, rinv, I);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_act_h3(const float* x, void* out, long long T, int I, int act, float s, hipStream_t st) {
+  const size_t n4 = (size_t)T * I / 4;
+  if (!n4) return 0;
+  if ((act == 0 && I % 16) || I % 4 || act < 0 || act > 1 || !(s > 0.f)) return (int)hipErrorInvalidValue;
+  act_h3_kernel<<<nblk(n4), 256, 0, st>>>(x, (f16_t*)out, n4, I, act, s);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_row_rstd_f32(const float* x, float* rstd, int R, int H, float eps, int center, hipStream_t st) {
+  if (R <= 0) return 0;
+  row_rstd_f32_kernel<<<(R + 3) / 4, 256, 0, st>>>(x, rstd, R, H, eps, center);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_lrp_ln_bwd_f32(const float* dy1, const float* rs, const float* w1, const float* dy2, const float* w2,
+                                 const float* resid, float* out, int R, int H, hipStream_t st) {
+  if (R <= 0) return 0;
+  lrp_ln_bwd_f32_kernel<<<(R + 3) / 4, 256, 0, st>>>(dy1, rs, w1, dy2, w2, resid, out, R, H);
+  return (int)hipGetLastError();
+}
+
+EDGE_API int edge_group_absprod(const float* x, const float* dx, float* out, int B, int S, int H, int out_stride,
+                                hipStream_t st) {
+  if (B <= 0 || S <= 0) return 0;
+  if (H % 64) return (int)hipErrorInvalidValue;
+  const int G = H / 64;
+  group_absprod_kernel<<<B * G, 256, 0, st>>>(x, dx, out, S, H, G, out_stride);
+  return (int)hipGetLastError();
+}

@@ -44,6 +44,8 @@ class Params:
     selection: str = "ratio"                 # "ratio" (int(ratio*S) least important) | "top_rho" (mass 1 - ratio kept)
     group_relevance: str = ""                # channel_group_relevance.json (head-group codecs rgroup / mixed_rgroup_int8)
     group_avg_bits: float = 4.0              # head-group codecs: average bits per channel of a group-quantized row
+    lrp_engine: str = "auto"                 # relevance pass: "auto" (HIP engine on a GPU, autograd on the CPU) |
+                                             # "hip" | "autograd" (AttnLRP rules as torch autograd, any device)
     output_dir: str = "."
     checkpoint_every: int = 1000             # windows between partial-result dumps (reference: 1000)
     resume: bool = True

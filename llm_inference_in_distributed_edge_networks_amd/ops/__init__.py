@@ -523,7 +523,8 @@ def lrp_attn_bwd(q, k, v, o, dO, lse):
     ``reference.lrp_attn_bwd``."""
     if not _gpu(q):
         return ref.lrp_attn_bwd(q, k, v, o, dO, lse)
-    _check_bf16(q, k, v, o, dO)
+    fp32 = q.dtype == torch.float32
+    (_check_f32 if fp32 else _check_bf16)(q, k, v, o, dO)
     B, Hq, S, D = q.shape
     Hkv = k.shape[1]
     assert D == 64 and k.shape == v.shape == (B, Hkv, S, D) and o.shape == dO.shape == (B * S, Hq * D)
@@ -532,8 +533,8 @@ def lrp_attn_bwd(q, k, v, o, dO, lse):
     Dl, rel = torch.empty(B, Hq, S, **f32), torch.empty(B, Hq, **f32)
     dq = torch.empty(B, Hq, S, D, **f32)
     dk, dv = torch.empty(B, Hq, S, D, **f32), torch.empty(B, Hq, S, D, **f32)
-    call("edge_lrp_attn_bwd", ptr(q), ptr(k), ptr(v), ptr(o), ptr(dO), ptr(lse), ptr(Dl), ptr(rel), ptr(dq), ptr(dk),
-         ptr(dv), B, Hq, Hkv, S, stream())
+    call("edge_lrp_attn_bwd_f32" if fp32 else "edge_lrp_attn_bwd", ptr(q), ptr(k), ptr(v), ptr(o), ptr(dO), ptr(lse),
+         ptr(Dl), ptr(rel), ptr(dq), ptr(dk), ptr(dv), B, Hq, Hkv, S, stream())
     return Dl, rel, dq, dk, dv
 
 
@@ -596,4 +597,117 @@ def lrp_ln_bwd(dy1, rs1, w1, dy2, rs2, w2, resid):
     out = torch.empty_like(resid)
     call("edge_lrp_ln_bwd", ptr(dy1), ptr(rs1), ptr(w1), ptr(dy2), ptr(rs2), ptr(w2), ptr(resid), ptr(out), R, H,
          stream())
+    return out
+
+
+# ---- fp32 AttnLRP (csrc/lrp_f32.hip): rule outputs as per-row-scaled h3 GEMM inputs ---------------------------
+def _rows_out(R: int, K: int, device):
+    return (torch.empty(R, 2 * K, dtype=torch.float16, device=device),
+            torch.empty(R, dtype=torch.float32, device=device))
+
+
+def _post(post, R):
+    if post is None:
+        return None
+    _check_f32(post)
+    assert post.numel() == R
+    return post
+
+
+def split_h3_dyn(x: torch.Tensor, post: torch.Tensor | None = None):
+    """fp32 [R, K] -> (h3 activation [R, 2K] with a per-row power-of-two scale s_r, rinv [R] = post / s_r): the
+    input of a backward GEMM (``linear_h3(..., rscale=rinv)`` undoes the scale exactly)."""
+    if not _gpu(x):
+        return ref.split_h3_dyn(x, post)
+    _check_f32(x)
+    R, K = x.shape
+    out, rinv = _rows_out(R, K, x.device)
+    call("edge_split_h3_dyn", ptr(x), ptr(out), ptr(rinv), ptr(_post(post, R)), R, K, stream())
+    return out, rinv
+
+
+def lrp_swiglu_bwd_h3(dm: torch.Tensor, gu: torch.Tensor, post: torch.Tensor | None = None):
+    """SwiGLU LRP rule (fp32 dm [T, I], saved gate|up pre-activations gu [T, 2I]) -> (h3 d[gate|up] [T, 4I], rinv)."""
+    if not _gpu(gu):
+        return ref.lrp_swiglu_bwd_h3(dm, gu, post)
+    _check_f32(dm, gu)
+    T, N2 = gu.shape
+    assert dm.shape == (T, N2 // 2)
+    out, rinv = _rows_out(T, N2, gu.device)
+    call("edge_lrp_swiglu_bwd_h3", ptr(dm), ptr(gu), ptr(out), ptr(rinv), ptr(_post(post, T)), T, N2 // 2, stream())
+    return out, rinv
+
+
+def lrp_gelu_bwd_h3(dy: torch.Tensor, a: torch.Tensor):
+    """GELU identity rule (fp32) -> (h3 [T, 2I], rinv)."""
+    if not _gpu(a):
+        return ref.lrp_gelu_bwd_h3(dy, a)
+    _check_f32(dy, a)
+    T, I = a.shape
+    out, rinv = _rows_out(T, I, a.device)
+    call("edge_lrp_gelu_bwd_h3", ptr(dy), ptr(a), ptr(out), ptr(rinv), T, I, stream())
+    return out, rinv
+
+
+def lrp_rope_pack_h3(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, post=None):
+    """Inverse RoPE + q scale + GQA sum + token-major scatter (fp32) -> (h3 d[q|k|v] [B*S, 2(Hq+2Hkv)64], rinv)."""
+    if not _gpu(dq):
+        return ref.lrp_rope_pack_h3(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, post)
+    _check_f32(dq, dk, dv, cos, sin)
+    assert dq.shape == dk.shape == dv.shape == (B, Hq, S, 64)
+    out, rinv = _rows_out(B * S, (Hq + 2 * Hkv) * 64, dq.device)
+    call("edge_lrp_rope_pack_h3", ptr(dq), ptr(dk), ptr(dv), ptr(cos), ptr(sin), ptr(out), ptr(rinv),
+         ptr(_post(post, B * S)), B, S, Hq, Hkv, rot_dim, float(q_scale), stream())
+    return out, rinv
+
+
+def act_h3(x: torch.Tensor, act: str, s: float) -> torch.Tensor:
+    """Forward activation of saved fp32 pre-activations ("swiglu_il": interleaved gate|up [T, 2I] -> [T, I];
+    "gelu": [T, I]) as the next GEMM's h3 input at the model scale ``s``."""
+    if not _gpu(x):
+        return ref.act_h3(x, act, s)
+    _check_f32(x)
+    T, N = x.shape
+    I = N // 2 if act == "swiglu_il" else N
+    out = torch.empty(T, 2 * I, dtype=torch.float16, device=x.device)
+    call("edge_act_h3", ptr(x), ptr(out), T, I, 0 if act == "swiglu_il" else 1, float(s), stream())
+    return out
+
+
+def row_rstd(x: torch.Tensor, eps: float, center: bool = False) -> torch.Tensor:
+    """fp32 rows -> rsqrt(mean(x^2) + eps) (RMSNorm), of the centred row with ``center`` (LayerNorm)."""
+    if not _gpu(x):
+        return ref.row_rstd(x, eps, center)
+    _check_f32(x)
+    R, H = x.shape
+    out = torch.empty(R, dtype=torch.float32, device=x.device)
+    call("edge_row_rstd_f32", ptr(x), ptr(out), R, H, float(eps), int(center), stream())
+    return out
+
+
+def lrp_ln_bwd_f32(dy1, rs, w1, dy2, w2, resid):
+    """fp32 LayerNorm rule of a dual norm sharing one input (and so one rstd ``rs``)."""
+    if not _gpu(resid):
+        return ref.lrp_ln_bwd(dy1, rs, w1, dy2, rs, w2, resid)
+    _check_f32(dy1, rs, w1, dy2, w2, resid)
+    R, H = resid.shape
+    out = torch.empty_like(resid)
+    call("edge_lrp_ln_bwd_f32", ptr(dy1), ptr(rs), ptr(w1), ptr(dy2), ptr(w2), ptr(resid), ptr(out), R, H, stream())
+    return out
+
+
+def group_absprod(x: torch.Tensor, dx: torch.Tensor, B: int, S: int, out: torch.Tensor | None = None):
+    """[B, H/64] sums of |x dx| per window and 64-channel group (into ``out`` [B, >= H/64] rows if given)."""
+    if not _gpu(x):
+        r = ref.group_absprod(x, dx, B, S)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    _check_f32(x, dx)
+    H = x.shape[1]
+    if out is None:
+        out = torch.empty(B, H // 64, dtype=torch.float32, device=x.device)
+    assert out.dtype == torch.float32 and out.stride(1) == 1
+    call("edge_group_absprod", ptr(x), ptr(dx), ptr(out), B, S, H, out.stride(0), stream())
     return out

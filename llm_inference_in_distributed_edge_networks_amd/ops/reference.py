@@ -360,3 +360,57 @@ def lrp_ln_bwd(dy1, rs1, w1, dy2, rs2, w2, resid):
     if dy2 is not None:
         out = out + one(dy2, rs2, w2)
     return out.to(resid.dtype)
+
+
+# ---- fp32 AttnLRP backward on h3 GEMMs (csrc/lrp_f32.hip) ---------------------------------------------------
+def h3_row_scales(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-row power-of-two scale s = 2^(15 - E) for max |row| = m 2^E, m in [0.5, 1) (s * max < 2^15; 1 for a zero
+    or non-finite row) and its inverse.  [R] each."""
+    mx = _f(x).abs().amax(-1)
+    ok = (mx > 0) & torch.isfinite(mx)
+    _, e = torch.frexp(torch.where(ok, mx, torch.ones_like(mx)))
+    sh = torch.where(ok, 15 - e, torch.zeros_like(e)).to(torch.float32)
+    return torch.exp2(sh), torch.exp2(-sh)
+
+
+def split_h3_dyn(x: torch.Tensor, post: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """fp32 rows [R, K] -> (h3 activation [R, 2K] of s_r x_r, rinv [R] = post / s_r): the GEMM input of a gradient,
+    whose per-row epilogue scale ``rinv`` undoes s exactly."""
+    s, inv = h3_row_scales(x)
+    xs = _f(x) * s.view(-1, 1)
+    hi = xs.to(torch.float16)
+    lo = (xs - hi.float()).to(torch.float16)
+    rinv = inv if post is None else inv * _f(post)
+    return torch.cat([hi, lo], -1).contiguous(), rinv
+
+
+def lrp_swiglu_bwd_h3(dm, gu, post=None):
+    """``lrp_swiglu_bwd`` in fp32, as a per-row-scaled h3 activation (csrc/lrp_f32.hip)."""
+    return split_h3_dyn(lrp_swiglu_bwd(_f(dm), _f(gu)), post)
+
+
+def lrp_gelu_bwd_h3(dy, a):
+    return split_h3_dyn(lrp_gelu_bwd(_f(dy), _f(a)))
+
+
+def lrp_rope_pack_h3(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, post=None):
+    return split_h3_dyn(lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale), post)
+
+
+def act_h3(x: torch.Tensor, act: str, s: float) -> torch.Tensor:
+    """SwiGLU (interleaved gate|up [T, 2I] -> [T, I]) or GELU of fp32 pre-activations, as the h3 activation at s."""
+    y = swiglu_il(_f(x)) if act == "swiglu_il" else gelu(_f(x))
+    return h3_act(y, s)
+
+
+def row_rstd(x: torch.Tensor, eps: float, center: bool = False) -> torch.Tensor:
+    xf = _f(x)
+    if center:
+        xf = xf - xf.mean(-1, keepdim=True)
+    return torch.rsqrt(xf.pow(2).mean(-1) + eps)
+
+
+def group_absprod(x: torch.Tensor, dx: torch.Tensor, B: int, S: int, group: int = 64) -> torch.Tensor:
+    """[B, H / group]: sum over each window's tokens and the group's channels of |x dx|."""
+    H = x.shape[-1]
+    return (_f(x) * _f(dx)).abs().view(B, S, H // group, group).sum((1, 3))

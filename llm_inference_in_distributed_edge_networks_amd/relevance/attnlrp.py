@@ -20,9 +20,10 @@ framework's own model weights ("efficient" LRP = Input x modified-Gradient):
 
 The tests check per-rule conservation (Gradient x Input through each rule sums to the output relevance)
 and that the head relevance computed from the head outputs equals the literal S x S probability hook.
-``head_relevance`` here is the autograd oracle (fp32, one window).  The production pass is
-``engine.RelevanceEngine``: the same rules as explicit backward kernels (``csrc/lrp.hip``), batched over
-windows, checked against this oracle by the tests.
+``head_relevance`` here is the autograd oracle (fp32, one window).  The production passes are the explicit-backward
+engines, batched over windows and checked against this oracle by the tests: ``engine_f32.RelevanceEngineH3`` at the
+reference's precision (fp32: h3 GEMMs, ``csrc/lrp_f32.hip``) and ``engine.RelevanceEngine`` with bf16 storage
+(``csrc/lrp.hip``).
 """
 from __future__ import annotations
 
@@ -225,24 +226,35 @@ def relevance_main(p) -> list:
     env = init_distributed(p.device)
     device = str(env.device)
     cfg = get_config(p.model or "qwen2-0.5b")
-    # engine: the reference's precision (fp32, "auto") runs the AttnLRP rules as autograd on plain PyTorch ops
-    # (head_relevance_batched); dtype "bf16" on the GPU runs the explicit-backward HIP engine (csrc/lrp.hip, ~10x
-    # faster, bf16 storage: head table within ~10 % of the fp32 one, tests/test_lrp_gpu.py)
+    # engine: on a GPU the explicit-backward HIP engines - fp32 ("auto" = the reference's precision): h3 GEMMs on
+    # the transposed weights + the fp32 attention rule (engine_f32.RelevanceEngineH3, head table within 1e-4 of the
+    # CPU fp32 oracle); bf16: csrc/lrp.hip with bf16 storage (engine.RelevanceEngine, within ~3 %).  The autograd
+    # rules (head_relevance_batched) run on the CPU, or anywhere with lrp_engine "autograd".
     dtype = resolve_dtype(p, device) if p.dtype != "auto" else torch.float32
     if p.window_batch <= 0:   # auto: 8 windows per relevance batch (forward + AttnLRP backward)
         p.window_batch = 8
-    fast = device.startswith("cuda") and dtype == torch.bfloat16
+    kind = getattr(p, "lrp_engine", "auto")
+    if kind not in ("auto", "hip", "autograd"):
+        raise ValueError(f"lrp_engine must be auto, hip or autograd (got {kind!r})")
+    on_gpu = device.startswith("cuda")
+    if kind == "hip" and not on_gpu:
+        raise ValueError("lrp_engine 'hip' needs a GPU")
+    use_hip = on_gpu and kind != "autograd"
     model, prov = build_model(cfg, device, dtype, weights=p.weights, seed=p.seed)
     ids, data_prov = token_stream(p.dataset, cfg.hf_id, cfg.vocab_size, p.synthetic_tokens, p.seed,
                                   strict=p.strict_data)
     wins = sliding_windows(ids.shape[1], p.max_length or 512, p.stride)
     if p.max_windows:
         wins = wins[: p.max_windows]
+    dname = str(dtype).replace("torch.", "")
     log(f"relevance: model={cfg.name} weights={prov} data={data_prov} windows={len(wins)} "
-        f"engine={'hip-bf16' if fast else 'autograd-' + str(dtype).replace('torch.', '')}")
+        f"engine={('hip-' if use_hip else 'autograd-') + dname}")
     from ..eval.windows import batches
-    from .engine import RelevanceEngine
-    eng = RelevanceEngine(model) if fast else None
+    eng = None
+    if use_hip:
+        from .engine import RelevanceEngine
+        from .engine_f32 import RelevanceEngineH3
+        eng = RelevanceEngineH3(model) if dtype == torch.float32 else RelevanceEngine(model)
     G = cfg.hidden_size // 64
     acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=device)
     cacc = torch.zeros(cfg.num_layers, G, dtype=torch.float64, device=device)
@@ -250,7 +262,7 @@ def relevance_main(p) -> list:
     for bi, b in enumerate(batches(ids, wins, max(1, p.window_batch))):
         if bi % env.world_size != env.rank:
             continue
-        if fast:
+        if eng is not None:
             rel, _, _, chan = eng.head_relevance(b.ids, want_channels=True)
         else:
             rel, _, _, chan = head_relevance_batched(model, b.ids.to(device), dtype)

@@ -98,26 +98,116 @@ def test_relevance_engine_gpu_vs_cpu(cfg):
     assert rel_err(wg / wg.sum(-1, keepdim=True), wc / wc.sum(-1, keepdim=True)) < 0.1
 
 
+@pytest.mark.parametrize("B,Hq,Hkv,S", [(2, 14, 2, 512), (1, 8, 8, 200), (3, 4, 2, 96), (1, 2, 1, 37)])
+def test_lrp_attn_bwd_f32(B, Hq, Hkv, S):
+    """fp32 attention LRP backward (fp32 matrix cores) vs the fp32 reference: fp32-rounding agreement."""
+    f = torch.float32
+    q = rnd(B, Hq, S, 64, s=0.5, seed=1, dtype=f) * 0.125
+    k = rnd(B, Hkv, S, 64, s=0.5, seed=2, dtype=f)
+    v = rnd(B, Hkv, S, 64, seed=3, dtype=f)
+    dO = rnd(B * S, Hq * 64, seed=4, dtype=f)
+    vt = torch.zeros(B, Hkv, 64, R.s_pad(S), dtype=f)
+    vt[..., :S] = v.transpose(-1, -2)
+    o, lse = R.attention(q, k, vt, S, need_lse=True)
+    ref = R.lrp_attn_bwd(q.double(), k.double(), v.double(), o.double(), dO.double(), lse.double())
+    got = ops.lrp_attn_bwd(*(t.to(DEV) for t in (q, k, v, o, dO)), lse.float().contiguous().to(DEV))
+    for n, g_, r_ in zip(["D", "rel", "dq", "dk", "dv"], got, ref):
+        assert g_.shape == r_.shape and g_.dtype == torch.float32, n
+        e = rel_err(g_, r_)
+        assert e < 2e-6, f"{n}: rel err {e:.3g}"
+
+
+def test_fp32_lrp_rule_kernels():
+    """Per-row-scaled h3 outputs of the fp32 rules: planes bit-identical to the reference split (split_h3_dyn,
+    rope pack) or within fp32 rounding of the rule (SwiGLU / GELU transcendentals), every row's max below 2^15."""
+    f = torch.float32
+    x = rnd(301, 896, seed=20, dtype=f) * torch.logspace(-6, 6, 301).view(-1, 1)
+    x[7] = 0.0
+    post = torch.rand(301) + 0.5
+    g3, gi = ops.split_h3_dyn(x.to(DEV), post.to(DEV))
+    r3, ri = R.split_h3_dyn(x, post)
+    assert torch.equal(g3.cpu(), r3) and torch.equal(gi.cpu(), ri)
+    assert g3.float().abs().max() < 2 ** 15
+    back = R.h3_to_f32(g3.cpu()) * (gi.cpu() / post).view(-1, 1)
+    assert rel_err(back, x) < 1e-7
+    # SwiGLU rule
+    gu, dm = rnd(97, 2 * 512, seed=21, dtype=f) * 3, rnd(97, 512, seed=22, dtype=f)
+    d3, di = ops.lrp_swiglu_bwd_h3(dm.to(DEV), gu.to(DEV), post[:97].to(DEV))
+    val = R.h3_to_f32(d3.cpu()) * di.cpu().view(-1, 1)
+    assert rel_err(val, R.lrp_swiglu_bwd(dm.double(), gu.double()) * post[:97].double().view(-1, 1)) < 1e-6
+    # GELU rule
+    a = rnd(97, 512, seed=23, dtype=f) * 3
+    d3, di = ops.lrp_gelu_bwd_h3(dm.to(DEV), a.to(DEV))
+    assert rel_err(R.h3_to_f32(d3.cpu()) * di.cpu().view(-1, 1), R.lrp_gelu_bwd(dm.double(), a.double())) < 1e-6
+    # forward activations at a fixed scale
+    for act, inp in (("swiglu_il", gu), ("gelu", a)):
+        got = R.h3_to_f32(ops.act_h3(inp.to(DEV), act, 2.0 ** 10).cpu(), 2.0 ** 10)
+        want = R.swiglu_il(inp.double()) if act == "swiglu_il" else R.gelu(inp.double())
+        assert rel_err(got, want) < 1e-6, act
+    # inverse RoPE + GQA sum + pack
+    B, S, Hq, Hkv = 2, 70, 4, 2
+    for rot in (64, 16):
+        cos, sin = R.rope_tables(128, rot, 1e4)
+        dq, dk, dv = (rnd(B, Hq, S, 64, seed=sd, dtype=f) for sd in (5, 6, 7))
+        want = R.lrp_rope_pack(dq.double(), dk.double(), dv.double(), cos.double(), sin.double(), B, S, Hq, Hkv,
+                               rot, 0.125)
+        g3, gi = ops.lrp_rope_pack_h3(dq.to(DEV), dk.to(DEV), dv.to(DEV), cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv,
+                                      rot, 0.125)
+        assert rel_err(R.h3_to_f32(g3.cpu()) * gi.cpu().view(-1, 1), want) < 1e-6
+    # norm statistics, LayerNorm rule, channel-group sums
+    y = rnd(300, 256, seed=24, dtype=f) * 2 + 0.5
+    for center in (False, True):
+        assert rel_err(ops.row_rstd(y.to(DEV), 1e-5, center), R.row_rstd(y.double(), 1e-5, center)) < 1e-6
+    rs = R.row_rstd(y, 1e-5, True)
+    dy1, dy2, res = (rnd(300, 256, seed=sd, dtype=f) for sd in (25, 26, 27))
+    w1, w2 = rnd(256, seed=28, dtype=f), rnd(256, seed=29, dtype=f)
+    got = ops.lrp_ln_bwd_f32(dy1.to(DEV), rs.to(DEV), w1.to(DEV), dy2.to(DEV), w2.to(DEV), res.to(DEV))
+    assert rel_err(got, R.lrp_ln_bwd(dy1.double(), rs.double(), w1.double(), dy2.double(), rs.double(),
+                                     w2.double(), res.double())) < 1e-6
+    xx, dd = rnd(3 * 50, 256, seed=30, dtype=f), rnd(3 * 50, 256, seed=31, dtype=f)
+    assert rel_err(ops.group_absprod(xx.to(DEV), dd.to(DEV), 3, 50), R.group_absprod(xx.double(), dd.double(), 3,
+                                                                                    50)) < 1e-6
+
+
+@pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX], ids=lambda c: c.name)
+def test_relevance_engine_h3_tiny_vs_autograd(cfg):
+    """fp32 HIP relevance engine vs the autograd oracle (fp64 on the CPU, same weights)."""
+    from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import head_relevance_batched
+    from llm_inference_in_distributed_edge_networks_amd.relevance.engine_f32 import RelevanceEngineH3
+    mg = DecoderLM.random_init(cfg, 3, device=DEV, std=0.05)
+    mc = DecoderLM.random_init(cfg, 3, std=0.05)
+    ids = torch.randint(0, cfg.vocab_size, (4, 128), generator=torch.Generator().manual_seed(2))
+    rg, ing, mxg, cg = RelevanceEngineH3(mg).head_relevance(ids.to(DEV), want_channels=True)
+    rc, inc, mxc, cc = head_relevance_batched(mc, ids, dtype=torch.float64)
+    for n, a, b in (("rel", rg, rc), ("in_rel", ing, inc), ("seed", mxg, mxc), ("chan", cg, cc)):
+        e = rel_err(a, b)
+        assert e < 1e-5, f"{n}: {e:.3g}"
+
+
 def test_fp32_calibration_table_matches_cpu_full_qwen2():
-    """The reference-precision calibration (dtype fp32 / auto: AttnLRP as autograd on the GPU) on the full
-    24-layer Qwen2-0.5B shape: normalised head table within 2 % (relative L2) of the CPU fp32 oracle on the same
-    random weights and windows, and the channel-group relevance too; the bf16 HIP engine's deviation is printed."""
+    """The reference-precision calibration on the full 24-layer Qwen2-0.5B (one 512-token window, bf16-valued random
+    weights as the HF checkpoint): the fp32 HIP engine's normalised head table and channel-group table within 1e-4
+    (relative L2) of the CPU fp32 autograd oracle on the same weights; the bf16 HIP engine within 4 %."""
     from llm_inference_in_distributed_edge_networks_amd.models import get_config
     from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import (head_relevance_batched,
                                                                                   normalize_per_layer)
     from llm_inference_in_distributed_edge_networks_amd.relevance.engine import RelevanceEngine
+    from llm_inference_in_distributed_edge_networks_amd.relevance.engine_f32 import RelevanceEngineH3
     cfg = get_config("qwen2-0.5b")
-    mc = DecoderLM.random_init(cfg, 7, std=0.02)
-    mg = DecoderLM.random_init(cfg, 7, device=DEV, std=0.02, h3=False)
-    ids = torch.randint(0, cfg.vocab_size, (2, 128), generator=torch.Generator().manual_seed(3))
+    mc = DecoderLM.random_init(cfg, 7, std=0.02, values=torch.bfloat16)
+    mg = DecoderLM.random_init(cfg, 7, device=DEV, std=0.02, values=torch.bfloat16)
+    ids = torch.randint(0, cfg.vocab_size, (1, 512), generator=torch.Generator().manual_seed(3))
     rc, _, _, cc = head_relevance_batched(mc, ids)
-    rg, _, _, cg = head_relevance_batched(mg, ids.to(DEV))
-    tc, tg = normalize_per_layer(rc.sum(0)), normalize_per_layer(rg.sum(0))
-    e_head = rel_err(tg, tc)
+    rg, _, _, cg = RelevanceEngineH3(mg).head_relevance(ids.to(DEV), want_channels=True)
+    tc = normalize_per_layer(rc.sum(0))
+    e_head = rel_err(normalize_per_layer(rg.sum(0)), tc)
     e_chan = rel_err(normalize_per_layer(cg.sum(0)), normalize_per_layer(cc.sum(0)))
+    e_raw = rel_err(rg, rc)
+    del mg
     mb = DecoderLM.random_init(cfg, 7, device=DEV, dtype=torch.bfloat16, std=0.02)
     rb, _, _ = RelevanceEngine(mb).head_relevance(ids.to(DEV))
     e_bf16 = rel_err(normalize_per_layer(rb.sum(0)), tc)
-    print(f"normalised head table vs CPU fp32: fp32 GPU {e_head:.2e}, bf16 HIP engine {e_bf16:.2e}; "
-          f"channel groups {e_chan:.2e}")
-    assert e_head < 0.02 and e_chan < 0.02
+    print(f"normalised head table vs CPU fp32: fp32 HIP engine {e_head:.2e} (raw {e_raw:.2e}), bf16 HIP engine "
+          f"{e_bf16:.2e}; channel groups {e_chan:.2e}")
+    assert e_head < 1e-4 and e_chan < 1e-4 and e_raw < 1e-4
+    assert e_bf16 < 0.04

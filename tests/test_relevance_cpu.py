@@ -1,5 +1,6 @@
 """AttnLRP rules (own re-implementation of the lxt rule set used by Experiments/Relevance/main.py)."""
 import torch
+import pytest
 
 from llm_inference_in_distributed_edge_networks_amd.models import TINY_NEOX, TINY_QWEN2, DecoderLM
 from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import (_IdentityAct, _UniformMatmul,
@@ -109,3 +110,20 @@ def test_batched_autograd_and_channel_relevance():
         rel_e, _, _, chan_e = RelevanceEngine(m).head_relevance(ids, want_channels=True)
         assert torch.allclose(rel_e, rel, rtol=1e-4, atol=1e-5)
         assert torch.allclose(chan_e, chan, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("arch", ["qwen2", "neox"])
+def test_h3_relevance_engine_cpu_equals_autograd(arch):
+    """The fp32 relevance engine's op sequence (forward with saves on h3 GEMMs, explicit LRP backward on the
+    transposed h3 weights with per-row gradient scales) on the CPU reference ops == the autograd oracle."""
+    from llm_inference_in_distributed_edge_networks_amd.models import TINY_NEOX, TINY_QWEN2, DecoderLM
+    from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import head_relevance_batched
+    from llm_inference_in_distributed_edge_networks_amd.relevance.engine_f32 import RelevanceEngineH3
+    cfg = TINY_QWEN2 if arch == "qwen2" else TINY_NEOX
+    m = DecoderLM.random_init(cfg, 0, h3=True)
+    ids = torch.randint(0, cfg.vocab_size, (3, 96), generator=torch.Generator().manual_seed(1))
+    got = RelevanceEngineH3(m).head_relevance(ids, want_channels=True)
+    want = head_relevance_batched(m, ids, dtype=torch.float64)
+    for n, a, b in zip(("rel", "in_rel", "seed", "chan"), got, want):
+        e = float((a.double() - b).norm() / b.norm())
+        assert e < 1e-5, (n, e)

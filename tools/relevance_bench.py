@@ -17,6 +17,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 from llm_inference_in_distributed_edge_networks_amd.models import DecoderLM, get_config  # noqa: E402
 from llm_inference_in_distributed_edge_networks_amd.relevance.engine import RelevanceEngine  # noqa: E402
+from llm_inference_in_distributed_edge_networks_amd.relevance.engine_f32 import RelevanceEngineH3  # noqa: E402
 
 REF_TOKENS_PER_S = 9331 * 512 / (77 * 60 + 20)
 
@@ -28,11 +29,17 @@ def main():
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="fp32: the reference-precision engine (h3 GEMMs, fp32 attention rule); bf16: bf16 storage")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args()
     cfg = get_config(a.model)
-    m = DecoderLM.random_init(cfg, 0, device="cuda", dtype=torch.bfloat16)
-    eng = RelevanceEngine(m)
+    if a.dtype == "fp32":   # bf16-valued fp32 weights: what the reference computes with (HF bf16 checkpoint upcast)
+        m = DecoderLM.random_init(cfg, 0, device="cuda", dtype=torch.float32, values=torch.bfloat16)
+        eng = RelevanceEngineH3(m)
+    else:
+        m = DecoderLM.random_init(cfg, 0, device="cuda", dtype=torch.bfloat16)
+        eng = RelevanceEngine(m)
     ids = torch.randint(0, cfg.vocab_size, (a.batch, a.seq), generator=torch.Generator().manual_seed(0)).cuda()
     for _ in range(a.warmup):
         rel, _, _ = eng.head_relevance(ids)
@@ -48,7 +55,7 @@ def main():
            "tokens_per_s": round(tps, 1), "reference_tokens_per_s_T4": round(REF_TOKENS_PER_S, 1),
            "vs_reference": round(tps / REF_TOKENS_PER_S, 1), "finite": bool(torch.isfinite(rel).all()),
            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2),
-           "data": "synthetic ids, random-init weights", "dtype": "bf16"}
+           "data": "synthetic ids, random-init weights", "dtype": a.dtype}
     print(json.dumps(out), flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:
