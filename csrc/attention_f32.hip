@@ -628,6 +628,164 @@ __global__ __launch_bounds__(256) void attn_colsum_f32_kernel(const float* __res
   }
 }
 
+// ---- importance scorers on the split-plane matrix cores (the forward's h3 scheme) ----------------------------------
+// Column sums of P for one (b, q head, 64-key block): sum over query rows i >= key of exp(q_i . k_j - lse_i).  The scores
+// are the forward's: q and k as scaled fp16 h3 planes (powers of two sq, sk from the model's bounds), three fp16 MFMA
+// products per score (v_mfma_f32_16x16x32_f16), so P is consistent with the LSE the forward wrote.  S = Q K^T keeps the
+// key on the lane column: wave w owns keys kb*64 + 16w + (lane & 15), its K planes live in registers for the whole
+// sweep, and the lane's 4 query rows per 16-row sub-tile are summed in-lane (two shuffles at the very end).  Query
+// tiles of 64 rows (from the key block's diagonal to S) are split into planes once per workgroup and staged in LDS for
+// all four waves; LSE in log2 units in LDS; the causal mask runs only on the diagonal tile; exp2 on v_exp_f32.
+__global__ __launch_bounds__(256) void attn_colsum_h3_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                             const float* __restrict__ lse, float* __restrict__ out,
+                                                             int B, int Hq, int Hkv, int S, float sq, float sk) {
+  __shared__ __attribute__((aligned(16))) char lq[2 * XPL];   // Q hi / lo planes of the current 64-row tile
+  __shared__ float l2[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            cl = lane & 15;
+  const int kb = blockIdx.x / (B * Hq);                   // key block 0 (most causal queries) first
+  const int bh = blockIdx.x - kb * (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
+  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
+  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const float* lh = lse + ((size_t)b * Hq + h) * S;
+  const float sc_log2 = FLOG2E / (sq * sk);
+
+  const int key = kb * 64 + wave * 16 + cl;
+  const int kld = key < S ? key : S - 1;
+  bf16x8_t kp[2][2];                      // B operand: K[key][d = 32 ks + 8g .. +7], hi / lo
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    float v[8];
+    const f32x4_t a = *(const f32x4_t*)(kh + (size_t)kld * 64 + 32 * ks + 8 * g);
+    const f32x4_t c = *(const f32x4_t*)(kh + (size_t)kld * 64 + 32 * ks + 8 * g + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = c[e]; }
+    split_planes<true>(v, sk, kp[ks]);
+  }
+  // staging: 64 rows x 64 floats, 16 consecutive floats (two 8-float chunks) per thread
+  const int srow = tid >> 2, scol = (tid & 3) * 16;
+  f32x4_t qreg[4];
+  auto load_tile = [&](int q0) {
+    const int r = q0 + srow;
+    if (r < S) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qreg[i] = *(const f32x4_t*)(qh + (size_t)r * 64 + scol + 4 * i);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qreg[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  float csum = 0.f;
+  const int qt0 = kb * 64;
+  load_tile(qt0);
+  for (int q0 = qt0; q0 < S; q0 += 64) {
+    __syncthreads();                       // every wave's reads of the previous tile retired
+#pragma unroll
+    for (int hc = 0; hc < 2; ++hc) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] = qreg[2 * hc][e]; v[4 + e] = qreg[2 * hc + 1][e]; }
+      bf16x8_t p[2];
+      split_planes<true>(v, sq, p);
+      const int c = scol / 8 + hc;
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) *(bf16x8_t*)(lq + pl * XPL + srow * 128 + ((c ^ xsw(srow)) << 4)) = p[pl];
+    }
+    if (tid < 64) l2[tid] = q0 + tid < S ? lh[q0 + tid] * FLOG2E : INFINITY;
+    __syncthreads();
+    if (q0 + 64 < S) load_tile(q0 + 64);
+    const bool diag = q0 == qt0;           // only the first query tile crosses the causal diagonal
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      f32x4_t st = {0.f, 0.f, 0.f, 0.f};
+      const int row = sub * 16 + cl;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t qf[2];
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) qf[pl] = xfrag(lq + pl * XPL, row, 4 * ks + g);
+        st = h3_dot(qf, kp[ks], st);
+      }
+      // st[r] = score(query q0 + sub*16 + 4g + r, key)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = sub * 16 + 4 * g + r;
+        float pv = __builtin_amdgcn_exp2f(fmaf(st[r], sc_log2, -l2[ql]));
+        if (diag && q0 + ql < key) pv = 0.f;
+        csum += pv;
+      }
+    }
+  }
+  csum += __shfl_xor(csum, 16, 64);
+  csum += __shfl_xor(csum, 32, 64);
+  if (g == 0 && key < S) out[((size_t)b * Hq + h) * S + key] = csum;
+}
+
+// Last-row probabilities P[S-1, :] of the G = Hq / Hkv query heads of one (b, kv head) at once: the G last query rows
+// are the MFMA A rows (up to 16), K the B columns, scores on the h3 planes as above; the G x S score rows go to LDS and a
+// block softmax per head row finishes in fp32.
+__global__ __launch_bounds__(256) void attn_lastrow_h3_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                              float* __restrict__ out, int Hq, int Hkv, int S,
+                                                              float sq, float sk) {
+  extern __shared__ float sc[];            // G x S scores
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int G = Hq / Hkv;
+  const int bk = blockIdx.x, b = bk / Hkv, hk = bk - b * Hkv;
+  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const float inv_s = 1.f / (sq * sk);
+  bf16x8_t qa[2][2];                       // A operand: row cl = head hk*G + cl (zero beyond G), d = 32 ks + 8g ..
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (cl < G) {
+      const float* qr = q + (((size_t)b * Hq + hk * G + cl) * S + (S - 1)) * 64 + 32 * ks + 8 * g;
+      const f32x4_t a = *(const f32x4_t*)qr, c = *(const f32x4_t*)(qr + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = c[e]; }
+    }
+    split_planes<true>(v, sq, qa[ks]);
+  }
+  for (int k0 = wave * 16; k0 < S; k0 += 64) {
+    const int key = k0 + cl, kld = key < S ? key : S - 1;
+    f32x4_t st = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      float v[8];
+      const f32x4_t a = *(const f32x4_t*)(kh + (size_t)kld * 64 + 32 * ks + 8 * g);
+      const f32x4_t c = *(const f32x4_t*)(kh + (size_t)kld * 64 + 32 * ks + 8 * g + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = c[e]; }
+      bf16x8_t kf[2];
+      split_planes<true>(v, sk, kf);
+      st = h3_dot(qa[ks], kf, st);
+    }
+    // st[r] = score(head row 4g + r, key)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hr = 4 * g + r;
+      if (hr < G && key < S) sc[hr * S + key] = st[r] * inv_s;
+    }
+  }
+  __syncthreads();
+  for (int hr = 0; hr < G; ++hr) {
+    float* row = sc + hr * S;
+    float mx = -INFINITY;
+    for (int j = tid; j < S; j += 256) mx = fmaxf(mx, row[j]);
+    mx = block_max<256>(mx, red);
+    float sum = 0.f;
+    for (int j = tid; j < S; j += 256) {
+      const float p = expf(row[j] - mx);
+      row[j] = p;
+      sum += p;
+    }
+    sum = block_sum<256>(sum, red);
+    const float inv = 1.f / sum;
+    float* orow = out + ((size_t)b * Hq + hk * G + hr) * S;
+    for (int j = tid; j < S; j += 256) orow[j] = row[j] * inv;
+  }
+}
+
 static int g_attn_f32_variant = 2;   // 0: split-plane MFMA kernel, 64 query rows per workgroup; 2 (default): the same
                                      // with 128 rows (8 waves); 1: native f32 MFMA kernel (A/B)
 EDGE_API int edge_attn_f32_set_variant(int v) {
@@ -674,19 +832,32 @@ EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float
   return (int)hipGetLastError();
 }
 
-EDGE_API int edge_attn_lastrow_f32(const float* q, const float* k, float* out, int B, int Hq, int Hkv, int S,
-                                   hipStream_t st) {
+// sq, sk > 0: scores on the scaled fp16 h3 planes (the forward's matrix-core scheme, the caller guarantees
+// s |x| <= 2^15 for q and k); 0: the native f32-MFMA / scalar kernels (exact fp32 products).
+EDGE_API int edge_attn_lastrow_f32(const float* q, const float* k, float* out, int B, int Hq, int Hkv, int S, float sq,
+                                   float sk, hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
-  if (Hq % Hkv || S > 16384) return (int)hipErrorInvalidValue;
+  if (Hkv <= 0 || Hq % Hkv || S > 16384) return (int)hipErrorInvalidValue;
+  const int G = Hq / Hkv;
+  if (sq > 0.f && sk > 0.f && G <= 16 && (size_t)G * S * sizeof(float) <= 60 * 1024) {
+    hipLaunchKernelGGL(attn_lastrow_h3_kernel, dim3(B * Hkv), dim3(256), G * S * sizeof(float), st, q, k, out, Hq, Hkv,
+                       S, sq, sk);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(attn_lastrow_f32_kernel, dim3(B * Hq), dim3(256), S * sizeof(float), st, q, k, out, Hq, Hkv, S);
   return (int)hipGetLastError();
 }
 
 EDGE_API int edge_attn_colsum_f32(const float* q, const float* k, const float* lse, float* out, int B, int Hq, int Hkv,
-                                  int S, hipStream_t st) {
+                                  int S, float sq, float sk, hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
-  if (Hq % Hkv) return (int)hipErrorInvalidValue;
+  if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
   const int nkb = (S + 63) / 64;
+  if (sq > 0.f && sk > 0.f) {
+    hipLaunchKernelGGL(attn_colsum_h3_kernel, dim3(B * Hq * nkb), dim3(256), 0, st, q, k, lse, out, B, Hq, Hkv, S, sq,
+                       sk);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(attn_colsum_f32_kernel, dim3(B * Hq * nkb), dim3(256), 0, st, q, k, lse, out, B, Hq, Hkv, S);
   return (int)hipGetLastError();
 }

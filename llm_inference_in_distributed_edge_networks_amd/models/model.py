@@ -415,9 +415,11 @@ class DecoderLM:
         kinds = self._stat_kinds(stats)
         q, k, o3, lse, h23 = self._attn_h3(i, x, B, S, need_lse="colsum" in kinds)
         st = None
-        if kinds:
-            st = AttnStats(lastrow=ops.attn_lastrow(q, k, S) if "lastrow" in kinds else None,
-                           colsum=ops.attn_colsum(q, k, lse, S) if "colsum" in kinds else None)
+        if kinds:   # the scores on the forward's scaled fp16 planes (consistent with its LSE)
+            sc = self.h3_layer[i]
+            qk = (sc["att_q"], sc["att_k"])
+            st = AttnStats(lastrow=ops.attn_lastrow(q, k, S, in_scales=qk) if "lastrow" in kinds else None,
+                           colsum=ops.attn_colsum(q, k, lse, S, in_scales=qk) if "colsum" in kinds else None)
         return self._mlp_h3(i, o3, x, h23), st
 
     def layer_rows(self, i: int, x: torch.Tensor, B: int, S: int, rows: torch.Tensor,

@@ -347,23 +347,34 @@ def set_attn_variant(v: int) -> None:
     call("edge_attn_set_variant", int(v))
 
 
-def attn_lastrow(q, k, S):
+def attn_lastrow(q, k, S, in_scales=None):
+    """P[S-1, :] per head [B, Hq, S] fp32.  fp32 q/k with ``in_scales`` = (s_q, s_k) (the attention's plane scales):
+    scores on the scaled fp16 planes of the forward (matrix cores); without: exact fp32 products."""
     if not _gpu(q):
         return ref.attn_lastrow(q, k, S)
     B, Hq = q.shape[:2]
     out = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
-    fn = "edge_attn_lastrow_f32" if q.dtype == torch.float32 else "edge_attn_lastrow"
-    call(fn, ptr(q), ptr(k), ptr(out), B, Hq, k.shape[1], S, stream())
+    if q.dtype == torch.float32:
+        sq, sk = in_scales if in_scales is not None else (0.0, 0.0)
+        call("edge_attn_lastrow_f32", ptr(q), ptr(k), ptr(out), B, Hq, k.shape[1], S, float(sq), float(sk), stream())
+        return out
+    call("edge_attn_lastrow", ptr(q), ptr(k), ptr(out), B, Hq, k.shape[1], S, stream())
     return out
 
 
-def attn_colsum(q, k, lse, S):
+def attn_colsum(q, k, lse, S, in_scales=None):
+    """Column sums sum_i P[i, j] per head [B, Hq, S] fp32 from q, k and the forward's row LSE.  fp32 q/k with
+    ``in_scales`` = (s_q, s_k): the split-plane matrix-core kernel (the forward's scores); without: exact fp32."""
     if not _gpu(q):
         return ref.attn_colsum(q, k, lse, S)
     B, Hq = q.shape[:2]
     out = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device)
-    fn = "edge_attn_colsum_f32" if q.dtype == torch.float32 else "edge_attn_colsum"
-    call(fn, ptr(q), ptr(k), ptr(lse.contiguous()), ptr(out), B, Hq, k.shape[1], S, stream())
+    if q.dtype == torch.float32:
+        sq, sk = in_scales if in_scales is not None else (0.0, 0.0)
+        call("edge_attn_colsum_f32", ptr(q), ptr(k), ptr(lse.contiguous()), ptr(out), B, Hq, k.shape[1], S, float(sq),
+             float(sk), stream())
+        return out
+    call("edge_attn_colsum", ptr(q), ptr(k), ptr(lse.contiguous()), ptr(out), B, Hq, k.shape[1], S, stream())
     return out
 
 

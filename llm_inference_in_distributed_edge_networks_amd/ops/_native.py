@@ -73,8 +73,8 @@ _SIGS = {
     "edge_gemm_qkv_rope_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f,
                                c_f, c_p],
     "edge_flash_attn_fwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_f, c_f, c_f, c_p],
-    "edge_attn_lastrow_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
-    "edge_attn_colsum_f32": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    "edge_attn_lastrow_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_f, c_p],
+    "edge_attn_colsum_f32": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_f, c_p],
     "edge_rmsnorm_f32": [c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_f, c_p],
     "edge_layernorm_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_f, c_f, c_p],
     "edge_split_h3": [c_p, c_p, c_p, c_i, c_i, c_f, c_p],

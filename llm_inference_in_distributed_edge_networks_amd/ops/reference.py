@@ -33,7 +33,8 @@ IL_BLOCK = 16  # gate/up interleave granularity (rows)
 
 
 def _f(x):
-    return x.float()
+    """fp32 view of an operand (fp64 stays fp64: the oracles also run in double precision for the tests)."""
+    return x if x.dtype == torch.float64 else x.float()
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:

@@ -246,6 +246,12 @@ def test_importance_stats_f32(B, S, Hq, Hkv):
     assert rel_err(lr, R.attn_lastrow(q.double(), k.double(), S)) < 2e-6
     cs = ops.attn_colsum(q.to(DEV), k.to(DEV), rl.float().to(DEV), S)
     assert rel_err(cs, R.attn_colsum(q.double(), k.double(), rl, S)) < 5e-6
+    # the split-plane matrix-core kernels (the model's fp32 path): scores on h3 planes at the bound scales
+    sc = (R.h3_scale(q.abs().max().item()), R.h3_scale(k.abs().max().item()))
+    lr = ops.attn_lastrow(q.to(DEV), k.to(DEV), S, in_scales=sc)
+    assert rel_err(lr, R.attn_lastrow(q.double(), k.double(), S)) < 2e-6
+    cs = ops.attn_colsum(q.to(DEV), k.to(DEV), rl.float().to(DEV), S, in_scales=sc)
+    assert rel_err(cs, R.attn_colsum(q.double(), k.double(), rl, S)) < 5e-6
 
 
 @pytest.mark.parametrize("R_", [200, 2048])
@@ -370,3 +376,80 @@ def test_mx_codecs_gpu_equal_cpu(codec, dtype):
         assert torch.equal(y_gpu, y_cpu)
     else:   # bf16 activations: the hi class is bf16 on the GPU, the MX values are exact in bf16 or rounded once
         assert (y_gpu - y_cpu).abs().max() <= 0.01 * y_cpu.abs().max()
+
+
+# ---- discriminating whole-model checks: final hidden state, peaked-output NLL, and their sensitivity ------------
+# (reference oracle: the monolithic fp32 model, Experiments/Qwen2-0.5B/qwen_layer_wise.py:78-104)
+HIDDEN_TOL, NLL_TOL = 1e-5, 1e-5
+
+
+def _model(cfg, seed, dev, values, head_scale):
+    """Random model of the exact architecture; ``head_scale`` multiplies the LM head (a power of two, so bf16 / fp16
+    values stay exact): logits then spread over tens of nats, the output distribution is peaked and the per-row NLL
+    moves with the hidden state instead of sitting at ~ln |V| (std-0.02 random heads give a near-uniform softmax)."""
+    from llm_inference_in_distributed_edge_networks_amd.models import DecoderLM
+    m = DecoderLM.random_init(cfg, seed, device=dev, dtype=torch.float32, values=values, h3=False)
+    w = m.w
+    w["head"] = w["head"] * head_scale
+    return DecoderLM(cfg, w, dev, torch.float32)
+
+
+def _hidden_and_nll(m, b):
+    from llm_inference_in_distributed_edge_networks_amd.eval.windows import window_nll
+    x = m.forward_hidden(b.ids)
+    rows = m.row_nll(x, b.rows, b.targets)
+    return x.double().cpu(), rows.double().cpu(), window_nll(rows, b).double().cpu()
+
+
+def _l2(a, b):
+    return float((a - b).norm() / b.norm())
+
+
+class _PerturbOneGemm:
+    """Wraps ops.linear_h3: the ``which``-th fp32 GEMM of a forward gets its product scaled by (1 + eps)."""
+
+    def __init__(self, which, eps):
+        self.which, self.eps, self.n, self.orig = which, eps, 0, ops.linear_h3
+
+    def __call__(self, a3, w3, alpha, *args, **kw):
+        self.n += 1
+        if self.n == self.which:
+            alpha = alpha * (1.0 + self.eps)
+        return self.orig(a3, w3, alpha, *args, **kw)
+
+
+@pytest.mark.parametrize("name,B,S,values", [("qwen2-0.5b", 2, 512, torch.bfloat16), ("qwen2-0.5b", 1, 512, None),
+                                            ("pythia-70m", 1, 2048, torch.float16)])
+def test_full_model_hidden_state_and_peaked_nll(name, B, S, values, monkeypatch):
+    """GPU fp32 mode vs the CPU fp32 model (same weights, same windows), whole model (24-layer Qwen2-0.5B, 6-layer
+    Pythia-70M): the final hidden state within 1e-5 relative L2 and, with a peaked output distribution (row NLLs
+    spread over tens of nats), the per-row NLL of every scored row within 1e-5 relative L2.  Sensitivity: the same checks run on a GPU forward whose layer-3
+    output projection is perturbed by 1e-4 relative must FAIL both tolerances (else they could not see an error of
+    that size)."""
+    from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
+    from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows
+    from llm_inference_in_distributed_edge_networks_amd.models import get_config
+    cfg = get_config(name)
+    toks = synthetic_stream(S * 4, cfg.vocab_size, 5)
+    wins = [w for w in sliding_windows(toks.shape[1], S, 32) if w.length == S][:B]
+    b = next(batches(toks, wins, B))
+    xc, nc, wc = _hidden_and_nll(_model(cfg, 1, "cpu", values, 32.0), b)
+    mg = _model(cfg, 1, DEV, values, 32.0)
+    bg = b.to(DEV)
+    xg, ng, wg = _hidden_and_nll(mg, bg)
+    e_h, e_n = _l2(xg, xc), _l2(ng, nc)
+    spread = float(nc.std())       # nats; ~0 for a near-uniform softmax (random head), tens of nats here
+    # layer 3's O projection: the 2nd fp32 GEMM of a layer (QKV has its own entry point), 3 per Qwen2 layer /
+    # 3 per NeoX layer after the QKV
+    per_layer = 3
+    pert = _PerturbOneGemm(3 * per_layer + 1, 1e-4)
+    monkeypatch.setattr(ops, "linear_h3", pert)
+    xp, npp, _ = _hidden_and_nll(mg, bg)
+    monkeypatch.setattr(ops, "linear_h3", pert.orig)
+    p_h, p_n = _l2(xp, xc), _l2(npp, nc)
+    print(f"{name} values={values}: row-NLL spread {spread:.1f} nats (mean {float(nc.mean()):.1f}, ln|V| "
+          f"{math.log(cfg.vocab_size):.1f}); clean: hidden {e_h:.2e}, "
+          f"row NLL {e_n:.2e}; layer-3 O-proj x (1 + 1e-4): hidden {p_h:.2e}, row NLL {p_n:.2e}")
+    assert spread > 1.0
+    assert e_h < HIDDEN_TOL and e_n < NLL_TOL
+    assert p_h > HIDDEN_TOL and p_n > NLL_TOL, "the tolerances do not detect a 1e-4 GEMM perturbation"

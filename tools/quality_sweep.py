@@ -44,9 +44,6 @@ def main():
     dtype = torch.bfloat16 if (dev == "cuda" and a.dtype == "bf16") else torch.float32
     cfg = get_config(a.model)
     m = DecoderLM.load_native(cfg, a.weights, dev, dtype)
-    # the explicit LRP engine runs the bf16 kernels on the GPU: calibrate head weights on a bf16 copy
-    m_rel = m if (dev == "cpu" or dtype == torch.bfloat16) else DecoderLM.load_native(cfg, a.weights, dev,
-                                                                                      torch.bfloat16)
     layers = [int(x) for x in a.layers.split(",")]
     ratios = [float(x) for x in a.ratios.split(",")]
 
@@ -54,7 +51,13 @@ def main():
     t0 = time.time()
     tr = local_text_bytes("train")
     wins = sliding_windows(tr.shape[1], 512, 512)[: a.relevance_windows]
-    eng = RelevanceEngine(m_rel)
+    # LRP calibration at the sweep's precision: the fp32 engine (h3 GEMMs, fp32 attention rule) in fp32 mode on a GPU,
+    # the bf16 engine in bf16 mode, the autograd rules on the CPU
+    if dev == "cuda" and dtype == torch.float32:
+        from llm_inference_in_distributed_edge_networks_amd.relevance.engine_f32 import RelevanceEngineH3
+        eng = RelevanceEngineH3(m)
+    else:
+        eng = RelevanceEngine(m)
     acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=dev)
     cacc = torch.zeros(cfg.num_layers, cfg.hidden_size // 64, dtype=torch.float64, device=dev)
     for b in batches(tr, wins, a.batch):
