@@ -280,8 +280,9 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_f32_kernel(const float* __res
 }
 
 // ---------------------------------------------------------------------------------------------
-// Per-row power-of-two h3 split of rule outputs.  Every kernel below computes its row twice: a max pass and a
-// store pass (the recomputation is a handful of L1/L2 hits, and no register array of a model-dependent width).
+// Per-row power-of-two h3 split of rule outputs: a max pass and a store pass over the row.  For the model widths
+// (rows up to 2048 / 8192 / 1024 values) a thread's values stay in registers between the two, so the row is read
+// once; wider rows recompute them (template parameter 0).
 
 // Inverse RoPE + q scale + GQA group sum of the dK/dV partials + scatter into the token-major d[q|k|v] row,
 // as a per-row-scaled h3 activation out3 [B*S, 2W] (W = (Hq + 2Hkv) 64), rinv[row] = 1/s * post[row].
@@ -322,6 +323,7 @@ __device__ __forceinline__ float rope_pack_value(const float* __restrict__ dq, c
   return val * scale;
 }
 
+template <int NIT>   // NIT > 0: W <= 64 NIT, the row's values stay in registers between the max and the store
 __global__ __launch_bounds__(256) void lrp_rope_pack_h3_kernel(const float* __restrict__ dq, const float* __restrict__ dk,
                                                                const float* __restrict__ dv,
                                                                const float* __restrict__ cosT,
@@ -333,22 +335,43 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_h3_kernel(const float* __re
   if (row >= B * S) return;
   const int b = row / S, s = row - b * S, W = (Hq + 2 * Hkv) * 64;
   float mx = 0.f;
-  for (int c = lane; c < W; c += 64)
-    mx = fmaxf(mx, fabsf(rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale)));
+  float cache[NIT > 0 ? NIT : 1];
+  if constexpr (NIT > 0) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int c = lane + 64 * it;
+      cache[it] = c < W ? rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale) : 0.f;
+      mx = fmaxf(mx, fabsf(cache[it]));
+    }
+  } else {
+    for (int c = lane; c < W; c += 64)
+      mx = fmaxf(mx, fabsf(rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale)));
+  }
   mx = wave_max(mx);
   float inv;
   const float sc = row_pow2_scale(mx, inv);
   f16_t* o = out + (size_t)row * (2 * W);
-  for (int c = lane; c < W; c += 64) {
+  auto put = [&](int c, float v) {
     float hi, lo;
-    split2h(sc * rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale), hi, lo);
+    split2h(sc * v, hi, lo);
     o[c] = __builtin_bit_cast(f16_t, (_Float16)hi);
     o[W + c] = __builtin_bit_cast(f16_t, (_Float16)lo);
+  };
+  if constexpr (NIT > 0) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int c = lane + 64 * it;
+      if (c < W) put(c, cache[it]);
+    }
+  } else {
+    for (int c = lane; c < W; c += 64)
+      put(c, rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale));
   }
   if (lane == 0) rinv[row] = inv * (post ? post[row] : 1.f);
 }
 
 // Plain fp32 rows [R, K] -> per-row-scaled h3 activation [R, 2K] + rinv.  One wave per row, 4 values per access.
+template <int NIT>   // NIT > 0: K <= 256 NIT, the row's values stay in registers (read once)
 __global__ __launch_bounds__(256) void split_h3_dyn_kernel(const float* __restrict__ x, f16_t* __restrict__ out,
                                                            float* __restrict__ rinv, const float* __restrict__ post,
                                                            int R, int K) {
@@ -356,18 +379,42 @@ __global__ __launch_bounds__(256) void split_h3_dyn_kernel(const float* __restri
   if (row >= R) return;
   const float* xr = x + (size_t)row * K;
   float mx = 0.f;
-  for (int c = lane * 4; c < K; c += 256) {
-    const f32x4_t v = *(const f32x4_t*)(xr + c);
-    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  f32x4_t cache[NIT > 0 ? NIT : 1];
+  if constexpr (NIT > 0) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int c = lane * 4 + it * 256;
+      if (c < K) {
+        cache[it] = *(const f32x4_t*)(xr + c);
+        const f32x4_t v = cache[it];
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+      }
+    }
+  } else {
+    for (int c = lane * 4; c < K; c += 256) {
+      const f32x4_t v = *(const f32x4_t*)(xr + c);
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
   }
   mx = wave_max(mx);
   float inv;
   const float sc = row_pow2_scale(mx, inv);
   f16_t* o = out + (size_t)row * (2 * K);
-  for (int c = lane * 4; c < K; c += 256) {
-    const f32x4_t v = *(const f32x4_t*)(xr + c);
-    const float vv[4] = {v[0], v[1], v[2], v[3]};
-    store_h3_4(o, K, c, vv, sc);
+  if constexpr (NIT > 0) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int c = lane * 4 + it * 256;
+      if (c < K) {
+        const float vv[4] = {cache[it][0], cache[it][1], cache[it][2], cache[it][3]};
+        store_h3_4(o, K, c, vv, sc);
+      }
+    }
+  } else {
+    for (int c = lane * 4; c < K; c += 256) {
+      const f32x4_t v = *(const f32x4_t*)(xr + c);
+      const float vv[4] = {v[0], v[1], v[2], v[3]};
+      store_h3_4(o, K, c, vv, sc);
+    }
   }
   if (lane == 0) rinv[row] = inv * (post ? post[row] : 1.f);
 }
@@ -392,6 +439,7 @@ __device__ __forceinline__ void swiglu_bwd8(const float* __restrict__ dmr, const
   }
 }
 
+template <int NIT>   // NIT > 0: a thread's <= NIT chunks of 8 columns stay in registers between the max and the store
 __global__ __launch_bounds__(256) void lrp_swiglu_bwd_h3_kernel(const float* __restrict__ dm,
                                                                 const float* __restrict__ gu, f16_t* __restrict__ out,
                                                                 float* __restrict__ rinv,
@@ -401,23 +449,48 @@ __global__ __launch_bounds__(256) void lrp_swiglu_bwd_h3_kernel(const float* __r
   const float* dmr = dm + (size_t)t * I;
   const float* gur = gu + (size_t)t * (2 * I);
   float mx = 0.f;
-  for (int c = threadIdx.x * 8; c < I; c += 256 * 8) {
-    float dg[8], du[8];
-    swiglu_bwd8(dmr, gur, c, dg, du);
+  float cg[NIT > 0 ? NIT : 1][8], cu[NIT > 0 ? NIT : 1][8];
+  if constexpr (NIT > 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) mx = fmaxf(mx, fmaxf(fabsf(dg[i]), fabsf(du[i])));
+    for (int it = 0; it < NIT; ++it) {
+      const int c = (threadIdx.x + it * 256) * 8;
+      if (c < I) {
+        swiglu_bwd8(dmr, gur, c, cg[it], cu[it]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mx = fmaxf(mx, fmaxf(fabsf(cg[it][i]), fabsf(cu[it][i])));
+      }
+    }
+  } else {
+    for (int c = threadIdx.x * 8; c < I; c += 256 * 8) {
+      float dg[8], du[8];
+      swiglu_bwd8(dmr, gur, c, dg, du);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mx = fmaxf(mx, fmaxf(fabsf(dg[i]), fabsf(du[i])));
+    }
   }
   mx = block_max<256>(mx, red);
   float inv;
   const float sc = row_pow2_scale(mx, inv);
   const int W = 2 * I;
   f16_t* o = out + (size_t)t * (2 * W);
-  for (int c = threadIdx.x * 8; c < I; c += 256 * 8) {
-    float dg[8], du[8];
-    swiglu_bwd8(dmr, gur, c, dg, du);
-    const int col = (c >> 4) * 32 + (c & 15);
-    store_h3_8(o, W, col, dg, sc);
-    store_h3_8(o, W, col + 16, du, sc);
+  if constexpr (NIT > 0) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int c = (threadIdx.x + it * 256) * 8;
+      if (c < I) {
+        const int col = (c >> 4) * 32 + (c & 15);
+        store_h3_8(o, W, col, cg[it], sc);
+        store_h3_8(o, W, col + 16, cu[it], sc);
+      }
+    }
+  } else {
+    for (int c = threadIdx.x * 8; c < I; c += 256 * 8) {
+      float dg[8], du[8];
+      swiglu_bwd8(dmr, gur, c, dg, du);
+      const int col = (c >> 4) * 32 + (c & 15);
+      store_h3_8(o, W, col, dg, sc);
+      store_h3_8(o, W, col + 16, du, sc);
+    }
   }
   if (threadIdx.x == 0) rinv[t] = inv * (post ? post[t] : 1.f);
 }
@@ -552,15 +625,22 @@ EDGE_API int edge_lrp_rope_pack_h3(const float* dq, const float* dk, const float
   const int R = B * S;
   if (R <= 0) return 0;
   if (rot_dim > 64 || rot_dim % 2 || Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
-  lrp_rope_pack_h3_kernel<<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S, Hq, Hkv,
-                                                        rot_dim, q_scale);
+  if ((Hq + 2 * Hkv) * 64 <= 2048)
+    lrp_rope_pack_h3_kernel<32><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S,
+                                                              Hq, Hkv, rot_dim, q_scale);
+  else
+    lrp_rope_pack_h3_kernel<0><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S, Hq,
+                                                             Hkv, rot_dim, q_scale);
   return (int)hipGetLastError();
 }
 
 EDGE_API int edge_split_h3_dyn(const float* x, void* out, float* rinv, const float* post, int R, int K, hipStream_t st) {
   if (R <= 0) return 0;
   if (K % 4) return (int)hipErrorInvalidValue;
-  split_h3_dyn_kernel<<<(R + 3) / 4, 256, 0, st>>>(x, (f16_t*)out, rinv, post, R, K);
+  if (K <= 1024)
+    split_h3_dyn_kernel<4><<<(R + 3) / 4, 256, 0, st>>>(x, (f16_t*)out, rinv, post, R, K);
+  else
+    split_h3_dyn_kernel<0><<<(R + 3) / 4, 256, 0, st>>>(x, (f16_t*)out, rinv, post, R, K);
   return (int)hipGetLastError();
 }
 
@@ -568,7 +648,10 @@ EDGE_API int edge_lrp_swiglu_bwd_h3(const float* dm, const float* gu, void* out,
                                     int T, int I, hipStream_t st) {
   if (T <= 0) return 0;
   if (I % 16) return (int)hipErrorInvalidValue;
-  lrp_swiglu_bwd_h3_kernel<<<T, 256, 0, st>>>(dm, gu, (f16_t*)out, rinv, post, I);
+  if (I <= 3 * 2048)   // Qwen2-0.5B: I = 4864, three 8-column chunks per thread (the row read once)
+    lrp_swiglu_bwd_h3_kernel<3><<<T, 256, 0, st>>>(dm, gu, (f16_t*)out, rinv, post, I);
+  else
+    lrp_swiglu_bwd_h3_kernel<0><<<T, 256, 0, st>>>(dm, gu, (f16_t*)out, rinv, post, I);
   return (int)hipGetLastError();
 }
 

@@ -380,7 +380,7 @@ def test_mx_codecs_gpu_equal_cpu(codec, dtype):
 
 # ---- discriminating whole-model checks: final hidden state, peaked-output NLL, and their sensitivity ------------
 # (reference oracle: the monolithic fp32 model, Experiments/Qwen2-0.5B/qwen_layer_wise.py:78-104)
-HIDDEN_TOL, NLL_TOL = 1e-5, 1e-5
+HIDDEN_TOL, NLL_TOL = 1e-5, 3e-6     # measured clean: <= 1.9e-6 / 5.7e-7; 1e-4-perturbed: >= 2.3e-5 / 6.0e-6
 
 
 def _model(cfg, seed, dev, values, head_scale):
@@ -423,7 +423,7 @@ class _PerturbOneGemm:
 def test_full_model_hidden_state_and_peaked_nll(name, B, S, values, monkeypatch):
     """GPU fp32 mode vs the CPU fp32 model (same weights, same windows), whole model (24-layer Qwen2-0.5B, 6-layer
     Pythia-70M): the final hidden state within 1e-5 relative L2 and, with a peaked output distribution (row NLLs
-    spread over tens of nats), the per-row NLL of every scored row within 1e-5 relative L2.  Sensitivity: the same checks run on a GPU forward whose layer-3
+    spread over tens of nats), the per-row NLL of every scored row within 3e-6 relative L2.  Sensitivity: the same checks run on a GPU forward whose layer-3
     output projection is perturbed by 1e-4 relative must FAIL both tolerances (else they could not see an error of
     that size)."""
     from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream

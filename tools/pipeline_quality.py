@@ -42,10 +42,13 @@ GRID = [
     (2, "last_row", "mixed_int4_int8", "-"), (4, "last_row", "mixed_int4_int8", "-"),
     (4, "last_row", "ref_int4_global", "-"), (8, "last_row", "mixed_int4_int8", "-"),
     (8, "last_row", "ref_int4_global", "-"),
-    # config 5: 8-stage, LRP-weighted importance, relevance-allocated head-group quantization
+    # config 5: 8-stage, LRP-weighted importance, relevance-allocated head-group quantization ("@bits" = average
+    # width of the group-quantized rows: at 4 bits the greedy plan is uniform for this model, at 3 it is not)
     (8, "weighted_importance", "mixed_rgroup_int8", "rel"), (8, "weighted_importance", "mixed_rgroup_int8", "uniform"),
+    (8, "weighted_importance", "mixed_rgroup_int8@3", "rel"), (8, "weighted_importance", "mixed_rgroup_int8@3", "uniform"),
     (8, "weighted_importance", "mixed_int4_int8", "-"), (8, "weighted_importance", "ref_int4_global", "-"),
-    (8, "weighted_importance", "rgroup", "rel"), (8, "weighted_importance", "rgroup", "uniform"),
+    (8, "last_row", "mixed_rgroup_int8@3", "rel"), (8, "last_row", "mixed_rgroup_int8@3", "uniform"),
+    (8, "weighted_importance", "rgroup@3", "rel"), (8, "weighted_importance", "rgroup@3", "uniform"),
 ]
 
 
@@ -91,14 +94,16 @@ def main():
            "data": f"python-stdlib-bytes/eval, {len(wins)} windows (max_length 512, stride 32)",
            "ratios": ratios, "group_avg_bits": a.group_bits, "head_weights": hw.tolist(),
            "channel_group_relevance": grel.tolist(), "rows": []}
-    for pp, meth, codec, plan in GRID:
+    for pp, meth, codec_spec, plan in GRID:
         t0 = time.time()
+        codec, _, bits = codec_spec.partition("@")
+        gbits = float(bits) if bits else a.group_bits
         pplan = PipelinePlan.balanced(cfg, pp, 512)
-        row = {"pp": pp, "boundaries": pplan.boundary_layers(), "method": meth, "codec": codec, "plan": plan,
-               "ppl": [], "wire_bytes_per_token": []}
+        row = {"pp": pp, "boundaries": pplan.boundary_layers(), "method": meth, "codec": codec_spec, "plan": plan,
+               "group_avg_bits": gbits, "ppl": [], "wire_bytes_per_token": []}
         for r in ratios:
             bc = BoundaryConfig(codec, r, meth, hw, group_relevance=grel if plan == "rel" else None,
-                                group_avg_bits=a.group_bits)
+                                group_avg_bits=gbits)
             pipe = LocalPipeline(m, pplan, bc)
             row["ppl"].append(pipe.evaluate(bl).ppl())
             wb = pipe.wire_bytes_per_token()
@@ -106,11 +111,11 @@ def main():
         if plan != "-":
             pipe_ = LocalPipeline(m, pplan, BoundaryConfig(codec, 0.5, meth, hw,
                                                            group_relevance=grel if plan == "rel" else None,
-                                                           group_avg_bits=a.group_bits))
+                                                           group_avg_bits=gbits))
             row["group_plans"] = {str(s.boundary): list(s.spec_out.plan) for s in pipe_.stages[:-1]}
         row["seconds"] = round(time.time() - t0, 2)
         out["rows"].append(row)
-        print(f"pp{pp} {meth:20s} {codec:18s} {plan:8s} " +
+        print(f"pp{pp} {meth:20s} {codec_spec:20s} {plan:8s} " +
               "  ".join(f"{p:.4f}@{w:.0f}B" for p, w in zip(row["ppl"], row["wire_bytes_per_token"])), flush=True)
 
     lines = [f"# Multi-boundary pipeline quality: {cfg.name} (trained), fp32, {out['data']}", "",
