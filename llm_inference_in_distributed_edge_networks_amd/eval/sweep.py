@@ -42,6 +42,7 @@ from ..importance import ImportanceTracker, canonical
 from ..models.model import DecoderLM
 from ..utils import trace
 from ..utils.checkpoint import SweepState
+from ..utils.graphs import GraphCache
 from .windows import WindowBatch, segment_mean, window_nll
 
 
@@ -75,7 +76,7 @@ class SweepConfig:
 
 
 class SweepEngine:
-    def __init__(self, model: DecoderLM, sc: SweepConfig):
+    def __init__(self, model: DecoderLM, sc: SweepConfig, use_graphs: bool = True):
         self.m, self.sc = model, sc
         self.spec = C.get_codec(sc.codec)
         self.rows = sc.rows()
@@ -93,6 +94,10 @@ class SweepEngine:
         # the model's last layer only at the scored rows (see DecoderLM.layer_rows)
         self.rows_only = os.environ.get("EDGE_LAST_LAYER_ALL_ROWS", "0") in ("", "0")
         self._dev = None               # [total_nll, sum_window_nll] increments on the model's device
+        # the unquantized prefix forward has a fixed launch sequence per batch signature: one HIP graph replay
+        need = self._needed()
+        self._imp_keys = [(meth, L) for meth in sorted(need) for L in sorted(need[meth])]
+        self._graphs = GraphCache(self._prefix_flat, enabled=use_graphs and model.device.type == "cuda")
         hw = sc.head_weights  # LRP head table on the model's device once
         self.head_weights = None if hw is None else torch.as_tensor(hw).to(self.m.device, torch.float32).contiguous()
 
@@ -110,8 +115,23 @@ class SweepEngine:
     def _imp_key(self, r: SweepMethod, L: int):
         return (canonical(r.method), r.source_layer if r.source_layer is not None else L)
 
+    def _prefix_flat(self, ids, rows, targets, row_window, n_rows):
+        """Graph-capturable prefix on tensors only: (base NLL, h_L for every boundary layer in order, importance for
+        every (method, layer) of ``_imp_keys``)."""
+        b = WindowBatch(ids, None, rows, targets, row_window, n_rows, None)
+        base, saved, imp = self._prefix_eager(b)
+        return (base, *[saved[L] for L in self.layers], *[imp[k] for k in self._imp_keys])
+
     def _prefix(self, batch: WindowBatch):
         """Unquantized forward: base per-window NLL, h_L per boundary layer, importance per (method, layer)."""
+        out = self._graphs(batch.ids, batch.rows, batch.targets, batch.row_window, batch.n_rows)
+        self.forward_tokens += batch.B * batch.S
+        nl = len(self.layers)
+        saved = dict(zip(self.layers, out[1:1 + nl]))
+        imp = dict(zip(self._imp_keys, out[1 + nl:]))
+        return out[0], saved, imp
+
+    def _prefix_eager(self, batch: WindowBatch):
         m, B, S = self.m, batch.B, batch.S
         need = self._needed()
         trackers = {meth: ImportanceTracker(meth, sorted(ls), m.cfg.num_heads, self.head_weights)
@@ -137,7 +157,6 @@ class SweepEngine:
             if i in self.layers:
                 saved[i] = x
         base = window_nll(m.row_nll(x, rows, batch.targets), batch)
-        self.forward_tokens += B * S
         imp = {(meth, L): trackers[meth].importance(L) for meth, ls in need.items() for L in ls}
         return base, saved, imp
 
