@@ -75,7 +75,10 @@ class GraphCache:
                 _PRERUN = False
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        with torch.cuda.graph(graph):
+        # thread_local: only this thread's stream-unsafe calls invalidate the capture.  Under RCCL the process
+        # group's watchdog thread keeps querying its events while a stage captures; in the default "global" mode such
+        # a query from another thread aborts the capture.
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             static_out = self.fn(*static_in)
         torch.cuda.synchronize()
         return graph, static_in, static_out

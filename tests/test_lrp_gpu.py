@@ -212,3 +212,23 @@ def test_fp32_calibration_table_matches_cpu_full_qwen2():
           f"{e_bf16:.2e}; channel groups {e_chan:.2e}")
     assert e_head < 1e-4 and e_chan < 1e-4 and e_raw < 1e-4
     assert e_bf16 < 0.06
+
+
+def test_fp32_calibration_table_matches_cpu_full_pythia():
+    """The same check on the full 6-layer Pythia-70M (GPT-NeoX: parallel residual, LayerNorm rule, GELU identity
+    rule, 25 % rotary), fp16-valued weights as the HF checkpoint, one 1024-token window."""
+    from llm_inference_in_distributed_edge_networks_amd.models import get_config
+    from llm_inference_in_distributed_edge_networks_amd.relevance.attnlrp import (head_relevance_batched,
+                                                                                  normalize_per_layer)
+    from llm_inference_in_distributed_edge_networks_amd.relevance.engine_f32 import RelevanceEngineH3
+    cfg = get_config("pythia-70m")
+    mc = DecoderLM.random_init(cfg, 4, std=0.02, values=torch.float16)
+    mg = DecoderLM.random_init(cfg, 4, device=DEV, std=0.02, values=torch.float16)
+    ids = torch.randint(0, cfg.vocab_size, (1, 1024), generator=torch.Generator().manual_seed(5))
+    rc, _, _, cc = head_relevance_batched(mc, ids)
+    rg, _, _, cg = RelevanceEngineH3(mg).head_relevance(ids.to(DEV), want_channels=True)
+    e_head = rel_err(normalize_per_layer(rg.sum(0)), normalize_per_layer(rc.sum(0)))
+    e_chan = rel_err(normalize_per_layer(cg.sum(0)), normalize_per_layer(cc.sum(0)))
+    print(f"pythia-70m normalised head table vs CPU fp32: {e_head:.2e} (raw {rel_err(rg, rc):.2e}); channel groups "
+          f"{e_chan:.2e}")
+    assert e_head < 1e-4 and e_chan < 1e-4

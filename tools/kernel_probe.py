@@ -1,0 +1,67 @@
+"""Run one fp32-mode kernel of the bench step at the bench shape a few times (for rocprofv3 --pmc passes and A/B).
+
+Shapes: Qwen2-0.5B, one 64-window micro-batch of 512 tokens (M = 32768), bf16-valued weights (two-product h3 GEMMs).
+  attn    fp32 flash attention, fp16 planes, h3 output (flash_attn_fwd_x6_kernel<true, 8, true>)
+  qkv     h3 QKV GEMM + bias + RoPE + scatter (256x192 tiles)
+  colsum  column-sum importance on the fp16 planes
+  norm    fp32 RMSNorm -> h3 planes
+Prints the mean time per call (events) as JSON."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from llm_inference_in_distributed_edge_networks_amd import ops  # noqa: E402
+from llm_inference_in_distributed_edge_networks_amd.ops import reference as R  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--op", default="attn", choices=["attn", "qkv", "colsum", "norm"])
+    ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--S", type=int, default=512)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    B, S, Hq, Hkv, H = a.B, a.S, 14, 2, 896
+    g = torch.Generator().manual_seed(0)
+    dev = "cuda"
+    if a.op in ("attn", "colsum"):
+        q = (torch.randn(B, Hq, S, 64, generator=g) * 0.125).to(dev)
+        k = torch.randn(B, Hkv, S, 64, generator=g).to(dev)
+        vt = torch.randn(B, Hkv, 64, ops.s_pad(S), generator=g).to(dev)
+        sc = (2.0 ** 12, 2.0 ** 12, 2.0 ** 12)
+        _, lse = ops.attention(q, k, vt, S, need_lse=True, h3=2.0 ** 10, in_scales=sc)
+        if a.op == "attn":
+            fn = lambda: ops.attention(q, k, vt, S, need_lse=False, h3=2.0 ** 10, in_scales=sc)   # noqa: E731
+        else:
+            fn = lambda: ops.attn_colsum(q, k, lse, S, in_scales=sc[:2])                          # noqa: E731
+    elif a.op == "qkv":
+        x = torch.randn(B * S, H, generator=g)
+        w = (torch.randn((Hq + 2 * Hkv) * 64, H, generator=g) * 0.02).bfloat16().float()
+        w3, sw = R.h3_weight(w)
+        x3 = ops.split_h3(x.to(dev), 2.0 ** 10)
+        bias = (torch.randn((Hq + 2 * Hkv) * 64, generator=g) * 0.02).to(dev)
+        cos, sin = R.rope_tables(4096, 64, 1e6)
+        cos, sin, w3 = cos.to(dev), sin.to(dev), w3.to(dev)
+        fn = lambda: ops.qkv_rope_h3(x3, w3, 1.0 / (2.0 ** 10 * sw), bias, cos, sin, B, S, Hq, Hkv, 64, 64,  # noqa
+                                     0.125)
+    else:
+        x = torch.randn(B * S, H, generator=g).to(dev)
+        w = (1 + 0.05 * torch.randn(H, generator=g)).to(dev)
+        fn = lambda: ops.rmsnorm(x, w, 1e-6, h3=2.0 ** 10)                                       # noqa: E731
+    fn()
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(a.iters):
+        fn()
+    en.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"op": a.op, "B": B, "S": S, "us_per_call": round(st.elapsed_time(en) / a.iters * 1e3, 2)}))
+
+
+if __name__ == "__main__":
+    main()

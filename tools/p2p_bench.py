@@ -22,9 +22,10 @@ def main():
     ap.add_argument("--sizes", default="1024,65536,1048576,11075584,29360128")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json-out", default="")
-    ap.add_argument("--transport", default="torch", choices=["torch", "ipc"],
+    ap.add_argument("--transport", default="torch", choices=["torch", "ipc", "rccl"],
                     help="torch: isend/irecv (RCCL); ipc: peer copies into the receiver's IPC-mapped slot ring "
-                         "(parallel/ipc.py, the hipMemcpyPeerAsync baseline)")
+                         "(parallel/ipc.py, the hipMemcpyPeerAsync baseline); rccl: the native per-edge RCCL "
+                         "channels (parallel/rccl.py)")
     a = ap.parse_args()
     env = init_distributed("auto")
     assert env.world_size == 2, "run with exactly 2 ranks"
@@ -72,6 +73,20 @@ def main():
             dist.barrier()
             rec["ipc_stream_GBps"] = n * a.iters / (time.perf_counter() - t0) / 1e9
             tr.close()
+        if a.transport == "rccl":
+            # one-way stream over the native channel of the edge (0, 1): per-op events, no host blocking
+            from llm_inference_in_distributed_edge_networks_amd.parallel.rccl import RcclComm
+            if not hasattr(main, "_rc"):
+                main._rc = RcclComm(env.rank, env.world_size, dev.index or 0, peers=[peer])
+            rc = main._rc
+            sync()
+            dist.barrier()
+            t0 = time.perf_counter()
+            hs = [rc.send(buf, 1) if env.rank == 0 else rc.recv(buf, 0) for _ in range(a.iters)]
+            for h in hs:
+                h.wait()
+            sync()
+            rec["rccl_native_stream_GBps"] = n * a.iters / (time.perf_counter() - t0) / 1e9
         res.append(rec)
         if env.rank == 0:
             print(json.dumps(res[-1]), flush=True)
