@@ -623,9 +623,21 @@ EDGE_API int edge_select(const float* imp, int B, int S, int k, void* msg, long 
   return (int)hipGetLastError();
 }
 
+// Constant lo-class mask (k = 0 or k = S): a kernel, not hipMemsetAsync - inside a captured HIP graph the memset node
+// was measured to lose its order against the message's zero fill (replays produced an all-zero mask for k = S).
+__global__ __launch_bounds__(256) void set_mask_kernel(uint32_t* __restrict__ mask, size_t nwords, uint32_t v) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < nwords) mask[i] = v;
+}
+
 EDGE_API int edge_set_mask(void* msg, long long off_mask, int B, int S, int all_lo, hipStream_t st) {
   const int mw = ((S + 63) / 64) * 2;
-  return (int)hipMemsetAsync((uint8_t*)msg + off_mask, all_lo ? 0xff : 0, (size_t)B * mw * 4, st);
+  const size_t n = (size_t)B * mw;
+  if (!n) return 0;
+  if (off_mask % 4) return (int)hipErrorInvalidValue;
+  set_mask_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>((uint32_t*)((uint8_t*)msg + off_mask), n,
+                                                                all_lo ? 0xffffffffu : 0u);
+  return (int)hipGetLastError();
 }
 
 // channel_stats: mode 0 max|x|, 1 mean+1e-8; only_lo restricts to lo-class rows.  out: [B, H] fp32

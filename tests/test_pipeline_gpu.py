@@ -33,6 +33,26 @@ def test_graph_replay_equals_eager(cfg, codec, ratio, method):
     assert eager.wire_bytes_per_token() == graphed.wire_bytes_per_token()
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("codec,ratio", [("mixed_int4_int8", 1.0), ("mixed_rgroup_int8", 1.0), ("int8_token", 0.5),
+                                         ("mixed_int4_int8", 0.0)])
+def test_graph_replay_constant_masks(dtype, codec, ratio):
+    """k = S (every token lo) and k = 0 / importance-free codecs set the lo mask with one constant fill; replayed
+    graphs must give the eager result on every batch (a hipMemsetAsync fill lost its order against the message's zero
+    fill inside captured graphs: the k = S mask replayed as all zeros)."""
+    m = DecoderLM.random_init(TINY_QWEN2, 2, device="cuda", dtype=dtype, std=0.05)
+    plan = PipelinePlan.from_split_layers(TINY_QWEN2.num_layers, [0, 1, 2])
+    eager = LocalPipeline(m, plan, BoundaryConfig(codec, ratio, "last_row"), use_graphs=False)
+    graphed = LocalPipeline(m, plan, BoundaryConfig(codec, ratio, "last_row"), use_graphs=True)
+    bl = [b.to("cuda") for b in batches(TOK, WINS, 4)]
+    for _ in range(3):
+        for b in bl:
+            e = eager.run_batch(b).clone()
+            g = graphed.run_batch(b).clone()
+            assert torch.isfinite(g).all() and torch.equal(e, g)
+    assert graphed.graphs.graphs, "nothing was captured"
+
+
 def test_gpu_sweep_equals_split_runner():
     m = DecoderLM.random_init(TINY_QWEN2, 0, device="cuda", dtype=torch.bfloat16, std=0.05)
     sc = SweepConfig(["regular_importance", "last_row"], [1, 2], [0, 0.5, 1.0], codec="mixed_int4_int8")
