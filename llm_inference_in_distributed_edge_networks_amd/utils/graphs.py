@@ -15,6 +15,7 @@ replay i reads; before replaying a slot again the caller makes the stream wait f
 """
 from __future__ import annotations
 
+import gc
 from typing import Callable
 
 import torch
@@ -78,8 +79,17 @@ class GraphCache:
         # thread_local: only this thread's stream-unsafe calls invalidate the capture.  Under RCCL the process
         # group's watchdog thread keeps querying its events while a stage captures; in the default "global" mode such
         # a query from another thread aborts the capture.
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            static_out = self.fn(*static_in)
+        # No garbage collection while capturing: a cycle collected mid-capture can hold a dropped CUDAGraph (e.g. of
+        # a pipeline rebuilt for another codec), and its destructor is not permitted while a stream captures.
+        gc.collect()
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                static_out = self.fn(*static_in)
+        finally:
+            if was:
+                gc.enable()
         torch.cuda.synchronize()
         return graph, static_in, static_out
 

@@ -53,6 +53,33 @@ def test_graph_replay_constant_masks(dtype, codec, ratio):
     assert graphed.graphs.graphs, "nothing was captured"
 
 
+def test_capture_survives_collection_of_dropped_graphs():
+    """A dropped pipeline is a reference cycle (its GraphCache holds its bound ``_step``) that still owns captured
+    graphs; a collection during another capture would run their destructors mid-capture (process abort).  gc
+    threshold 1 makes the collector run at almost every allocation, so without the capture-time gc guard this
+    aborts."""
+    import gc
+    m = DecoderLM.random_init(TINY_QWEN2, 2, device="cuda", dtype=torch.float32, std=0.05)
+    plan = PipelinePlan.from_split_layers(TINY_QWEN2.num_layers, [0, 1, 2])
+    bl = [b.to("cuda") for b in batches(TOK, WINS, 4)]
+    old = gc.get_threshold()
+    try:
+        ref = None
+        for r in (0.25, 0.5, 0.75):
+            pipe = LocalPipeline(m, plan, BoundaryConfig("mixed_int4_int8", r, "last_row"))
+            pipe.evaluate(bl)
+            pipe.evaluate(bl)
+            assert pipe.graphs.graphs
+            out = pipe.evaluate(bl).ppl()
+            ref = LocalPipeline(m, plan, BoundaryConfig("mixed_int4_int8", r, "last_row"),
+                                use_graphs=False).evaluate(bl).ppl()
+            assert abs(out - ref) <= 1e-6 * ref
+            gc.set_threshold(1, 1, 1)
+            del pipe
+    finally:
+        gc.set_threshold(*old)
+
+
 def test_gpu_sweep_equals_split_runner():
     m = DecoderLM.random_init(TINY_QWEN2, 0, device="cuda", dtype=torch.bfloat16, std=0.05)
     sc = SweepConfig(["regular_importance", "last_row"], [1, 2], [0, 0.5, 1.0], codec="mixed_int4_int8")

@@ -101,18 +101,20 @@ def main():
         pplan = PipelinePlan.balanced(cfg, pp, 512)
         row = {"pp": pp, "boundaries": pplan.boundary_layers(), "method": meth, "codec": codec_spec, "plan": plan,
                "group_avg_bits": gbits, "ppl": [], "wire_bytes_per_token": []}
+        pipe = None
         for r in ratios:
             bc = BoundaryConfig(codec, r, meth, hw, group_relevance=grel if plan == "rel" else None,
                                 group_avg_bits=gbits)
-            pipe = LocalPipeline(m, pplan, bc)
+            if pipe is None:
+                pipe = LocalPipeline(m, pplan, bc)
+            else:
+                pipe.set_boundary(bc)     # one pipeline per row: its graphs are dropped, not left to the collector
             row["ppl"].append(pipe.evaluate(bl).ppl())
             wb = pipe.wire_bytes_per_token()
             row["wire_bytes_per_token"].append(sum(wb) / len(wb))
-        if plan != "-":
-            pipe_ = LocalPipeline(m, pplan, BoundaryConfig(codec, 0.5, meth, hw,
-                                                           group_relevance=grel if plan == "rel" else None,
-                                                           group_avg_bits=gbits))
-            row["group_plans"] = {str(s.boundary): list(s.spec_out.plan) for s in pipe_.stages[:-1]}
+            if plan != "-" and r == 0.5:
+                row["group_plans"] = {str(s.boundary): list(s.spec_out.plan) for s in pipe.stages[:-1]}
+        pipe.graphs.clear()
         row["seconds"] = round(time.time() - t0, 2)
         out["rows"].append(row)
         print(f"pp{pp} {meth:20s} {codec_spec:20s} {plan:8s} " +
