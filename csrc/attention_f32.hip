@@ -289,15 +289,23 @@ __device__ __forceinline__ f32x4_t plane_dot(const bf16x8_t (&a)[F16 ? 2 : 3], c
 // v are scaled by the powers of two sq, sk, sv (model bounds, so every plane stays in the fp16 range) and the
 // probabilities by 2^(15 - TAU) (p <= 2^TAU under the lazy rescale); the scores are unscaled in the exp and the
 // output in the final normalisation.
-template <bool H3OUT, int NW, bool F16>
+// KVP (with F16 and NW = 8): k / vt are not fp32 but the scaled fp16 h3 planes the QKV GEMM epilogue wrote
+// (kp [B, Hkv, 2, S, 64], vp [B, Hkv, 2, 64, s_pad], V^T keys in the P^T operand order: gemm.hip kv_plane_pos); the
+// K / V^T tiles are then staged by LDS DMA (global_load_lds, 16 bytes a lane, swizzle on the source address) into
+// two buffers - no register staging, no per-tile split, one barrier per key tile, tile kb + 1 in flight while tile kb
+// is computed.
+template <bool H3OUT, int NW, bool F16, bool KVP = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(const float* __restrict__ q,
-                                                                  const float* __restrict__ k,
-                                                                  const float* __restrict__ vt, void* __restrict__ o,
+                                                                  const void* __restrict__ kin,
+                                                                  const void* __restrict__ vtin, void* __restrict__ o,
                                                                   float* __restrict__ lse,
                                                                   const float* __restrict__ n_rows, int B, int Hq,
                                                                   int Hkv, int S, int s_pad, float h3s, float sq,
                                                                   float sk, float sv) {
+  static_assert(!KVP || (F16 && NW == 8), "plane staging: h3 planes, 8 waves (8 KiB per DMA round)");
   constexpr int NPL = F16 ? 2 : 3;
+  const float* __restrict__ k = (const float*)kin;
+  const float* __restrict__ vt = (const float*)vtin;
   // probability scale 2^(15 - FTAU) of the fp16 planes, applied in the exp2 argument (the row sum l_run and the
   // probabilities carry it; the normalisation and the LSE take it out)
   constexpr float LSP = F16 ? 7.f : 0.f;
@@ -325,8 +333,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
   const float* qh = q + ((size_t)b * Hq + h) * S * 64;
   const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
   const float* vh = vt + ((size_t)b * Hkv + hk) * 64 * (size_t)s_pad;
-  char* const lk = smem;
-  char* const lv = smem + NPL * XPL;
+  char* lk = smem;
+  char* lv = smem + NPL * XPL;
 
   const int q0 = qb * QB + wave * 16;
   const int qrow = q0 + ql;
@@ -403,14 +411,40 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     }
   };
 
+  // KVP: DMA of key tile kb into buffer kb & 1 (4 plane tiles of 8 KiB: K hi, K lo, V^T hi, V^T lo); wave w stages
+  // rows 8 w .. 8 w + 7 of each, lane -> (row 8 w + lane / 8, LDS chunk lane % 8 = global chunk (lane % 8) ^ xsw(row))
+  const char* kph = (const char*)((const f16_t*)kin + ((size_t)b * Hkv + hk) * 2 * S * 64);
+  const char* vph = (const char*)((const f16_t*)vtin + ((size_t)b * Hkv + hk) * 2 * 64 * (size_t)s_pad);
+  const int drow = wave * 8 + (lane >> 3);
+  const int dchunk = ((lane & 7) ^ xsw(drow)) << 4;
+  auto dma_tile = [&](int kb) {
+    char* buf = smem + (kb & 1) * 4 * XPL + wave * 1024;
+    const size_t kr = (size_t)min(kb * 64 + drow, S - 1);
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+      glds16(kph + ((size_t)pl * S + kr) * 128 + dchunk, buf + pl * XPL);
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+      glds16(vph + (((size_t)pl * 64 + drow) * s_pad + kb * 64) * 2 + dchunk, buf + (2 + pl) * XPL);
+  };
+
   const int nkb = min((qb + 1) * QB, S + 63) / 64;   // key tiles up to this block's last query row
   const int kmax = (q0 + 15) / 64;  // last key tile this wave needs (wave-uniform)
-  load_tile(0);
+  if constexpr (KVP) dma_tile(0);
+  else load_tile(0);
   for (int kb = 0; kb < nkb; ++kb) {
-    __syncthreads();                 // every wave's reads of the previous tile retired
-    write_tile();
-    __syncthreads();                 // planes of tile kb visible
-    if (kb + 1 < nkb) load_tile(kb + 1);
+    if constexpr (KVP) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of tile kb landed
+      __syncthreads();       // every wave's pieces landed; every wave's reads of tile kb - 1 (buffer (kb + 1) & 1) done
+      if (kb + 1 < nkb) dma_tile(kb + 1);
+      lk = smem + (kb & 1) * 4 * XPL;
+      lv = lk + 2 * XPL;
+    } else {
+      __syncthreads();                 // every wave's reads of the previous tile retired
+      write_tile();
+      __syncthreads();                 // planes of tile kb visible
+      if (kb + 1 < nkb) load_tile(kb + 1);
+    }
     if (kb > kmax) continue;
     // S^T = K Q^T over the 4 key blocks of 16
     f32x4_t st[4];
@@ -793,6 +827,14 @@ EDGE_API int edge_attn_f32_set_variant(int v) {
   return 0;
 }
 
+template <bool H3OUT>
+static void launch_plane_attn(dim3 grid, hipStream_t st, const float* q, const void* kp, const void* vp, void* o,
+                              float* lse, const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float h3s,
+                              float sq, float sk, float sv) {
+  hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<H3OUT, 8, true, true>), grid, dim3(512), 8 * XPL, st, q, kp, vp, o,
+                     lse, n_rows, B, Hq, Hkv, S, s_pad, h3s, sq, sk, sv);
+}
+
 template <bool H3OUT, int NW, bool F16>
 static void launch_split_attn(dim3 grid, hipStream_t st, const float* q, const float* k, const float* vt, void* o,
                               float* lse, const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float h3s,
@@ -829,6 +871,22 @@ EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float
     hipLaunchKernelGGL(flash_attn_fwd_f32_kernel<false>, grid, dim3(256), 4 * FTILE, st, q, k, vt, o, lse, n_rows, B,
                        Hq, Hkv, S, s_pad, out_h3_scale);
   }
+  return (int)hipGetLastError();
+}
+
+// fp32 attention from the K / V^T h3 planes of edge_gemm_qkv_rope_f32 (kp / vp at scales sk / sv; q fp32, split at
+// sq): the KVP kernel.  Same arguments and outputs as edge_flash_attn_fwd_f32 otherwise.
+EDGE_API int edge_flash_attn_fwd_h3p(const float* q, const void* kp, const void* vp, void* o, float* lse,
+                                    const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float out_h3_scale,
+                                    float sq, float sk, float sv, hipStream_t st) {
+  if (B <= 0 || S <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv || s_pad % 64 || s_pad < S || out_h3_scale < 0.f) return (int)hipErrorInvalidValue;
+  if (!(sq > 0.f && sk > 0.f && sv > 0.f) || ((uintptr_t)kp & 15) || ((uintptr_t)vp & 15))
+    return (int)hipErrorInvalidValue;
+  const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
+  const dim3 gx(8 * maxcnt * G * ((S + 127) / 128));
+  (out_h3_scale > 0.f ? launch_plane_attn<true> : launch_plane_attn<false>)(gx, st, q, kp, vp, o, lse, n_rows, B, Hq,
+                                                                            Hkv, S, s_pad, out_h3_scale, sq, sk, sv);
   return (int)hipGetLastError();
 }
 

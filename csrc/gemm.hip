@@ -47,6 +47,9 @@ struct GemmArgs {
   bf16_t* qout; bf16_t* kout; bf16_t* vtout;
   const float* cosT; const float* sinT;
   int S, Hq, Hkv, s_pad; float q_scale;
+  // fp32 QKV, optional: K / V^T also as scaled fp16 h3 planes for the attention kernel's LDS-DMA staging
+  // (kp [B, Hkv, 2, S, 64], vp [B, Hkv, 2, 64, s_pad] in the kernel's key order; kv_plane_pos)
+  f16_t* kp; f16_t* vp; float kv_sk, kv_sv;
   // LSE
   const int64_t* targets; float* part_max; float* part_sum; float* tgt_logit; int nparts;
   // fused RMSNorm: consumer side (row scale rscale[m] = rsqrt(mean(x_m^2) + eps), the norm weight is
@@ -239,6 +242,25 @@ __device__ __forceinline__ void swiglu_h3_lines_4w(const GemmArgs& a, f32x4_t (&
   }
 }
 
+// ---- K / V^T h3 planes from the fp32 QKV epilogues (GemmArgs::kp / vp).  split2h of s x: bit-identical to the split
+// flash_attn_fwd_x6_kernel applies to the fp32 K / V^T it stages itself.  V^T keys are stored in the order the
+// kernel's P^T operand holds them: within each 32-key block, lane group g's k-slots 8g..8g+7 are keys
+// {4g..4g+3, 16+4g..16+4g+3}, so key 32 s + 16 hf + 4 a + r sits at element 8 (4 s + a) + 4 hf + r of its 64-key tile.
+__device__ __forceinline__ int kv_plane_pos(int pos) {
+  const int k = pos & 63;
+  return (pos & ~63) | ((4 * (k >> 5) + ((k >> 2) & 3)) << 3) | (((k >> 4) & 1) << 2) | (k & 3);
+}
+__device__ __forceinline__ void store_k_planes4(const GemmArgs& a, int b, int hk, int pos, int d, const float (&v)[4]) {
+  store_h3_4(a.kp + ((size_t)(b * a.Hkv + hk) * 2 * a.S + pos) * 64, a.S * 64, d, v, a.kv_sk);
+}
+__device__ __forceinline__ void store_vt_plane1(const GemmArgs& a, int b, int hv, int pos, int d, float v) {
+  float hi, lo;
+  split2h(v * a.kv_sv, hi, lo);
+  const size_t o = ((size_t)(b * a.Hkv + hv) * 2 * 64 + d) * a.s_pad + kv_plane_pos(pos);
+  a.vp[o] = __builtin_bit_cast(uint16_t, (_Float16)hi);
+  a.vp[o + (size_t)64 * a.s_pad] = __builtin_bit_cast(uint16_t, (_Float16)lo);
+}
+
 // ---- fp32-execution epilogues (EPI >= EPI_F32).  Same ownership as gemm_epilogue below: lane owns rows
 // m0 + wm*WTM + i*16 + (lane&15) and columns nw + j*16 + 4*(lane>>4) + r of the wave's 64-column slab, so every
 // output is 4 consecutive fp32 values (one 16-byte store) or 4 consecutive values of each of the two h3 planes.
@@ -309,12 +331,24 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           *(f32x4_t*)(dst + j * 16 + g * 4) = f32x4_t{v[j][0] * sc, v[j][1] * sc, v[j][2] * sc, v[j][3] * sc};
+        if (head >= a.Hq && a.kp) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) store_k_planes4(a, b, head - a.Hq, pos, j * 16 + g * 4, v[j]);
+        }
       } else {
-        float* dst = a.vtf + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
+        if (a.vtf) {
+          float* dst = a.vtf + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dst[(size_t)(j * 16 + g * 4 + r) * a.s_pad] = v[j][r];
+            for (int r = 0; r < 4; ++r) dst[(size_t)(j * 16 + g * 4 + r) * a.s_pad] = v[j][r];
+        }
+        if (a.vp) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) store_vt_plane1(a, b, head - a.Hq - a.Hkv, pos, j * 16 + g * 4 + r, v[j][r]);
+        }
       }
     }
     return;
@@ -1738,12 +1772,26 @@ __device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[
                                  : a.kf + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
         *(f32x4_t*)(dst + d) = lo * sc;
         *(f32x4_t*)(dst + d + 32) = hi * sc;
+        if (head >= a.Hq && a.kp) {
+          const float l4[4] = {lo[0], lo[1], lo[2], lo[3]}, h4[4] = {hi[0], hi[1], hi[2], hi[3]};
+          store_k_planes4(a, b, head - a.Hq, pos, d, l4);
+          store_k_planes4(a, b, head - a.Hq, pos, d + 32, h4);
+        }
       } else {
-        float* dst = a.vtf + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
+        if (a.vtf) {
+          float* dst = a.vtf + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          dst[(size_t)(d + r) * a.s_pad] = lo[r];
-          dst[(size_t)(d + 32 + r) * a.s_pad] = hi[r];
+          for (int r = 0; r < 4; ++r) {
+            dst[(size_t)(d + r) * a.s_pad] = lo[r];
+            dst[(size_t)(d + 32 + r) * a.s_pad] = hi[r];
+          }
+        }
+        if (a.vp) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            store_vt_plane1(a, b, head - a.Hq - a.Hkv, pos, d + r, lo[r]);
+            store_vt_plane1(a, b, head - a.Hq - a.Hkv, pos, d + 32 + r, hi[r]);
+          }
         }
       }
     }
@@ -2700,9 +2748,12 @@ EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, 
 // fp32 QKV projection + bias + RoPE + head-major scatter: X [M, 2K] (h3 activation), W [(Hq+2Hkv)*64, 3K] (h3
 // weight), alpha = 1 / (s_x s_w), fp32 bias, fp32 outputs q [B,Hq,S,64] (x q_scale), k [B,Hkv,S,64],
 // vt [B,Hkv,64,s_pad].
+// kp / vp (optional, both or neither): K and V^T also as scaled fp16 h3 planes at scales kv_sk / kv_sv (GemmArgs);
+// with them vt may be null (the plane-staged attention reads no fp32 V^T).
 EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* bias, float* q, float* k, float* vt,
                                     const float* cosT, const float* sinT, int M, int Kx, int kplane, int S, int Hq,
-                                    int Hkv, int rot_dim, int s_pad, float q_scale, float alpha, hipStream_t st) {
+                                    int Hkv, int rot_dim, int s_pad, float q_scale, float alpha, void* kp, void* vp,
+                                    float kv_sk, float kv_sv, hipStream_t st) {
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
   a.pairb = Kx == 2 * kplane;
@@ -2712,8 +2763,12 @@ EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* b
   a.biasf = bias; a.qf = q; a.kf = k; a.vtf = vt;
   a.cosT = cosT; a.sinT = sinT; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.s_pad = s_pad;
   a.q_scale = q_scale;
+  a.kp = (f16_t*)kp; a.vp = (f16_t*)vp; a.kv_sk = kv_sk; a.kv_sv = kv_sv;
   if (!bias || M % S || !h3_geometry_ok(Kx, kplane) || ((uintptr_t)bias & 15) || !(alpha > 0.f))
     return (int)hipErrorInvalidValue;
+  if ((kp == nullptr) != (vp == nullptr) || (kp && (!(kv_sk > 0.f) || !(kv_sv > 0.f) || ((uintptr_t)kp & 7))))
+    return (int)hipErrorInvalidValue;
+  if (!q || !k || (!vt && !vp)) return (int)hipErrorInvalidValue;   // fp32 V^T may be skipped when its planes are out
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
   switch (rot_dim) {

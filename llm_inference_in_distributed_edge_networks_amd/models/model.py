@@ -57,6 +57,9 @@ class AttnStats:
 
 
 _H3_KEYS = ("wqkv", "wo", "wgu", "wd", "wfc", "wproj")
+# fp32 mode: the QKV GEMM writes K / V^T also as h3 planes and the attention stages them by LDS DMA (bit-identical
+# result; EDGE_ATTN_KV_PLANES=0 keeps the kernel's own per-tile split, for A/B)
+_KV_PLANES = os.environ.get("EDGE_ATTN_KV_PLANES", "1") != "0"
 
 
 def _rownorm(w: torch.Tensor) -> torch.Tensor:
@@ -394,10 +397,17 @@ class DecoderLM:
         else:
             h3, h23 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps,
                                          h3=(sc["qkv"], sc["mlp"]))
-        q, k, vt = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S, cfg.num_heads,
-                                   cfg.num_kv_heads, cfg.head_dim, cfg.rotary_dim, self.q_scale)
+        kvp = None
+        if _KV_PLANES and x.is_cuda:   # the QKV GEMM also emits K / V^T planes; attention stages them by LDS DMA
+            q, k, vt, kp, vp = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S,
+                                               cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, cfg.rotary_dim,
+                                               self.q_scale, kv_scales=(sc["att_k"], sc["o"]))
+            kvp = (kp, vp)
+        else:
+            q, k, vt = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S,
+                                       cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, cfg.rotary_dim, self.q_scale)
         o3, lse = ops.attention(q, k, vt, S, need_lse=need_lse, n_rows=n_rows, h3=sc["o"],
-                                in_scales=(sc["att_q"], sc["att_k"], sc["o"]))
+                                in_scales=(sc["att_q"], sc["att_k"], sc["o"]), kv_planes=kvp)
         return q, k, o3, lse, h23
 
     def _mlp_h3(self, i, o3, x, h23):

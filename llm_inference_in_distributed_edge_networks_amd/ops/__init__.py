@@ -307,7 +307,7 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     return q, k, vt
 
 
-def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scales=None):
+def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scales=None, kv_planes=None):
     """Causal GQA flash attention -> (o [B*S, Hq*64], lse [B,Hq,S] or None).
 
     ``n_rows`` ([B] fp32, scored rows per window as in ``WindowBatch.n_rows``): only query rows
@@ -315,7 +315,9 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scal
     output rows are then undefined.  fp32 q/k/vt run the fp32 kernels; ``h3`` = s > 0 then writes s * o as the
     2-plane h3 activation [B*S, 2*Hq*64] the O-projection consumes.  ``in_scales`` = (s_q, s_k, s_v), powers of two
     with s |x| <= 2^15 for every element of q, k and v: the matrix work runs on scaled fp16 planes (three products;
-    the model derives them from weight bounds), else on three bf16 planes (six products)."""
+    the model derives them from weight bounds), else on three bf16 planes (six products).  ``kv_planes`` = (kp, vp)
+    from ``qkv_rope_h3(kv_scales=(s_k, s_v))`` (with ``in_scales``): the kernel stages those planes by LDS DMA
+    instead of splitting the fp32 K / V^T itself (the same result bit for bit)."""
     if not _gpu(q):
         o, lse = ref.attention(q, k, vt, S, need_lse)
         return (ref.h3_act(o, h3) if h3 else o), lse
@@ -326,6 +328,18 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scal
     if n_rows is not None:
         nr = n_rows.to(device=q.device, dtype=torch.float32).contiguous()
         assert nr.numel() == B
+    if q.dtype == torch.float32 and kv_planes is not None:
+        kp, vp = kv_planes
+        sp = vp.shape[-1]
+        _check_f32(q)
+        assert in_scales is not None and kp.dtype == torch.float16 and vp.dtype == torch.float16
+        assert kp.shape == (B, Hkv, 2, S, D) and vp.shape == (B, Hkv, 2, D, sp) and sp % 64 == 0 and sp >= S
+        assert kp.is_contiguous() and vp.is_contiguous() and kp.is_cuda and vp.is_cuda
+        o = _out_f32_or_h3(B * S, Hq * D, h3, q.device)
+        sq, sk, sv = in_scales
+        call("edge_flash_attn_fwd_h3p", ptr(q), ptr(kp), ptr(vp), ptr(o), ptr(lse), ptr(nr), B, Hq, Hkv, S, sp,
+             float(h3), float(sq), float(sk), float(sv), stream())
+        return o, lse
     if q.dtype == torch.float32:
         _check_f32(q, k, vt)
         assert D == 64 and vt.shape[-1] % 64 == 0 and vt.shape[-1] >= S
@@ -471,12 +485,18 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
     return out
 
 
-def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale):
-    """fp32 fused QKV projection + bias + RoPE + head-major scatter from h3 operands -> fp32 (q, k, vt)."""
+def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, kv_scales=None):
+    """fp32 fused QKV projection + bias + RoPE + head-major scatter from h3 operands -> fp32 (q, k, vt).
+
+    ``kv_scales`` = (s_k, s_v): also the K / V^T h3 planes at those scales for ``attention(kv_planes=...)`` ->
+    (q, k, vt, kp, vp); on the GPU ``vt`` is then None (the planes replace it)."""
     if not _gpu(a3):
         y = ref.h3_matmul(a3, w3, alpha)            # x @ w.T, then the rest of the fused op on fp32
         eye = torch.eye(y.shape[1], dtype=torch.float32)
-        return ref.qkv_rope(y, eye, bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
+        q, k, vt = ref.qkv_rope(y, eye, bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
+        if kv_scales is None:
+            return q, k, vt
+        return (q, k, vt) + ref.kv_planes(k, vt, *kv_scales)   # vt is zero-padded to s_pad(S) already
     kp, Kx = _check_h3(a3, w3, alpha)
     _check_f32(bias)
     assert D == 64, "HIP attention path is specialised for head_dim 64"
@@ -485,10 +505,19 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
     f32 = dict(dtype=torch.float32, device=a3.device)
     q = torch.empty(B, Hq, S, D, **f32)
     k = torch.empty(B, Hkv, S, D, **f32)
-    vt = torch.zeros(B, Hkv, D, sp, **f32) if sp != S else torch.empty(B, Hkv, D, sp, **f32)
+    kpl = vpl = vt = None
+    if kv_scales is None:
+        vt = torch.zeros(B, Hkv, D, sp, **f32) if sp != S else torch.empty(B, Hkv, D, sp, **f32)
+    else:   # the planes replace the fp32 V^T (only the attention reads it)
+        f16 = dict(dtype=torch.float16, device=a3.device)
+        kpl = torch.empty(B, Hkv, 2, S, D, **f16)
+        vpl = torch.zeros(B, Hkv, 2, D, sp, **f16) if sp != S else torch.empty(B, Hkv, 2, D, sp, **f16)
+    sk_, sv_ = kv_scales if kv_scales is not None else (0.0, 0.0)
     call("edge_gemm_qkv_rope_f32", ptr(a3), ptr(w3), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, kp, S,
-         Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), stream())
-    return q, k, vt
+         Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), ptr(kpl), ptr(vpl), float(sk_), float(sv_), stream())
+    if kv_scales is None:
+        return q, k, vt
+    return q, k, vt, kpl, vpl
 
 
 def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch.Tensor) -> torch.Tensor:

@@ -215,6 +215,24 @@ def split2h(x: torch.Tensor, s: float) -> tuple[torch.Tensor, torch.Tensor]:
     return hi, lo
 
 
+def kv_plane_perm(S_pad: int) -> torch.Tensor:
+    """Key order of the V^T h3 planes (gemm.hip kv_plane_pos): element index of key p within its row."""
+    p = torch.arange(S_pad)
+    k = p % 64
+    return (p - k) + ((4 * (k >> 5) + ((k >> 2) & 3)) << 3) + (((k >> 4) & 1) << 2) + (k & 3)
+
+
+def kv_planes(k: torch.Tensor, vt: torch.Tensor, sk: float, sv: float):
+    """fp32 K [B, Hkv, S, D] / V^T [B, Hkv, D, S_pad] -> the scaled fp16 h3 planes the fp32 QKV GEMM writes for the
+    plane-staged attention: kp [B, Hkv, 2, S, D], vp [B, Hkv, 2, D, S_pad] (keys in kv_plane_perm order)."""
+    kh, kl = split2h(k, sk)
+    vh, vl = split2h(vt, sv)
+    vp = torch.stack([vh, vl], 2)
+    out = torch.empty_like(vp)
+    out[..., kv_plane_perm(vt.shape[-1])] = vp
+    return torch.stack([kh, kl], 2).contiguous(), out.contiguous()
+
+
 def h3_act(x: torch.Tensor, s: float) -> torch.Tensor:
     """fp32 [R, K] -> 2-plane h3 activation [R, 2K] fp16 = [hi | lo] of s x (what the fp32-mode kernels emit for
     GEMM inputs)."""

@@ -187,6 +187,70 @@ def test_qkv_rope_h3(B, S, Hq, Hkv, rot, tile, two_term):
     assert rel_err(q, rq) < 4e-6 and rel_err(k, rk) < 4e-6 and rel_err(vt, rv) < 4e-6
 
 
+@pytest.mark.parametrize("B,S,Hq,Hkv,rot", [(2, 512, 14, 2, 64), (2, 100, 14, 2, 64), (1, 2048, 8, 8, 16),
+                                             (3, 200, 14, 2, 0), (64, 512, 14, 2, 64)])
+@pytest.mark.parametrize("tile", ["auto", "192", "256"])
+def test_qkv_kv_planes(B, S, Hq, Hkv, rot, tile):
+    """K / V^T h3 planes from the fp32 QKV epilogues (128x128, 256x192 and 256x256 tiles) are the split of the fp32
+    K / V^T, bit for bit, V^T keys in the attention kernel's P^T order and zero key padding; q and K unchanged."""
+    H = 896 if Hq == 14 else 512
+    Nq = (Hq + 2 * Hkv) * 64
+    x = rnd(B * S, H, seed=33)
+    w = rnd(Nq, H, s=1 / math.sqrt(H), seed=34).to(torch.bfloat16).float()
+    b = rnd(Nq, s=0.1, seed=35)
+    cos, sin = R.rope_tables(4096, max(rot, 2), 1e6 if rot == 64 else 1e4)
+    sx = R.h3_scale(x.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    sk, sv = 2.0 ** 9, 2.0 ** 11
+    try:
+        if tile == "192":
+            ops.set_gemm_tile(192)
+        elif tile == "256":
+            ops.set_gemm_qkv192(0)
+        q, k, vt, kp, vp = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV),
+                                           cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125,
+                                           kv_scales=(sk, sv))
+        q2, k2, vt2 = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV), cos.to(DEV),
+                                      sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_gemm_tile(0)
+        ops.set_gemm_qkv192(1)
+    assert vt is None and torch.equal(q, q2) and torch.equal(k, k2)   # the planes replace the fp32 V^T
+    rkp, rvp = R.kv_planes(k.cpu(), vt2.cpu(), sk, sv)
+    assert torch.equal(kp.cpu(), rkp)
+    assert torch.equal(vp.cpu(), rvp)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (3, 100, 14, 2), (1, 2048, 8, 8), (2, 64, 4, 1),
+                                         (2, 200, 14, 2)])
+@pytest.mark.parametrize("h3", [False, True])
+def test_attention_kv_planes_bit_identical(B, S, Hq, Hkv, h3):
+    """The LDS-DMA plane-staged attention (K / V^T planes from the QKV epilogue) equals the kernel that splits the
+    fp32 K / V^T itself (variant 2, 128 query rows, fp16 planes): output and LSE bit for bit, and the scored-rows mode
+    on its rows."""
+    q = rnd(B, Hq, S, 64, seed=46) * 0.5
+    k = rnd(B, Hkv, S, 64, seed=47) * 2
+    v = rnd(B, Hkv, S, 64, seed=48)
+    sp = R.s_pad(S)
+    vt = torch.zeros(B, Hkv, 64, sp)
+    vt[..., :S] = v.transpose(-1, -2)
+    s = R.h3_scale(v.abs().max().item()) if h3 else 0.0
+    sc = tuple(R.h3_scale(t.abs().max().item()) for t in (q, k, v))
+    kp, vp = R.kv_planes(k, vt, sc[1], sc[2])
+    args = (q.to(DEV), k.to(DEV), vt.to(DEV), S)
+    planes = (kp.to(DEV), vp.to(DEV))
+    o1, l1 = ops.attention(*args, need_lse=True, h3=s, in_scales=sc)
+    o2, l2 = ops.attention(q.to(DEV), k.to(DEV), None, S, need_lse=True, h3=s, in_scales=sc, kv_planes=planes)
+    assert torch.equal(o1, o2) and torch.equal(l1, l2)
+    n_rows = torch.tensor([float(min(31 + 40 * i, S - 2)) for i in range(B)], device=DEV)
+    o3, _ = ops.attention(*args, n_rows=n_rows, h3=s, in_scales=sc, kv_planes=planes)
+    W = o1.shape[1]
+    for bi in range(B):
+        lo = S - 1 - int(n_rows[bi])
+        assert torch.equal(o3.view(B, S, W)[bi, lo:], o1.view(B, S, W)[bi, lo:])
+
+
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (3, 100, 14, 2), (1, 2048, 8, 8), (2, 64, 4, 1)])
 @pytest.mark.parametrize("h3", [False, True])
 @pytest.mark.parametrize("variant,planes", [(0, "bf16"), (1, "bf16"), (2, "bf16"), (0, "fp16"), (2, "fp16")])
@@ -334,6 +398,26 @@ def test_full_model_nll_matches_cpu_fp32(name, B, S, values):
     cpu, gpu = _full_model_nll(get_config(name), B, S, values=values)
     rel = ((gpu - cpu).abs() / cpu.abs()).max().item()
     assert rel < 1e-4, (rel, cpu.tolist(), gpu.tolist())
+
+
+@pytest.mark.parametrize("name", ["qwen2-0.5b", "pythia-70m"])
+def test_full_model_kv_planes_identical(name, monkeypatch):
+    """The fp32 model with the plane-staged attention (default) equals the per-tile-split attention bit for bit."""
+    from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
+    from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows
+    from llm_inference_in_distributed_edge_networks_amd.models import DecoderLM, get_config
+    from llm_inference_in_distributed_edge_networks_amd.models import model as MM
+    cfg = get_config(name)
+    S = 512
+    toks = synthetic_stream(S * 4, cfg.vocab_size, 0)
+    b = next(batches(toks, [w for w in sliding_windows(toks.shape[1], S, 32) if w.length == S][:3], 3)).to(DEV)
+    m = DecoderLM.random_init(cfg, 0, device=DEV, dtype=torch.float32, values=torch.bfloat16)
+    out = {}
+    for flag in (True, False):
+        monkeypatch.setattr(MM, "_KV_PLANES", flag)
+        x = m.forward_hidden(b.ids)
+        out[flag] = (x.clone(), m.row_nll(x, b.rows, b.targets).clone())
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(32768, 9728, 896, "swiglu"), (4096, 2048, 512, "gelu"),

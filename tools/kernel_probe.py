@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--S", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--kv-planes", type=int, default=0, help="attn: stage K / V^T h3 planes by LDS DMA")
     a = ap.parse_args()
     B, S, Hq, Hkv, H = a.B, a.S, 14, 2, 896
     g = torch.Generator().manual_seed(0)
@@ -35,7 +36,12 @@ def main():
         sc = (2.0 ** 12, 2.0 ** 12, 2.0 ** 12)
         _, lse = ops.attention(q, k, vt, S, need_lse=True, h3=2.0 ** 10, in_scales=sc)
         if a.op == "attn":
-            fn = lambda: ops.attention(q, k, vt, S, need_lse=False, h3=2.0 ** 10, in_scales=sc)   # noqa: E731
+            kvp = None
+            if a.kv_planes:
+                kp, vp = R.kv_planes(k.cpu(), vt.cpu(), sc[1], sc[2])
+                kvp = (kp.to(dev), vp.to(dev))
+            fn = lambda: ops.attention(q, k, vt, S, need_lse=False, h3=2.0 ** 10, in_scales=sc,   # noqa: E731
+                                       kv_planes=kvp)
         else:
             fn = lambda: ops.attn_colsum(q, k, lse, S, in_scales=sc[:2])                          # noqa: E731
     elif a.op == "qkv":
@@ -60,7 +66,8 @@ def main():
         fn()
     en.record()
     torch.cuda.synchronize()
-    print(json.dumps({"op": a.op, "B": B, "S": S, "us_per_call": round(st.elapsed_time(en) / a.iters * 1e3, 2)}))
+    print(json.dumps({"op": a.op, "kv_planes": a.kv_planes, "B": B, "S": S,
+                      "us_per_call": round(st.elapsed_time(en) / a.iters * 1e3, 2)}))
 
 
 if __name__ == "__main__":
