@@ -1787,6 +1787,9 @@ __device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[
           }
         }
         if (a.vp) {
+#if EDGE_TUNING_BUILD
+          if (a.skip_epi == 6) continue;   // timing ablation: no V^T plane stores (wrong results)
+#endif
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             store_vt_plane1(a, b, head - a.Hq - a.Hkv, pos, d + r, lo[r]);

@@ -36,6 +36,8 @@ SHAPES = {  # name: (M, N, K, act, bias, resid)
     "h3_2t_down_b64": (32768, 896, 2 * 4864, "h3", False, True),
     "h3_2t_o_proj_b64": (32768, 896, 2 * 896, "h3", False, True),
     "h3_2t_qkv_rope_b64": (32768, 1152, 2 * 896, "h3_qkv_rope", True, False),
+    # the production fp32 QKV: K / V^T also emitted as the attention's h3 planes (no fp32 V^T)
+    "h3_2t_qkv_rope_kvp_b64": (32768, 1152, 2 * 896, "h3_qkv_rope_kvp", True, False),
 }
 
 
@@ -84,7 +86,9 @@ def main():
             # "/m<k>": W7 epilogue memory mode k (bit 0 nt stores, bit 1 nt residual loads)
             # "/nob1": B tiles staged on even K-tiles only, "/nob": no B staging (four-wave kernel, wrong results)
             # "/notrans": SwiGLU h3 epilogue without its two transcendentals (four-wave kernel, wrong results)
-            noepi = {"/noepi": 1, "/nostore": 2, "/nob1": 3, "/nob": 4, "/notrans": 5}.get("/" + spec.rpartition("/")[2], 0)
+            last = spec.rpartition("/")[2]
+            # "/novp": QKV epilogue without the V^T plane stores (four-wave 192 kernel, wrong results)
+            noepi = {"/noepi": 1, "/nostore": 2, "/nob1": 3, "/nob": 4, "/notrans": 5, "/novp": 6}.get("/" + last, 0)
             if noepi:
                 spec = spec.rpartition("/")[0]
             mode = int(spec.partition("/m")[2] or 0)
@@ -99,6 +103,8 @@ def main():
                     ops.qkv_rope(x, w, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
                 elif act == "h3_qkv_rope":
                     ops.qkv_rope_h3(x, w, 1.0, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
+                elif act == "h3_qkv_rope_kvp":
+                    ops.qkv_rope_h3(x, w, 1.0, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125, kv_scales=(1.0, 1.0))
                 elif act == "h3_swiglu":
                     ops.linear_h3(x, w, 1.0, act="swiglu_il")
                 elif act == "h3":
@@ -108,7 +114,7 @@ def main():
                 ops._native.lib().edge_gemm_set_skip_epi(0)
                 ops._native.lib().edge_gemm_set_w7_mode(0)
             return f
-        if act in ("qkv_rope", "h3_qkv_rope"):
+        if act in ("qkv_rope", "h3_qkv_rope", "h3_qkv_rope_kvp"):
             cos, sin = (t.to(dev) for t in ops.rope_tables(512, 64, 1e6))
         variants = {t: mk(t) for t in tiles}
         ours = variants[tiles[0]]
