@@ -91,11 +91,13 @@ def test_relevance_engine_gpu_vs_cpu(cfg):
     ids = torch.randint(0, cfg.vocab_size, (4, 128), generator=torch.Generator().manual_seed(2))
     rg, ing, mxg = RelevanceEngine(mg).head_relevance(ids.to(DEV))
     rc, inc, mxc = RelevanceEngine(mc).head_relevance(ids)
-    assert rel_err(mxg, mxc) < 2e-2
-    assert rel_err(rg, rc) < 0.1, rel_err(rg, rc)
+    assert rel_err(mxg, mxc) < 1e-2
+    # measured on MI355X (profiles/r03m_lrp_bf16_err.jsonl, seeds 2-4): per-head relevance <= 0.76 %, normalised
+    # table <= 2.8 % (the 3.2 % of docs/RESULTS.md is the full-size Qwen2 table)
+    assert rel_err(rg, rc) < 0.02, rel_err(rg, rc)
     # the calibrated table (normalised per layer over all windows) is what weighted_importance consumes
     wg, wc = rg.sum(0), rc.sum(0)
-    assert rel_err(wg / wg.sum(-1, keepdim=True), wc / wc.sum(-1, keepdim=True)) < 0.1
+    assert rel_err(wg / wg.sum(-1, keepdim=True), wc / wc.sum(-1, keepdim=True)) < 0.04
 
 
 @pytest.mark.parametrize("B,Hq,Hkv,S", [(2, 14, 2, 512), (1, 8, 8, 200), (3, 4, 2, 96), (1, 2, 1, 37)])

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--S", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--kv-planes", type=int, default=0, help="attn: stage K / V^T h3 planes by LDS DMA")
+    ap.add_argument("--save", default="", help="save the op's output tensors here (bit-exact A/B of two builds)")
+    ap.add_argument("--compare", default="", help="compare the op's output bit for bit with a --save file")
     a = ap.parse_args()
     B, S, Hq, Hkv, H = a.B, a.S, 14, 2, 896
     g = torch.Generator().manual_seed(0)
@@ -58,8 +60,16 @@ def main():
         x = torch.randn(B * S, H, generator=g).to(dev)
         w = (1 + 0.05 * torch.randn(H, generator=g)).to(dev)
         fn = lambda: ops.rmsnorm(x, w, 1e-6, h3=2.0 ** 10)                                       # noqa: E731
-    fn()
+    out = fn()
     torch.cuda.synchronize()
+    outs = [t.detach().cpu() for t in (out if isinstance(out, (tuple, list)) else (out,)) if torch.is_tensor(t)]
+    if a.save:
+        torch.save(outs, a.save)
+    if a.compare:
+        ref = torch.load(a.compare, weights_only=True)
+        same = [bool(torch.equal(x, y)) for x, y in zip(outs, ref)]
+        diff = [float((x.double() - y.double()).abs().max()) for x, y in zip(outs, ref)]
+        print(json.dumps({"op": a.op, "bit_identical": same, "max_abs_diff": diff}))
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     st.record()
     for _ in range(a.iters):
