@@ -270,6 +270,42 @@ __device__ __forceinline__ void split_frag_h(const float (&v)[8], float s, bf16x
   hi = __builtin_bit_cast(bf16x8_t, H);
   lo = __builtin_bit_cast(bf16x8_t, L);
 }
+// the unscaled split of the probabilities (the loop's hot split): hi by v_cvt_pk_f16_f32, lo = f16(x - hi) by
+// v_fma_mixlo_f16 / v_fma_mixhi_f16 straight from the fp32 value and the f16 hi half (x - hi is exact, one RNE to
+// f16: the same bits as split_frag_h's convert-back / packed subtract / convert, in 3 instead of 5 VALU per pair;
+// packed-f32 VALU beside MFMAs is the expensive kind).  Operands are VALU results (no MFMA -> asm hazard).
+__device__ __forceinline__ uint32_t mix_lo2(float x0, float x1, uint32_t h) {
+  uint32_t r;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(r) : "v"(x0), "v"(h), "v"(x1));
+  return r;
+}
+// row max over the lane halves without fmaxf's sNaN canonicalisation (two v_max_f32 x, x per step; the scores are
+// finite or -inf): the permlane swap's outputs are VALU results (no MFMA -> asm hazard)
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float xor_max16_raw(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax_raw(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor_max32_raw(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax_raw(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ void split_frag_h1(const float (&v)[8], bf16x8_t& hi, bf16x8_t& lo) {
+  u32x4_t H, L;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    H[e] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{v[2 * e], v[2 * e + 1]}, f16x2_t));
+    L[e] = mix_lo2(v[2 * e], v[2 * e + 1], H[e]);
+  }
+  hi = __builtin_bit_cast(bf16x8_t, H);
+  lo = __builtin_bit_cast(bf16x8_t, L);
+}
 // NPL planes of 8 values: three bf16 planes (x6) or two scaled fp16 planes (h3)
 template <bool F16>
 __device__ __forceinline__ void split_planes(const float (&v)[8], float s, bf16x8_t (&p)[F16 ? 2 : 3]) {
@@ -474,7 +510,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[kt][r]);
-    mloc = xor_max32(xor_max16(mloc));
+    if constexpr (F16) mloc = xor_max32_raw(xor_max16_raw(mloc));
+    else mloc = xor_max32(xor_max16(mloc));
     const float mc = mloc * sc_log2;
     if (__builtin_amdgcn_ballot_w64(mc > m2 + FTAU)) {  // wave-uniform lazy rescale
       const float mn = fmaxf(m2, mc);
@@ -502,7 +539,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
 #pragma unroll
       for (int r = 0; r < 4; ++r) { pv8[r] = st[2 * sk][r]; pv8[4 + r] = st[2 * sk + 1][r]; }
       bf16x8_t pp[NPL];
-      split_planes<F16>(pv8, 1.f, pp);
+      if constexpr (F16) split_frag_h1(pv8, pp[0], pp[1]);
+      else split_planes<F16>(pv8, 1.f, pp);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int row = dt * 16 + ql;

@@ -54,8 +54,9 @@ def main():
         bias = (torch.randn((Hq + 2 * Hkv) * 64, generator=g) * 0.02).to(dev)
         cos, sin = R.rope_tables(4096, 64, 1e6)
         cos, sin, w3 = cos.to(dev), sin.to(dev), w3.to(dev)
+        kvs = (2.0 ** 6, 2.0 ** 6) if a.kv_planes else None   # the K / V^T planes the attention stages by DMA
         fn = lambda: ops.qkv_rope_h3(x3, w3, 1.0 / (2.0 ** 10 * sw), bias, cos, sin, B, S, Hq, Hkv, 64, 64,  # noqa
-                                     0.125)
+                                     0.125, kv_scales=kvs)
     else:
         x = torch.randn(B * S, H, generator=g).to(dev)
         w = (1 + 0.05 * torch.randn(H, generator=g)).to(dev)
