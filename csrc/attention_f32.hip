@@ -563,11 +563,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     u32x2_t hw[4], lw[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      float hi[4], lo[4];
+      float hi[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) split2h(oacc[dt][r] * inv * h3s, hi[r], lo[r]);
-      hw[dt] = u32x2_t{pack_h2(hi[0], hi[1]), pack_h2(hi[2], hi[3])};
-      lw[dt] = u32x2_t{pack_h2(lo[0], lo[1]), pack_h2(lo[2], lo[3])};
+      for (int r = 0; r < 4; ++r) hi[r] = oacc[dt][r] * inv * h3s;
+      const u32x2_t t0 = split2h_pk(hi[0], hi[1]), t1 = split2h_pk(hi[2], hi[3]);
+      hw[dt] = u32x2_t{t0[0], t1[0]};
+      lw[dt] = u32x2_t{t0[1], t1[1]};
     }
 #pragma unroll
     for (int q2 = 0; q2 < 2; ++q2) {

@@ -58,6 +58,19 @@ __device__ __forceinline__ void split2h(float x, float& hi, float& lo) {
 __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
   return __builtin_bit_cast(uint32_t, f16x2_t{(_Float16)a, (_Float16)b});
 }
+// split2h of a value pair as packed planes: H = [hi(x0) | hi(x1)] by v_cvt_pk_f16_f32, L = [lo(x0) | lo(x1)] with
+// lo = f16(x - hi) straight from the fp32 value and the f16 hi half by v_fma_mixlo_f16 / v_fma_mixhi_f16 (x - hi is
+// exact, one RNE to f16): bit-identical to split2h + pack_h2 in 3 VALU instead of 5-6.  The asm's operands are the
+// fp32 inputs and the convert's result; the convert reads the inputs first, so any MFMA -> VALU hazard on them is
+// resolved by the compiler-visible instruction before the asm issues.
+__device__ __forceinline__ u32x2_t split2h_pk(float x0, float x1) {   // -> {H, L}
+  const uint32_t H = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{x0, x1}, f16x2_t));
+  uint32_t L;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(L) : "v"(x0), "v"(H), "v"(x1));
+  return u32x2_t{H, L};
+}
 // column of the 2-plane activation row holding column kp of A' (K = plane width; K-blocks never straddle a K-tile)
 __device__ __forceinline__ int h3_acol(int kp, int K) {
   const int j = kp / K;                          // A' block 0..2: planes lo hi hi
@@ -65,22 +78,19 @@ __device__ __forceinline__ int h3_acol(int kp, int K) {
 }
 // Store s * v[0..3] at column `col` of an h3 activation row (plane width K): two 8-byte stores.
 __device__ __forceinline__ void store_h3_4(f16_t* __restrict__ row, int K, int col, const float (&v)[4], float s) {
-  float hi[4], lo[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) split2h(v[e] * s, hi[e], lo[e]);
-  *(u32x2_t*)(row + col) = u32x2_t{pack_h2(hi[0], hi[1]), pack_h2(hi[2], hi[3])};
-  *(u32x2_t*)(row + (size_t)K + col) = u32x2_t{pack_h2(lo[0], lo[1]), pack_h2(lo[2], lo[3])};
+  const float x0 = v[0] * s, x1 = v[1] * s, x2 = v[2] * s, x3 = v[3] * s;
+  const u32x2_t t0 = split2h_pk(x0, x1), t1 = split2h_pk(x2, x3);
+  *(u32x2_t*)(row + col) = u32x2_t{t0[0], t1[0]};
+  *(u32x2_t*)(row + (size_t)K + col) = u32x2_t{t0[1], t1[1]};
 }
 // 8 consecutive values: two 16-byte stores.
 __device__ __forceinline__ void store_h3_8(f16_t* __restrict__ row, int K, int col, const float (&v)[8], float s) {
-  float hi[8], lo[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) split2h(v[e] * s, hi[e], lo[e]);
   u32x4_t wh, wl;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    wh[e] = pack_h2(hi[2 * e], hi[2 * e + 1]);
-    wl[e] = pack_h2(lo[2 * e], lo[2 * e + 1]);
+    const u32x2_t t = split2h_pk(v[2 * e] * s, v[2 * e + 1] * s);
+    wh[e] = t[0];
+    wl[e] = t[1];
   }
   *(u32x4_t*)(row + col) = wh;
   *(u32x4_t*)(row + (size_t)K + col) = wl;

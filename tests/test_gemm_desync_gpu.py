@@ -1,0 +1,88 @@
+"""Epilogue desync of the four-wave GEMMs (csrc/gemm.hip GemmArgs::split_h): the odd workgroups of each XCD run the
+first K-tiles of their last tile first, park the raw accumulators in a per-call workspace and finish that tile last.
+The accumulation order of every output is unchanged, so the result must be bit-identical to the plain persistent
+walk - for every epilogue family the bench runs (SwiGLU h3 planes, fp32 residual in place, QKV + RoPE + K / V^T
+planes, LM-head LSE) and for split points other than the default half tile."""
+import pytest
+import torch
+
+from llm_inference_in_distributed_edge_networks_amd import ops
+from llm_inference_in_distributed_edge_networks_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rnd(*shape, s=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * s
+
+
+def h3_operands(M, N, K, seed):
+    x = rnd(M, K, seed=seed)
+    w = (rnd(N, K, s=0.02, seed=seed + 1)).bfloat16().float()   # bf16 values: the two-product (paired-B) GEMM
+    w3, sw = R.h3_weight(w)
+    s = 2.0 ** 10
+    return R.h3_act(x, s).to(DEV), w3.to(DEV), 1.0 / (s * sw)
+
+
+def each_split(fn):
+    outs = {}
+    prev = ops.get_gemm_split()
+    try:
+        for k in (0, -1, 2, 6):
+            ops.set_gemm_split(k)
+            r = fn()
+            torch.cuda.synchronize()
+            outs[k] = [t.clone() for t in (r if isinstance(r, (tuple, list)) else (r,)) if torch.is_tensor(t)]
+    finally:
+        ops.set_gemm_split(prev)
+    return outs
+
+
+def assert_identical(outs):
+    for k, o in outs.items():
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b), f"split {k} differs from the plain walk"
+
+
+@pytest.mark.parametrize("M,N,K,kind", [(8192, 9728, 896, "swiglu"), (32768, 896, 896, "resid"),
+                                         (32768, 896, 4864, "resid")])
+def test_desync_bit_identical_linear(M, N, K, kind):
+    a3, w3, alpha = h3_operands(M, N, K, 1)
+    if kind == "swiglu":
+        fn = lambda: ops.linear_h3(a3, w3, alpha, act="swiglu_il", out_scale=64.0)   # noqa: E731
+    else:
+        res = rnd(M, N, seed=5).to(DEV)
+        fn = lambda: ops.linear_h3(a3, w3, alpha, residual=res)                       # noqa: E731
+    assert_identical(each_split(fn))
+
+
+def test_desync_bit_identical_inplace_residual():
+    """C aliases the residual (the down projection's out=y): a parked tile's epilogue still reads its own rows."""
+    M, N, K = 32768, 896, 896
+    a3, w3, alpha = h3_operands(M, N, K, 2)
+    y0 = rnd(M, N, seed=6).to(DEV)
+
+    def fn():
+        y = y0.clone()
+        return ops.linear_h3(a3, w3, alpha, residual=y, out=y)
+    assert_identical(each_split(fn))
+
+
+def test_desync_bit_identical_qkv_planes():
+    B, S, Hq, Hkv = 64, 512, 14, 2
+    a3, w3, alpha = h3_operands(B * S, (Hq + 2 * Hkv) * 64, 896, 3)
+    bias = rnd((Hq + 2 * Hkv) * 64, s=0.02, seed=7).to(DEV)
+    cos, sin = R.rope_tables(4096, 64, 1e6)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    fn = lambda: ops.qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, 64, 64, 0.125,   # noqa: E731
+                                 kv_scales=(64.0, 64.0))
+    assert_identical(each_split(fn))
+
+
+def test_desync_bit_identical_lse_head():
+    R_, V, K = 2048, 18432, 896   # 8 x 72 = 576 tiles: two or more per workgroup
+    a3, w3, alpha = h3_operands(R_, V, K, 4)
+    tgt = torch.randint(0, V, (R_,), generator=torch.Generator().manual_seed(8)).to(DEV)
+    assert_identical(each_split(lambda: ops.head_nll_h3(a3, w3, alpha, tgt)))

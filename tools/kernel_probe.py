@@ -5,6 +5,8 @@ Shapes: Qwen2-0.5B, one 64-window micro-batch of 512 tokens (M = 32768), bf16-va
   qkv     h3 QKV GEMM + bias + RoPE + scatter (256x192 tiles)
   colsum  column-sum importance on the fp16 planes
   norm    fp32 RMSNorm -> h3 planes
+  gateup  h3 gate/up GEMM + SwiGLU -> h3 planes (two products)
+  down    h3 down GEMM + fp32 residual (two products)
 Prints the mean time per call (events) as JSON."""
 import argparse
 import json
@@ -20,7 +22,7 @@ from llm_inference_in_distributed_edge_networks_amd.ops import reference as R  #
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--op", default="attn", choices=["attn", "qkv", "colsum", "norm"])
+    ap.add_argument("--op", default="attn", choices=["attn", "qkv", "colsum", "norm", "gateup", "down"])
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--S", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
@@ -57,6 +59,18 @@ def main():
         kvs = (2.0 ** 6, 2.0 ** 6) if a.kv_planes else None   # the K / V^T planes the attention stages by DMA
         fn = lambda: ops.qkv_rope_h3(x3, w3, 1.0 / (2.0 ** 10 * sw), bias, cos, sin, B, S, Hq, Hkv, 64, 64,  # noqa
                                      0.125, kv_scales=kvs)
+    elif a.op in ("gateup", "down"):   # h3 SwiGLU GEMM -> h3 planes / down GEMM + fp32 residual (two products)
+        K, N = (H, 9728) if a.op == "gateup" else (4864, H)
+        x = torch.randn(B * S, K, generator=g)
+        w = (torch.randn(N, K, generator=g) * 0.02).bfloat16().float()
+        w3, sw = R.h3_weight(w)
+        x3 = ops.split_h3(x.to(dev), 2.0 ** 10) if K == H else R.h3_act(x, 2.0 ** 10).to(dev)
+        w3 = w3.to(dev)
+        if a.op == "gateup":
+            fn = lambda: ops.linear_h3(x3, w3, 1.0 / (2.0 ** 10 * sw), act="swiglu_il", out_scale=2.0 ** 6)  # noqa
+        else:
+            res = torch.randn(B * S, N, generator=g).to(dev)
+            fn = lambda: ops.linear_h3(x3, w3, 1.0 / (2.0 ** 10 * sw), residual=res)                      # noqa
     else:
         x = torch.randn(B * S, H, generator=g).to(dev)
         w = (1 + 0.05 * torch.randn(H, generator=g)).to(dev)
