@@ -68,12 +68,6 @@ struct GemmArgs {
                  // t -> A plane (t odd: hi, even: lo) column 64 (t >> 1), B column 64 (t >> 1) (b_kcol)
   float alpha = 1.f;      // h3: 1 / (s_a s_b), the product's scale (applied with the row scale)
   float out_scale = 1.f;  // h3 outputs (SwiGLU / GELU): the next GEMM's input scale s_a
-  // four-wave kernel, epilogue desync: odd workgroups of each XCD run the first split_h K-tiles of their LAST tile
-  // first (accumulators saved raw to ws), then their other tiles, then the rest of the last tile (accumulators
-  // restored): their epilogues fall half a tile after the even workgroups' (bit-identical result; 0 = off)
-  float* ws = nullptr;
-  int split_h = 0;
-  size_t ws_bytes = 0;   // host side: the workspace handed to this GEMM call (edge_gemm_set_ws)
 };
 
 // element column of A holding GEMM column k (k a K-tile start)
@@ -1894,23 +1888,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   const int tile0 = walk.first, G = walk.stride;
   if (tile0 >= walk.end) return;
   const int nk = a.K / 64;
-  const int ntw = (walk.end - 1 - tile0) / G + 1;   // tiles of this workgroup
-  const int total = ntw * nk;                       // K-tiles of this workgroup
-  // epilogue desync (GemmArgs::split_h): segment s of the workgroup's K-tile sequence -> (tile, first K-tile, end
-  // K-tile, mode 0 = whole tile / 1 = partial, accumulators saved / 2 = rest of a partial tile, accumulators restored)
-  const bool ph1 = PF == 0 && a.split_h > 0 && ntw >= 2 && ((blockIdx.x >> 3) & 1);   // wave-uniform
-  const int nseg = ph1 ? ntw + 1 : ntw;
-  auto seg = [&](int sg, int& tl, int& kb, int& ke, int& md) {
-    if (!ph1) {
-      tl = tile0 + sg * G, kb = 0, ke = nk, md = 0;
-    } else if (sg == 0) {
-      tl = tile0 + (ntw - 1) * G, kb = 0, ke = a.split_h, md = 1;
-    } else if (sg < ntw) {
-      tl = tile0 + (sg - 1) * G, kb = 0, ke = nk, md = 0;
-    } else {
-      tl = tile0 + (ntw - 1) * G, kb = a.split_h, ke = nk, md = 2;
-    }
-  };
+  const int total = ((walk.end - 1 - tile0) / G + 1) * nk;   // K-tiles of this workgroup
 
   // ---- DMA: wave w stages 1-KiB blocks w, w+4, ... of each operand tile (8 rows of 128 B each)
   const char* sa = nullptr;
@@ -1934,12 +1912,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       ob[i] = (uint32_t)(min(rb, a.N - 1 - n0) * a.ldb + ((lane & 7) ^ swz(r)) * 8) * 2u;
     }
   };
-  int st_q = 0, st_kt = 0, st_tile = tile0, st_seg = 0, st_kend = nk;
-  {
-    int md_;
-    seg(0, st_tile, st_kt, st_kend, md_);
-  }
-  set_stage_tile(st_tile);
+  int st_q = 0, st_kt = 0, st_tile = tile0;
+  set_stage_tile(tile0);
   // item r < 8: A block, else B block r - 8 (with PB into the K-tile pair's slot; its callers skip the B items of
   // odd K-tiles at compile time)
   auto dma_item = [&](int r, char* buf, int kba, int kb) {
@@ -1960,10 +1934,10 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   auto advance_stage = [&]() {   // the DMA stream stops (repeats its last K-tile) at the end
     ++st_q;
     if (st_q >= total) {
-      st_kt = st_kend - 1;
-    } else if (++st_kt == st_kend) {
-      int md_;
-      seg(++st_seg, st_tile, st_kt, st_kend, md_);
+      st_kt = nk - 1;
+    } else if (++st_kt == nk) {
+      st_kt = 0;
+      st_tile += G;
       set_stage_tile(st_tile);
     }
     st_kba = a_kcol(a, st_kt * 64) * 2;
@@ -2075,19 +2049,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   for (int j = 0; j < NJ; ++j) DS_READ_B128(XB[j], bbase[0], j * 2048);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-  // kbeg: the segment's first K-tile, whose MFMAs start the accumulators from zero (-1 for a restored segment)
-  int tile, kt, kend, cmode, cseg = 0, m0, n0;
-  seg(0, tile, kt, kend, cmode);
-  int kbeg = kt;
+  int tile = tile0, kt = 0, m0, n0;
   tile_origin(tile, a.M, a.N, 256, BN, m0, n0);
-  // raw accumulators of a partial tile: wave w's 8 x NJ f32x4 at ws[(block 4 + w) 8 NJ 64 + (i NJ + j) 64 + lane]
-  // (the address is formed where it is used: a pointer live across the K loop costs two VGPRs there)
-  // SGPR base per group of four f32x4 (the 13-bit immediate reaches 4 KiB) + one 32-bit lane offset (saddr form)
-  auto ws_base = [&](int q4) {
-    const uint64_t p = (uint64_t)a.ws + ((uint64_t)blockIdx.x * 4 + wave) * (8 * NJ * 64 * 16) + (uint64_t)q4 * 4096;
-    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)p) |
-           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);   // wave-uniform: SGPR pair
-  };
   float rs[8];
   auto load_rs = [&](int mt) {
     if constexpr (BN == 256) {
@@ -2113,7 +2076,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     const uint32_t boB = PB ? ((t >> 1) & 1) * TB : bo, bnB = PB ? (((t + 1) >> 1) & 1) * TB : bn;
     // M(t,0) on X, K-half 1 of K-tile t -> Y
     __builtin_amdgcn_sched_barrier(0);
-    if (kt == kbeg) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, std::false_type{}, std::true_type{}, dmab_c);
+    if (kt == 0) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, std::false_type{}, std::true_type{}, dmab_c);
     else mma(XA, XB, YA, YB, bo, boB, 1, std::false_type{}, std::false_type{}, std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < total) {
@@ -2135,20 +2098,11 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ++kt;
-    if (decltype(end_c)::value && kt == kend) {
+    if (decltype(end_c)::value && kt == nk) {
       // all MFMAs of the tile were issued; the epilogue reads the accumulators after they drain
       MFMA_DRAIN();
       __builtin_amdgcn_sched_barrier(0);
-      if (cmode == 1) {   // partial tile (desync): the raw accumulators to the workspace straight from the AGPRs
-        const uint32_t lo16 = (threadIdx.x & 63) * 16;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3" : : "v"(lo16), "a"(acc[i][j]),
-                         "s"(ws_base((i * NJ + j) >> 2)), "i"(((i * NJ + j) & 3) * 1024) : "memory");
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (BN == 256 && EPI == EPI_H3_SWIGLU) {
+      if constexpr (BN == 256 && EPI == EPI_H3_SWIGLU) {
 #if EDGE_TUNING_BUILD
         if (a.skip_epi != 1)   // timing ablation: no epilogue (wrong results)
 #endif
@@ -2218,22 +2172,11 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      if (++cseg < nseg) {
-        seg(cseg, tile, kt, kend, cmode);
-        kbeg = cmode == 2 ? -1 : kt;
+      kt = 0;
+      tile += G;
+      if (tile < walk.end) {
         tile_origin(tile, a.M, a.N, 256, BN, m0, n0);
         load_rs(m0);
-        if (cmode == 2) {   // the rest of the partial tile: its saved accumulators loaded straight into the AGPRs
-          const uint32_t lo16 = (threadIdx.x & 63) * 16;
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-              asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=a"(acc[i][j]) : "v"(lo16),
-                           "s"(ws_base((i * NJ + j) >> 2)), "i"(((i * NJ + j) & 3) * 1024) : "memory");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (asm loads: the compiler does not count them)
-          ACC_SETTLE();
-        }
       }
       // the next tile's first K-half fragments again (K-tile t+1 landed in buffer bn before this K-tile's barrier):
       // re-reading them here leaves the copies read during M(t,1) dead across the epilogue, which gets their VGPRs
@@ -2496,29 +2439,10 @@ static int launch_8p(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// Epilogue desync of the four-wave kernel (GemmArgs::split_h): g_split -1 = auto (half the tile's K-tiles), 0 = off,
-// k > 0 = k K-tiles.  The workspace for the saved accumulators is handed over by edge_gemm_set_ws right before the
-// GEMM call that may use it and is consumed by that launch (never reused by a later one: its memory belongs to the
-// caller's allocation of that call).
-static int g_split = 0;   // default off until the same-box A/B says otherwise (ops.set_gemm_split, EDGE_GEMM_SPLIT)
-static void* g_ws = nullptr;
-static size_t g_ws_bytes = 0;
-static size_t w4_ws_bytes(int BN) { return (size_t)num_cus() * 4 * 8 * (BN / 32) * 64 * 16; }
-
 template <int EPI, int RH, int PF, int BN, bool PB>
-static int launch_4w_pb(const GemmArgs& args, hipStream_t st) {
-  GemmArgs a = args;
+static int launch_4w_pb(const GemmArgs& a, hipStream_t st) {
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   const int grid = std::min(tiles, num_cus());
-  const int nk = a.K / 64;
-  int h = g_split < 0 ? (nk / 2) & ~1 : g_split & ~1;
-  // Only the epilogue families its bit-identity tests cover (tests/test_gemm_desync_gpu.py): the SwiGLU h3 planes
-  // (256), the 256x224 fp32 residual / bias and the 256x192 QKV.  Not the generic 256-wide path: the LM-head LSE's
-  // desync test faulted on the GPU once (cause not found), so that path stays on the plain walk.
-  constexpr bool covered = (BN == 256 && EPI == EPI_H3_SWIGLU) || BN == 224 || BN == 192;
-  if (!covered || PF > 0 || h <= 0 || h >= nk || tiles < 2 * grid || !a.ws || a.ws_bytes < w4_ws_bytes(BN)) h = 0;
-  a.split_h = h;
-  if (!h) a.ws = nullptr;
   constexpr int lds = w4::Geo<BN>::LDS + (PF > 0 ? 1024 : 0);
   static bool attr = false;
   if (!attr) {
@@ -2585,11 +2509,6 @@ static int launch_w7(const GemmArgs& a, hipStream_t st) {
 template <int EPI, int RH = 0>
 static int launch(const GemmArgs& args, hipStream_t st) {
   GemmArgs a = args;
-  // the workspace handed over for this call (consumed here: a later call never sees it)
-  a.ws = (float*)g_ws;
-  a.ws_bytes = g_ws_bytes;
-  g_ws = nullptr;
-  g_ws_bytes = 0;
   a.walk = g_walk;
   a.skip_epi = EDGE_TUNING_BUILD ? g_skip_epi : 0;
   a.rs_lds = g_rs_lds;
@@ -2699,20 +2618,6 @@ EDGE_API int edge_gemm_set_qkv192(int on) {
   g_qkv192 = on;
   return 0;
 }
-
-// epilogue desync of the four-wave GEMMs: -1 auto, 0 off, k K-tiles (see launch_4w_pb)
-EDGE_API int edge_gemm_set_split(int k) {
-  g_split = k;
-  return 0;
-}
-EDGE_API int edge_gemm_get_split() { return g_split; }
-// workspace for the NEXT GEMM launch only (bytes >= edge_gemm_ws_bytes()); consumed by it
-EDGE_API int edge_gemm_set_ws(void* p, long long bytes) {
-  g_ws = p;
-  g_ws_bytes = bytes > 0 ? (size_t)bytes : 0;
-  return 0;
-}
-EDGE_API long long edge_gemm_ws_bytes() { return (long long)w4_ws_bytes(256); }
 
 EDGE_API int edge_gemm_set_w7(int on) {
   g_w7 = on;

@@ -191,36 +191,6 @@ def set_gemm_qkv192(on) -> None:
     call("edge_gemm_set_qkv192", int(on))
 
 
-def set_gemm_split(k: int) -> None:
-    """Epilogue desync of the four-wave GEMMs (A/B and tests): half of each XCD's workgroups run the first k K-tiles
-    of their last tile first (raw accumulators parked in a per-call workspace) and finish it last, so their epilogues
-    fall half a tile after the others' and the chip's HBM store bursts halve.  -1 = auto (half a tile, default),
-    0 = off.  Bit-identical results either way (same accumulation order)."""
-    call("edge_gemm_set_split", int(k))
-
-
-def get_gemm_split() -> int:
-    return int(lib().edge_gemm_get_split())
-
-
-_WS_BYTES: int | None = None
-
-
-def _gemm_ws(dev) -> torch.Tensor | None:
-    """Workspace for the NEXT GEMM launch's epilogue desync (edge_gemm_set_ws; the launch consumes it, so a later
-    GEMM never sees this allocation).  Returned so the caller keeps it alive across the launch; stream-ordered reuse
-    by the caching allocator (and its graph-capture pool) is safe after that."""
-    global _WS_BYTES
-    L = lib()
-    if not hasattr(L, "edge_gemm_set_ws"):   # an older build under A/B
-        return None
-    if _WS_BYTES is None:   # 4 waves x 8 x 8 f32x4 accumulators x 64 lanes per workgroup, one workgroup per CU
-        _WS_BYTES = torch.cuda.get_device_properties(dev).multi_processor_count * 4 * 8 * 8 * 64 * 16
-    ws = torch.empty(_WS_BYTES, dtype=torch.uint8, device=dev)
-    L.edge_gemm_set_ws(ws.data_ptr(), _WS_BYTES)
-    return ws
-
-
 def set_gemm_walk(chunked) -> None:
     """Persistent 256x256 GEMMs: XCD-contiguous tile chunks (default) or the grid-strided walk.  A/B only.
     2 = chunked for the four-wave kernel too (it walks strided otherwise)."""
@@ -302,7 +272,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None,
     rs = None if norm is None else _norm_scale(norm, K)
     ssq_out = torch.empty(M, gemm_ssq_parts(M, N, K, act, bias is not None, residual is not None),
                           dtype=torch.float32, device=x.device) if want_ssq else None
-    _ws = _gemm_ws(x.device)
     call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), _ACT[act], ptr(rs), ptr(ssq_out), stream())
     if want_ssq:
@@ -332,7 +301,6 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     if ssq is not None:
         if _QKV_ROW_RSCALE or ssq.shape[1] not in (8, 14) or not ssq.is_contiguous() or ssq.data_ptr() % 16:
             rs, ssq = _norm_scale(norm, K), None
-    _ws = _gemm_ws(x.device)
     call("edge_gemm_qkv_rope", ptr(x), ptr(wqkv), ptr(bqkv), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, K, S,
          Hq, Hkv, rot_dim, sp, float(q_scale), ptr(rs), ptr(ssq), 0 if ssq is None else ssq.shape[1], float(eps),
          stream())
@@ -455,7 +423,6 @@ def head_nll(h, w, targets):
     tgt = torch.empty(R, dtype=torch.float32, device=h.device)
     nll = torch.empty(R, dtype=torch.float32, device=h.device)
     t64 = targets.to(torch.int64).contiguous()
-    _ws = _gemm_ws(h.device)
     call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, 0, 0.0, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
@@ -512,7 +479,6 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
         out = torch.empty(M, 2 * No, dtype=torch.float16, device=a3.device)
         ldc = 2 * No
         code = _ACT[act]
-    _ws = _gemm_ws(a3.device)
     call("edge_gemm_f32", ptr(a3), ptr(w3), ptr(out), M, N, Kx, kp, a3.stride(0), w3.stride(0), ldc, ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), code, ptr(rscale), float(alpha),
          float(out_scale), stream())
@@ -547,7 +513,6 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
         kpl = torch.empty(B, Hkv, 2, S, D, **f16)
         vpl = torch.zeros(B, Hkv, 2, D, sp, **f16) if sp != S else torch.empty(B, Hkv, 2, D, sp, **f16)
     sk_, sv_ = kv_scales if kv_scales is not None else (0.0, 0.0)
-    _ws = _gemm_ws(a3.device)
     call("edge_gemm_qkv_rope_f32", ptr(a3), ptr(w3), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, kp, S,
          Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), ptr(kpl), ptr(vpl), float(sk_), float(sv_), stream())
     if kv_scales is None:
@@ -568,7 +533,6 @@ def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch
     pmax, psum = torch.empty(R, nparts, **f32), torch.empty(R, nparts, **f32)
     tgt, nll = torch.empty(R, **f32), torch.empty(R, **f32)
     t64 = targets.to(torch.int64).contiguous()
-    _ws = _gemm_ws(a3.device)
     call("edge_gemm_lse", ptr(a3), ptr(w3), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, kp, float(alpha),
          stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
@@ -589,7 +553,6 @@ def linear_rowscale(x: torch.Tensor, w: torch.Tensor, rscale: torch.Tensor, resi
     N = w.shape[0]
     out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     rs = rscale.to(torch.float32).contiguous()
-    _ws = _gemm_ws(x.device)
     call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), None,
          ptr(residual), 0 if residual is None else residual.stride(0), 0, ptr(rs), None, stream())
     return out

@@ -42,9 +42,6 @@ _SIGS = {
     "edge_gemm_set_rs_lds": [c_i],
     "edge_gemm_set_lse256": [c_i],
     "edge_gemm_set_w7_mode": [c_i],
-    "edge_gemm_set_split": [c_i],
-    "edge_gemm_get_split": [],
-    "edge_gemm_set_ws": [c_p, c_ll],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],
@@ -119,9 +116,6 @@ def _apply_tuning_env(L) -> None:
         L.edge_gemm_set_rs_lds(0)
     if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # N = 896 GEMMs back on the 256x256 tiles
         L.edge_gemm_set_w7(0)
-    sp = os.environ.get("EDGE_GEMM_SPLIT")  # four-wave GEMM epilogue desync: -1 auto, 0 off, k K-tiles
-    if sp and hasattr(L, "edge_gemm_set_split"):
-        L.edge_gemm_set_split(int(sp))
 
 
 def available() -> bool:
