@@ -68,6 +68,8 @@ struct GemmArgs {
                  // t -> A plane (t odd: hi, even: lo) column 64 (t >> 1), B column 64 (t >> 1) (b_kcol)
   float alpha = 1.f;      // h3: 1 / (s_a s_b), the product's scale (applied with the row scale)
   float out_scale = 1.f;  // h3 outputs (SwiGLU / GELU): the next GEMM's input scale s_a
+  int stagger = 0;        // four-wave kernel: the odd workgroups of each XCD start stagger x 1024 cycles late, so
+                          // the chip's epilogue store bursts split in two (A/B; ops.set_gemm_stagger)
 };
 
 // element column of A holding GEMM column k (k a K-tile start)
@@ -326,9 +328,11 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
         const float sc = head < a.Hq ? a.q_scale : 1.f;
         float* dst = head < a.Hq ? a.qf + (((size_t)b * a.Hq + head) * a.S + pos) * 64
                                  : a.kf + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
+        if (head < a.Hq || a.kf) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          *(f32x4_t*)(dst + j * 16 + g * 4) = f32x4_t{v[j][0] * sc, v[j][1] * sc, v[j][2] * sc, v[j][3] * sc};
+          for (int j = 0; j < 4; ++j)
+            *(f32x4_t*)(dst + j * 16 + g * 4) = f32x4_t{v[j][0] * sc, v[j][1] * sc, v[j][2] * sc, v[j][3] * sc};
+        }
         if (head >= a.Hq && a.kp) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) store_k_planes4(a, b, head - a.Hq, pos, j * 16 + g * 4, v[j]);
@@ -1769,8 +1773,10 @@ __device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[
         const float sc = head < a.Hq ? a.q_scale : 1.f;
         float* dst = head < a.Hq ? a.qf + (((size_t)b * a.Hq + head) * a.S + pos) * 64
                                  : a.kf + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
-        *(f32x4_t*)(dst + d) = lo * sc;
-        *(f32x4_t*)(dst + d + 32) = hi * sc;
+        if (head < a.Hq || a.kf) {   // (fp32 K skipped when only its planes are wanted: head is wave-uniform)
+          *(f32x4_t*)(dst + d) = lo * sc;
+          *(f32x4_t*)(dst + d + 32) = hi * sc;
+        }
         if (head >= a.Hq && a.kp) {
           const float l4[4] = {lo[0], lo[1], lo[2], lo[3]}, h4[4] = {hi[0], hi[1], hi[2], hi[3]};
           store_k_planes4(a, b, head - a.Hq, pos, d, l4);
@@ -1889,6 +1895,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   if (tile0 >= walk.end) return;
   const int nk = a.K / 64;
   const int total = ((walk.end - 1 - tile0) / G + 1) * nk;   // K-tiles of this workgroup
+  if (a.stagger > 0 && ((blockIdx.x >> 3) & 1)) {   // wave-uniform: s_sleep 16 = 1024 cycles
+    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(16);
+  }
 
   // ---- DMA: wave w stages 1-KiB blocks w, w+4, ... of each operand tile (8 rows of 128 B each)
   const char* sa = nullptr;
@@ -2477,6 +2486,7 @@ static bool use_w7(int M, int N, int K, int epi) {
   return g_w7 && (long long)((M + 255) / 256) * (N / 224) >= 256;
 }
 
+static int g_stagger = 0;   // four-wave kernel start stagger of the odd workgroups (GemmArgs::stagger)
 static int g_w7_mode = 0;  // W7 epilogue memory-traffic variant (A/B): bit 0 nt stores, bit 1 nt residual loads
 
 template <int EPI, int MODE>
@@ -2510,6 +2520,7 @@ template <int EPI, int RH = 0>
 static int launch(const GemmArgs& args, hipStream_t st) {
   GemmArgs a = args;
   a.walk = g_walk;
+  a.stagger = g_stagger;
   a.skip_epi = EDGE_TUNING_BUILD ? g_skip_epi : 0;
   a.rs_lds = g_rs_lds;
   if constexpr (epi_plain(EPI)) {
@@ -2616,6 +2627,11 @@ EDGE_API int edge_gemm_set_qkv256(int on) {
 
 EDGE_API int edge_gemm_set_qkv192(int on) {
   g_qkv192 = on;
+  return 0;
+}
+
+EDGE_API int edge_gemm_set_stagger(int k) {
+  g_stagger = k < 0 ? 0 : (k > 64 ? 64 : k);
   return 0;
 }
 
@@ -2770,7 +2786,8 @@ EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* b
     return (int)hipErrorInvalidValue;
   if ((kp == nullptr) != (vp == nullptr) || (kp && (!(kv_sk > 0.f) || !(kv_sv > 0.f) || ((uintptr_t)kp & 7))))
     return (int)hipErrorInvalidValue;
-  if (!q || !k || (!vt && !vp)) return (int)hipErrorInvalidValue;   // fp32 V^T may be skipped when its planes are out
+  // fp32 K / V^T may be skipped when their planes are written
+  if (!q || (!k && !kp) || (!vt && !vp)) return (int)hipErrorInvalidValue;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;
   switch (rot_dim) {

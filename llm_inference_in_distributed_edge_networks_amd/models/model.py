@@ -60,6 +60,8 @@ _H3_KEYS = ("wqkv", "wo", "wgu", "wd", "wfc", "wproj")
 # fp32 mode: the QKV GEMM writes K / V^T also as h3 planes and the attention stages them by LDS DMA (bit-identical
 # result; EDGE_ATTN_KV_PLANES=0 keeps the kernel's own per-tile split, for A/B)
 _KV_PLANES = os.environ.get("EDGE_ATTN_KV_PLANES", "1") != "0"
+# fp32 K from the QKV GEMM only on layers whose importance scorers read it (EDGE_QKV_K32=1: every layer, for A/B)
+_K32_ALWAYS = os.environ.get("EDGE_QKV_K32", "0") == "1"
 
 
 def _rownorm(w: torch.Tensor) -> torch.Tensor:
@@ -388,8 +390,9 @@ class DecoderLM:
                 raise ValueError(kd)
         return kinds
 
-    def _attn_h3(self, i, x, B, S, need_lse=False, n_rows=None):
-        """fp32 mode: norm(s) -> h3 QKV GEMM (+bias+RoPE) -> fp32 attention with h3 output."""
+    def _attn_h3(self, i, x, B, S, need_lse=False, n_rows=None, need_k=True):
+        """fp32 mode: norm(s) -> h3 QKV GEMM (+bias+RoPE) -> fp32 attention with h3 output (``need_k=False``: no
+        fp32 K on the GPU, only its planes for the attention - k is then None)."""
         cfg, L, sc = self.cfg, self.layers[i], self.h3_layer[i]
         h23 = None
         if cfg.arch == "qwen2":
@@ -401,7 +404,8 @@ class DecoderLM:
         if _KV_PLANES and x.is_cuda:   # the QKV GEMM also emits K / V^T planes; attention stages them by LDS DMA
             q, k, vt, kp, vp = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S,
                                                cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, cfg.rotary_dim,
-                                               self.q_scale, kv_scales=(sc["att_k"], sc["o"]))
+                                               self.q_scale, kv_scales=(sc["att_k"], sc["o"]),
+                                               need_k=need_k or _K32_ALWAYS)
             kvp = (kp, vp)
         else:
             q, k, vt = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S,
@@ -423,7 +427,7 @@ class DecoderLM:
 
     def _layer_h3(self, i, x, B, S, stats):
         kinds = self._stat_kinds(stats)
-        q, k, o3, lse, h23 = self._attn_h3(i, x, B, S, need_lse="colsum" in kinds)
+        q, k, o3, lse, h23 = self._attn_h3(i, x, B, S, need_lse="colsum" in kinds, need_k=bool(kinds))
         st = None
         if kinds:   # the scores on the forward's scaled fp16 planes (consistent with its LSE)
             sc = self.h3_layer[i]
@@ -446,7 +450,7 @@ class DecoderLM:
         Hq, Hkv, D = cfg.num_heads, cfg.num_kv_heads, cfg.head_dim
         rows = rows.to(self.device)
         if self.h3:
-            _, _, o3, _, h23 = self._attn_h3(i, x, B, S, n_rows=n_rows)
+            _, _, o3, _, h23 = self._attn_h3(i, x, B, S, n_rows=n_rows, need_k=False)
             return self._mlp_h3(i, o3.index_select(0, rows), x.index_select(0, rows),
                                 None if h23 is None else h23.index_select(0, rows))
         h2 = None

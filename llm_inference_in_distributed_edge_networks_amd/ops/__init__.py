@@ -191,6 +191,12 @@ def set_gemm_qkv192(on) -> None:
     call("edge_gemm_set_qkv192", int(on))
 
 
+def set_gemm_stagger(k: int) -> None:
+    """Four-wave GEMMs (A/B): the odd workgroups of each XCD start k x 1024 cycles late, so the chip-wide epilogue
+    store bursts split in two (0 = off, the default)."""
+    call("edge_gemm_set_stagger", int(k))
+
+
 def set_gemm_walk(chunked) -> None:
     """Persistent 256x256 GEMMs: XCD-contiguous tile chunks (default) or the grid-strided walk.  A/B only.
     2 = chunked for the four-wave kernel too (it walks strided otherwise)."""
@@ -322,7 +328,7 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scal
         o, lse = ref.attention(q, k, vt, S, need_lse)
         return (ref.h3_act(o, h3) if h3 else o), lse
     B, Hq, _, D = q.shape
-    Hkv = k.shape[1]
+    Hkv = k.shape[1] if k is not None else kv_planes[0].shape[1]   # (k may be None when its planes are given)
     lse = torch.empty(B, Hq, S, dtype=torch.float32, device=q.device) if need_lse else None
     nr = None
     if n_rows is not None:
@@ -485,11 +491,12 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
     return out
 
 
-def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, kv_scales=None):
+def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, kv_scales=None, need_k=True):
     """fp32 fused QKV projection + bias + RoPE + head-major scatter from h3 operands -> fp32 (q, k, vt).
 
     ``kv_scales`` = (s_k, s_v): also the K / V^T h3 planes at those scales for ``attention(kv_planes=...)`` ->
-    (q, k, vt, kp, vp); on the GPU ``vt`` is then None (the planes replace it)."""
+    (q, k, vt, kp, vp); on the GPU ``vt`` is then None (the planes replace it), and with ``need_k=False`` so is the
+    fp32 ``k`` (the attention stages the planes; only the importance scorers read fp32 K)."""
     if not _gpu(a3):
         y = ref.h3_matmul(a3, w3, alpha)            # x @ w.T, then the rest of the fused op on fp32
         eye = torch.eye(y.shape[1], dtype=torch.float32)
@@ -504,7 +511,7 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
     sp = s_pad(S)
     f32 = dict(dtype=torch.float32, device=a3.device)
     q = torch.empty(B, Hq, S, D, **f32)
-    k = torch.empty(B, Hkv, S, D, **f32)
+    k = torch.empty(B, Hkv, S, D, **f32) if (need_k or kv_scales is None) else None
     kpl = vpl = vt = None
     if kv_scales is None:
         vt = torch.zeros(B, Hkv, D, sp, **f32) if sp != S else torch.empty(B, Hkv, D, sp, **f32)

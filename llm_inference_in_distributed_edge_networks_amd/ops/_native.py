@@ -42,6 +42,7 @@ _SIGS = {
     "edge_gemm_set_rs_lds": [c_i],
     "edge_gemm_set_lse256": [c_i],
     "edge_gemm_set_w7_mode": [c_i],
+    "edge_gemm_set_stagger": [c_i],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],
@@ -116,6 +117,9 @@ def _apply_tuning_env(L) -> None:
         L.edge_gemm_set_rs_lds(0)
     if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # N = 896 GEMMs back on the 256x256 tiles
         L.edge_gemm_set_w7(0)
+    st = os.environ.get("EDGE_GEMM_STAGGER")  # four-wave GEMMs: odd workgroups start st x 1024 cycles late
+    if st and hasattr(L, "edge_gemm_set_stagger"):
+        L.edge_gemm_set_stagger(int(st))
 
 
 def available() -> bool:
