@@ -593,218 +593,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
   }
 }
 
-// KVP kernel with two 16-row query tiles per wave: 4 waves x 32 rows = the same 128 query rows per workgroup as
-// flash_attn_fwd_x6_kernel<.., 8, true, true>, but every K and V^T fragment read from LDS feeds both tiles' MFMAs
-// (half the LDS reads, DMA instructions and barriers per MFMA), at half the waves per SIMD.  A wave's 32 rows lie in
-// one 64-key block (q0 is a multiple of 32), so both tiles end at the same key tile and share its diagonal mask test.
-// Same arithmetic per row as the eight-wave kernel (bit-identical output and LSE).
-template <bool H3OUT>
-__global__ __launch_bounds__(256, 2) void flash_attn_fwd_h3p2_kernel(const float* __restrict__ q,
-                                                                     const void* __restrict__ kin,
-                                                                     const void* __restrict__ vtin,
-                                                                     void* __restrict__ o, float* __restrict__ lse,
-                                                                     const float* __restrict__ n_rows, int B, int Hq,
-                                                                     int Hkv, int S, int s_pad, float h3s, float sq,
-                                                                     float sk, float sv) {
-  constexpr int RT = 2, QB = 128;
-  constexpr float LSP = 7.f;
-  static_assert(FTAU == 8.f, "LSP assumes p <= 2^8");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const float sc_log2 = FLOG2E / (sq * sk);
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
-            ql = lane & 15;
-  const int nqb = (S + QB - 1) / QB;
-  const int G = Hq / Hkv, NG = B * Hkv;
-  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-  const int cnt = (NG - xcd + 7) >> 3;
-  const int per_qb = cnt * G;
-  if (j >= per_qb * nqb) return;
-  const int qb = nqb - 1 - j / per_qb;
-  const int rem = j - (nqb - 1 - qb) * per_qb;
-  const int grp = xcd + 8 * (rem / G);
-  const int b = grp / Hkv, hk = grp - b * Hkv, h = hk * G + rem % G;
-  if (n_rows && qb * QB + QB - 1 < S - 1 - (int)n_rows[b]) return;  // scored-rows mode (last layer)
-
-  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
-  const int q0 = qb * QB + wave * 32;   // tile rt holds rows q0 + 16 rt + ql
-  int qrow[RT];
-  bf16x8_t qp[RT][2][2];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    qrow[rt] = q0 + 16 * rt + ql;
-    const int qld = qrow[rt] < S ? qrow[rt] : S - 1;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      float v[8];
-      const f32x4_t a = *(const f32x4_t*)(qh + (size_t)qld * 64 + 32 * ks + 8 * g);
-      const f32x4_t c = *(const f32x4_t*)(qh + (size_t)qld * 64 + 32 * ks + 8 * g + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = c[e]; }
-      split_planes<true>(v, sq, qp[rt][ks]);
-    }
-  }
-  f32x4_t oacc[RT][4];
-  float m2[RT], l_run[RT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    m2[rt] = -INFINITY;
-    l_run[rt] = 0.f;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) oacc[rt][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  }
-
-  // DMA of key tile kb into buffer kb & 1 (K hi, K lo, V^T hi, V^T lo planes of 8 KiB): wave w stages rows
-  // 16 w .. 16 w + 15 of each, 8 rows per instruction (lane -> row + lane / 8, LDS chunk lane % 8 = global chunk
-  // (lane % 8) ^ xsw(row))
-  const char* kph = (const char*)((const f16_t*)kin + ((size_t)b * Hkv + hk) * 2 * S * 64);
-  const char* vph = (const char*)((const f16_t*)vtin + ((size_t)b * Hkv + hk) * 2 * 64 * (size_t)s_pad);
-  auto dma_tile = [&](int kb) {
-    char* buf = smem + (kb & 1) * 4 * XPL;
-#pragma unroll
-    for (int s8 = 0; s8 < 2; ++s8) {
-      const int drow = wave * 16 + 8 * s8 + (lane >> 3);
-      const int dchunk = ((lane & 7) ^ xsw(drow)) << 4;
-      char* wb = buf + (wave * 16 + 8 * s8) * 128;
-      const size_t kr = (size_t)min(kb * 64 + drow, S - 1);
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) glds16(kph + ((size_t)pl * S + kr) * 128 + dchunk, wb + pl * XPL);
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl)
-        glds16(vph + (((size_t)pl * 64 + drow) * s_pad + kb * 64) * 2 + dchunk, wb + (2 + pl) * XPL);
-    }
-  };
-
-  const int nkb = min((qb + 1) * QB, S + 63) / 64;   // key tiles up to this block's last query row
-  const int kmax = (q0 + 31) / 64;                    // both tiles' last key tile (wave-uniform)
-  dma_tile(0);
-  for (int kb = 0; kb < nkb; ++kb) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of tile kb landed
-    __syncthreads();       // every wave's pieces landed; every wave's reads of tile kb - 1 (buffer (kb + 1) & 1) done
-    if (kb + 1 < nkb) dma_tile(kb + 1);
-    const char* lk = smem + (kb & 1) * 4 * XPL;
-    const char* lv = lk + 2 * XPL;
-    if (kb > kmax) continue;
-    // S^T = K Q^T over the 4 key blocks of 16, each K fragment feeding both query tiles
-    f32x4_t st[RT][4];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const int row = kt * 16 + ql;
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) st[rt][kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t kf[2];
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl) kf[pl] = xfrag(lk + pl * XPL, row, 4 * ks + g);
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) st[rt][kt] = plane_dot<true>(kf, qp[rt][ks], st[rt][kt]);
-      }
-    }
-    if (__builtin_expect(kb * 64 + 63 > q0 || kb * 64 + 63 >= S, 0)) {   // causal / sequence-end mask (scalar branch)
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const int lim = min(qrow[rt], S - 1) - kb * 64 - 4 * g;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (kt * 16 + r > lim) st[rt][kt][r] = -INFINITY;
-      }
-    }
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      float mloc = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[rt][kt][r]);
-      mloc = xor_max32_raw(xor_max16_raw(mloc));
-      const float mc = mloc * sc_log2;
-      if (__builtin_amdgcn_ballot_w64(mc > m2[rt] + FTAU)) {  // wave-uniform lazy rescale
-        const float mn = fmaxf(m2[rt], mc);
-        const float alpha = __builtin_amdgcn_exp2f(m2[rt] - mn);
-        m2[rt] = mn;
-        l_run[rt] *= alpha;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) oacc[rt][d] *= alpha;
-      }
-      float ps = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(st[rt][kt][r], sc_log2, LSP - m2[rt]));
-          st[rt][kt][r] = pv;
-          ps += pv;
-        }
-      l_run[rt] += ps;
-    }
-    // O^T += V^T P^T, each V^T fragment feeding both query tiles
-#pragma unroll
-    for (int sk2 = 0; sk2 < 2; ++sk2) {
-      bf16x8_t pp[RT][2];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        float pv8[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { pv8[r] = st[rt][2 * sk2][r]; pv8[4 + r] = st[rt][2 * sk2 + 1][r]; }
-        split_frag_h1(pv8, pp[rt][0], pp[rt][1]);
-      }
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int row = dt * 16 + ql;
-        bf16x8_t vf[2];
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl) vf[pl] = xfrag(lv + pl * XPL, row, 4 * sk2 + g);
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) oacc[rt][dt] = plane_dot<true>(vf, pp[rt], oacc[rt][dt]);
-      }
-    }
-  }
-
-  const int W = Hq * 64;
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    float lr = l_run[rt];
-    lr += __shfl_xor(lr, 16, 64);
-    lr += __shfl_xor(lr, 32, 64);
-    const float inv = 1.f / (lr * sv);
-    u32x4_t oh[2], ol[2];
-    if constexpr (H3OUT) {
-      u32x2_t hw[4], lw[4];
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        float hi[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hi[r] = oacc[rt][dt][r] * inv * h3s;
-        const u32x2_t t0 = split2h_pk(hi[0], hi[1]), t1 = split2h_pk(hi[2], hi[3]);
-        hw[dt] = u32x2_t{t0[0], t1[0]};
-        lw[dt] = u32x2_t{t0[1], t1[1]};
-      }
-#pragma unroll
-      for (int q2 = 0; q2 < 2; ++q2) {
-        oh[q2] = pair_swap16(hw[2 * q2], hw[2 * q2 + 1]);
-        ol[q2] = pair_swap16(lw[2 * q2], lw[2 * q2 + 1]);
-      }
-    }
-    if (qrow[rt] < S) {
-      if constexpr (H3OUT) {
-        f16_t* orow = (f16_t*)o + ((size_t)b * S + qrow[rt]) * (size_t)(2 * W) + h * 64;
-#pragma unroll
-        for (int q2 = 0; q2 < 2; ++q2) {
-          *(u32x4_t*)(orow + q2 * 32 + pair_col(g)) = oh[q2];
-          *(u32x4_t*)(orow + W + q2 * 32 + pair_col(g)) = ol[q2];
-        }
-      } else {
-        float* orow = (float*)o + ((size_t)b * S + qrow[rt]) * (size_t)W + h * 64;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(orow + dt * 16 + 4 * g) = oacc[rt][dt] * inv;
-      }
-      if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow[rt]] = (m2[rt] - LSP) * 0.6931471805599453f + logf(lr);
-    }
-  }
-}
-
 // Last-row probabilities: one workgroup per (b, h); P[S-1, j] = softmax_j(q_{S-1} . k_j), fp32 throughout.
 __global__ __launch_bounds__(256) void attn_lastrow_f32_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                                float* __restrict__ out, int Hq, int Hkv, int S) {
@@ -1078,22 +866,12 @@ EDGE_API int edge_attn_f32_set_variant(int v) {
   return 0;
 }
 
-static int g_attn_h3p_rt2 = 0;   // KVP attention: 1 = four waves with two query tiles each (A/B), 0 = eight waves
-EDGE_API int edge_attn_h3p_set_rt2(int on) {
-  g_attn_h3p_rt2 = on;
-  return 0;
-}
-
 template <bool H3OUT>
 static void launch_plane_attn(dim3 grid, hipStream_t st, const float* q, const void* kp, const void* vp, void* o,
                               float* lse, const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float h3s,
                               float sq, float sk, float sv) {
-  if (g_attn_h3p_rt2)
-    hipLaunchKernelGGL((flash_attn_fwd_h3p2_kernel<H3OUT>), grid, dim3(256), 8 * XPL, st, q, kp, vp, o, lse, n_rows, B,
-                       Hq, Hkv, S, s_pad, h3s, sq, sk, sv);
-  else
-    hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<H3OUT, 8, true, true>), grid, dim3(512), 8 * XPL, st, q, kp, vp, o,
-                       lse, n_rows, B, Hq, Hkv, S, s_pad, h3s, sq, sk, sv);
+  hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<H3OUT, 8, true, true>), grid, dim3(512), 8 * XPL, st, q, kp, vp, o,
+                     lse, n_rows, B, Hq, Hkv, S, s_pad, h3s, sq, sk, sv);
 }
 
 template <bool H3OUT, int NW, bool F16>

@@ -51,7 +51,6 @@ _SIGS = {
     "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_set_variant": [c_i],
     "edge_attn_f32_set_variant": [c_i],
-    "edge_attn_h3p_set_rt2": [c_i],
     "edge_attn_lastrow": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_colsum": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_head_combine": [c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p],
@@ -118,8 +117,6 @@ def _apply_tuning_env(L) -> None:
         L.edge_gemm_set_rs_lds(0)
     if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # N = 896 GEMMs back on the 256x256 tiles
         L.edge_gemm_set_w7(0)
-    if os.environ.get("EDGE_ATTN_RT2") and hasattr(L, "edge_attn_h3p_set_rt2"):  # KVP attention, 4 waves x 2 tiles
-        L.edge_attn_h3p_set_rt2(int(os.environ["EDGE_ATTN_RT2"]))
     st = os.environ.get("EDGE_GEMM_STAGGER")  # four-wave GEMMs: odd workgroups start st x 1024 cycles late
     if st and hasattr(L, "edge_gemm_set_stagger"):
         L.edge_gemm_set_stagger(int(st))
