@@ -1,0 +1,15 @@
+# Final check of the round's tree: all GPU tests, smoke, bench (the driver's three measurements).
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc"; grep -v amdgpu.ids gpurun_out/$name.log | tail -${TAIL:-3}
+  return $rc
+}
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit $?
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+TAIL=1 step bench 300 python bench.py --steps 10 --warmup 3 --json-out gpurun_out/bench.json || exit $?
+exit 0
