@@ -105,10 +105,40 @@ def _free_port() -> int:
     return port
 
 
+def visible_gpu_count() -> int:
+    """GPUs this process could use, counted without touching the HIP runtime (the launcher parent must not
+    initialise it before it starts the ranks): GPU nodes of the KFD topology in sysfs (nodes with SIMDs), capped by
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set.  0 = unknown (the ranks check)."""
+    n = 0
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        n = 0
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids)) if n else len(ids)
+    return n
+
+
+def shared_gpu() -> bool:
+    return os.environ.get("EDGE_SHARED_GPU", "0") not in ("", "0")
+
+
 def launch_mode(a) -> str:
     """"torchrun" (rank env present), "self" (--gpus N > 1 without it: spawn the ranks) or "single".
 
-    Called before any GPU call: ``torch.cuda.device_count()`` does not initialise the HIP runtime."""
+    Called before any GPU call, and makes none itself: the visible-GPU check reads sysfs and the environment
+    (``visible_gpu_count``); the ranks check their devices again after they start."""
     if "WORLD_SIZE" in os.environ and "RANK" in os.environ:
         world = int(os.environ["WORLD_SIZE"])
         if world != a.gpus:
@@ -119,9 +149,8 @@ def launch_mode(a) -> str:
         raise SystemExit(f"bench.py: --gpus must be >= 1 (got {a.gpus})")
     if a.gpus == 1:
         return "single"
-    ndev = torch.cuda.device_count()
-    shared = os.environ.get("EDGE_SHARED_GPU", "0") not in ("", "0")
-    if 0 < ndev < a.gpus and not shared:
+    ndev = visible_gpu_count()
+    if 0 < ndev < a.gpus and not shared_gpu():
         raise SystemExit(f"bench.py: --gpus {a.gpus} but only {ndev} GPU(s) are visible")
     return "self"
 
@@ -151,7 +180,7 @@ def rank_devices(env) -> list:
     return out
 
 
-def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None):
+def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None, probe_sizes=()):
     """Build the model/pipeline for ``dtype`` (random weights with ``values`` precision) and time ``timed_steps``
     steps after ``warmup``.  Returns a dict."""
     dev = env.device
@@ -167,6 +196,14 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
                                   with_embed=(stage == 0), with_head=(stage == pp - 1), values=values)
         runner = DistributedPipeline(model, plan, bcfg, grid, env.rank, use_graphs=not a.no_graphs,
                                      transport=a.transport)
+    probe = None
+    if dist_pp and probe_sizes:
+        # per pipeline edge, before the timed region: a 1 MiB and a boundary-sized message on the active transport
+        # (a first multi-GPU run shows a p2p pathology here instead of only as recv_wait_ms)
+        mine = runner.probe_p2p(probe_sizes)
+        gathered = [None] * world
+        torch.distributed.all_gather_object(gathered, mine)
+        probe = sorted((r for g in gathered for r in g), key=lambda r: (r["stage"], r["edge"][0], r["bytes"]))
 
     # ---- data: synthetic stream of WikiText-2 test length, HF sliding windows, staged on device
     tokens = synthetic_stream(299_078, cfg.vocab_size, a.seed)
@@ -231,7 +268,7 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
     gc.collect()
     if dev.type == "cuda":
         torch.cuda.empty_cache()
-    return {"dt": dt, "ppl": ppl, "prov": prov, "stages": stage_reports}
+    return {"dt": dt, "ppl": ppl, "prov": prov, "stages": stage_reports, "p2p": probe}
 
 
 def main():
@@ -254,13 +291,19 @@ def main():
             PipelinePlan.balanced(cfg, pp, a.max_length, a.stride / a.max_length))
     dtype = DTYPES[a.dtype] if env.device.type == "cuda" else torch.float32
 
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    if env.device.type == "cuda" and torch.cuda.device_count() < (1 if shared_gpu() else local_world):
+        raise SystemExit(f"bench.py: rank {env.rank} sees {torch.cuda.device_count()} GPU(s), "
+                         f"needs {local_world} (one per local rank)")
     values = torch.bfloat16 if a.weight_values == "bf16" else None
-    main_run = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup, values)
+    spec = C.get_codec(a.codec)
+    msg_bytes = C.message_bytes(spec, a.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
+    main_run = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup, values,
+                       probe_sizes=(1 << 20, int(msg_bytes)))
     dt = main_run["dt"]
     tok_per_step = grid.dp * a.microbatches * a.batch * a.max_length
     scored_per_step = grid.dp * a.microbatches * a.batch * a.stride
     value = tok_per_step * a.steps / dt
-    spec = C.get_codec(a.codec)
     wires = [C.message_bytes(spec, a.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
              / (a.batch * a.max_length)] * (pp - 1)
     second = fp32w = None
@@ -294,6 +337,8 @@ def main():
     }
     if main_run["stages"]:
         out["stages"] = main_run["stages"]
+    if main_run["p2p"] is not None:
+        out["p2p"] = main_run["p2p"]
     if fp32w is not None:   # the same fp32 run on full-fp32 random weight values (three-product h3 GEMMs)
         out["value_fp32_weights"] = round(tok_per_step * a.steps / fp32w["dt"], 1)
         out["ms_per_step_fp32_weights"] = round(1000 * fp32w["dt"] / a.steps, 3)
@@ -304,6 +349,13 @@ def main():
         out["ppl_random_weights_bf16"] = second["ppl"]
         if second["stages"]:
             out["stages_bf16"] = second["stages"]
+    fail = os.environ.get("EDGE_BENCH_FAIL_RANK")       # test hook: this rank dies after its measurement
+    if fail is not None and int(fail) == env.rank:
+        raise RuntimeError(f"EDGE_BENCH_FAIL_RANK: rank {env.rank} fails on purpose")
+    if env.is_dist:
+        # every rank finished its measurement: only then does rank 0 report (a failed rank means no JSON line,
+        # and the launcher - or the self-launching parent - exits non-zero)
+        torch.distributed.barrier()
     if env.is_main:
         print(json.dumps(out), flush=True)
         if a.json_out:

@@ -70,7 +70,20 @@ struct GemmArgs {
   float out_scale = 1.f;  // h3 outputs (SwiGLU / GELU): the next GEMM's input scale s_a
   int stagger = 0;        // four-wave kernel: the odd workgroups of each XCD start stagger x 1024 cycles late, so
                           // the chip's epilogue store bursts split in two (A/B; ops.set_gemm_stagger)
+  // four-wave kernel, epilogue desync (split_h > 0): the odd workgroups of each XCD run the first split_h K-tiles of
+  // their LAST tile first (raw accumulators parked in ws), then their other tiles, then the rest of the last tile
+  // (accumulators restored), so their epilogues fall half a tile after the even workgroups' and the chip's store
+  // bursts halve.  Same accumulation order: bit-identical results.  ws is an explicit launch argument (a persistent
+  // per-device buffer, ops._gemm_ws), never a per-call allocation handed over through a process-global.
+  float* ws = nullptr;
+  long long ws_floats = 0;  // size of ws (floats): workgroups whose park area does not fit run the plain walk
+  int split_h = 0;
+  int* err = nullptr;       // checked builds (EDGE_GEMM_CHECKS): set to a nonzero code when a bounds check fails
 };
+
+#ifndef EDGE_GEMM_CHECKS
+#define EDGE_GEMM_CHECKS EDGE_TUNING_BUILD
+#endif
 
 // element column of A holding GEMM column k (k a K-tile start)
 __device__ __forceinline__ int a_kcol(const GemmArgs& a, int k) {
@@ -1874,8 +1887,10 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
 // against the same weight columns) lives in the B region of buffer p & 1 and is staged with the pair's even K-tile
 // only - a quarter less L2 -> LDS traffic.  The K loop is unrolled by two so that every DMA / read switch stays
 // compile-time (nk is even: pairs never straddle tiles).
-template <int EPI, int RH, int PF, int BN, bool PB = false>
+// DS: the epilogue-desync variant (GemmArgs::split_h); DS = false compiles none of its code (the default kernels).
+template <int EPI, int RH, int PF, int BN, bool PB = false, bool DS = false>
 __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
+  static_assert(!DS || PF == 0, "desync: no prefetch stream");
   static_assert(!PB || (epi_f32(EPI) && PF == 0), "paired B: h3 GEMMs without the prefetch stream");
   static_assert(BN != 192 || (EPI == EPI_F32_QKV_ROPE && (RH == 0 || RH == 32)), "192-wide tiles: fp32 QKV only");
   static_assert(BN == 192 || BN == 224 || BN == 256, "tile width");
@@ -1894,10 +1909,38 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   const int tile0 = walk.first, G = walk.stride;
   if (tile0 >= walk.end) return;
   const int nk = a.K / 64;
-  const int total = ((walk.end - 1 - tile0) / G + 1) * nk;   // K-tiles of this workgroup
+  const int ntw = (walk.end - 1 - tile0) / G + 1;   // tiles of this workgroup
+  const int total = ntw * nk;                       // K-tiles of this workgroup
   if (a.stagger > 0 && ((blockIdx.x >> 3) & 1)) {   // wave-uniform: s_sleep 16 = 1024 cycles
     for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(16);
   }
+  // epilogue desync (GemmArgs::split_h): segment s of the workgroup's K-tile sequence -> (tile, first K-tile, end
+  // K-tile, mode 0 = whole tile / 1 = partial tile, accumulators parked / 2 = rest of a partial tile, accumulators
+  // restored).  The segments' K-tile counts sum to total, and split_h is even (paired-B K-tile pairs never straddle
+  // a segment boundary).  The workgroup's park area must lie inside ws: checked once, uniform over its waves.
+  const bool ws_fits = DS && (long long)(blockIdx.x + 1) * 4 * 8 * NJ * 256 <= a.ws_floats;
+#if EDGE_GEMM_CHECKS
+  if (DS && a.split_h > 0 && !ws_fits && a.err) *a.err = 2;
+#endif
+  const bool ph1 = DS && a.split_h > 0 && ws_fits && ntw >= 2 && ((blockIdx.x >> 3) & 1);   // wave-uniform
+  const int nseg = ph1 ? ntw + 1 : ntw;
+  auto seg = [&](int sg, int& tl, int& kb, int& ke, int& md) {
+    if (!ph1) {
+      tl = tile0 + sg * G, kb = 0, ke = nk, md = 0;
+    } else if (sg == 0) {
+      tl = tile0 + (ntw - 1) * G, kb = 0, ke = a.split_h, md = 1;
+    } else if (sg < ntw) {
+      tl = tile0 + (sg - 1) * G, kb = 0, ke = nk, md = 0;
+    } else {
+      tl = tile0 + (ntw - 1) * G, kb = a.split_h, ke = nk, md = 2;
+    }
+#if EDGE_GEMM_CHECKS
+    if (sg < 0 || sg >= nseg || tl < tile0 || tl >= walk.end || kb < 0 || ke > nk || kb >= ke) {
+      if (a.err) *a.err = 1;
+      tl = tile0, kb = 0, ke = nk, md = 0;
+    }
+#endif
+  };
 
   // ---- DMA: wave w stages 1-KiB blocks w, w+4, ... of each operand tile (8 rows of 128 B each)
   const char* sa = nullptr;
@@ -1921,8 +1964,12 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       ob[i] = (uint32_t)(min(rb, a.N - 1 - n0) * a.ldb + ((lane & 7) ^ swz(r)) * 8) * 2u;
     }
   };
-  int st_q = 0, st_kt = 0, st_tile = tile0;
-  set_stage_tile(tile0);
+  int st_q = 0, st_kt = 0, st_tile = tile0, st_seg = 0, st_kend = nk;
+  {
+    int md_;
+    seg(0, st_tile, st_kt, st_kend, md_);
+  }
+  set_stage_tile(st_tile);
   // item r < 8: A block, else B block r - 8 (with PB into the K-tile pair's slot; its callers skip the B items of
   // odd K-tiles at compile time)
   auto dma_item = [&](int r, char* buf, int kba, int kb) {
@@ -1943,10 +1990,10 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   auto advance_stage = [&]() {   // the DMA stream stops (repeats its last K-tile) at the end
     ++st_q;
     if (st_q >= total) {
-      st_kt = nk - 1;
-    } else if (++st_kt == nk) {
-      st_kt = 0;
-      st_tile += G;
+      st_kt = st_kend - 1;
+    } else if (++st_kt == st_kend) {
+      int md_;
+      seg(++st_seg, st_tile, st_kt, st_kend, md_);
       set_stage_tile(st_tile);
     }
     st_kba = a_kcol(a, st_kt * 64) * 2;
@@ -2058,8 +2105,37 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   for (int j = 0; j < NJ; ++j) DS_READ_B128(XB[j], bbase[0], j * 2048);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-  int tile = tile0, kt = 0, m0, n0;
+  // kbeg: the segment's first K-tile, whose MFMAs start the accumulators from zero (-1 for a restored segment)
+  int tile, kt, kend, cmode, cseg = 0, m0, n0;
+  seg(0, tile, kt, kend, cmode);
+  int kbeg = kt;
   tile_origin(tile, a.M, a.N, 256, BN, m0, n0);
+  // parked accumulators of a partial tile: wave w of workgroup b keeps its 8 NJ f32x4 in groups of four,
+  // group g at byte ws + ((b 4 + w) 8 NJ + 4 g) 1024, member e at + e 1024, lane l at + 16 l.  The stores and loads
+  // go straight from / to the AGPRs (a compiler-visible copy through VGPRs makes the allocator spill ~190 VGPRs of
+  // this kernel), so their hazards are padded by hand inside each statement (cdna_hip_programming.md §5.7):
+  //   - s_nop 4 first: the SGPR base is fresh from v_readfirstlane (a VALU SGPR write), and a VMEM instruction that
+  //     reads an SGPR needs 5 wait states after one.  hipcc pads that only for instructions it can see; the round-3
+  //     version had no pad, so a store / load could take a stale base: the GPU faults it showed
+  //     (docs/ARCHITECTURE.md §GEMM);
+  //   - s_nop 1 after the dwordx4 stores: their data registers must not be overwritten before the stores read them;
+  //   - the loads and their vmcnt(0) in ONE statement (hipcc cannot count asm loads), then s_nop 4 before the MFMAs
+  //     read the restored accumulators.
+  auto ws_base = [&](int g) {
+    const uint64_t p = (uint64_t)a.ws + (((uint64_t)blockIdx.x * 4 + wave) * (8 * NJ) + 4 * g) * 1024;
+    // readfirstlane returns int: zero-extend the low word through uint32_t (a sign extension would OR 0xffffffff
+    // into the high word whenever bit 31 of the address is set - the round-3 fault, see docs/ARCHITECTURE.md §GEMM)
+    uint64_t r = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);   // SGPR pair
+#if EDGE_GEMM_CHECKS
+    // the base the asm will use, checked against the workspace (a wrong one is replaced by ws itself: no fault)
+    if (r < (uint64_t)a.ws || r + 4096 > (uint64_t)a.ws + (uint64_t)a.ws_floats * 4) {
+      if (a.err) *a.err = 3;
+      r = (uint64_t)a.ws;
+    }
+#endif
+    return r;
+  };
   float rs[8];
   auto load_rs = [&](int mt) {
     if constexpr (BN == 256) {
@@ -2085,7 +2161,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     const uint32_t boB = PB ? ((t >> 1) & 1) * TB : bo, bnB = PB ? (((t + 1) >> 1) & 1) * TB : bn;
     // M(t,0) on X, K-half 1 of K-tile t -> Y
     __builtin_amdgcn_sched_barrier(0);
-    if (kt == 0) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, std::false_type{}, std::true_type{}, dmab_c);
+    if (kt == kbeg) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, std::false_type{}, std::true_type{}, dmab_c);
     else mma(XA, XB, YA, YB, bo, boB, 1, std::false_type{}, std::false_type{}, std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < total) {
@@ -2107,11 +2183,29 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ++kt;
-    if (decltype(end_c)::value && kt == nk) {
+    if (decltype(end_c)::value && kt == kend) {
       // all MFMAs of the tile were issued; the epilogue reads the accumulators after they drain
       MFMA_DRAIN();
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (BN == 256 && EPI == EPI_H3_SWIGLU) {
+      if (DS && cmode == 1) {   // partial tile (desync): park the raw accumulators
+        const uint32_t lo16 = lane * 16;
+#pragma unroll
+        for (int g = 0; g < 2 * NJ; ++g) {
+          const int q0 = 4 * g;
+          asm volatile(
+              "s_nop 4\n\t"
+              "global_store_dwordx4 %0, %1, %5\n\t"
+              "global_store_dwordx4 %0, %2, %5 offset:1024\n\t"
+              "global_store_dwordx4 %0, %3, %5 offset:2048\n\t"
+              "global_store_dwordx4 %0, %4, %5 offset:3072\n\t"
+              "s_nop 1"
+              :
+              : "v"(lo16), "a"(acc[q0 / NJ][q0 % NJ]), "a"(acc[(q0 + 1) / NJ][(q0 + 1) % NJ]),
+                "a"(acc[(q0 + 2) / NJ][(q0 + 2) % NJ]), "a"(acc[(q0 + 3) / NJ][(q0 + 3) % NJ]), "s"(ws_base(g))
+              : "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (BN == 256 && EPI == EPI_H3_SWIGLU) {
 #if EDGE_TUNING_BUILD
         if (a.skip_epi != 1)   // timing ablation: no epilogue (wrong results)
 #endif
@@ -2181,11 +2275,31 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      kt = 0;
-      tile += G;
-      if (tile < walk.end) {
+      if (++cseg < nseg) {
+        seg(cseg, tile, kt, kend, cmode);
+        kbeg = cmode == 2 ? -1 : kt;
         tile_origin(tile, a.M, a.N, 256, BN, m0, n0);
         load_rs(m0);
+        if (DS && cmode == 2) {   // the rest of the partial tile: its parked accumulators back into the AGPRs
+          const uint32_t lo16 = lane * 16;
+#pragma unroll
+          for (int g = 0; g < 2 * NJ; ++g) {
+            const int q0 = 4 * g;
+            asm volatile(
+                "s_nop 4\n\t"
+                "global_load_dwordx4 %0, %4, %5\n\t"
+                "global_load_dwordx4 %1, %4, %5 offset:1024\n\t"
+                "global_load_dwordx4 %2, %4, %5 offset:2048\n\t"
+                "global_load_dwordx4 %3, %4, %5 offset:3072\n\t"
+                "s_waitcnt vmcnt(0)\n\t"
+                "s_nop 4"
+                : "=&a"(acc[q0 / NJ][q0 % NJ]), "=&a"(acc[(q0 + 1) / NJ][(q0 + 1) % NJ]),
+                  "=&a"(acc[(q0 + 2) / NJ][(q0 + 2) % NJ]), "=&a"(acc[(q0 + 3) / NJ][(q0 + 3) % NJ])
+                : "v"(lo16), "s"(ws_base(g))
+                : "memory");
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       // the next tile's first K-half fragments again (K-tile t+1 landed in buffer bn before this K-tile's barrier):
       // re-reading them here leaves the copies read during M(t,1) dead across the epilogue, which gets their VGPRs
@@ -2448,11 +2562,56 @@ static int launch_8p(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// Epilogue desync of the four-wave kernel (GemmArgs::split_h): g_split -1 = auto (half the tile's K-tiles, even),
+// 0 = off, k > 0 = k K-tiles.  The workspace is one persistent buffer per device, registered once by the caller
+// (edge_gemm_set_ws; ops._gemm_ws keeps the tensor alive for the life of the process) and handed to every launch
+// as a kernel argument.  GEMMs that use it must not run concurrently on one device (one compute stream per device:
+// LocalPipeline, one stage per rank, the sweep engine).
+static int g_split = 0;
+constexpr int kMaxDev = 64;
+static float* g_ws_dev[kMaxDev] = {};
+static long long g_ws_floats_dev[kMaxDev] = {};
+static int* g_err_dev[kMaxDev] = {};
+static long long w4_ws_floats(int grid, int BN) { return (long long)grid * 4 * 8 * (BN / 32) * 256; }
+
 template <int EPI, int RH, int PF, int BN, bool PB>
-static int launch_4w_pb(const GemmArgs& a, hipStream_t st) {
+static int launch_4w_pb(const GemmArgs& args, hipStream_t st) {
+  GemmArgs a = args;
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   const int grid = std::min(tiles, num_cus());
+  const int nk = a.K / 64;
+  int h = g_split < 0 ? (nk / 2) & ~1 : g_split & ~1;
+  if (PF > 0 || h <= 0 || h >= nk || tiles < 2 * grid) h = 0;
+  if (h) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= kMaxDev || !g_ws_dev[dev] || g_ws_floats_dev[dev] < w4_ws_floats(grid, BN)) {
+      h = 0;
+    } else {
+      a.ws = g_ws_dev[dev];
+      a.ws_floats = g_ws_floats_dev[dev];
+      a.err = g_err_dev[dev];
+    }
+  }
+  // (the desync kernels exist for the families the bench runs and its tests cover: h3 two-product GEMMs, the bf16
+  // SwiGLU GEMM and the LM-head LSE)
+  constexpr bool ds_ok = PF == 0 && ((epi_f32(EPI) && PB) || EPI == EPI_SWIGLU || EPI == EPI_LSE);
+  if (!ds_ok) h = 0;
+  a.split_h = h;
+  if (!h) a.ws = nullptr, a.ws_floats = 0;
   constexpr int lds = w4::Geo<BN>::LDS + (PF > 0 ? 1024 : 0);
+  if constexpr (ds_ok) {
+    if (h) {
+      static bool attr_ds = false;
+      if (!attr_ds) {
+        (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, PF, BN, PB, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr_ds = true;
+      }
+      hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, PF, BN, PB, true>), dim3(grid), dim3(256), lds, st, a);
+      return (int)hipGetLastError();
+    }
+  }
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, PF, BN, PB>,
@@ -2634,6 +2793,25 @@ EDGE_API int edge_gemm_set_stagger(int k) {
   g_stagger = k < 0 ? 0 : (k > 64 ? 64 : k);
   return 0;
 }
+
+// epilogue desync of the four-wave GEMMs: -1 auto, 0 off, k K-tiles (see launch_4w_pb)
+EDGE_API int edge_gemm_set_split(int k) {
+  g_split = k;
+  return 0;
+}
+EDGE_API int edge_gemm_get_split() { return g_split; }
+// the current device's persistent desync workspace (floats >= edge_gemm_ws_floats()); err: optional device int that
+// checked builds set on a failed bounds check.  The caller keeps both alive for as long as the library is used.
+EDGE_API int edge_gemm_set_ws(void* p, long long floats, void* err) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return (int)hipErrorInvalidDevice;
+  g_ws_dev[dev] = (float*)p;
+  g_ws_floats_dev[dev] = p ? floats : 0;
+  g_err_dev[dev] = (int*)err;
+  return 0;
+}
+EDGE_API long long edge_gemm_ws_floats() { return w4_ws_floats(num_cus(), 256); }
+EDGE_API int edge_gemm_checked_build() { return EDGE_GEMM_CHECKS; }
 
 EDGE_API int edge_gemm_set_w7(int on) {
   g_w7 = on;

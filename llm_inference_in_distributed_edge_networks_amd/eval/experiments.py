@@ -26,7 +26,7 @@ from .. import codec as C
 from ..config import Params, dump_json, resolve_device, resolve_dtype, resolve_window_batch
 from ..importance import canonical, load_head_weights
 from ..models import build_model, get_config
-from ..parallel.dist import all_reduce_sum, get_env, init_distributed
+from ..parallel.dist import all_reduce_sum, broadcast_object, get_env, init_distributed
 from ..utils.checkpoint import SweepState
 from ..utils.logging import log, progress_bar
 from .data import token_stream
@@ -88,7 +88,7 @@ def importance_sweep(p: Params, default_model: str, out_name: str) -> dict:
         path = p.head_weights or _default_head_weights()
         hw = load_head_weights(path) if path and os.path.exists(path) else None
         if hw is None:
-            raise FileNotFoundError("weighted_importance needs attention_head_weights.json "
+            raise FileNotFoundError("weighted_importance needs attention_head_weights.json / .pkl "
                                     "(run Experiments/Relevance/main.py or set params['head_weights'])")
     rows = [SweepMethod(m, m, selection=p.selection) for m in methods]
     sc = SweepConfig(rows, p.layers_of_interest, p.ratios, p.codec, hw, group_relevance=_group_relevance(p),
@@ -222,8 +222,11 @@ def _default_group_relevance() -> str | None:
 
 
 def _default_head_weights() -> str | None:
-    for c in ("attention_head_weights.json", "../Relevance/attention_head_weights.json",
-              "../../attention_head_weights.json"):
+    """The LRP head-weight table: ours (JSON, Experiments/Relevance) or the reference's pickle at the place its
+    Qwen2 sweep reads it (``../../attention_head_weights.pkl``, Experiments/Qwen2-0.5B/main.py:129-130)."""
+    for c in ("attention_head_weights.json", "attention_head_weights.pkl", "../Relevance/attention_head_weights.json",
+              "../Relevance/attention_head_weights.pkl", "../../attention_head_weights.json",
+              "../../attention_head_weights.pkl"):
         if os.path.exists(c):
             return c
     return None
@@ -277,7 +280,7 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
     if "weighted_importance" in methods:
         path = p.head_weights or _default_head_weights()
         if not (path and os.path.exists(path)):
-            raise FileNotFoundError("weighted_importance needs attention_head_weights.json "
+            raise FileNotFoundError("weighted_importance needs attention_head_weights.json / .pkl "
                                     "(run Experiments/Relevance/main.py or set params['head_weights'])")
         hw = load_head_weights(path)
     grel = _group_relevance(p)
@@ -287,6 +290,11 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
     state = SweepState(os.path.join(p.output_dir, f"pipeline_results.rank{env.rank}.ckpt.json"), p.config_hash(),
                        enabled=p.resume, shard=(env.rank, env.world_size, f"pipeline/{p.window_batch}"))
     saved = state.load() or {}
+    if distributed:
+        # pipeline stages exchange boundary messages batch by batch, so every rank must resume at the same point:
+        # rank 0's checkpoint is the one (its sums are the all-reduced totals, like every rank's); a rank whose own
+        # file is one chunk ahead or behind (a job killed between two ranks' saves) follows it
+        saved = broadcast_object(saved, src=0)
     results.update(saved.get("results", {}))
     bl = list(batches(ids, wins, p.window_batch))
     toks = sum(w.end - w.begin for w in wins)
@@ -309,38 +317,43 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
                 runner.set_boundary(bcfg)
             part = saved.get("partial") if saved.get("partial", {}).get("key") == [m, str(r)] else None
             tot, ntok, sec = (part["total_nll"], part["n_tokens"], part["seconds"]) if part else (0.0, 0.0, 0.0)
-            wsum, wcnt = (part["wire_sum"], part["wire_n"]) if part else (0.0, 0)
+            # wire bytes and the tokens they carried, summed over the boundaries (and replicas) and over the chunks,
+            # so a resumed run reports the uninterrupted run's bytes per token (variable-k codecs included)
+            wbytes, wtoks = (part["wire_bytes"], part["wire_tokens"]) if part else (0.0, 0.0)
+            prev_b = prev_t = 0.0            # the runner's counters restart at set_boundary / construction
             start = part["next_batch"] if part else 0
             for c0 in range(start, len(bl), chunk):
                 t0 = time.perf_counter()
                 piece = bl[c0:c0 + chunk]
                 if distributed:
                     acc, info = runner.evaluate(piece)
-                    wire = torch.tensor([info["wire_bytes_per_token"] if stage < pp - 1 else 0.0],
-                                        dtype=torch.float64, device=env.device if env.backend == "nccl" else "cpu")
+                    wire = torch.tensor([info["wire_bytes"], info["wire_tokens"]], dtype=torch.float64,
+                                        device=env.device if env.backend == "nccl" else "cpu")
                     all_reduce_sum(wire)
-                    wire_pt = float(wire) / (grid.dp * max(1, pp - 1))
+                    cb, ct = float(wire[0]), float(wire[1])
                 else:
                     acc = runner.evaluate(piece)
-                    wb = runner.wire_bytes_per_token()
-                    wire_pt = sum(wb) / len(wb) if wb else 0.0
+                    cb, ct = runner.wire_totals()
                 if device.startswith("cuda"):
                     torch.cuda.synchronize()
                 sec += time.perf_counter() - t0
                 tot += acc.total_nll
                 ntok += acc.n_tokens
-                wsum, wcnt = wire_pt, 1          # the stage byte counters are cumulative over the run
+                wbytes += cb - prev_b
+                wtoks += ct - prev_t
+                prev_b, prev_t = cb, ct
                 if c0 + chunk < len(bl):
                     state.save({"results": results, "partial": {
                         "key": [m, str(r)], "next_batch": c0 + chunk, "total_nll": tot, "n_tokens": ntok,
-                        "seconds": sec, "wire_sum": wsum, "wire_n": wcnt}})
+                        "seconds": sec, "wire_bytes": wbytes, "wire_tokens": wtoks}})
             ppl = math.exp(tot / ntok) if ntok else float("nan")
+            wire_pt = wbytes / wtoks if wtoks else 0.0
             results.setdefault(m, {})[str(r)] = {"ppl": ppl, "total_nll": tot, "n_tokens": ntok,
-                                                 "wire_bytes_per_token": wsum / max(1, wcnt),
+                                                 "wire_bytes_per_token": wire_pt,
                                                  "tokens_per_s": toks / max(sec, 1e-9), "seconds": sec}
             state.save({"results": results})
             if env.is_main:
-                log(f"{m:20s} ratio={r:<5} ppl={ppl:.4f} wire={wsum / max(1, wcnt):.1f} B/token "
+                log(f"{m:20s} ratio={r:<5} ppl={ppl:.4f} wire={wire_pt:.1f} B/token "
                     f"({toks / max(sec, 1e-9):,.0f} tok/s)")
     if runner is not None and distributed:
         runner.close()

@@ -46,10 +46,111 @@ def needs_all_layers(method: str) -> bool:
 
 
 def load_head_weights(path: str) -> torch.Tensor:
-    """``attention_head_weights.json`` ([layers][heads], Relevance/main.py:127-128) -> fp32 tensor."""
-    with open(path) as f:
-        w = json.load(f)
-    return torch.tensor(w, dtype=torch.float32)
+    """LRP head weights ``[layers][heads]`` -> fp32 tensor, from ``attention_head_weights.json`` (what
+    ``Experiments/Relevance/main.py:127-128`` writes) or ``attention_head_weights.pkl`` (what the reference's Qwen2
+    sweep reads, ``Experiments/Qwen2-0.5B/main.py:129-130``, written by ``pickle.dump`` in
+    ``Notebooks/attention_head_weights_via_relevance.ipynb``).  A pickle is never unpickled by ``pickle``: see
+    :func:`_load_table_pickle`."""
+    if path.endswith(".pkl") or path.endswith(".pickle"):
+        w = _load_table_pickle(path)
+    else:
+        with open(path) as f:
+            w = json.load(f)
+    return _validated_table(w, path)
+
+
+def _validated_table(w, path: str) -> torch.Tensor:
+    if isinstance(w, torch.Tensor):
+        w = w.tolist()
+    ok = isinstance(w, (list, tuple)) and len(w) > 0 and all(isinstance(r, (list, tuple)) and len(r) > 0 for r in w)
+    ok = ok and all(isinstance(v, (int, float)) and not isinstance(v, bool) for r in w for v in r)
+    if not ok or len({len(r) for r in w}) != 1:
+        raise ValueError(f"{path}: head weights must be a [layers][heads] table of numbers")
+    return torch.tensor([[float(v) for v in r] for r in w], dtype=torch.float32)
+
+
+# pickle opcodes a list / tuple of lists / tuples of numbers is made of (any protocol); everything that could name,
+# build or call an object (GLOBAL, STACK_GLOBAL, REDUCE, BUILD, INST, OBJ, NEWOBJ, PERSID, EXT*, ...) is refused
+_TABLE_OPS = {"PROTO", "FRAME", "STOP", "MARK", "EMPTY_LIST", "LIST", "APPEND", "APPENDS", "EMPTY_TUPLE", "TUPLE",
+              "TUPLE1", "TUPLE2", "TUPLE3", "BINFLOAT", "FLOAT", "BININT", "BININT1", "BININT2", "INT", "LONG",
+              "LONG1", "MEMOIZE", "PUT", "BINPUT", "LONG_BINPUT", "GET", "BINGET", "LONG_BINGET"}
+
+
+def _load_table_pickle(path: str):
+    """A numbers table from a pickle file, executing nothing from it.
+
+    First ``torch.load(path, weights_only=True)`` (torch's restricted unpickler; it reads protocol <= 2 and
+    ``torch.save`` files).  It refuses protocol-4 framing (``pickle.dump``'s default, opcode FRAME), which is what the
+    reference notebook writes, so a refused file is then decoded by walking its opcode stream with
+    ``pickletools.genops`` (a decoder: it constructs nothing) and rebuilding the value from a whitelist of list /
+    tuple / number / memo opcodes.  Any other opcode - a class, a callable, a persistent id - is refused."""
+    import pickle
+    import pickletools
+    import warnings
+    try:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")   # (its note on protocols it was not written for)
+            return torch.load(path, weights_only=True)
+    except (pickle.UnpicklingError, RuntimeError, EOFError, AttributeError, ValueError):
+        pass
+    with open(path, "rb") as f:
+        data = f.read()
+    stack: list = []
+    marks: list[int] = []
+    memo: dict[int, object] = {}
+    result = None
+    for op, arg, _pos in pickletools.genops(data):
+        n = op.name
+        if n not in _TABLE_OPS:
+            raise ValueError(f"{path}: refusing pickle opcode {n} (only lists / tuples of numbers are accepted)")
+        if n in ("PROTO", "FRAME"):
+            continue
+        if n == "MARK":
+            marks.append(len(stack))
+        elif n == "EMPTY_LIST":
+            stack.append([])
+        elif n == "EMPTY_TUPLE":
+            stack.append(())
+        elif n in ("LIST", "TUPLE"):
+            k = marks.pop()
+            items = stack[k:]
+            del stack[k:]
+            stack.append(list(items) if n == "LIST" else tuple(items))
+        elif n in ("TUPLE1", "TUPLE2", "TUPLE3"):
+            k = int(n[-1])
+            items = tuple(stack[-k:])
+            del stack[-k:]
+            stack.append(items)
+        elif n == "APPEND":
+            v = stack.pop()
+            if not isinstance(stack[-1], list):
+                raise ValueError(f"{path}: APPEND to a non-list")
+            stack[-1].append(v)
+        elif n == "APPENDS":
+            k = marks.pop()
+            items = stack[k:]
+            del stack[k:]
+            if not isinstance(stack[-1], list):
+                raise ValueError(f"{path}: APPENDS to a non-list")
+            stack[-1].extend(items)
+        elif n in ("BINFLOAT", "FLOAT", "BININT", "BININT1", "BININT2", "INT", "LONG", "LONG1"):
+            if isinstance(arg, bool) or not isinstance(arg, (int, float)):
+                raise ValueError(f"{path}: non-numeric scalar {arg!r}")
+            stack.append(arg)
+        elif n == "MEMOIZE":
+            memo[len(memo)] = stack[-1]
+        elif n in ("PUT", "BINPUT", "LONG_BINPUT"):
+            memo[int(arg)] = stack[-1]
+        elif n in ("GET", "BINGET", "LONG_BINGET"):
+            stack.append(memo[int(arg)])
+        elif n == "STOP":
+            if len(stack) != 1 or marks:
+                raise ValueError(f"{path}: malformed pickle")
+            result = stack.pop()
+            break
+    if result is None:
+        raise ValueError(f"{path}: no value in pickle")
+    return result
 
 
 class ImportanceTracker:

@@ -197,6 +197,60 @@ def set_gemm_stagger(k: int) -> None:
     call("edge_gemm_set_stagger", int(k))
 
 
+def set_gemm_split(k: int) -> None:
+    """Epilogue desync of the four-wave GEMMs: half of each XCD's workgroups run the first k K-tiles of their last
+    tile first (raw accumulators parked in a persistent per-device workspace) and finish it last, so their epilogues
+    fall half a tile after the others' and the chip's store bursts halve.  -1 = auto (half a tile), 0 = off.
+    Bit-identical results either way (same accumulation order)."""
+    global _SPLIT
+    call("edge_gemm_set_split", int(k))
+    _SPLIT = int(k)
+    if _SPLIT and torch.cuda.is_available():
+        _gemm_ws(torch.device("cuda", torch.cuda.current_device()))
+
+
+def get_gemm_split() -> int:
+    return _split()
+
+
+_SPLIT: int | None = None
+_WS: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+def _split() -> int:
+    global _SPLIT
+    if _SPLIT is None:
+        L = lib()
+        _SPLIT = int(L.edge_gemm_get_split()) if hasattr(L, "edge_gemm_get_split") else 0
+    return _SPLIT
+
+
+def _gemm_ws(dev: torch.device) -> None:
+    """Register this device's desync workspace with the kernel library, once: a persistent buffer kept in ``_WS``
+    for the life of the process, handed to every four-wave launch as a kernel argument (no per-call allocation, so
+    no lifetime to get wrong).  Nothing to do while the desync is off."""
+    if not _split():
+        return
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx in _WS:
+        return
+    n = int(lib().edge_gemm_ws_floats())
+    with torch.cuda.device(idx):
+        ws = torch.empty(n, dtype=torch.float32, device=f"cuda:{idx}")
+        err = torch.zeros(4, dtype=torch.int32, device=f"cuda:{idx}")
+        call("edge_gemm_set_ws", ws.data_ptr(), n, err.data_ptr())
+    _WS[idx] = (ws, err)
+
+
+def gemm_check_errors(dev=None) -> int:
+    """Checked builds (EDGE_GEMM_CHECKS / the tuning build): the device error word of the desync workspace - 0 when
+    no bounds check failed (1: segment table, 2: workspace offset)."""
+    idx = torch.cuda.current_device() if dev is None else torch.device(dev).index or 0
+    if idx not in _WS:
+        return 0
+    return int(_WS[idx][1][0].item())
+
+
 def set_gemm_walk(chunked) -> None:
     """Persistent 256x256 GEMMs: XCD-contiguous tile chunks (default) or the grid-strided walk.  A/B only.
     2 = chunked for the four-wave kernel too (it walks strided otherwise)."""
@@ -278,6 +332,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None,
     rs = None if norm is None else _norm_scale(norm, K)
     ssq_out = torch.empty(M, gemm_ssq_parts(M, N, K, act, bias is not None, residual is not None),
                           dtype=torch.float32, device=x.device) if want_ssq else None
+    _gemm_ws(x.device)
     call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), _ACT[act], ptr(rs), ptr(ssq_out), stream())
     if want_ssq:
@@ -307,6 +362,7 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     if ssq is not None:
         if _QKV_ROW_RSCALE or ssq.shape[1] not in (8, 14) or not ssq.is_contiguous() or ssq.data_ptr() % 16:
             rs, ssq = _norm_scale(norm, K), None
+    _gemm_ws(x.device)
     call("edge_gemm_qkv_rope", ptr(x), ptr(wqkv), ptr(bqkv), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, K, S,
          Hq, Hkv, rot_dim, sp, float(q_scale), ptr(rs), ptr(ssq), 0 if ssq is None else ssq.shape[1], float(eps),
          stream())
@@ -429,6 +485,7 @@ def head_nll(h, w, targets):
     tgt = torch.empty(R, dtype=torch.float32, device=h.device)
     nll = torch.empty(R, dtype=torch.float32, device=h.device)
     t64 = targets.to(torch.int64).contiguous()
+    _gemm_ws(h.device)
     call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, 0, 0.0, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
@@ -485,6 +542,7 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
         out = torch.empty(M, 2 * No, dtype=torch.float16, device=a3.device)
         ldc = 2 * No
         code = _ACT[act]
+    _gemm_ws(a3.device)
     call("edge_gemm_f32", ptr(a3), ptr(w3), ptr(out), M, N, Kx, kp, a3.stride(0), w3.stride(0), ldc, ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), code, ptr(rscale), float(alpha),
          float(out_scale), stream())
@@ -520,6 +578,7 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
         kpl = torch.empty(B, Hkv, 2, S, D, **f16)
         vpl = torch.zeros(B, Hkv, 2, D, sp, **f16) if sp != S else torch.empty(B, Hkv, 2, D, sp, **f16)
     sk_, sv_ = kv_scales if kv_scales is not None else (0.0, 0.0)
+    _gemm_ws(a3.device)
     call("edge_gemm_qkv_rope_f32", ptr(a3), ptr(w3), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, kp, S,
          Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), ptr(kpl), ptr(vpl), float(sk_), float(sv_), stream())
     if kv_scales is None:
@@ -540,6 +599,7 @@ def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch
     pmax, psum = torch.empty(R, nparts, **f32), torch.empty(R, nparts, **f32)
     tgt, nll = torch.empty(R, **f32), torch.empty(R, **f32)
     t64 = targets.to(torch.int64).contiguous()
+    _gemm_ws(a3.device)
     call("edge_gemm_lse", ptr(a3), ptr(w3), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, kp, float(alpha),
          stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
@@ -560,6 +620,7 @@ def linear_rowscale(x: torch.Tensor, w: torch.Tensor, rscale: torch.Tensor, resi
     N = w.shape[0]
     out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     rs = rscale.to(torch.float32).contiguous()
+    _gemm_ws(x.device)
     call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), None,
          ptr(residual), 0 if residual is None else residual.stride(0), 0, ptr(rs), None, stream())
     return out

@@ -43,6 +43,11 @@ _SIGS = {
     "edge_gemm_set_lse256": [c_i],
     "edge_gemm_set_w7_mode": [c_i],
     "edge_gemm_set_stagger": [c_i],
+    "edge_gemm_set_split": [c_i],
+    "edge_gemm_get_split": [],
+    "edge_gemm_set_ws": [c_p, c_ll, c_p],
+    "edge_gemm_ws_floats": [],
+    "edge_gemm_checked_build": [],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],
@@ -94,6 +99,9 @@ _SIGS = {
 }
 
 
+_LL_RESULT = {"edge_gemm_ws_floats"}
+
+
 class NativeLibraryMissing(RuntimeError):
     pass
 
@@ -120,6 +128,9 @@ def _apply_tuning_env(L) -> None:
     st = os.environ.get("EDGE_GEMM_STAGGER")  # four-wave GEMMs: odd workgroups start st x 1024 cycles late
     if st and hasattr(L, "edge_gemm_set_stagger"):
         L.edge_gemm_set_stagger(int(st))
+    sp = os.environ.get("EDGE_GEMM_SPLIT")  # four-wave GEMM epilogue desync: -1 auto, 0 off, k K-tiles
+    if sp and hasattr(L, "edge_gemm_set_split"):
+        L.edge_gemm_set_split(int(sp))
 
 
 def available() -> bool:
@@ -140,7 +151,7 @@ def lib():
                 continue  # an older build under A/B: entry points it predates stay unbound
             fn = getattr(L, name)
             fn.argtypes = argt
-            fn.restype = c_i
+            fn.restype = c_ll if name in _LL_RESULT else c_i
         _lib = L
         if tuning():
             _apply_tuning_env(L)

@@ -208,6 +208,12 @@ class IpcP2P:
 
     def close(self):
         self.quiesce()
+        if self.credit_pg is not None:    # the credit group's communicator / streams (one per transport)
+            try:
+                dist.destroy_process_group(self.credit_pg)
+            except (RuntimeError, ValueError):
+                pass
+            self.credit_pg = None
         for p in self._files:
             try:
                 os.unlink(p)

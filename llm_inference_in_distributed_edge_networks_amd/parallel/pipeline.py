@@ -85,8 +85,12 @@ class StageStats:
 
     @property
     def bytes_per_token(self) -> float:
-        b = self.wire_bytes + (float(self.kvar_bytes) if self.kvar_bytes is not None else 0.0)
-        return b / self.wire_tokens if self.wire_tokens else 0.0
+        b, t = self.totals()
+        return b / t if t else 0.0
+
+    def totals(self) -> tuple[float, float]:
+        """(bytes sent across the outgoing boundary, tokens they carried) since this runner was created."""
+        return self.wire_bytes + (float(self.kvar_bytes) if self.kvar_bytes is not None else 0.0), float(self.wire_tokens)
 
 
 class StageRunner:
@@ -238,6 +242,12 @@ class LocalPipeline:
     def wire_bytes_per_token(self) -> list[float]:
         return [s.stats.bytes_per_token for s in self.stages[:-1]]
 
+    def wire_totals(self) -> tuple[float, float]:
+        """(bytes, tokens) summed over the boundaries since the last ``set_boundary``: their ratio is the mean
+        wire bytes per token per boundary."""
+        tot = [s.stats.totals() for s in self.stages[:-1]]
+        return sum(b for b, _ in tot), sum(t for _, t in tot)
+
 
 class DistributedPipeline:
     """One pipeline stage per rank; ``grid.dp`` replicas share the window batches round-robin."""
@@ -282,6 +292,55 @@ class DistributedPipeline:
 
     def _stage_step(self, ids, rows, targets, row_window, n_rows, msg_in=None, carry_in=None):
         return self.runner.forward(ids, rows, targets, row_window, n_rows, msg_in, carry_in)
+
+    def probe_p2p(self, sizes, iters: int = 10, warm: int = 2) -> list[dict]:
+        """Time the active transport on every pipeline edge (SURVEY §5.8 p2p latency / bandwidth), before a run:
+        per message size, the sender streams ``iters`` messages to its next stage and stops its clock when the
+        receiver's acknowledgement (a 4-byte process-group message, after the receiver's stream is synchronised)
+        arrives.  ``warm`` untimed messages first (RCCL connects a channel on its first message).  Edges are
+        probed in stage order, every replica at once; collective over all ranks.  Returns the sender's rows
+        ``{edge, stage, bytes, p2p_us, p2p_GBps}`` (one per size; receivers and the last stage return [])."""
+        import torch.distributed as dist
+        dev = self.device
+        cuda = dev.type == "cuda"
+        ctl_dev = dev if (cuda and dist.get_backend() == "nccl") else torch.device("cpu")
+
+        def sync():
+            if cuda:
+                torch.cuda.synchronize(dev)
+
+        rows = []
+        for s in range(self.grid.pp - 1):
+            if self.stage not in (s, s + 1):
+                continue
+            for nbytes in sizes:
+                buf = torch.zeros(int(nbytes), dtype=torch.uint8, device=dev)
+                ctl = torch.zeros(1, dtype=torch.int32, device=ctl_dev)
+                for n, timed in ((warm, False), (iters, True)):
+                    if self.stage == s:
+                        dist.recv(ctl, self.next)            # the receiver has posted nothing yet: start together
+                        sync()
+                        t0 = time.perf_counter()
+                        hs = [self.tr.send(buf, self.next) for _ in range(n)]
+                        for h in hs:
+                            h.wait()
+                        dist.recv(ctl, self.next)            # acknowledgement: all n arrived
+                        sync()
+                        dt = time.perf_counter() - t0
+                        if timed:
+                            rows.append({"edge": [self.rank, self.next], "stage": s, "bytes": int(nbytes),
+                                         "p2p_us": round(1e6 * dt / n, 2),
+                                         "p2p_GBps": round(n * nbytes / dt / 1e9, 3)})
+                    else:
+                        dist.send(ctl, self.prev)
+                        hs = [self.tr.recv(buf, self.prev) for _ in range(n)]
+                        for h in hs:
+                            h.wait()
+                        sync()
+                        dist.send(ctl, self.prev)
+                if hasattr(self.tr, "quiesce"):              # IPC: both ends of the edge settle their credits
+                    self.tr.quiesce()
+        return rows
 
     def my_batches(self, batches):
         for i, b in enumerate(batches):
@@ -405,6 +464,8 @@ class DistributedPipeline:
         acc = PPLAccumulator()
         acc.total_nll, acc.n_tokens = float(acc_local[0]), float(acc_local[1])
         report["wire_bytes_per_token"] = self.runner.stats.bytes_per_token
+        # this rank's cumulative counters since set_boundary (the last stage sends nothing)
+        report["wire_bytes"], report["wire_tokens"] = self.runner.stats.totals() if not self.runner.last else (0.0, 0.0)
         return acc, report
 
     def close(self) -> None:

@@ -103,9 +103,11 @@ class RcclComm:
     created by its lower rank and handed to the other through the process group's key-value store (no
     collective), and the edges are initialised in one global order (sorted rank pairs), so the blocking
     ``ncclCommInitRank`` calls of a chain of stages cannot wait on each other in a cycle.  ``peers=None`` with
-    ``world == 1`` is the single-GPU loopback (``sendrecv`` to itself, ``all_reduce_sum_f64``)."""
+    ``world == 1`` is the single-GPU loopback (``sendrecv`` to itself, ``all_reduce_sum_f64``).
 
-    _generation = 0
+    The store keys of one construction live under a namespace rank 0 draws and broadcasts (construction is
+    collective over the default group, as every rank builds its pipeline), so keys never depend on how many
+    communicators each rank built before; the reader deletes a key once it has the id."""
 
     def __init__(self, rank: int, world: int, device: int, unique_id: bytes | None = None, peers=None):
         self.rank, self.world, self.device = rank, world, device
@@ -114,8 +116,7 @@ class RcclComm:
             if world != 1:
                 raise ValueError("RcclComm over several ranks needs its peers (the pipeline neighbours)")
             peers = [rank]
-        RcclComm._generation += 1
-        gen = RcclComm._generation
+        gen = self._namespace() if world > 1 else ""
         for key in sorted({channel_key(rank, p) for p in peers if p is not None}):
             ranks = tuple(sorted(set(key)))
             if len(ranks) == 1:
@@ -137,7 +138,15 @@ class RcclComm:
         _ok(L.edge_rccl_unique_id(buf), "ncclGetUniqueId")
         return buf.raw
 
-    def _exchange_id(self, gen: int, ranks: tuple) -> bytes:
+    @staticmethod
+    def _namespace() -> str:
+        import secrets
+
+        from .dist import broadcast_object
+        import torch.distributed as dist
+        return broadcast_object(secrets.token_hex(8) if dist.get_rank() == 0 else None, src=0)
+
+    def _exchange_id(self, gen: str, ranks: tuple) -> bytes:
         import torch.distributed as dist
         store = dist.distributed_c10d._get_default_store()
         k = f"edge_rccl/{gen}/{ranks[0]}-{ranks[1]}"
@@ -145,7 +154,12 @@ class RcclComm:
             uid = self.make_unique_id()
             store.set(k, uid)
             return uid
-        return bytes(store.get(k))
+        uid = bytes(store.get(k))
+        try:
+            store.delete_key(k)
+        except (AttributeError, RuntimeError, NotImplementedError):
+            pass
+        return uid
 
     def _channel(self, peer: int) -> _Channel:
         try:

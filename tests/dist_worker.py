@@ -189,3 +189,29 @@ def run_lanes(rank, world, port, lanes, out_path):
             json.dump({"ppl": acc.ppl()}, f)
     tr.close()
     shutdown()
+
+
+def run_driver(rank, world, port, params, crash_at, out_dir):
+    """pipeline_experiment on one rank of a gloo job; crash_at > 0: the job dies (every rank, before its crash_at-th
+    evaluate call, so no rank is left inside a collective) after writing its per-rank checkpoints."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from llm_inference_in_distributed_edge_networks_amd.config import Params
+    from llm_inference_in_distributed_edge_networks_amd.eval import experiments as E
+    from llm_inference_in_distributed_edge_networks_amd.parallel import pipeline as P
+    from llm_inference_in_distributed_edge_networks_amd.parallel import shutdown
+    if crash_at:
+        orig, calls = P.DistributedPipeline.evaluate, {"n": 0}
+
+        def flaky(self, *a, **k):
+            calls["n"] += 1
+            if calls["n"] == crash_at:
+                raise KeyboardInterrupt("simulated crash")
+            return orig(self, *a, **k)
+        P.DistributedPipeline.evaluate = flaky
+    try:
+        E.pipeline_experiment(Params.from_dict(dict(params, output_dir=out_dir)), "qwen2-0.5b")
+    except KeyboardInterrupt:
+        pass
+    shutdown()

@@ -133,8 +133,11 @@ def test_pipeline_driver_resumes_mid_run(tmp_path, monkeypatch):
 
     def params(d):
         d.mkdir()
+        # top_rho: variable-k messages, so the bytes per token differ per batch and a resumed run must carry the
+        # byte and token sums of the chunks before the crash
         return Params.from_dict({"model": "tiny-qwen2", "split_layers": [1], "codec": "mixed_int4_int8",
-                                 "methods": ["last_row"], "ratios": [0.25, 0.75], "max_length": 128, "stride": 32,
+                                 "methods": ["last_row"], "selection": "top_rho", "ratios": [0.25, 0.75],
+                                 "max_length": 128, "stride": 32,
                                  "window_batch": 2, "dataset": "synthetic", "synthetic_tokens": 1200,
                                  "device": "cpu", "checkpoint_every": 4, "output_dir": str(d)})
     full = E.pipeline_experiment(params(tmp_path / "full"), "qwen2-0.5b")["results"]
@@ -157,3 +160,5 @@ def test_pipeline_driver_resumes_mid_run(tmp_path, monkeypatch):
     for r in ("0.25", "0.75"):
         assert res["last_row"][r]["ppl"] == pytest.approx(full["last_row"][r]["ppl"], rel=1e-9)
         assert res["last_row"][r]["n_tokens"] == full["last_row"][r]["n_tokens"]
+        assert res["last_row"][r]["wire_bytes_per_token"] == pytest.approx(
+            full["last_row"][r]["wire_bytes_per_token"], rel=1e-12)

@@ -62,6 +62,12 @@ def test_bench_contract_cpu(n):
     assert d["dtype"] == "fp32" and d["metric"].startswith("WikiText-2 PPL + inter-stage bytes/token")
     if n > 1:   # per-stage GPU-time breakdown rows, one per rank
         assert len(d["stages"]) == n and {s["stage"] for s in d["stages"]} == {0, 1}
+        # the p2p probe of every pipeline edge (one per replica), a 1 MiB and a boundary-sized message
+        assert len(d["p2p"]) == 2 * dp
+        for row in d["p2p"]:
+            assert row["stage"] == 0 and row["edge"][1] == row["edge"][0] + 1
+            assert row["p2p_us"] > 0 and row["p2p_GBps"] > 0
+        assert {row["bytes"] for row in d["p2p"]} == {1 << 20, round(d["wire_bytes_per_token"][0] * 2 * 128)}
 
 
 @pytest.mark.parametrize("pp", [4, 8])
@@ -137,3 +143,31 @@ def test_bench_refuses_gpus_world_size_mismatch():
     r = _torchrun(2, BENCH + ["--gpus", "4"])
     assert r.returncode != 0
     assert "--gpus 4 but the launcher started WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.parametrize("rank", [1, 0])
+def test_bench_failed_rank_exits_nonzero_without_json(rank):
+    """A rank that dies (here on purpose, after its measurement) must leave the self-launching parent with a
+    non-zero exit code and NO JSON line: rank 0 reports only after every rank passed the final barrier."""
+    env = dict(_env(), EDGE_BENCH_FAIL_RANK=str(rank))
+    r = subprocess.run([sys.executable] + BENCH + ["--gpus", "2"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")], r.stdout
+    assert "fails on purpose" in r.stderr
+
+
+def test_visible_gpu_count_without_hip(monkeypatch):
+    """The launcher parent counts GPUs from sysfs / the visibility variables, never through the HIP runtime."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    base = bench.visible_gpu_count()          # 0 here (no KFD topology), the GPU count on a GPU box
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2")
+    assert bench.visible_gpu_count() == (min(base, 3) if base else 3)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpu_count() == 0
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    launch = src[src.index("def launch_mode"):src.index("def self_launch")]
+    assert "torch.cuda" not in launch
