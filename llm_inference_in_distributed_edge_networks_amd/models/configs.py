@@ -102,7 +102,17 @@ BYTE_QWEN2 = ModelConfig(
     rope_theta=1e4, rotary_dim=64, max_position=2048, tie_embeddings=True,
 )
 
-PRESETS = {c.name: c for c in (QWEN2_0_5B, PYTHIA_70M, TINY_QWEN2, TINY_NEOX, BYTE_QWEN2)}
+# The exact Qwen2-0.5B depth and width (24 layers, H 896, 14 / 2 heads, I 4864, rope theta 1e6) with a byte
+# vocabulary: the quality experiments at the reference's real boundary depths (layers 3 / 11 / 18 / 22 / 23 of 24,
+# Notebooks/qwen2-0.5B_experiment.ipynb) on a model trained here (tools/train_tiny_lm.py), since no checkpoint is
+# reachable.
+BYTE_QWEN2_24 = ModelConfig(
+    name="byte-qwen2-24", arch="qwen2", vocab_size=512, hidden_size=896, num_layers=24,
+    num_heads=14, num_kv_heads=2, head_dim=64, intermediate_size=4864, norm_eps=1e-6,
+    rope_theta=1e6, rotary_dim=64, max_position=2048, tie_embeddings=True,
+)
+
+PRESETS = {c.name: c for c in (QWEN2_0_5B, PYTHIA_70M, TINY_QWEN2, TINY_NEOX, BYTE_QWEN2, BYTE_QWEN2_24)}
 ALIASES = {
     "Qwen/Qwen2-0.5B": "qwen2-0.5b", "qwen2": "qwen2-0.5b", "Qwen2-0.5B": "qwen2-0.5b",
     "EleutherAI/pythia-70m": "pythia-70m", "pythia": "pythia-70m", "Pythia-70M": "pythia-70m",

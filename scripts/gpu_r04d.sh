@@ -29,4 +29,16 @@ for i in 1 2; do
     python -c "import json; d=json.load(open('$O/bisect_${t}_$i.json')); print('bisect $t $i', d['value'], d['ppl_random_weights'])"
   done
 done
+# (4) fp32 AttnLRP at the 64-window benchmark size: throughput + kernel profile
+timeout -k 10 240 python tools/relevance_bench.py --dtype fp32 --batch 64 --json-out $O/relevance_fp32_b64.json \
+  > $O/relevance_fp32_b64.log 2>&1 || { echo "relevance bench failed"; tail -20 $O/relevance_fp32_b64.log; exit 1; }
+tail -1 $O/relevance_fp32_b64.log
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/lrp_prof -o run -- \
+  python3 $R/tools/relevance_bench.py --dtype fp32 --batch 64 --iters 3 --warmup 1 > $R/$O/lrp_prof.log 2>&1 \
+  || { echo "lrp profile failed"; tail -20 $R/$O/lrp_prof.log; exit 1; }
+cd $R
+python tools/prof_summary.py $(ls $O/lrp_prof/*kernel_stats.csv $O/lrp_prof/*/*kernel_stats.csv 2>/dev/null | head -1) \
+  "fp32 AttnLRP, Qwen2-0.5B, 64 windows x 512" > $O/lrp_kernel_stats.md || true
+head -20 $O/lrp_kernel_stats.md
 exit 0

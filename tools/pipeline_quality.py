@@ -52,6 +52,17 @@ GRID = [
 ]
 
 
+def stage_plan(cfg, pp: int, splits: str) -> PipelinePlan:
+    if splits == "bench":
+        from llm_inference_in_distributed_edge_networks_amd.models import QWEN2_0_5B
+        if cfg.num_layers != QWEN2_0_5B.num_layers:
+            raise ValueError("--splits bench needs a model with Qwen2-0.5B's 24 layers")
+        if pp == 2:   # bench.py --split 11 (the reference notebook's middle layer)
+            return PipelinePlan.from_split_layers(cfg.num_layers, [11])
+        return PipelinePlan(cfg.num_layers, PipelinePlan.balanced(QWEN2_0_5B, pp, 512, 32 / 512).bounds)
+    return PipelinePlan.balanced(cfg, pp, 512)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="byte-qwen2")
@@ -62,6 +73,10 @@ def main():
     ap.add_argument("--group-bits", type=float, default=4.0, help="average bits of the head-group codecs")
     ap.add_argument("--relevance-windows", type=int, default=256)
     ap.add_argument("--json-out", default="gpurun_out/pipeline_quality.json")
+    ap.add_argument("--splits", default="balanced", choices=["balanced", "bench"],
+                    help="stage boundaries: cost-balanced for this model, or the bench's splits for Qwen2-0.5B "
+                         "(pp 2: after layer 11; pp 4 / 8: balanced with the 151936-row LM head) - the same layer "
+                         "indices on a 24-layer model")
     a = ap.parse_args()
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     cfg = get_config(a.model)
@@ -98,7 +113,7 @@ def main():
         t0 = time.time()
         codec, _, bits = codec_spec.partition("@")
         gbits = float(bits) if bits else a.group_bits
-        pplan = PipelinePlan.balanced(cfg, pp, 512)
+        pplan = stage_plan(cfg, pp, a.splits)
         row = {"pp": pp, "boundaries": pplan.boundary_layers(), "method": meth, "codec": codec_spec, "plan": plan,
                "group_avg_bits": gbits, "ppl": [], "wire_bytes_per_token": []}
         pipe = None

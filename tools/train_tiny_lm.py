@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--lr", type=float, default=2e-3)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--warmup", type=int, default=200, help="linear learning-rate warmup steps")
+    ap.add_argument("--eval-every", type=float, default=15.0, help="seconds between held-out evaluations")
     a = ap.parse_args()
     torch.manual_seed(a.seed)
     dev = "cuda"
@@ -77,7 +79,7 @@ def main():
         if el > budget:
             break
         frac = el / budget
-        lr = a.lr * min(1.0, (step + 1) / 200) * (0.1 + 0.9 * 0.5 * (1 + math.cos(math.pi * frac)))
+        lr = a.lr * min(1.0, (step + 1) / a.warmup) * (0.1 + 0.9 * 0.5 * (1 + math.cos(math.pi * frac)))
         for grp in opt.param_groups:
             grp["lr"] = lr
         idx = torch.randint(0, data.numel() - a.seq - 1, (a.batch,), device=dev, generator=g)
@@ -90,7 +92,7 @@ def main():
         torch.nn.utils.clip_grad_norm_(params, 1.0)
         opt.step()
         step += 1
-        if el - last_print > 15:
+        if el - last_print > a.eval_every:
             last_print = el
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
                 hl = F.cross_entropy(forward(w, cfg, held[:, :-1], cos, sin).float().view(-1, cfg.vocab_size),
