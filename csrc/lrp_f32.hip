@@ -280,6 +280,253 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_f32_kernel(const float* __res
 }
 
 // ---------------------------------------------------------------------------------------------
+// The same two sweeps on the bf16 matrix cores ("x6", the split of the forward's first fp32 attention): every
+// operand - q, k, v, dO, and the in-register P and dS - is split into three bf16 planes x = x0 + x1 + x2 (24
+// significant bits, exact: common.h split3), and each product is the six plane products with i + j <= 2, small terms
+// first, on v_mfma_f32_16x16x32_bf16 (1024 FLOP per cycle against the f32 MFMA's 64: 2.7x per useful FLOP).  No
+// scales are needed (bf16 has fp32's exponent range), so the gradients keep their dynamic range with no bounds.
+//
+// 16x16x32 fragments: lane l holds A[row l&15][k 8(l>>4)+j] and B[k 8(l>>4)+j][col l&15], C[row 4(l>>4)+r][col l&15].
+// A score tile computed with the query (dkdv) or the key (dq) on the C rows puts 4 rows of a 16-row block on a lane;
+// two such blocks give the lane the 8 k-slots of a 32-deep reduction over those rows, in the order
+// slot 8g + j <-> row perm(g, j) = (j < 4 ? 4g + j : 16 + 4g + j - 4): the probabilities / dS are then the lane's own
+// A / B fragments, and the other operand is staged transposed in LDS with its rows in that order (X6T images).
+namespace {
+constexpr int X6P = 32 * 64 * 2;   // one bf16 plane of a 32 x 64 tile (bytes)
+
+__device__ __forceinline__ int x6sw(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ f32x4_t mfma_bf16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4_t x6dot(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4_t c) {
+  c = mfma_bf16(a[2], b[0], c);
+  c = mfma_bf16(a[0], b[2], c);
+  c = mfma_bf16(a[1], b[1], c);
+  c = mfma_bf16(a[1], b[0], c);
+  c = mfma_bf16(a[0], b[1], c);
+  return mfma_bf16(a[0], b[0], c);
+}
+__device__ __forceinline__ void split3_frag(const float (&v)[8], bf16x8_t (&p)[3]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float p0, p1, p2;
+    split3(v[e], p0, p1, p2);
+    p[0][e] = (__bf16)p0;
+    p[1][e] = (__bf16)p1;
+    p[2][e] = (__bf16)p2;
+  }
+}
+// the slot of row r (0..31) of a 32-row block in the permuted k order
+__device__ __forceinline__ int x6_slot(int r) { return r < 16 ? 8 * (r >> 2) + (r & 3) : 8 * ((r - 16) >> 2) + 4 + (r & 3); }
+
+// Stage a 32 x 64 fp32 tile (rows row0.., row stride ld floats; rows >= nrows zero) as three bf16 planes, row-major
+// ([32][64], 16-byte chunks swizzled by x6sw(row): A / B fragments by one ds_read_b128) and, with T, also transposed
+// ([64][32 slots] in the x6_slot order, 64-byte rows: the fragments of a reduction over the tile's rows).
+template <bool T>
+__device__ __forceinline__ void stage_x6(const float* __restrict__ src, size_t ld, int row0, int nrows, char* rm,
+                                         char* tr) {
+  const int t = threadIdx.x, r = t >> 3, c = t & 7;   // row r, 8 columns 8c .. 8c+7
+  const int gr = row0 + r;
+  float v[8];
+  if (gr < nrows) {
+    const f32x4_t a = *(const f32x4_t*)(src + (size_t)gr * ld + 8 * c);
+    const f32x4_t b = *(const f32x4_t*)(src + (size_t)gr * ld + 8 * c + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = a[e], v[4 + e] = b[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  }
+  bf16x8_t p[3];
+  split3_frag(v, p);
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) *(bf16x8_t*)(rm + pl * X6P + r * 128 + ((c ^ x6sw(r)) << 4)) = p[pl];
+  if constexpr (T) {
+    const int sl = x6_slot(r);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) *(__bf16*)(tr + pl * X6P + (8 * c + e) * 64 + sl * 2) = p[pl][e];
+  }
+}
+__device__ __forceinline__ void rm_frags(const char* img, int row, int chunk, bf16x8_t (&f)[3]) {
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * X6P + row * 128 + ((chunk ^ x6sw(row)) << 4));
+}
+__device__ __forceinline__ void tr_frags(const char* img, int row, int g, bf16x8_t (&f)[3]) {
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * X6P + row * 64 + g * 16);
+}
+// the lane's 8 values of row `row` (its key / query), columns 8 kg + 32 ks .. +7, split into planes
+__device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8_t (&f)[2][3], int g) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const f32x4_t a = *(const f32x4_t*)(rowp + 32 * ks + 8 * g);
+    const f32x4_t b = *(const f32x4_t*)(rowp + 32 * ks + 8 * g + 4);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = a[e], v[4 + e] = b[e];
+    split3_frag(v, f[ks]);
+  }
+}
+}  // namespace
+
+// dK, dV partials per q head (inputs and outputs as lrp_attn_dkdv_f32_kernel).  Workgroup = (b, q head, 64-key
+// block), heaviest first; wave w owns keys kb 64 + 16 w + cl.  Per 32-query tile: S = Q K^T and dA = dO V^T with the
+// query on the C rows (the lane's K / V planes in registers for the whole sweep), P = exp(S - lse), dS = P (dA/2 - D),
+// then dV += P^T dO and dK += dS^T Q over the tile's 32 queries (P / dS the lane's A fragments, dO / Q from the
+// transposed images).
+__global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                               const float* __restrict__ v,
+                                                               const float* __restrict__ dO,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ D, float* __restrict__ dk,
+                                                               float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
+  __shared__ __attribute__((aligned(16))) char sQ[3 * X6P], sO[3 * X6P], sQT[3 * X6P], sOT[3 * X6P];
+  __shared__ float sL[32], sD[32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int kb = blockIdx.x / (B * Hq);
+  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
+  const int key = kb * 64 + wave * 16 + cl;
+  const int keyc = key < S ? key : S - 1;
+  bf16x8_t kf[2][3], vf[2][3];
+  row_frags(k + (((size_t)b * Hkv + hk) * S + keyc) * 64, kf, g);
+  row_frags(v + (((size_t)b * Hkv + hk) * S + keyc) * 64, vf, g);
+  f32x4_t dka[4], dva[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
+  const float* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
+  const float* lh = lse + ((size_t)b * Hq + h) * S;
+  const float* dh = D + ((size_t)b * Hq + h) * S;
+  for (int q0 = kb * 64; q0 < S; q0 += 32) {
+    __syncthreads();
+    stage_x6<true>(qh, 64, q0, S, sQ, sQT);
+    stage_x6<true>(doh, (size_t)Hq * 64, q0, S, sO, sOT);
+    if (tid < 32) {
+      const int qi = q0 + tid;
+      sL[tid] = qi < S ? lh[qi] : INFINITY;
+      sD[tid] = qi < S ? dh[qi] : 0.f;
+    }
+    __syncthreads();
+    float pv[8], dsv[8];   // k-slot order: j < 4 -> sub-block 0 row 4g + j, j >= 4 -> sub-block 1 row 4g + j - 4
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t qa[3], oa[3];
+        rm_frags(sQ, sub * 16 + cl, 4 * ks + g, qa);
+        rm_frags(sO, sub * 16 + cl, 4 * ks + g, oa);
+        sc = x6dot(qa, kf[ks], sc);
+        da = x6dot(oa, vf[ks], da);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = sub * 16 + 4 * g + r, qi = q0 + ql;
+        const bool ok = qi < S && key <= qi && key < S;
+        const float pr = ok ? expf(sc[r] - sL[ql]) : 0.f;
+        pv[4 * sub + r] = pr;
+        dsv[4 * sub + r] = pr * (0.5f * da[r] - sD[ql]);
+      }
+    }
+    bf16x8_t pf[3], dsf[3];
+    split3_frag(pv, pf);
+    split3_frag(dsv, dsf);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x8_t ob[3], qb[3];
+      tr_frags(sOT, dt * 16 + cl, g, ob);
+      tr_frags(sQT, dt * 16 + cl, g, qb);
+      dva[dt] = x6dot(pf, ob, dva[dt]);
+      dka[dt] = x6dot(dsf, qb, dka[dt]);
+    }
+  }
+  // C[row = key 16w + 4g + r][col = d 16dt + cl]
+  float* dkh = dk + ((size_t)b * Hq + h) * S * 64;
+  float* dvh = dv + ((size_t)b * Hq + h) * S * 64;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int kr = kb * 64 + wave * 16 + g * 4 + r;
+    if (kr < S) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dkh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dka[dt][r];
+        dvh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dva[dt][r];
+      }
+    }
+  }
+}
+
+// dQ (inputs and output as lrp_attn_dq_f32_kernel).  Workgroup = (b, h, 64-query block), heaviest (last) first; wave
+// w owns queries qb 64 + 16 w + cl.  Per 32-key tile: S^T = K Q^T and dA^T = V dO^T with the key on the C rows (the
+// lane's Q / dO planes in registers), dS^T = P^T (dA^T/2 - D), then dQ^T += K^T dS^T over the tile's 32 keys.
+__global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                             const float* __restrict__ v, const float* __restrict__ dO,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ D, float* __restrict__ dq,
+                                                             int B, int Hq, int Hkv, int S) {
+  __shared__ __attribute__((aligned(16))) char sK[3 * X6P], sV[3 * X6P], sKT[3 * X6P];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int nqb = (S + 63) / 64;
+  const int qb = nqb - 1 - blockIdx.x / (B * Hq);
+  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
+  const int qi = qb * 64 + wave * 16 + cl;
+  const int qic = qi < S ? qi : S - 1;
+  bf16x8_t qf[2][3], of[2][3];
+  row_frags(q + (((size_t)b * Hq + h) * S + qic) * 64, qf, g);
+  row_frags(dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64, of, g);
+  const float lq = lse[((size_t)b * Hq + h) * S + qic];
+  const float dq_ = D[((size_t)b * Hq + h) * S + qic];
+  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const float* vh = v + ((size_t)b * Hkv + hk) * S * 64;
+  f32x4_t acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int kend = min(S, qb * 64 + 64);
+  for (int k0 = 0; k0 < kend; k0 += 32) {
+    __syncthreads();
+    stage_x6<true>(kh, 64, k0, S, sK, sKT);
+    stage_x6<false>(vh, 64, k0, S, sV, nullptr);
+    __syncthreads();
+    float dsv[8];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t ka[3], va[3];
+        rm_frags(sK, sub * 16 + cl, 4 * ks + g, ka);
+        rm_frags(sV, sub * 16 + cl, 4 * ks + g, va);
+        sc = x6dot(ka, qf[ks], sc);
+        da = x6dot(va, of[ks], da);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + sub * 16 + 4 * g + r;
+        const bool ok = qi < S && kj <= qi;
+        const float pr = ok ? expf(sc[r] - lq) : 0.f;
+        dsv[4 * sub + r] = pr * (0.5f * da[r] - dq_);
+      }
+    }
+    bf16x8_t dsf[3];
+    split3_frag(dsv, dsf);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x8_t kt[3];
+      tr_frags(sKT, dt * 16 + cl, g, kt);
+      acc[dt] = x6dot(kt, dsf, acc[dt]);
+    }
+  }
+  // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
+  if (qi < S) {
+    float* o = dq + (((size_t)b * Hq + h) * S + qi) * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = 0.5f * acc[dt];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Per-row power-of-two h3 split of rule outputs: a max pass and a store pass over the row.  For the model widths
 // (rows up to 2048 / 8192 / 1024 values) a thread's values stay in registers between the two, so the row is read
 // once; wider rows recompute them (template parameter 0).
@@ -607,6 +854,8 @@ __global__ __launch_bounds__(256) void group_absprod_kernel(const float* __restr
 // ---------------------------------------------------------------------------------------------
 static inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
 
+static int g_lrp_attn_x6 = 1;
+
 EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* v, const float* o, const float* dO,
                                    const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, int B,
                                    int Hq, int Hkv, int S, hipStream_t st) {
@@ -614,9 +863,20 @@ EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* 
   if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
   const int nb = (S + 63) / 64;
   lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
-  lrp_attn_dkdv_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-  lrp_attn_dq_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+  if (g_lrp_attn_x6) {
+    lrp_attn_dkdv_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+    lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+  } else {
+    lrp_attn_dkdv_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+    lrp_attn_dq_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+  }
   return (int)hipGetLastError();
+}
+
+// A/B and tests: 1 = the bf16 matrix-core (x6) sweeps (default), 0 = the f32-MFMA sweeps
+EDGE_API int edge_lrp_attn_set_x6(int on) {
+  g_lrp_attn_x6 = on;
+  return 0;
 }
 
 EDGE_API int edge_lrp_rope_pack_h3(const float* dq, const float* dk, const float* dv, const float* cosT,

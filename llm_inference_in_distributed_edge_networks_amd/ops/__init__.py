@@ -646,6 +646,12 @@ def lrp_attn_bwd(q, k, v, o, dO, lse):
     return Dl, rel, dq, dk, dv
 
 
+def set_lrp_attn_x6(on) -> None:
+    """fp32 AttnLRP attention backward: the bf16 matrix-core sweeps on three-plane splits (1, default) or the f32
+    MFMA sweeps (0).  A/B and tests."""
+    call("edge_lrp_attn_set_x6", int(on))
+
+
 def lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, dtype=torch.bfloat16):
     if not _gpu(dq):
         return ref.lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, dtype)

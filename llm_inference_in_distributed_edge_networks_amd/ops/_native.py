@@ -87,6 +87,7 @@ _SIGS = {
     "edge_split_h3": [c_p, c_p, c_p, c_i, c_i, c_f, c_p],
     "edge_embedding_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     # fp32 AttnLRP backward (csrc/lrp_f32.hip)
+    "edge_lrp_attn_set_x6": [c_i],
     "edge_lrp_attn_bwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_lrp_rope_pack_h3": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_split_h3_dyn": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
@@ -128,6 +129,9 @@ def _apply_tuning_env(L) -> None:
     st = os.environ.get("EDGE_GEMM_STAGGER")  # four-wave GEMMs: odd workgroups start st x 1024 cycles late
     if st and hasattr(L, "edge_gemm_set_stagger"):
         L.edge_gemm_set_stagger(int(st))
+    lx = os.environ.get("EDGE_LRP_ATTN_X6")  # fp32 AttnLRP attention backward: 1 bf16-plane sweeps, 0 f32 MFMA
+    if lx and hasattr(L, "edge_lrp_attn_set_x6"):
+        L.edge_lrp_attn_set_x6(int(lx))
     sp = os.environ.get("EDGE_GEMM_SPLIT")  # four-wave GEMM epilogue desync: -1 auto, 0 off, k K-tiles
     if sp and hasattr(L, "edge_gemm_set_split"):
         L.edge_gemm_set_split(int(sp))

@@ -16,9 +16,17 @@ replay i reads; before replaying a slot again the caller makes the stream wait f
 from __future__ import annotations
 
 import gc
+import os
 from typing import Callable
 
 import torch
+
+# A/B (EDGE_TUNING=1 EDGE_GRAPH_GC_OFF=0|1): the collector disabled for the whole capture (round-3 default) or only
+# the collection before it
+_TUNE = os.environ.get("EDGE_TUNING", "0") not in ("", "0")
+_GC_OFF_IN_CAPTURE = not (_TUNE and os.environ.get("EDGE_GRAPH_GC_OFF", "1") == "0")
+# A/B (EDGE_TUNING=1 EDGE_GRAPH_GC_COLLECT=0|1): the explicit collection before each capture
+_GC_COLLECT = not (_TUNE and os.environ.get("EDGE_GRAPH_GC_COLLECT", "1") == "0")
 
 
 _PRERUN = False
@@ -81,9 +89,11 @@ class GraphCache:
         # a query from another thread aborts the capture.
         # No garbage collection while capturing: a cycle collected mid-capture can hold a dropped CUDAGraph (e.g. of
         # a pipeline rebuilt for another codec), and its destructor is not permitted while a stream captures.
-        gc.collect()
+        if _GC_COLLECT:
+            gc.collect()
         was = gc.isenabled()
-        gc.disable()
+        if _GC_OFF_IN_CAPTURE:
+            gc.disable()
         try:
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 static_out = self.fn(*static_in)

@@ -29,10 +29,16 @@ for i in 1 2; do
     python -c "import json; d=json.load(open('$O/bisect_${t}_$i.json')); print('bisect $t $i', d['value'], d['ppl_random_weights'])"
   done
 done
-# (4) fp32 AttnLRP at the 64-window benchmark size: throughput + kernel profile
-timeout -k 10 240 python tools/relevance_bench.py --dtype fp32 --batch 64 --json-out $O/relevance_fp32_b64.json \
-  > $O/relevance_fp32_b64.log 2>&1 || { echo "relevance bench failed"; tail -20 $O/relevance_fp32_b64.log; exit 1; }
-tail -1 $O/relevance_fp32_b64.log
+# (4) fp32 AttnLRP at the 64-window benchmark size: the bf16-plane (x6) attention backward tested against fp64,
+# the full-size calibration table against the CPU, throughput x6 vs f32 MFMA, kernel profile
+timeout -k 10 600 $T tests/test_lrp_gpu.py -k "lrp_attn_bwd or calibration_table" > $O/test_lrp.log 2>&1 || { echo "lrp tests failed"; tail -30 $O/test_lrp.log; exit 1; }
+tail -1 $O/test_lrp.log
+for x in 1 0 1; do
+  EDGE_TUNING=1 EDGE_LRP_ATTN_X6=$x timeout -k 10 240 python tools/relevance_bench.py --dtype fp32 --batch 64 \
+    --json-out $O/relevance_fp32_b64_x6$x.json > $O/relevance_fp32_b64_x6$x.log 2>&1 \
+    || { echo "relevance bench failed"; tail -20 $O/relevance_fp32_b64_x6$x.log; exit 1; }
+  echo "x6=$x $(tail -1 $O/relevance_fp32_b64_x6$x.log)"
+done
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/lrp_prof -o run -- \
   python3 $R/tools/relevance_bench.py --dtype fp32 --batch 64 --iters 3 --warmup 1 > $R/$O/lrp_prof.log 2>&1 \

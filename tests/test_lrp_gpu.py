@@ -100,9 +100,47 @@ def test_relevance_engine_gpu_vs_cpu(cfg):
     assert rel_err(wg / wg.sum(-1, keepdim=True), wc / wc.sum(-1, keepdim=True)) < 0.04
 
 
+@pytest.mark.parametrize("x6", [1, 0])
 @pytest.mark.parametrize("B,Hq,Hkv,S", [(2, 14, 2, 512), (1, 8, 8, 200), (3, 4, 2, 96), (1, 2, 1, 37)])
-def test_lrp_attn_bwd_f32(B, Hq, Hkv, S):
-    """fp32 attention LRP backward (fp32 matrix cores) vs the fp32 reference: fp32-rounding agreement."""
+def test_lrp_attn_bwd_f32(B, Hq, Hkv, S, x6):
+    """fp32 attention LRP backward vs the fp64 reference: fp32-rounding agreement for both sweeps - the bf16
+    matrix-core split (x6 = 1, three bf16 planes, six products; the default) and the f32 MFMA (x6 = 0)."""
+    ops.set_lrp_attn_x6(x6)
+    try:
+        _lrp_attn_bwd_f32_case(B, Hq, Hkv, S)
+    finally:
+        ops.set_lrp_attn_x6(1)
+
+
+def test_lrp_attn_bwd_x6_dynamic_range():
+    """Gradients have no a-priori bound.  The bf16 planes carry fp32's exponent range (no scales), so every output is
+    exactly equivariant under a power-of-two scaling of dO (2^-40 and 2^+40: bit-identical after unscaling), and rows
+    of dO spread over 24 binades keep the fp32-level error of the unit-scale case."""
+    B, Hq, Hkv, S = 1, 4, 2, 160
+    f = torch.float32
+    q = rnd(B, Hq, S, 64, s=0.5, seed=11, dtype=f) * 0.125
+    k = rnd(B, Hkv, S, 64, s=0.5, seed=12, dtype=f)
+    v = rnd(B, Hkv, S, 64, seed=13, dtype=f)
+    dO = rnd(B * S, Hq * 64, seed=14, dtype=f)
+    vt = torch.zeros(B, Hkv, 64, R.s_pad(S), dtype=f)
+    vt[..., :S] = v.transpose(-1, -2)
+    o, lse = R.attention(q, k, vt, S, need_lse=True)
+    dev = [t.to(DEV) for t in (q, k, v, o)]
+    lse_d = lse.float().contiguous().to(DEV)
+    base = ops.lrp_attn_bwd(*dev, dO.to(DEV), lse_d)
+    for e in (-40, 40):
+        got = ops.lrp_attn_bwd(*dev, (dO * 2.0 ** e).to(DEV), lse_d)
+        for n, g_, b_ in zip(["D", "rel", "dq", "dk", "dv"], got, base):
+            assert torch.equal(g_ * 2.0 ** -e, b_), f"{n}: not equivariant under dO x 2^{e}"
+    # mixed magnitudes: dO rows over 2^-40 .. 2^40; the error measured against fp64 on the global scale
+    dOm = dO * (2.0 ** torch.linspace(-40, 40, B * S).round()).view(-1, 1)
+    ref = R.lrp_attn_bwd(q.double(), k.double(), v.double(), o.double(), dOm.double(), lse.double())
+    got = ops.lrp_attn_bwd(*dev, dOm.to(DEV), lse_d)
+    for n, g_, r_ in zip(["D", "rel", "dq", "dk", "dv"], got, ref):
+        assert rel_err(g_, r_) < 2e-6, n
+
+
+def _lrp_attn_bwd_f32_case(B, Hq, Hkv, S):
     f = torch.float32
     q = rnd(B, Hq, S, 64, s=0.5, seed=1, dtype=f) * 0.125
     k = rnd(B, Hkv, S, 64, s=0.5, seed=2, dtype=f)
