@@ -28,11 +28,15 @@ enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_G
        // outputs, fp32 bias / residual, h3-layout outputs for epilogues whose result feeds the next GEMM, or the LM
        // head's LSE partials
        EPI_F32 = 8, EPI_F32_BIAS = 9, EPI_F32_RESID = 10, EPI_F32_BIAS_RESID = 11, EPI_H3_BIAS_GELU = 12,
-       EPI_H3_SWIGLU = 13, EPI_F32_QKV_ROPE = 14, EPI_F32_LSE = 15 };
+       EPI_H3_SWIGLU = 13, EPI_F32_QKV_ROPE = 14, EPI_F32_LSE = 15,
+       // fp32 output = colscale[n] * product + fp32 residual: the relevance engine's input gradients through a
+       // projection whose RMSNorm weight is applied on the output columns (the transposed weight then stays exact in
+       // fp16: two products instead of three)
+       EPI_F32_RESID_CS = 16 };
 constexpr bool epi_f32(int e) { return e >= EPI_F32; }
 constexpr bool epi_plain(int e) {  // none / bias / residual epilogues (the 256x224 kernel's set)
   return e == EPI_NONE || e == EPI_BIAS || e == EPI_RESID || e == EPI_BIAS_RESID || e == EPI_F32 ||
-         e == EPI_F32_BIAS || e == EPI_F32_RESID || e == EPI_F32_BIAS_RESID;
+         e == EPI_F32_BIAS || e == EPI_F32_RESID || e == EPI_F32_BIAS_RESID || e == EPI_F32_RESID_CS;
 }
 
 struct GemmArgs {
@@ -56,6 +60,7 @@ struct GemmArgs {
   // pre-folded into B) and producer side (per-row sum of squares of the stored bf16 outputs, one
   // partial per 64-column slab: ssq_out[m, n/64])
   const float* rscale; float* ssq_out;
+  const float* colscale;   // EPI_F32_RESID_CS: per-output-column factor of the product
   // consumer side without a row_rscale launch (QKV): rscale[m] computed at tile start from the producer's
   // partials, rsqrt(sum_p ssq_in[m, p] * norm_inv_k + norm_eps); takes precedence over rscale
   const float* ssq_in; int ssq_parts; float norm_inv_k, norm_eps;
@@ -416,12 +421,17 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
       for (int j = 0; j < 4; ++j) {
         const int n = nw + j * 16 + g * 4;
         float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (EPI == EPI_F32_RESID_CS) {
+          const f32x4_t cw = *(const f32x4_t*)(a.colscale + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] *= cw[r];
+        }
         if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID) {
           const f32x4_t bw = *(const f32x4_t*)(a.biasf + n);
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] += bw[r];
         }
-        if constexpr (EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID) {
+        if constexpr (EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID || EPI == EPI_F32_RESID_CS) {
           const f32x4_t rw = *(const f32x4_t*)(a.residf + (size_t)m * a.ldr + n);
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] += rw[r];
@@ -1592,7 +1602,7 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
   if constexpr (epi_f32(EPI)) {
     // fp32 execution: fp32 bias / residual / output.  Residuals are loaded two row groups at a time (all four
     // would be 112 VGPRs and spill at this kernel's 256-register budget), each pair before that pair's stores.
-    constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID;
+    constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID || EPI == EPI_F32_RESID_CS;
 #pragma unroll
     for (int ih = 0; ih < w7::MI; ih += 2) {
       f32x4_t rv[2][w7::NJ];
@@ -1615,6 +1625,7 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
 #pragma unroll
         for (int j = 0; j < w7::NJ; ++j) {
           f32x4_t o = acc[ih + i][j] * rsm;
+          if constexpr (EPI == EPI_F32_RESID_CS) o *= *(const f32x4_t*)(a.colscale + nw + j * 16 + g * 4);
           if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID)
             o += *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
           if constexpr (RESF) o += rv[i][j];
@@ -1827,15 +1838,20 @@ __device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[
 template <int EPI>
 __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (&acc)[8][7], int m0, int n0,
                                                     int lane, int wm, int wn) {
-  constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID;
+  constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID || EPI == EPI_F32_RESID_CS;
   constexpr bool BIAS = EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID;
+  constexpr bool CS = EPI == EPI_F32_RESID_CS;
   const int g = lane >> 4;
   const int nw = n0 + wn * 112;
   const int rbase = m0 + wm * 128 + (lane & 15);
-  f32x4_t bw[BIAS ? 7 : 1];
+  f32x4_t bw[BIAS || CS ? 7 : 1];   // bias, or the column scales (never both)
   if constexpr (BIAS) {
 #pragma unroll
     for (int j = 0; j < 7; ++j) bw[j] = *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
+  }
+  if constexpr (CS) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) bw[j] = *(const f32x4_t*)(a.colscale + nw + j * 16 + g * 4);
   }
   f32x4_t rv[2][2][RESF ? 7 : 1];
   float rsv[2][2];
@@ -1872,6 +1888,7 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
 #pragma unroll
         for (int j = 0; j < 7; ++j) {
           f32x4_t o = c[i2][j] * rsv[buf][i2];
+          if constexpr (CS) o *= bw[j];
           if constexpr (BIAS) o += bw[j];
           if constexpr (RESF) o += rv[buf][i2][j];
           *(f32x4_t*)(row + j * 16) = o;
@@ -2595,7 +2612,7 @@ static int launch_4w_pb(const GemmArgs& args, hipStream_t st) {
   }
   // (the desync kernels exist for the families the bench runs and its tests cover: h3 two-product GEMMs, the bf16
   // SwiGLU GEMM and the LM-head LSE)
-  constexpr bool ds_ok = PF == 0 && ((epi_f32(EPI) && PB) || EPI == EPI_SWIGLU || EPI == EPI_LSE);
+  constexpr bool ds_ok = PF == 0 && EPI != EPI_F32_RESID_CS && ((epi_f32(EPI) && PB) || EPI == EPI_SWIGLU || EPI == EPI_LSE);
   if (!ds_ok) h = 0;
   a.split_h = h;
   if (!h) a.ws = nullptr, a.ws_floats = 0;
@@ -2939,6 +2956,30 @@ EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, 
   if (bias) return launch<EPI_F32_BIAS>(a, st);
   if (resid) return launch<EPI_F32_RESID>(a, st);
   return launch<EPI_F32>(a, st);
+}
+
+// EPI_F32_RESID_CS: C = colscale[n] * rscale[m] * alpha * (A . B^T) + resid (h3 operands as edge_gemm_f32; C may
+// alias resid).
+EDGE_API int edge_gemm_f32_cs(const void* A, const void* B, float* C, int M, int N, int Kx, int kplane, int lda, int ldb,
+                              int ldc, const float* colscale, const float* resid, int ldr, const float* rscale,
+                              float alpha, hipStream_t st) {
+  GemmArgs a{};
+  a.rscale = rscale;
+  a.colscale = colscale;
+  a.alpha = alpha;
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B;
+  a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.residf = resid; a.ldr = ldr; a.Cf = C;
+  a.h3k = kplane;
+  a.pairb = Kx == 2 * kplane;
+  if (!colscale || !resid || !h3_geometry_ok(Kx, kplane) || lda < 2 * kplane || ldb < (a.pairb ? kplane : Kx) ||
+      !(alpha > 0.f))
+    return (int)hipErrorInvalidValue;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  if (((uintptr_t)C & 15) || ldc % 4 || ldr % 4 || ((uintptr_t)resid & 15) || ((uintptr_t)colscale & 15))
+    return (int)hipErrorInvalidValue;
+  return launch<EPI_F32_RESID_CS>(a, st);
 }
 
 // fp32 QKV projection + bias + RoPE + head-major scatter: X [M, 2K] (h3 activation), W [(Hq+2Hkv)*64, 3K] (h3

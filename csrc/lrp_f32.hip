@@ -319,34 +319,52 @@ __device__ __forceinline__ void split3_frag(const float (&v)[8], bf16x8_t (&p)[3
 // the slot of row r (0..31) of a 32-row block in the permuted k order
 __device__ __forceinline__ int x6_slot(int r) { return r < 16 ? 8 * (r >> 2) + (r & 3) : 8 * ((r - 16) >> 2) + 4 + (r & 3); }
 
-// Stage a 32 x 64 fp32 tile (rows row0.., row stride ld floats; rows >= nrows zero) as three bf16 planes, row-major
-// ([32][64], 16-byte chunks swizzled by x6sw(row): A / B fragments by one ds_read_b128) and, with T, also transposed
-// ([64][32 slots] in the x6_slot order, 64-byte rows: the fragments of a reduction over the tile's rows).
-template <bool T>
-__device__ __forceinline__ void stage_x6(const float* __restrict__ src, size_t ld, int row0, int nrows, char* rm,
-                                         char* tr) {
-  const int t = threadIdx.x, r = t >> 3, c = t & 7;   // row r, 8 columns 8c .. 8c+7
-  const int gr = row0 + r;
-  float v[8];
-  if (gr < nrows) {
-    const f32x4_t a = *(const f32x4_t*)(src + (size_t)gr * ld + 8 * c);
-    const f32x4_t b = *(const f32x4_t*)(src + (size_t)gr * ld + 8 * c + 4);
+// A 32 x 64 fp32 tile staged as three bf16 planes, row-major ([32][64], 16-byte chunks swizzled by x6sw(row): A / B
+// fragments by one ds_read_b128) and, with T, also transposed ([64][32 slots] in the x6_slot order, 64-byte rows: the
+// fragments of a reduction over the tile's rows).  Thread t owns rows 2 (t >> 4) and 2 (t >> 4) + 1, columns
+// 4 (t & 15) .. +3: two 16-byte global loads (x6_load, issued a tile ahead so their latency hides under the previous
+// tile's MFMAs), and the two rows' slots are adjacent, so every transposed write is one 4-byte bf16 pair (x6_store).
+struct X6Regs { f32x4_t v[2]; };
+__device__ __forceinline__ void x6_load(const float* __restrict__ src, size_t ld, int row0, int nrows, X6Regs& R) {
+  const int t = threadIdx.x, r = 2 * (t >> 4), c = 4 * (t & 15);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = a[e], v[4 + e] = b[e];
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  for (int i = 0; i < 2; ++i) {
+    const int gr = row0 + r + i;
+    R.v[i] = gr < nrows ? *(const f32x4_t*)(src + (size_t)gr * ld + c) : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
-  bf16x8_t p[3];
-  split3_frag(v, p);
+}
+template <bool T>
+__device__ __forceinline__ void x6_store(const X6Regs& R, char* rm, char* tr) {
+  const int t = threadIdx.x, r = 2 * (t >> 4), c4 = t & 15;
+  uint32_t w[2][3][2];   // [row][plane][column pair]: packed bf16 pairs
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl) *(bf16x8_t*)(rm + pl * X6P + r * 128 + ((c ^ x6sw(r)) << 4)) = p[pl];
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+      float a0, a1, a2, b0, b1, b2;
+      split3(R.v[i][e], a0, a1, a2);
+      split3(R.v[i][e + 1], b0, b1, b2);
+      w[i][0][e >> 1] = pack_bf2(a0, b0);
+      w[i][1][e >> 1] = pack_bf2(a1, b1);
+      w[i][2][e >> 1] = pack_bf2(a2, b2);
+    }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = r + i;
+    const int off = row * 128 + (((c4 >> 1) ^ x6sw(row)) << 4) + (c4 & 1) * 8;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) *(u32x2_t*)(rm + pl * X6P + off) = u32x2_t{w[i][pl][0], w[i][pl][1]};
+  }
   if constexpr (T) {
-    const int sl = x6_slot(r);
+    const int sl = x6_slot(r);   // rows r, r + 1 -> slots sl, sl + 1
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) *(__bf16*)(tr + pl * X6P + (8 * c + e) * 64 + sl * 2) = p[pl][e];
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t lo = (w[0][pl][e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+        const uint32_t hi = (w[1][pl][e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+        *(uint32_t*)(tr + pl * X6P + (4 * c4 + e) * 64 + sl * 2) = lo | (hi << 16);
+      }
   }
 }
 __device__ __forceinline__ void rm_frags(const char* img, int row, int chunk, bf16x8_t (&f)[3]) {
@@ -399,15 +417,24 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
   const float* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
   const float* lh = lse + ((size_t)b * Hq + h) * S;
   const float* dh = D + ((size_t)b * Hq + h) * S;
-  for (int q0 = kb * 64; q0 < S; q0 += 32) {
-    __syncthreads();
-    stage_x6<true>(qh, 64, q0, S, sQ, sQT);
-    stage_x6<true>(doh, (size_t)Hq * 64, q0, S, sO, sOT);
+  X6Regs rq, ro;
+  float nl = INFINITY, nd = 0.f;
+  auto fetch = [&](int q0) {   // the tile's global values into registers (a tile ahead)
+    x6_load(qh, 64, q0, S, rq);
+    x6_load(doh, (size_t)Hq * 64, q0, S, ro);
     if (tid < 32) {
       const int qi = q0 + tid;
-      sL[tid] = qi < S ? lh[qi] : INFINITY;
-      sD[tid] = qi < S ? dh[qi] : 0.f;
+      nl = qi < S ? lh[qi] : INFINITY;
+      nd = qi < S ? dh[qi] : 0.f;
     }
+  };
+  fetch(kb * 64);
+  for (int q0 = kb * 64; q0 < S; q0 += 32) {
+    __syncthreads();
+    x6_store<true>(rq, sQ, sQT);
+    x6_store<true>(ro, sO, sOT);
+    if (tid < 32) sL[tid] = nl, sD[tid] = nd;
+    if (q0 + 32 < S) fetch(q0 + 32);
     __syncthreads();
     float pv[8], dsv[8];   // k-slot order: j < 4 -> sub-block 0 row 4g + j, j >= 4 -> sub-block 1 row 4g + j - 4
 #pragma unroll
@@ -484,10 +511,17 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
 #pragma unroll
   for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int kend = min(S, qb * 64 + 64);
+  X6Regs rk, rv;
+  x6_load(kh, 64, 0, S, rk);
+  x6_load(vh, 64, 0, S, rv);
   for (int k0 = 0; k0 < kend; k0 += 32) {
     __syncthreads();
-    stage_x6<true>(kh, 64, k0, S, sK, sKT);
-    stage_x6<false>(vh, 64, k0, S, sV, nullptr);
+    x6_store<true>(rk, sK, sKT);
+    x6_store<false>(rv, sV, nullptr);
+    if (k0 + 32 < kend) {   // the next key tile's values under this tile's MFMAs
+      x6_load(kh, 64, k0 + 32, S, rk);
+      x6_load(vh, 64, k0 + 32, S, rv);
+    }
     __syncthreads();
     float dsv[8];
 #pragma unroll

@@ -505,18 +505,22 @@ def split_h3(x: torch.Tensor, s: float, rows: torch.Tensor | None = None) -> tor
 
 
 def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, residual=None, act=None, out=None,
-              rscale=None, out_scale: float = 1.0) -> torch.Tensor:
+              rscale=None, out_scale: float = 1.0, colscale=None) -> torch.Tensor:
     """fp32-accurate ``act(rscale * (x @ w.T) + bias) + residual`` from h3 operands (a3 [M, 2K] the 2-plane
     activation of s_a x, w3 [N, 3K] the h3 weight of w at scale s_w, alpha = 1 / (s_a s_w)).
 
     act None -> fp32 [M, N] (``residual`` fp32, may alias ``out``); act "gelu" / "swiglu_il" -> the activation as
-    the 2-plane h3 activation of ``out_scale`` * act(...) ([M, 2N] / [M, N]) for the next GEMM."""
+    the 2-plane h3 activation of ``out_scale`` * act(...) ([M, 2N] / [M, N]) for the next GEMM.
+    ``colscale`` [N] (with a residual, no bias / act): ``colscale * rscale * (x @ w.T) + residual`` - a norm weight on
+    the output columns instead of folded into w, which then keeps a weight exact in fp16 on two products."""
     M = a3.shape[0]
     N = w3.shape[0]
     if not _gpu(a3):
         y = ref.h3_matmul(a3, w3, alpha)
         if rscale is not None:
             y = y * rscale.float().view(-1, 1)
+        if colscale is not None:
+            y = y * colscale.float().view(1, -1)
         if bias is not None:
             y = y + bias.float()
         if act == "gelu":
@@ -531,7 +535,15 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
             return out
         return y
     kp, Kx = _check_h3(a3, w3, alpha)
-    _check_f32(bias, residual, rscale)
+    _check_f32(bias, residual, rscale, colscale)
+    if colscale is not None:
+        if residual is None or bias is not None or act is not None:
+            raise ValueError("colscale: a residual GEMM without bias / activation")
+        if out is None:
+            out = torch.empty(M, N, dtype=torch.float32, device=a3.device)
+        call("edge_gemm_f32_cs", ptr(a3), ptr(w3), ptr(out), M, N, Kx, kp, a3.stride(0), w3.stride(0), out.stride(0),
+             ptr(colscale), ptr(residual), residual.stride(0), ptr(rscale), float(alpha), stream())
+        return out
     if act is None:
         if out is None:
             out = torch.empty(M, N, dtype=torch.float32, device=a3.device)

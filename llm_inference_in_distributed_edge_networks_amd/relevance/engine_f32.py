@@ -11,7 +11,8 @@ and runs every matrix product at fp32 accuracy on the matrix cores:
   norms' detached row scales, q / k / v / o / LSE and the gate|up (fc) pre-activations;
 * backward per layer, in reverse, with no autograd and no S x S tensor:
   - input-gradient GEMMs on the TRANSPOSED weights, on the same h3 GEMM (weights split once at construction;
-    the RMSNorm weight folded into the QKV / gate|up transposes).  A gradient has no a-priori bound, so every
+    the RMSNorm weights applied on those GEMMs' output columns, so a transpose of bf16-valued weights stays exact in
+    fp16 and runs on two products).  A gradient has no a-priori bound, so every
     GEMM input row is split with its own power-of-two scale (max |row| just under 2^15) and the GEMM's per-row
     epilogue scale multiplies by the exact inverse - times the detached norm's rstd where a norm sits between;
   - the LRP rules that feed a GEMM (SwiGLU / GELU identity + uniform rules, inverse RoPE + GQA sum) write that
@@ -51,8 +52,10 @@ class RelevanceEngineH3:
         for L in model.layers:
             t = {}
             if self.qwen:
-                t["wqkvT3"], t["a_qkvT"] = t3(R.fold_norm_weight(L["wqkv"], L["ln1_w"]))
-                t["wguT3"], t["a_guT"] = t3(R.fold_norm_weight(L["wgu"], L["ln2_w"]))
+                # the RMSNorm weights stay out of the transposes (applied on the GEMMs' output columns, colscale):
+                # the transposes of bf16 / fp16-valued weights are then exact in fp16 - two products, not three
+                t["wqkvT3"], t["a_qkvT"] = t3(L["wqkv"])
+                t["wguT3"], t["a_guT"] = t3(L["wgu"])
                 t["wdT3"], t["a_dT"] = t3(L["wd"])
             else:
                 t["wqkvT3"], t["a_qkvT"] = t3(L["wqkv"])
@@ -141,7 +144,7 @@ class RelevanceEngineH3:
             if self.qwen:
                 dm = ops.linear_h3(dx3, t["wdT3"], t["a_dT"], rscale=rinv)
                 dgu3, rinv_gu = ops.lrp_swiglu_bwd_h3(dm, sv["gu"], post=sv["rs2"])
-                dy = ops.linear_h3(dgu3, t["wguT3"], t["a_guT"], rscale=rinv_gu, residual=dx)
+                dy = ops.linear_h3(dgu3, t["wguT3"], t["a_guT"], rscale=rinv_gu, residual=dx, colscale=L["ln2_w"])
                 dy3, rinv_y = ops.split_h3_dyn(dy)
             else:
                 dp = ops.linear_h3(dx3, t["wprojT3"], t["a_projT"], rscale=rinv)
@@ -154,7 +157,7 @@ class RelevanceEngineH3:
             dqkv3, rinv_q = ops.lrp_rope_pack_h3(dq, dk, dv, m.cos, m.sin, B, S, Hq, Hkv, cfg.rotary_dim, m.q_scale,
                                                  post=sv["rs1"] if self.qwen else None)
             if self.qwen:
-                dx = ops.linear_h3(dqkv3, t["wqkvT3"], t["a_qkvT"], rscale=rinv_q, residual=dy)
+                dx = ops.linear_h3(dqkv3, t["wqkvT3"], t["a_qkvT"], rscale=rinv_q, residual=dy, colscale=L["ln1_w"])
             else:
                 dh1 = ops.linear_h3(dqkv3, t["wqkvT3"], t["a_qkvT"], rscale=rinv_q)
                 dx = ops.lrp_ln_bwd_f32(dh1, sv["rs1"], L["ln1_w"], dh2, L["ln2_w"], dx)

@@ -140,6 +140,23 @@ def test_linear_h3_loose_scale(slack):
     test_linear_h3_fp32_accuracy(2048, 896, 4864, "resid", slack)
 
 
+@pytest.mark.parametrize("M,N,K", [(32768, 896, 9728), (8192, 896, 1152), (300, 896, 896), (2048, 1024, 640)])
+def test_linear_h3_colscale(M, N, K):
+    """colscale[n] * rscale[m] * (x @ w.T) + residual (the relevance engine's norm-weighted input gradients): the
+    four-wave 256x224 kernel (M = 32768), the 128x128 kernel (small M) and the 256-wide generic path, two products
+    (bf16-valued weights), in place on the residual, fp32-level against fp64."""
+    x, w, r = rnd(M, K, seed=40), rnd(N, K, s=0.03, seed=41).bfloat16().float(), rnd(M, N, seed=42)
+    cs, rs = 1 + 0.3 * rnd(N, seed=43), torch.rand(M, generator=torch.Generator().manual_seed(44)) + 0.5
+    sx = R.h3_scale(x.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    rd = r.to(DEV)
+    y = ops.linear_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), residual=rd, out=rd, rscale=rs.to(DEV),
+                      colscale=cs.to(DEV))
+    assert y.data_ptr() == rd.data_ptr()
+    ref = (x.double() @ w.double().t()) * rs.double().view(-1, 1) * cs.double().view(1, -1) + r.double()
+    assert rel_err(y, ref) < 2e-6
+
+
 def test_linear_h3_inplace_residual():
     M, K, N = 32768, 896, 896
     x, w, r = rnd(M, K, seed=20), rnd(N, K, s=0.03, seed=21), rnd(M, N, seed=22)
