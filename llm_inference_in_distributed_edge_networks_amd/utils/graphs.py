@@ -25,8 +25,11 @@ import torch
 # the collection before it
 _TUNE = os.environ.get("EDGE_TUNING", "0") not in ("", "0")
 _GC_OFF_IN_CAPTURE = not (_TUNE and os.environ.get("EDGE_GRAPH_GC_OFF", "1") == "0")
-# A/B (EDGE_TUNING=1 EDGE_GRAPH_GC_COLLECT=0|1): the explicit collection before each capture
-_GC_COLLECT = not (_TUNE and os.environ.get("EDGE_GRAPH_GC_COLLECT", "1") == "0")
+# A/B (EDGE_TUNING=1 EDGE_GRAPH_GC_COLLECT=1): an explicit collection before each capture.  Round 3 added one (with
+# the collector off during the capture, which alone keeps a dropped pipeline's CUDAGraph destructor out of a capture);
+# it cost 2.2 % of the fp32 bench and 3.8 % of the bf16 one, same-box, three interleaved rounds
+# (profiles/r04h/gc_ab_and_lrp.txt: fp32 734.1-734.5 k without vs 717.6-719.4 k with, bf16 1.374-1.378 M vs 1.319-1.338 M).
+_GC_COLLECT = _TUNE and os.environ.get("EDGE_GRAPH_GC_COLLECT", "0") == "1"
 
 
 _PRERUN = False
@@ -88,7 +91,8 @@ class GraphCache:
         # group's watchdog thread keeps querying its events while a stage captures; in the default "global" mode such
         # a query from another thread aborts the capture.
         # No garbage collection while capturing: a cycle collected mid-capture can hold a dropped CUDAGraph (e.g. of
-        # a pipeline rebuilt for another codec), and its destructor is not permitted while a stream captures.
+        # a pipeline rebuilt for another codec), and its destructor is not permitted while a stream captures.  (No
+        # collection forced before it either: measured slower, see _GC_COLLECT.)
         if _GC_COLLECT:
             gc.collect()
         was = gc.isenabled()

@@ -154,7 +154,7 @@ def test_linear_h3_colscale(M, N, K):
                       colscale=cs.to(DEV))
     assert y.data_ptr() == rd.data_ptr()
     ref = (x.double() @ w.double().t()) * rs.double().view(-1, 1) * cs.double().view(1, -1) + r.double()
-    assert rel_err(y, ref) < 2e-6
+    assert rel_err(y, ref) < 4e-6     # fp32 level at K up to 9728 (a CPU fp32 GEMM: ~2e-6 there)
 
 
 def test_linear_h3_inplace_residual():
