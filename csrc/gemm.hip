@@ -84,6 +84,8 @@ struct GemmArgs {
   long long ws_floats = 0;  // size of ws (floats): workgroups whose park area does not fit run the plain walk
   int split_h = 0;
   int* err = nullptr;       // checked builds (EDGE_GEMM_CHECKS): set to a nonzero code when a bounds check fails
+  float* raw = nullptr;     // EPI_H3_SWIGLU, optional: the scaled pre-activations (gate|up interleaved) as fp32 [M, N]
+                            // too, bit-identical to EPI_F32 (the AttnLRP forward saves them for the SwiGLU rule)
 };
 
 #ifndef EDGE_GEMM_CHECKS
@@ -200,6 +202,16 @@ __device__ __forceinline__ void swiglu_h3_rowgroup(const GemmArgs& a, const f32x
   L = pair_swap16(lw[0], lw[1]);
 }
 
+// GemmArgs::raw: the 16-column groups acc4[0..3] of row m (columns n + 16 j + 4g .. + 3) times the product scale f,
+// the values EPI_F32 stores.
+__device__ __forceinline__ void swiglu_raw_store(const GemmArgs& a, const f32x4_t (&acc4)[4], float f, int m, int n,
+                                                 int g) {
+  if (m >= a.M) return;
+  float* dst = a.raw + (size_t)m * a.N + n + 4 * g;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) *(f32x4_t*)(dst + 16 * j) = acc4[j] * f;
+}
+
 // Exchange of two 16-byte chunks between lanes r and r ^ 8 of each 16-lane row (DPP row_ror:8): lanes r < 8 keep X
 // and get the X of lane r + 8 in B; lanes r >= 8 get the Y of lane r - 8 in A and keep Y in B.  For X / Y = the
 // chunks of row r in the left / right 64-byte half of a 128-byte line, A then holds rows 0-7 and B rows 8-15 of the
@@ -235,6 +247,11 @@ __device__ __forceinline__ void swiglu_h3_lines_4w(const GemmArgs& a, f32x4_t (&
       asm volatile("" : "+v"(c0[j]), "+v"(c1[j]));
     }
     const float f = rs[i] * a.alpha;
+    if (a.raw) {
+      const int m = m0 + wm * 128 + i * 16 + r;
+      swiglu_raw_store(a, c0, f, m, n0 + wn * 128, g);
+      swiglu_raw_store(a, c1, f, m, n0 + wn * 128 + 64, g);
+    }
     u32x4_t H0, L0, H1, L1;
     swiglu_h3_rowgroup(a, c0, f, H0, L0);
     swiglu_h3_rowgroup(a, c1, f, H1, L1);
@@ -378,6 +395,7 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
     const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
     if constexpr (EPI == EPI_H3_SWIGLU) {
       u32x4_t H, Lw;
+      if (a.raw) swiglu_raw_store(a, acc[i], rs[i] * a.alpha, m, nw, g);
       swiglu_h3_rowgroup(a, acc[i], rs[i] * a.alpha, H, Lw);
 #if EDGE_TUNING_BUILD
       if (a.skip_epi == 2) {   // timing ablation: epilogue computed, not stored (wrong results)
@@ -2956,6 +2974,29 @@ EDGE_API int edge_gemm_f32(const void* A, const void* B, void* C, int M, int N, 
   if (bias) return launch<EPI_F32_BIAS>(a, st);
   if (resid) return launch<EPI_F32_RESID>(a, st);
   return launch<EPI_F32>(a, st);
+}
+
+// EPI_H3_SWIGLU that also stores the scaled pre-activations: raw = rscale[m] * alpha * (A . B^T) as fp32 [M, N]
+// (what edge_gemm_f32 with act 0 returns, bit for bit) next to the SwiGLU h3 planes in C (as edge_gemm_f32 act 2).
+EDGE_API int edge_gemm_f32_swiglu_raw(const void* A, const void* B, void* C, float* raw, int M, int N, int Kx,
+                                      int kplane, int lda, int ldb, int ldc, const float* rscale, float alpha,
+                                      float out_scale, hipStream_t st) {
+  if (!raw || ((uintptr_t)raw & 15) || N % 16) return (int)hipErrorInvalidValue;
+  GemmArgs a{};
+  a.rscale = rscale;
+  a.alpha = alpha; a.out_scale = out_scale;
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B;
+  a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.h3k = kplane;
+  a.pairb = Kx == 2 * kplane;
+  if (!h3_geometry_ok(Kx, kplane) || lda < 2 * kplane || ldb < (a.pairb ? kplane : Kx) || !(alpha > 0.f) ||
+      !(out_scale > 0.f) || ldc != 2 * (N / 2) || ((uintptr_t)C & 15))
+    return (int)hipErrorInvalidValue;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  a.C = (bf16_t*)C;
+  a.raw = raw;
+  return launch<EPI_H3_SWIGLU>(a, st);
 }
 
 // EPI_F32_RESID_CS: C = colscale[n] * rscale[m] * alpha * (A . B^T) + resid (h3 operands as edge_gemm_f32; C may

@@ -561,6 +561,28 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
     return out
 
 
+def linear_h3_swiglu_raw(a3: torch.Tensor, w3: torch.Tensor, alpha: float, out_scale: float, rscale=None):
+    """``linear_h3(..., act="swiglu_il", out_scale)`` that also returns the fp32 pre-activations
+    ``rscale * (x @ w.T)`` (interleaved gate|up [M, N], bit-identical to ``linear_h3`` without ``act``) from the same
+    GEMM: the SwiGLU planes and the saved pre-activations of the AttnLRP forward in one pass, instead of an fp32 GEMM
+    plus an ``act_h3`` pass re-reading its output -> (planes [M, N], pre-activations [M, N])."""
+    M, N = a3.shape[0], w3.shape[0]
+    if not _gpu(a3):
+        y = ref.h3_matmul(a3, w3, alpha)
+        if rscale is not None:
+            y = y * rscale.float().view(-1, 1)
+        g, u = ref.deinterleave_gate_up(y)
+        return ref.h3_act(torch.nn.functional.silu(g) * u, out_scale), y
+    kp, Kx = _check_h3(a3, w3, alpha)
+    _check_f32(rscale)
+    planes = torch.empty(M, N, dtype=torch.float16, device=a3.device)
+    raw = torch.empty(M, N, dtype=torch.float32, device=a3.device)
+    _gemm_ws(a3.device)
+    call("edge_gemm_f32_swiglu_raw", ptr(a3), ptr(w3), ptr(planes), ptr(raw), M, N, Kx, kp, a3.stride(0),
+         w3.stride(0), N, ptr(rscale), float(alpha), float(out_scale), stream())
+    return planes, raw
+
+
 def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, kv_scales=None, need_k=True):
     """fp32 fused QKV projection + bias + RoPE + head-major scatter from h3 operands -> fp32 (q, k, vt).
 

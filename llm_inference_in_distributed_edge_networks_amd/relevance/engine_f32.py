@@ -90,9 +90,10 @@ class RelevanceEngineH3:
             if self.qwen:
                 y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], residual=x)
                 sv["rs2"] = ops.row_rstd(y, eps)
-                gu = ops.linear_h3(ops.rmsnorm(y, L["ln2_w"], eps, h3=sc["mlp"]), L["wgu3"], sc["a_wgu"])
-                sv["gu"] = gu
-                x = ops.linear_h3(ops.act_h3(gu, "swiglu_il", sc["down"]), L["wd3"], sc["a_wd"], residual=y)
+                # one GEMM: the SwiGLU planes for the down projection and the saved pre-activations for its rule
+                a3, sv["gu"] = ops.linear_h3_swiglu_raw(ops.rmsnorm(y, L["ln2_w"], eps, h3=sc["mlp"]), L["wgu3"],
+                                                        sc["a_wgu"], sc["down"])
+                x = ops.linear_h3(a3, L["wd3"], sc["a_wd"], residual=y)
             else:
                 y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], L["bo"], residual=x)
                 a = ops.linear_h3(h23, L["wfc3"], sc["a_wfc"], L["bfc"])

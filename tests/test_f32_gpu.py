@@ -157,6 +157,25 @@ def test_linear_h3_colscale(M, N, K):
     assert rel_err(y, ref) < 4e-6     # fp32 level at K up to 9728 (a CPU fp32 GEMM: ~2e-6 there)
 
 
+@pytest.mark.parametrize("M,two_term", [(32768, True), (32768, False), (1000, True), (257, False)])
+def test_linear_h3_swiglu_raw(M, two_term):
+    """One GEMM for the SwiGLU planes and the saved pre-activations (AttnLRP forward): the planes bit-identical to
+    act="swiglu_il" and the pre-activations bit-identical to the plain fp32 GEMM - four-wave 256x256 (M = 32768),
+    the small-M kernels and partial row tiles, two and three products."""
+    K, N = 896, 2 * 4864
+    x, w = rnd(M, K, seed=50), rnd(N, K, s=0.03, seed=51)
+    if two_term:
+        w = w.bfloat16().float()
+    sx = R.h3_scale(x.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    a3, w3 = R.h3_act(x, sx).to(DEV), w3.to(DEV)
+    rs = (torch.rand(M, generator=torch.Generator().manual_seed(52)) + 0.5).to(DEV)
+    al = 1.0 / (sx * sw)
+    planes, raw = ops.linear_h3_swiglu_raw(a3, w3, al, 64.0, rscale=rs)
+    assert torch.equal(planes, ops.linear_h3(a3, w3, al, act="swiglu_il", out_scale=64.0, rscale=rs))
+    assert torch.equal(raw, ops.linear_h3(a3, w3, al, rscale=rs))
+
+
 def test_linear_h3_inplace_residual():
     M, K, N = 32768, 896, 896
     x, w, r = rnd(M, K, seed=20), rnd(N, K, s=0.03, seed=21), rnd(M, N, seed=22)
