@@ -321,12 +321,25 @@ __device__ __forceinline__ int x6_slot(int r) { return r < 16 ? 8 * (r >> 2) + (
 
 // A 32 x 64 fp32 tile staged as three bf16 planes, row-major ([32][64], 16-byte chunks swizzled by x6sw(row): A / B
 // fragments by one ds_read_b128) and, with T, also transposed ([64][32 slots] in the x6_slot order, 64-byte rows: the
-// fragments of a reduction over the tile's rows).  Thread t owns rows 2 (t >> 4) and 2 (t >> 4) + 1, columns
-// 4 (t & 15) .. +3: two 16-byte global loads (x6_load, issued a tile ahead so their latency hides under the previous
-// tile's MFMAs), and the two rows' slots are adjacent, so every transposed write is one 4-byte bf16 pair (x6_store).
+// fragments of a reduction over the tile's rows).  Thread t owns the row pair 2 rp, 2 rp + 1 and columns 4 c4 .. +3
+// (x6_own): two 16-byte global loads (x6_load, issued a tile ahead so their latency hides under the previous tile's
+// MFMAs), and the two rows' slots are adjacent, so every transposed write is one 4-byte bf16 pair (x6_store).
+// Bank conflicts (MI355X_MICROARCH §LDS): the transposed writes of a 32-lane half go to rows d = 4 c4 + e, all of one
+// parity, i.e. to 16 of the 32 write banks.  The ownership puts row pairs {a, a + 1, a + 8, a + 9} in every half, whose
+// slots fill all four dwords of a 16-byte chunk, and the chunk of row d is XOR-swizzled by x6tsw(d): the writes are
+// then 2-way (free on ds_write_b32) and the transposed ds_read_b128 conflict-free (the first layout, 16 c4 x 2 row
+// pairs per half and no swizzle, was 16-way on every transposed write).
 struct X6Regs { f32x4_t v[2]; };
+__device__ __forceinline__ int x6tsw(int d) { return ((d >> 2) & 1) | ((((d >> 2) ^ (d >> 3)) & 1) << 1); }
+__device__ __forceinline__ void x6_own(int t, int& r, int& c4) {
+  const int w = t >> 6, l = t & 63, q = (l >> 3) & 3;
+  r = 2 * (2 * w + (q & 1) + 8 * (q >> 1));
+  c4 = (l & 7) + 8 * (l >> 5);
+}
 __device__ __forceinline__ void x6_load(const float* __restrict__ src, size_t ld, int row0, int nrows, X6Regs& R) {
-  const int t = threadIdx.x, r = 2 * (t >> 4), c = 4 * (t & 15);
+  int r, c4;
+  x6_own(threadIdx.x, r, c4);
+  const int c = 4 * c4;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int gr = row0 + r + i;
@@ -335,7 +348,8 @@ __device__ __forceinline__ void x6_load(const float* __restrict__ src, size_t ld
 }
 template <bool T>
 __device__ __forceinline__ void x6_store(const X6Regs& R, char* rm, char* tr) {
-  const int t = threadIdx.x, r = 2 * (t >> 4), c4 = t & 15;
+  int r, c4;
+  x6_own(threadIdx.x, r, c4);
   uint32_t w[2][3][2];   // [row][plane][column pair]: packed bf16 pairs
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -363,7 +377,8 @@ __device__ __forceinline__ void x6_store(const X6Regs& R, char* rm, char* tr) {
       for (int e = 0; e < 4; ++e) {
         const uint32_t lo = (w[0][pl][e >> 1] >> ((e & 1) * 16)) & 0xffffu;
         const uint32_t hi = (w[1][pl][e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-        *(uint32_t*)(tr + pl * X6P + (4 * c4 + e) * 64 + sl * 2) = lo | (hi << 16);
+        const int d = 4 * c4 + e;
+        *(uint32_t*)(tr + pl * X6P + d * 64 + ((((sl >> 3) ^ x6tsw(d))) << 4) + (sl & 7) * 2) = lo | (hi << 16);
       }
   }
 }
@@ -373,7 +388,7 @@ __device__ __forceinline__ void rm_frags(const char* img, int row, int chunk, bf
 }
 __device__ __forceinline__ void tr_frags(const char* img, int row, int g, bf16x8_t (&f)[3]) {
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * X6P + row * 64 + g * 16);
+  for (int pl = 0; pl < 3; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * X6P + row * 64 + ((g ^ x6tsw(row)) << 4));
 }
 // the lane's 8 values of row `row` (its key / query), columns 8 kg + 32 ks .. +7, split into planes
 __device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8_t (&f)[2][3], int g) {
@@ -389,12 +404,11 @@ __device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8
 }
 }  // namespace
 
-// dK, dV partials per q head (inputs and outputs as lrp_attn_dkdv_f32_kernel).  Workgroup = (b, q head, 128-key
-// block), heaviest first; wave w owns the two 16-key groups kb 128 + 32 w + 16 kg + cl (kg = 0, 1): every staged
-// fragment feeds both groups, so a 32-query tile's staging and LDS reads are spread over 192 MFMAs per wave.  Per
-// tile: S = Q K^T and dA = dO V^T with the query on the C rows (the lane's K / V planes in registers for the whole
-// sweep), P = exp(S - lse), dS = P (dA/2 - D), then dV += P^T dO and dK += dS^T Q over the tile's 32 queries (P / dS
-// the lane's A fragments, dO / Q from the transposed images).
+// dK, dV partials per q head (inputs and outputs as lrp_attn_dkdv_f32_kernel).  Workgroup = (b, q head, 64-key
+// block), heaviest first; wave w owns keys kb 64 + 16 w + cl.  Per 32-query tile: S = Q K^T and dA = dO V^T with the
+// query on the C rows (the lane's K / V planes in registers for the whole sweep), P = exp(S - lse), dS = P (dA/2 - D),
+// then dV += P^T dO and dK += dS^T Q over the tile's 32 queries (P / dS the lane's A fragments, dO / Q from the
+// transposed images).
 __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                                const float* __restrict__ v,
                                                                const float* __restrict__ dO,
@@ -406,20 +420,14 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int kb = blockIdx.x / (B * Hq);
   const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
-  int key[2];
-  bf16x8_t kf[2][2][3], vf[2][2][3];
+  const int key = kb * 64 + wave * 16 + cl;
+  const int keyc = key < S ? key : S - 1;
+  bf16x8_t kf[2][3], vf[2][3];
+  row_frags(k + (((size_t)b * Hkv + hk) * S + keyc) * 64, kf, g);
+  row_frags(v + (((size_t)b * Hkv + hk) * S + keyc) * 64, vf, g);
+  f32x4_t dka[4], dva[4];
 #pragma unroll
-  for (int kg = 0; kg < 2; ++kg) {
-    key[kg] = kb * 128 + wave * 32 + kg * 16 + cl;
-    const int keyc = key[kg] < S ? key[kg] : S - 1;
-    row_frags(k + (((size_t)b * Hkv + hk) * S + keyc) * 64, kf[kg], g);
-    row_frags(v + (((size_t)b * Hkv + hk) * S + keyc) * 64, vf[kg], g);
-  }
-  f32x4_t dka[2][4], dva[2][4];
-#pragma unroll
-  for (int kg = 0; kg < 2; ++kg)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) dka[kg][d] = dva[kg][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const float* qh = q + ((size_t)b * Hq + h) * S * 64;
   const float* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
   const float* lh = lse + ((size_t)b * Hq + h) * S;
@@ -435,82 +443,66 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
       nd = qi < S ? dh[qi] : 0.f;
     }
   };
-  fetch(kb * 128);
-  for (int q0 = kb * 128; q0 < S; q0 += 32) {
+  fetch(kb * 64);
+  for (int q0 = kb * 64; q0 < S; q0 += 32) {
     __syncthreads();
     x6_store<true>(rq, sQ, sQT);
     x6_store<true>(ro, sO, sOT);
     if (tid < 32) sL[tid] = nl, sD[tid] = nd;
     if (q0 + 32 < S) fetch(q0 + 32);
     __syncthreads();
-    // k-slot order of P / dS: j < 4 -> sub-block 0 row 4g + j, j >= 4 -> sub-block 1 row 4g + j - 4
-    float pv[2][8], dsv[2][8];
+    float pv[8], dsv[8];   // k-slot order: j < 4 -> sub-block 0 row 4g + j, j >= 4 -> sub-block 1 row 4g + j - 4
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      f32x4_t sc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, da[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t qa[3], oa[3];
         rm_frags(sQ, sub * 16 + cl, 4 * ks + g, qa);
         rm_frags(sO, sub * 16 + cl, 4 * ks + g, oa);
-#pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
-          sc[kg] = x6dot(qa, kf[kg][ks], sc[kg]);
-          da[kg] = x6dot(oa, vf[kg][ks], da[kg]);
-        }
+        sc = x6dot(qa, kf[ks], sc);
+        da = x6dot(oa, vf[ks], da);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = sub * 16 + 4 * g + r, qi = q0 + ql;
-#pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
-          const bool ok = qi < S && key[kg] <= qi && key[kg] < S;
-          const float pr = ok ? expf(sc[kg][r] - sL[ql]) : 0.f;
-          pv[kg][4 * sub + r] = pr;
-          dsv[kg][4 * sub + r] = pr * (0.5f * da[kg][r] - sD[ql]);
-        }
+        const bool ok = qi < S && key <= qi && key < S;
+        const float pr = ok ? expf(sc[r] - sL[ql]) : 0.f;
+        pv[4 * sub + r] = pr;
+        dsv[4 * sub + r] = pr * (0.5f * da[r] - sD[ql]);
       }
     }
-    bf16x8_t pf[2][3], dsf[2][3];
-#pragma unroll
-    for (int kg = 0; kg < 2; ++kg) {
-      split3_frag(pv[kg], pf[kg]);
-      split3_frag(dsv[kg], dsf[kg]);
-    }
+    bf16x8_t pf[3], dsf[3];
+    split3_frag(pv, pf);
+    split3_frag(dsv, dsf);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x8_t ob[3], qb[3];
       tr_frags(sOT, dt * 16 + cl, g, ob);
       tr_frags(sQT, dt * 16 + cl, g, qb);
-#pragma unroll
-      for (int kg = 0; kg < 2; ++kg) {
-        dva[kg][dt] = x6dot(pf[kg], ob, dva[kg][dt]);
-        dka[kg][dt] = x6dot(dsf[kg], qb, dka[kg][dt]);
-      }
+      dva[dt] = x6dot(pf, ob, dva[dt]);
+      dka[dt] = x6dot(dsf, qb, dka[dt]);
     }
   }
-  // C[row = key 32w + 16kg + 4g + r][col = d 16dt + cl]
+  // C[row = key 16w + 4g + r][col = d 16dt + cl]
   float* dkh = dk + ((size_t)b * Hq + h) * S * 64;
   float* dvh = dv + ((size_t)b * Hq + h) * S * 64;
 #pragma unroll
-  for (int kg = 0; kg < 2; ++kg)
+  for (int r = 0; r < 4; ++r) {
+    const int kr = kb * 64 + wave * 16 + g * 4 + r;
+    if (kr < S) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int kr = kb * 128 + wave * 32 + kg * 16 + g * 4 + r;
-      if (kr < S) {
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          dkh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dka[kg][dt][r];
-          dvh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dva[kg][dt][r];
-        }
+      for (int dt = 0; dt < 4; ++dt) {
+        dkh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dka[dt][r];
+        dvh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dva[dt][r];
       }
     }
+  }
 }
 
-// dQ (inputs and output as lrp_attn_dq_f32_kernel).  Workgroup = (b, h, 128-query block), heaviest (last) first;
-// wave w owns the two 16-query groups qb 128 + 32 w + 16 qg + cl.  Per 32-key tile: S^T = K Q^T and dA^T = V dO^T
-// with the key on the C rows (the lane's Q / dO planes in registers), dS^T = P^T (dA^T/2 - D), then
-// dQ^T += K^T dS^T over the tile's 32 keys; every staged K / V / K^T fragment feeds both query groups.
+// dQ (inputs and output as lrp_attn_dq_f32_kernel).  Workgroup = (b, h, 64-query block), heaviest (last) first; wave
+// w owns queries qb 64 + 16 w + cl.  Per 32-key tile: S^T = K Q^T and dA^T = V dO^T with the key on the C rows (the
+// lane's Q / dO planes in registers), dS^T = P^T (dA^T/2 - D), then dQ^T += K^T dS^T over the tile's 32 keys.
 __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                              const float* __restrict__ v, const float* __restrict__ dO,
                                                              const float* __restrict__ lse,
@@ -518,29 +510,22 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
                                                              int B, int Hq, int Hkv, int S) {
   __shared__ __attribute__((aligned(16))) char sK[3 * X6P], sV[3 * X6P], sKT[3 * X6P];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int nqb = (S + 127) / 128;
+  const int nqb = (S + 63) / 64;
   const int qb = nqb - 1 - blockIdx.x / (B * Hq);
   const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
-  int qi[2];
-  float lq[2], dq_[2];
-  bf16x8_t qf[2][2][3], of[2][2][3];
-#pragma unroll
-  for (int qg = 0; qg < 2; ++qg) {
-    qi[qg] = qb * 128 + wave * 32 + qg * 16 + cl;
-    const int qic = qi[qg] < S ? qi[qg] : S - 1;
-    row_frags(q + (((size_t)b * Hq + h) * S + qic) * 64, qf[qg], g);
-    row_frags(dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64, of[qg], g);
-    lq[qg] = lse[((size_t)b * Hq + h) * S + qic];
-    dq_[qg] = D[((size_t)b * Hq + h) * S + qic];
-  }
+  const int qi = qb * 64 + wave * 16 + cl;
+  const int qic = qi < S ? qi : S - 1;
+  bf16x8_t qf[2][3], of[2][3];
+  row_frags(q + (((size_t)b * Hq + h) * S + qic) * 64, qf, g);
+  row_frags(dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64, of, g);
+  const float lq = lse[((size_t)b * Hq + h) * S + qic];
+  const float dq_ = D[((size_t)b * Hq + h) * S + qic];
   const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
   const float* vh = v + ((size_t)b * Hkv + hk) * S * 64;
-  f32x4_t acc[2][4];
+  f32x4_t acc[4];
 #pragma unroll
-  for (int qg = 0; qg < 2; ++qg)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) acc[qg][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int kend = min(S, qb * 128 + 128);
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int kend = min(S, qb * 64 + 64);
   X6Regs rk, rv;
   x6_load(kh, 64, 0, S, rk);
   x6_load(vh, 64, 0, S, rv);
@@ -553,51 +538,40 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
       x6_load(vh, 64, k0 + 32, S, rv);
     }
     __syncthreads();
-    float dsv[2][8];
+    float dsv[8];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      f32x4_t sc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, da[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t ka[3], va[3];
         rm_frags(sK, sub * 16 + cl, 4 * ks + g, ka);
         rm_frags(sV, sub * 16 + cl, 4 * ks + g, va);
-#pragma unroll
-        for (int qg = 0; qg < 2; ++qg) {
-          sc[qg] = x6dot(ka, qf[qg][ks], sc[qg]);
-          da[qg] = x6dot(va, of[qg][ks], da[qg]);
-        }
+        sc = x6dot(ka, qf[ks], sc);
+        da = x6dot(va, of[ks], da);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kj = k0 + sub * 16 + 4 * g + r;
-#pragma unroll
-        for (int qg = 0; qg < 2; ++qg) {
-          const bool ok = qi[qg] < S && kj <= qi[qg];
-          const float pr = ok ? expf(sc[qg][r] - lq[qg]) : 0.f;
-          dsv[qg][4 * sub + r] = pr * (0.5f * da[qg][r] - dq_[qg]);
-        }
+        const bool ok = qi < S && kj <= qi;
+        const float pr = ok ? expf(sc[r] - lq) : 0.f;
+        dsv[4 * sub + r] = pr * (0.5f * da[r] - dq_);
       }
     }
-    bf16x8_t dsf[2][3];
-#pragma unroll
-    for (int qg = 0; qg < 2; ++qg) split3_frag(dsv[qg], dsf[qg]);
+    bf16x8_t dsf[3];
+    split3_frag(dsv, dsf);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x8_t kt[3];
       tr_frags(sKT, dt * 16 + cl, g, kt);
-#pragma unroll
-      for (int qg = 0; qg < 2; ++qg) acc[qg][dt] = x6dot(kt, dsf[qg], acc[qg][dt]);
+      acc[dt] = x6dot(kt, dsf, acc[dt]);
     }
   }
-  // acc[qg][dt][r] = dQ^T[d = 16dt + 4g + r][query qi[qg]]
+  // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
+  if (qi < S) {
+    float* o = dq + (((size_t)b * Hq + h) * S + qi) * 64;
 #pragma unroll
-  for (int qg = 0; qg < 2; ++qg) {
-    if (qi[qg] < S) {
-      float* o = dq + (((size_t)b * Hq + h) * S + qi[qg]) * 64;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = 0.5f * acc[qg][dt];
-    }
+    for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = 0.5f * acc[dt];
   }
 }
 
@@ -939,9 +913,8 @@ EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* 
   const int nb = (S + 63) / 64;
   lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
   if (g_lrp_attn_x6) {
-    const int nb2 = (S + 127) / 128;   // 128-key / 128-query workgroups (two 16-row groups per wave)
-    lrp_attn_dkdv_x6_kernel<<<B * Hq * nb2, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-    lrp_attn_dq_x6_kernel<<<B * Hq * nb2, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+    lrp_attn_dkdv_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+    lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
   } else {
     lrp_attn_dkdv_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
     lrp_attn_dq_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);

@@ -96,6 +96,17 @@ def with_plan(spec: CodecSpec, plan) -> CodecSpec:
     return replace(spec, plan=plan)
 
 
+def boundary_group_relevance(table, boundary: int, groups: int) -> list:
+    """The channel-group relevance of the tensor crossing the boundary after layer ``boundary`` from a
+    [layers][groups] table of the relevance ENTERING each layer (``channel_group_relevance.json``): row
+    ``boundary + 1``.  After the last layer the tensor is the final norm's input, which the table does not hold;
+    its last row (the stream entering the last layer) stands in.  No table: every group equal."""
+    if table is None:
+        return [1.0] * groups
+    t = torch.as_tensor(table, dtype=torch.float32)
+    return [float(v) for v in t[min(boundary + 1, t.shape[0] - 1)]]
+
+
 def allocate_group_bits(relevance, avg_bits: float = 4.0) -> tuple:
     """Relevance-driven bit allocation over the 64-channel groups of a boundary.
 

@@ -166,8 +166,7 @@ class SweepEngine:
         if not C.wire.needs_plan(spec):
             return spec
         G = self.m.cfg.hidden_size // C.wire.GROUP
-        rel = [1.0] * G if self.sc.group_relevance is None else \
-            [float(v) for v in torch.as_tensor(self.sc.group_relevance, dtype=torch.float32)[L + 1]]
+        rel = C.wire.boundary_group_relevance(self.sc.group_relevance, L, G)
         return C.wire.with_plan(spec, C.wire.allocate_group_bits(rel, self.sc.group_avg_bits))
 
     def _k(self, ratio, S, spec=None):

@@ -59,8 +59,7 @@ class BoundaryConfig:
         if boundary is None or not C.wire.needs_plan(spec):
             return spec
         G = hidden // C.wire.GROUP
-        rel = [1.0] * G if self.group_relevance is None else \
-            [float(v) for v in torch.as_tensor(self.group_relevance, dtype=torch.float32)[boundary + 1]]
+        rel = C.wire.boundary_group_relevance(self.group_relevance, boundary, G)
         return C.wire.with_plan(spec, C.wire.allocate_group_bits(rel, self.group_avg_bits))
 
     @property

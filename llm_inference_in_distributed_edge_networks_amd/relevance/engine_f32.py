@@ -21,6 +21,11 @@ and runs every matrix product at fp32 accuracy on the matrix cores:
     (``v_mfma_f32_16x16x4_f32``), emitting rel[b, h] = sum_ij A_ij dA_ij = 0.5 sum_i dO_i . O_i;
   - the channel-group relevance sum |x dx| of the residual stream entering every layer (``group_absprod``).
 
+The seed sits on the last position of each window, so in the LAST layer everything after the attention - O
+projection, MLP, their norms - matters at those B rows only, forward and backward (the other rows' output
+relevance is exactly zero): that layer runs them on the gathered rows and scatters dO / dy back (as
+``DecoderLM.layer_rows`` does for the scored rows of the NLL path).
+
 CPU tensors run the same sequence on the PyTorch reference ops (the model must then be built with ``h3=True``);
 the tests check it against the autograd oracle ``attnlrp.head_relevance_batched``.
 """
@@ -72,6 +77,8 @@ class RelevanceEngineH3:
         x = m.embed(ids)
         emb = x
         saves = []
+        last = torch.arange(B, device=ids.device) * S + (S - 1)   # the seeded rows
+        nl = len(m.layers)
         for i, L in enumerate(m.layers):
             sc = m.h3_layer[i]
             sv = {"x": x}
@@ -86,7 +93,14 @@ class RelevanceEngineH3:
                                        cfg.rotary_dim, m.q_scale)
             o, lse = ops.attention(q, k, vt, S, need_lse=True, in_scales=(sc["att_q"], sc["att_k"], sc["o"]))
             sv.update(q=q, k=k, v=vt[..., :S].transpose(-1, -2).contiguous(), o=o, lse=lse.contiguous())
-            o3 = ops.split_h3(o, sc["o"])
+            if i == nl - 1:   # only the seeded rows reach the seed: O-proj and MLP on those rows (x -> [B, H])
+                sv["rows"] = last
+                x = x.index_select(0, last)
+                if not self.qwen:
+                    h23 = h23.index_select(0, last)
+                o3 = ops.split_h3(o, sc["o"], rows=last)
+            else:
+                o3 = ops.split_h3(o, sc["o"])
             if self.qwen:
                 y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], residual=x)
                 sv["rs2"] = ops.row_rstd(y, eps)
@@ -104,9 +118,10 @@ class RelevanceEngineH3:
         return emb, x, saves
 
     def _seed(self, x: torch.Tensor, B: int, S: int):
-        """d(mx * mx) / d x_final with the final norm's normaliser detached: only the last row of each window."""
+        """d(mx * mx) / d x_final with the final norm's normaliser detached: only the last row of each window
+        (x_final is already those rows, [B, H]) -> (the seed gradient [B, H], the seed logits)."""
         m, cfg = self.m, self.m.cfg
-        last = x.view(B, S, -1)[:, -1].contiguous()
+        last = x
         w = m.w["norm_w"]
         if self.qwen:
             rstd = ops.row_rstd(last, cfg.norm_eps)
@@ -120,9 +135,7 @@ class RelevanceEngineH3:
         g = mx.view(-1, 1) * m.w["head"].index_select(0, idx) * rstd.view(-1, 1) * w
         if not self.qwen:
             g = g - g.mean(-1, keepdim=True)
-        dx = torch.zeros_like(x)
-        dx.view(B, S, -1)[:, -1] = g
-        return dx, mx
+        return g.contiguous(), mx
 
     @torch.no_grad()
     def head_relevance(self, ids: torch.Tensor, want_channels: bool = False, group: int = 64):
@@ -141,6 +154,7 @@ class RelevanceEngineH3:
             else None
         for i in range(cfg.num_layers - 1, -1, -1):
             L, t, sv = m.layers[i], self.T[i], saves[i]
+            rows = sv.get("rows")   # last layer: dx is the seeded rows only [B, H]
             dx3, rinv = ops.split_h3_dyn(dx)
             if self.qwen:
                 dm = ops.linear_h3(dx3, t["wdT3"], t["a_dT"], rscale=rinv)
@@ -153,6 +167,11 @@ class RelevanceEngineH3:
                 dh2 = ops.linear_h3(dfc3, t["wfcT3"], t["a_fcT"], rscale=rinv_fc)
                 dy, dy3, rinv_y = dx, dx3, rinv           # parallel residual: the attention branch sees dx
             dO = ops.linear_h3(dy3, t["woT3"], t["a_oT"], rscale=rinv_y)
+            if rows is not None:   # back to every row: zero outside the seeded rows
+                dO = torch.zeros(B * S, dO.shape[1], dtype=dO.dtype, device=dO.device).index_copy_(0, rows, dO)
+                dy = torch.zeros(B * S, H, dtype=dy.dtype, device=dy.device).index_copy_(0, rows, dy)
+                if not self.qwen:
+                    dh2 = torch.zeros(B * S, H, dtype=dh2.dtype, device=dh2.device).index_copy_(0, rows, dh2)
             _, r, dq, dk, dv = ops.lrp_attn_bwd(sv["q"], sv["k"], sv["v"], sv["o"], dO, sv["lse"])
             rel[:, i] = r
             dqkv3, rinv_q = ops.lrp_rope_pack_h3(dq, dk, dv, m.cos, m.sin, B, S, Hq, Hkv, cfg.rotary_dim, m.q_scale,
@@ -161,7 +180,7 @@ class RelevanceEngineH3:
                 dx = ops.linear_h3(dqkv3, t["wqkvT3"], t["a_qkvT"], rscale=rinv_q, residual=dy, colscale=L["ln1_w"])
             else:
                 dh1 = ops.linear_h3(dqkv3, t["wqkvT3"], t["a_qkvT"], rscale=rinv_q)
-                dx = ops.lrp_ln_bwd_f32(dh1, sv["rs1"], L["ln1_w"], dh2, L["ln2_w"], dx)
+                dx = ops.lrp_ln_bwd_f32(dh1, sv["rs1"], L["ln1_w"], dh2, L["ln2_w"], dy)
             if want_channels:
                 ops.group_absprod(sv["x"], dx, B, S, out=chan[:, i])
             saves[i] = None

@@ -227,6 +227,17 @@ def test_group_bits_allocation():
     assert sum(allocate_group_bits(rel, 3.0)) <= 3 * len(rel)
 
 
+def test_boundary_group_relevance_rows():
+    """Boundary after layer L -> the table row of the stream entering L + 1; after the LAST layer (the reference's
+    layer 23 of 24) the table's last row - the quality sweep at boundary 23 indexed past the table before."""
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import boundary_group_relevance
+    table = [[float(10 * i + g) for g in range(3)] for i in range(24)]
+    assert boundary_group_relevance(table, 11, 3) == table[12]
+    assert boundary_group_relevance(table, 22, 3) == table[23]
+    assert boundary_group_relevance(table, 23, 3) == table[23]
+    assert boundary_group_relevance(None, 23, 3) == [1.0, 1.0, 1.0]
+
+
 @pytest.mark.parametrize("name", ["rgroup", "mixed_rgroup_int8"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_group_codec_roundtrip(name, dtype):

@@ -73,6 +73,26 @@ def main():
     out = {"model": cfg.name, "weights": a.weights, "dtype": a.dtype if dev == "cuda" else "fp32", "data": f"python-stdlib-bytes/eval, {len(wins)} windows "
            "(max_length 512, stride 32)", "methods": METHODS, "layers": layers, "ratios": ratios,
            "head_weights": hw.tolist(), "channel_group_relevance": grel.tolist(), "codecs": {}}
+    # outlier structure of the boundary tensors: what a one-global-scale quantizer (ref_int4_global) is sensitive to.
+    # peak/rms = max |x| over the batch / rms of x; token_peak = median over tokens of max_c |x_tc| / rms_t
+    with torch.no_grad():
+        b0 = next(iter(batches(ev, wins, a.batch)))
+        x = m.embed(b0.ids)
+        outl = {}
+        for i in range(cfg.num_layers):
+            x, _ = m.layer(i, x, b0.B, b0.S)
+            if i in layers:
+                xf = x.float()
+                rms_t = xf.pow(2).mean(1).sqrt()
+                xw = xf.view(b0.B, b0.S, -1)   # Q1 scales per window: |x| < max / 14 rounds to 0
+                outl[i] = {"peak_over_rms": float(xf.abs().max() / xf.pow(2).mean().sqrt()),
+                           "token_peak_over_rms_median": float((xf.abs().amax(1) / rms_t).median()),
+                           "int4_global_zero_fraction": float((xw.abs() < xw.abs().amax((1, 2), keepdim=True) / 14)
+                                                              .float().mean())}
+    out["boundary_outliers"] = outl
+    print("boundary outliers (peak/rms, median token peak/rms, fraction rounding to 0 under one global int4 scale): "
+          + "; ".join(f"L{L}: {v['peak_over_rms']:.1f}, {v['token_peak_over_rms_median']:.1f}, "
+                      f"{v['int4_global_zero_fraction']:.2f}" for L, v in sorted(outl.items())), flush=True)
     for codec in a.codecs.split(","):
         t0 = time.time()
         # head-group codecs: "name@bits" = relevance-allocated plans of that average width, "name@bitsu" = the
