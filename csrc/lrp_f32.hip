@@ -290,11 +290,14 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_f32_kernel(const float* __res
 // A score tile computed with the query (dkdv) or the key (dq) on the C rows puts 4 rows of a 16-row block on a lane;
 // two such blocks give the lane the 8 k-slots of a 32-deep reduction over those rows, in the order
 // slot 8g + j <-> row perm(g, j) = (j < 4 ? 4g + j : 16 + 4g + j - 4): the probabilities / dS are then the lane's own
-// A / B fragments, and the other operand is staged transposed in LDS with its rows in that order (X6T images).
+// A / B fragments, and the other operand is read from its row-major LDS image in that row order by transposing reads.
 namespace {
 constexpr int X6P = 32 * 64 * 2;   // one bf16 plane of a 32 x 64 tile (bytes)
 
-__device__ __forceinline__ int x6sw(int r) { return (r >> 1) & 7; }
+// 16-byte chunk swizzle of the row-major images (128-byte rows): conflict-free for the b64 staging writes, the b128
+// row-fragment reads and the ds_read_b64_tr_b16 transposed reads alike (searched over the XOR maps of the row bits
+// with the bank model of MI355X_MICROARCH §LDS; the plain (r >> 1) & 7 is 2-way on the writes and the tr reads)
+__device__ __forceinline__ int x6sw(int r) { return (((r >> 1) & 1) << 1) | ((((r >> 1) ^ (r >> 2)) & 1) << 2); }
 __device__ __forceinline__ f32x4_t mfma_bf16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -316,21 +319,15 @@ __device__ __forceinline__ void split3_frag(const float (&v)[8], bf16x8_t (&p)[3
     p[2][e] = (__bf16)p2;
   }
 }
-// the slot of row r (0..31) of a 32-row block in the permuted k order
-__device__ __forceinline__ int x6_slot(int r) { return r < 16 ? 8 * (r >> 2) + (r & 3) : 8 * ((r - 16) >> 2) + 4 + (r & 3); }
 
-// A 32 x 64 fp32 tile staged as three bf16 planes, row-major ([32][64], 16-byte chunks swizzled by x6sw(row): A / B
-// fragments by one ds_read_b128) and, with T, also transposed ([64][32 slots] in the x6_slot order, 64-byte rows: the
-// fragments of a reduction over the tile's rows).  Thread t owns the row pair 2 rp, 2 rp + 1 and columns 4 c4 .. +3
-// (x6_own): two 16-byte global loads (x6_load, issued a tile ahead so their latency hides under the previous tile's
-// MFMAs), and the two rows' slots are adjacent, so every transposed write is one 4-byte bf16 pair (x6_store).
-// Bank conflicts (MI355X_MICROARCH §LDS): the transposed writes of a 32-lane half go to rows d = 4 c4 + e, all of one
-// parity, i.e. to 16 of the 32 write banks.  The ownership puts row pairs {a, a + 1, a + 8, a + 9} in every half, whose
-// slots fill all four dwords of a 16-byte chunk, and the chunk of row d is XOR-swizzled by x6tsw(d): the writes are
-// then 2-way (free on ds_write_b32) and the transposed ds_read_b128 conflict-free (the first layout, 16 c4 x 2 row
-// pairs per half and no swizzle, was 16-way on every transposed write).
+// A 32 x 64 fp32 tile staged as three bf16 planes, row-major only ([32][64], 16-byte chunks swizzled by x6sw(row)):
+// A / B fragments by one ds_read_b128 (rm_frags), and the fragments of a reduction over the tile's rows straight from
+// the same image by the hardware-transposing ds_read_b64_tr_b16 (tr_frags).  Thread t owns the row pair 2 rp, 2 rp + 1
+// and columns 4 c4 .. +3 (x6_own): two 16-byte global loads (x6_load, issued a tile ahead so their latency hides under
+// the previous tile's MFMAs) and one 8-byte write per row and plane (x6_store).  History: the first version also wrote
+// a transposed image ([64][32 slots], 4-byte bf16 pairs) whose writes were 16-way bank conflicts; conflict-free, it
+// still cost 24 of the 36 staging writes per thread and tile.
 struct X6Regs { f32x4_t v[2]; };
-__device__ __forceinline__ int x6tsw(int d) { return ((d >> 2) & 1) | ((((d >> 2) ^ (d >> 3)) & 1) << 1); }
 __device__ __forceinline__ void x6_own(int t, int& r, int& c4) {
   const int w = t >> 6, l = t & 63, q = (l >> 3) & 3;
   r = 2 * (2 * w + (q & 1) + 8 * (q >> 1));
@@ -346,8 +343,7 @@ __device__ __forceinline__ void x6_load(const float* __restrict__ src, size_t ld
     R.v[i] = gr < nrows ? *(const f32x4_t*)(src + (size_t)gr * ld + c) : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
 }
-template <bool T>
-__device__ __forceinline__ void x6_store(const X6Regs& R, char* rm, char* tr) {
+__device__ __forceinline__ void x6_store(const X6Regs& R, char* rm) {
   int r, c4;
   x6_own(threadIdx.x, r, c4);
   uint32_t w[2][3][2];   // [row][plane][column pair]: packed bf16 pairs
@@ -369,26 +365,29 @@ __device__ __forceinline__ void x6_store(const X6Regs& R, char* rm, char* tr) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) *(u32x2_t*)(rm + pl * X6P + off) = u32x2_t{w[i][pl][0], w[i][pl][1]};
   }
-  if constexpr (T) {
-    const int sl = x6_slot(r);   // rows r, r + 1 -> slots sl, sl + 1
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t lo = (w[0][pl][e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-        const uint32_t hi = (w[1][pl][e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-        const int d = 4 * c4 + e;
-        *(uint32_t*)(tr + pl * X6P + d * 64 + ((((sl >> 3) ^ x6tsw(d))) << 4) + (sl & 7) * 2) = lo | (hi << 16);
-      }
-  }
 }
 __device__ __forceinline__ void rm_frags(const char* img, int row, int chunk, bf16x8_t (&f)[3]) {
 #pragma unroll
   for (int pl = 0; pl < 3; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * X6P + row * 128 + ((chunk ^ x6sw(row)) << 4));
 }
-__device__ __forceinline__ void tr_frags(const char* img, int row, int g, bf16x8_t (&f)[3]) {
+// B (or A) fragment of a reduction over the image's 32 rows in the permuted k order (slot 8g + j <-> row perm(g, j)), for columns 16 dt .. + 15: lane
+// (cl, g) gets column 16 dt + cl of rows 4g .. 4g + 3 (slots 8g .. 8g + 3) and 16 + 4g .. + 3 (slots 8g + 4 .. + 7),
+// two ds_read_b64_tr_b16 per plane (lane 4q + p of a 16-lane group addresses row q of the 4-row block, columns
+// 4p .. 4p + 3; every lane of the wave must execute it).
+typedef short x6s4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void tr_frags(const char* img, int dt, int g, int cl, bf16x8_t (&f)[3]) {
+  const int q = cl >> 2, p = cl & 3, ch = 2 * dt + (p >> 1);
+  const int r0 = 4 * g + q, r1 = 16 + 4 * g + q;
+  const int o0 = r0 * 128 + ((ch ^ x6sw(r0)) << 4) + (p & 1) * 8;
+  const int o1 = r1 * 128 + ((ch ^ x6sw(r1)) << 4) + (p & 1) * 8;
 #pragma unroll
-  for (int pl = 0; pl < 3; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * X6P + row * 64 + ((g ^ x6tsw(row)) << 4));
+  for (int pl = 0; pl < 3; ++pl) {
+    typedef __attribute__((address_space(3))) x6s4_t lds_s4;
+    const x6s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * X6P + o0));
+    const x6s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * X6P + o1));
+    const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    f[pl] = __builtin_bit_cast(bf16x8_t, v);
+  }
 }
 // the lane's 8 values of row `row` (its key / query), columns 8 kg + 32 ks .. +7, split into planes
 __device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8_t (&f)[2][3], int g) {
@@ -408,14 +407,14 @@ __device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8
 // block), heaviest first; wave w owns keys kb 64 + 16 w + cl.  Per 32-query tile: S = Q K^T and dA = dO V^T with the
 // query on the C rows (the lane's K / V planes in registers for the whole sweep), P = exp(S - lse), dS = P (dA/2 - D),
 // then dV += P^T dO and dK += dS^T Q over the tile's 32 queries (P / dS the lane's A fragments, dO / Q from the
-// transposed images).
+// row-major images by transposing reads).
 __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                                const float* __restrict__ v,
                                                                const float* __restrict__ dO,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ D, float* __restrict__ dk,
                                                                float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) char sQ[3 * X6P], sO[3 * X6P], sQT[3 * X6P], sOT[3 * X6P];
+  __shared__ __attribute__((aligned(16))) char sQ[3 * X6P], sO[3 * X6P];
   __shared__ float sL[32], sD[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int kb = blockIdx.x / (B * Hq);
@@ -446,8 +445,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
   fetch(kb * 64);
   for (int q0 = kb * 64; q0 < S; q0 += 32) {
     __syncthreads();
-    x6_store<true>(rq, sQ, sQT);
-    x6_store<true>(ro, sO, sOT);
+    x6_store(rq, sQ);
+    x6_store(ro, sO);
     if (tid < 32) sL[tid] = nl, sD[tid] = nd;
     if (q0 + 32 < S) fetch(q0 + 32);
     __syncthreads();
@@ -478,8 +477,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x8_t ob[3], qb[3];
-      tr_frags(sOT, dt * 16 + cl, g, ob);
-      tr_frags(sQT, dt * 16 + cl, g, qb);
+      tr_frags(sO, dt, g, cl, ob);
+      tr_frags(sQ, dt, g, cl, qb);
       dva[dt] = x6dot(pf, ob, dva[dt]);
       dka[dt] = x6dot(dsf, qb, dka[dt]);
     }
@@ -508,7 +507,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ D, float* __restrict__ dq,
                                                              int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) char sK[3 * X6P], sV[3 * X6P], sKT[3 * X6P];
+  __shared__ __attribute__((aligned(16))) char sK[3 * X6P], sV[3 * X6P];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int nqb = (S + 63) / 64;
   const int qb = nqb - 1 - blockIdx.x / (B * Hq);
@@ -531,8 +530,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
   x6_load(vh, 64, 0, S, rv);
   for (int k0 = 0; k0 < kend; k0 += 32) {
     __syncthreads();
-    x6_store<true>(rk, sK, sKT);
-    x6_store<false>(rv, sV, nullptr);
+    x6_store(rk, sK);
+    x6_store(rv, sV);
     if (k0 + 32 < kend) {   // the next key tile's values under this tile's MFMAs
       x6_load(kh, 64, k0 + 32, S, rk);
       x6_load(vh, 64, k0 + 32, S, rv);
@@ -563,7 +562,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x8_t kt[3];
-      tr_frags(sKT, dt * 16 + cl, g, kt);
+      tr_frags(sK, dt, g, cl, kt);
       acc[dt] = x6dot(kt, dsf, acc[dt]);
     }
   }

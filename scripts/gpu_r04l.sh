@@ -1,0 +1,18 @@
+# Round 4: same-box A/B of the x6 AttnLRP staging: transposed images (conflict-free, build/ab_lrp = 795c7b9) vs
+# row-major images + ds_read_b64_tr_b16 (this tree), three interleaved rounds at 64 windows.
+set -o pipefail
+O=gpurun_out/r04l
+mkdir -p $O
+export TMPDIR=/tmp
+for i in 1 2 3; do
+  for v in img tr; do
+    case $v in
+      img) envs="EDGE_KERNEL_LIB=$PWD/build/ab_lrp/libedge_kernels.so" ;;
+      tr) envs="" ;;
+    esac
+    env $envs timeout -k 10 240 python tools/relevance_bench.py --dtype fp32 --batch 64 \
+      --json-out $O/rel_$v$i.json > $O/rel_$v$i.log 2>&1 || { echo "relevance bench $v$i failed"; tail -20 $O/rel_$v$i.log; exit 1; }
+    python -c "import json; d=json.load(open('$O/rel_$v$i.json')); print('$v$i', d['tokens_per_s'], d['ms_per_batch'])"
+  done
+done
+exit 0
