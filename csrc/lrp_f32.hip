@@ -665,6 +665,76 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_h3_kernel(const float* __re
   if (lane == 0) rinv[row] = inv * (post ? post[row] : 1.f);
 }
 
+// Same, 4 consecutive columns per lane (16-byte loads of the partials, the rotation partners and cos / sin; 8-byte
+// plane stores): the rotated half-widths are multiples of 4 (rot_dim % 8 == 0), so a lane's 4 columns rotate
+// together.  NIT = ceil(W / 256) groups of 4 columns per lane stay in registers between the row max and the stores.
+template <int NIT>
+__global__ __launch_bounds__(256) void lrp_rope_pack_h3_v4_kernel(const float* __restrict__ dq,
+                                                                  const float* __restrict__ dk,
+                                                                  const float* __restrict__ dv,
+                                                                  const float* __restrict__ cosT,
+                                                                  const float* __restrict__ sinT,
+                                                                  f16_t* __restrict__ out, float* __restrict__ rinv,
+                                                                  const float* __restrict__ post, int B, int S, int Hq,
+                                                                  int Hkv, int rot_dim, float q_scale) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B * S) return;
+  const int b = row / S, s = row - b * S, W = (Hq + 2 * Hkv) * 64, G = Hq / Hkv, half = rot_dim >> 1;
+  float v[NIT][4];
+  float mx = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = 4 * lane + 256 * it;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[it][e] = 0.f;
+    if (c >= W) continue;
+    const int hh = c >> 6, d = c & 63;
+    const float* src;
+    float scale = 1.f;
+    bool rope = true;
+    int ng = 1;
+    if (hh < Hq) {
+      src = dq + (((size_t)b * Hq + hh) * S + s) * 64;
+      scale = q_scale;
+    } else if (hh < Hq + Hkv) {
+      src = dk + (((size_t)b * Hq + (hh - Hq) * G) * S + s) * 64;
+      ng = G;
+    } else {
+      src = dv + (((size_t)b * Hq + (hh - Hq - Hkv) * G) * S + s) * 64;
+      ng = G;
+      rope = false;
+    }
+    const bool rot = rope && d < rot_dim;
+    const int dp = !rot ? d : (d < half ? d + half : d - half);
+    f32x4_t x0 = {0.f, 0.f, 0.f, 0.f}, xp = {0.f, 0.f, 0.f, 0.f};
+    for (int gi = 0; gi < ng; ++gi) {
+      x0 += *(const f32x4_t*)(src + (size_t)gi * S * 64 + d);
+      if (rot) xp += *(const f32x4_t*)(src + (size_t)gi * S * 64 + dp);
+    }
+    f32x4_t val = x0;
+    if (rot) {
+      const int j = d < half ? d : d - half;
+      const f32x4_t cs = *(const f32x4_t*)(cosT + (size_t)s * half + j), sn = *(const f32x4_t*)(sinT + (size_t)s * half + j);
+      val = d < half ? x0 * cs + xp * sn : x0 * cs - xp * sn;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[it][e] = val[e] * scale;
+      mx = fmaxf(mx, fabsf(v[it][e]));
+    }
+  }
+  mx = wave_max(mx);
+  float inv;
+  const float sc = row_pow2_scale(mx, inv);
+  f16_t* o = out + (size_t)row * (2 * W);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = 4 * lane + 256 * it;
+    if (c < W) store_h3_4(o, W, c, v[it], sc);
+  }
+  if (lane == 0) rinv[row] = inv * (post ? post[row] : 1.f);
+}
+
 // Plain fp32 rows [R, K] -> per-row-scaled h3 activation [R, 2K] + rinv.  One wave per row, 4 values per access.
 template <int NIT>   // NIT > 0: K <= 256 NIT, the row's values stay in registers (read once)
 __global__ __launch_bounds__(256) void split_h3_dyn_kernel(const float* __restrict__ x, f16_t* __restrict__ out,
@@ -933,7 +1003,14 @@ EDGE_API int edge_lrp_rope_pack_h3(const float* dq, const float* dk, const float
   const int R = B * S;
   if (R <= 0) return 0;
   if (rot_dim > 64 || rot_dim % 2 || Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
-  if ((Hq + 2 * Hkv) * 64 <= 2048)
+  const int W = (Hq + 2 * Hkv) * 64;
+  if (rot_dim % 8 == 0 && W <= 1280) {   // Qwen2-0.5B: W = 1152, 5 column groups per lane
+    lrp_rope_pack_h3_v4_kernel<5><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S,
+                                                                Hq, Hkv, rot_dim, q_scale);
+  } else if (rot_dim % 8 == 0 && W <= 2048) {
+    lrp_rope_pack_h3_v4_kernel<8><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S,
+                                                                Hq, Hkv, rot_dim, q_scale);
+  } else if (W <= 2048)
     lrp_rope_pack_h3_kernel<32><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S,
                                                               Hq, Hkv, rot_dim, q_scale);
   else
