@@ -263,7 +263,7 @@ __device__ __forceinline__ void* out_row(void* y, size_t r, int H, float h3s) {
 template <int NCH>
 __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           void* __restrict__ y, const int* __restrict__ rows, int R,
-                                                          int H, float eps, float h3s) {
+                                                          int H, float eps, float h3s, float* __restrict__ rstd_out) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
   const int src_row = rows ? rows[r] : r;
@@ -276,6 +276,7 @@ __global__ __launch_bounds__(256) void rmsnorm_f32_kernel(const float* __restric
     for (int j = 0; j < 8; ++j) ss = fmaf(v[c][j], v[c][j], ss);
   ss = wave_sum(ss);
   const float rs = 1.f / sqrtf(ss / (float)H + eps);
+  if (rstd_out && (threadIdx.x & 63) == 0) rstd_out[r] = rs;   // the normaliser itself (AttnLRP saves it detached)
   load_row_f32<NCH>(w, H, g);
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
@@ -360,7 +361,16 @@ EDGE_API int edge_rmsnorm_f32(const float* x, const float* w, void* y, const int
                               float h3_scale, hipStream_t st) {
   if (H % 8 || R <= 0 || h3_scale < 0.f) return R == 0 ? 0 : (int)hipErrorInvalidValue;
   dim3 grid((R + 3) / 4);
-  DISPATCH_NCH(H, rmsnorm_f32_kernel<NCH><<<grid, 256, 0, st>>>(x, w, y, rows, R, H, eps, h3_scale));
+  DISPATCH_NCH(H, rmsnorm_f32_kernel<NCH><<<grid, 256, 0, st>>>(x, w, y, rows, R, H, eps, h3_scale, nullptr));
+  return (int)hipGetLastError();
+}
+
+// edge_rmsnorm_f32 that also writes the row normalisers rsqrt(mean(x^2) + eps) to rstd [R]
+EDGE_API int edge_rmsnorm_f32_rstd(const float* x, const float* w, void* y, const int* rows, int R, int H, float eps,
+                                   float h3_scale, float* rstd, hipStream_t st) {
+  if (H % 8 || R <= 0 || h3_scale < 0.f || !rstd) return R == 0 ? 0 : (int)hipErrorInvalidValue;
+  dim3 grid((R + 3) / 4);
+  DISPATCH_NCH(H, rmsnorm_f32_kernel<NCH><<<grid, 256, 0, st>>>(x, w, y, rows, R, H, eps, h3_scale, rstd));
   return (int)hipGetLastError();
 }
 

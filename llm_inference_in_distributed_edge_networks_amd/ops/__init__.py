@@ -86,20 +86,31 @@ def _out_f32_or_h3(R: int, H: int, h3: float, device) -> torch.Tensor:
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, rows: torch.Tensor | None = None,
-            h3: float = 0.0) -> torch.Tensor:
+            h3: float = 0.0, rstd_out: torch.Tensor | None = None) -> torch.Tensor:
     """RMSNorm of ``x[rows]`` (all rows if ``rows`` is None).  fp32 ``x`` with ``h3`` = s > 0: output as the
-    2-plane h3 activation of s * y (the next GEMM's input)."""
+    2-plane h3 activation of s * y (the next GEMM's input).  ``rstd_out`` (fp32 [R]): also the row normalisers
+    rsqrt(mean(x^2) + eps) the norm applied (fp32 ``x``; what ``row_rstd`` computes, without a second pass)."""
     if not _gpu(x):
-        y = ref.rmsnorm(x if rows is None else x.index_select(0, rows.long()), w, eps)
+        xs = x if rows is None else x.index_select(0, rows.long())
+        if rstd_out is not None:
+            rstd_out.copy_(ref.row_rstd(xs, eps))
+        y = ref.rmsnorm(xs, w, eps)
         return ref.h3_act(y, h3) if h3 else y
     R = x.shape[0] if rows is None else rows.numel()
     H = x.shape[1]
     rows32 = None if rows is None else rows.to(torch.int32).contiguous()
     if x.dtype == torch.float32:
-        _check_f32(x, w)
+        _check_f32(x, w, rstd_out)
         y = _out_f32_or_h3(R, H, h3, x.device)
+        if rstd_out is not None:
+            assert rstd_out.shape == (R,)
+            call("edge_rmsnorm_f32_rstd", ptr(x), ptr(w), ptr(y), ptr(rows32), R, H, float(eps), float(h3),
+                 ptr(rstd_out), stream())
+            return y
         call("edge_rmsnorm_f32", ptr(x), ptr(w), ptr(y), ptr(rows32), R, H, float(eps), float(h3), stream())
         return y
+    if rstd_out is not None:
+        raise TypeError("rstd_out: fp32 activations only")
     _check_bf16(x, w)
     y = torch.empty(R, H, dtype=x.dtype, device=x.device)
     call("edge_rmsnorm", ptr(x), ptr(w), ptr(y), ptr(rows32), R, H, float(eps), stream())

@@ -82,9 +82,9 @@ class RelevanceEngineH3:
         for i, L in enumerate(m.layers):
             sc = m.h3_layer[i]
             sv = {"x": x}
-            if self.qwen:
-                sv["rs1"] = ops.row_rstd(x, eps)
-                h13 = ops.rmsnorm(x, L["ln1_w"], eps, h3=sc["qkv"])
+            if self.qwen:   # the norms' own row normalisers, saved detached (no separate row_rstd pass)
+                sv["rs1"] = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+                h13 = ops.rmsnorm(x, L["ln1_w"], eps, h3=sc["qkv"], rstd_out=sv["rs1"])
             else:
                 sv["rs1"] = ops.row_rstd(x, eps, center=True)
                 h13, h23 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], eps,
@@ -103,10 +103,10 @@ class RelevanceEngineH3:
                 o3 = ops.split_h3(o, sc["o"])
             if self.qwen:
                 y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], residual=x)
-                sv["rs2"] = ops.row_rstd(y, eps)
+                sv["rs2"] = torch.empty(y.shape[0], dtype=torch.float32, device=y.device)
+                h23 = ops.rmsnorm(y, L["ln2_w"], eps, h3=sc["mlp"], rstd_out=sv["rs2"])
                 # one GEMM: the SwiGLU planes for the down projection and the saved pre-activations for its rule
-                a3, sv["gu"] = ops.linear_h3_swiglu_raw(ops.rmsnorm(y, L["ln2_w"], eps, h3=sc["mlp"]), L["wgu3"],
-                                                        sc["a_wgu"], sc["down"])
+                a3, sv["gu"] = ops.linear_h3_swiglu_raw(h23, L["wgu3"], sc["a_wgu"], sc["down"])
                 x = ops.linear_h3(a3, L["wd3"], sc["a_wd"], residual=y)
             else:
                 y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], L["bo"], residual=x)

@@ -55,6 +55,11 @@ def test_rmsnorm_f32(H):
     rows = torch.tensor([5, 0, 299, 17])
     y3r = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6, rows.to(DEV), h3=s)
     assert rel_err(R.h3_to_f32(y3r, s), ref[rows]) < 2e-6
+    # the row normalisers as a side output (the AttnLRP forward saves them): same planes, rstd at fp32 level
+    rs = torch.empty(300, device=DEV)
+    y3s = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-6, h3=s, rstd_out=rs)
+    assert torch.equal(y3s, y3)
+    assert rel_err(rs, R.row_rstd(x, 1e-6)) < 1e-6
 
 
 def test_layernorm_dual_f32():
