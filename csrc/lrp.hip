@@ -28,41 +28,45 @@
 // MFMA: v_mfma_f32_16x16x32_bf16 everywhere.  Lane l holds A[row = l&15][k = 8(l>>4)..+7],
 // B[k = 8(l>>4)..+7][col = l&15] and C[row = 4(l>>4)+r][col = l&15].  Products whose K dimension is the
 // token axis reuse the lane-local probabilities of two 16-token sub-tiles as the A (or B) operand, with the
-// token order permuted as kappa(g, j) = 16(j>>2) + 4g + (j&3); the other operand is read from a transposed
-// LDS tile in the same order (the forward kernel's P.V trick).
+// token order permuted as kappa(g, j) = 16(j>>2) + 4g + (j&3); the other operand is read in the same order from
+// the row-major LDS tile by the hardware-transposing ds_read_b64_tr_b16 (no transposed copy is staged).
 #include "common.h"
 
 namespace {
-constexpr int LD_ROW = 72;   // row-major 64-wide bf16 tile, padded row (144 B) -> conflict-light b128 reads
-constexpr int LD_T = 40;     // transposed [64][32] tile, padded row (80 B)
+// Row-major 32 x 64 bf16 tiles, 128-byte rows, 16-byte chunks XOR-swizzled by tsw(row): conflict-free for the
+// staging writes, the b128 row-fragment reads and the transposed reads (the same map as csrc/lrp_f32.hip x6sw).
+// History: the first version padded the rows (144 B) and staged a transposed [64][40] copy with 2-byte writes that
+// were 8-way bank conflicts.
+__device__ __forceinline__ int tsw(int r) { return (((r >> 1) & 1) << 1) | ((((r >> 1) ^ (r >> 2)) & 1) << 2); }
 
 __device__ __forceinline__ bf16x8_t ld_row_frag(const bf16_t* t, int row, int col) {
-  return *(const bf16x8_t*)(t + row * LD_ROW + col);
+  return *(const bf16x8_t*)(t + row * 64 + (((col >> 3) ^ tsw(row)) << 3));
 }
 
-// B (or A) operand over the permuted token axis from a transposed [64][LD_T] tile: element j <-> token
-// kappa(g, j) of the 32-token tile, row `d`.
-__device__ __forceinline__ bf16x8_t ld_t_frag(const bf16_t* t, int d, int g) {
-  const u32x2_t lo = *(const u32x2_t*)(t + d * LD_T + 4 * g);
-  const u32x2_t hi = *(const u32x2_t*)(t + d * LD_T + 16 + 4 * g);
-  u32x4_t v = {lo[0], lo[1], hi[0], hi[1]};
+// B (or A) operand over the permuted token axis for columns 16 dt .. + 15: lane (cl, g) gets column 16 dt + cl of
+// tokens kappa(g, 0..7) = 4g .. 4g + 3, 16 + 4g .. + 3, two ds_read_b64_tr_b16 (lane 4q + p of a 16-lane group
+// addresses token row q of the 4-row block, columns 4p .. 4p + 3; every lane of the wave executes it).
+typedef short s4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8_t ld_t_frag(const bf16_t* t, int dt, int g, int cl) {
+  typedef __attribute__((address_space(3))) s4_t lds_s4;
+  const int q = cl >> 2, p = cl & 3, ch = 2 * dt + (p >> 1);
+  const int r0 = 4 * g + q, r1 = 16 + 4 * g + q;
+  const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(t + r0 * 64 + ((ch ^ tsw(r0)) << 3) + (p & 1) * 4));
+  const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(t + r1 * 64 + ((ch ^ tsw(r1)) << 3) + (p & 1) * 4));
+  const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-// Stage 32 rows x 64 bf16 (row stride `ld` elements, rows clamped to < nrows) into a row-major tile and,
-// if `tt` != nullptr, its transpose.  256 threads: one 16 B chunk each.
-__device__ __forceinline__ void stage32(const bf16_t* __restrict__ src, size_t ld, int row0, int nrows, bf16_t* tr,
-                                        bf16_t* tt) {
+// 32 rows x 64 bf16 (row stride `ld` elements, rows clamped to < nrows): one 16-byte chunk per thread, loaded into
+// a register (a tile ahead) and stored into the swizzled row-major tile.
+__device__ __forceinline__ u32x4_t load32(const bf16_t* __restrict__ src, size_t ld, int row0, int nrows) {
   const int t = threadIdx.x, r = t >> 3, c = (t & 7) * 8;
-  int gr = row0 + r;
-  u32x4_t v = {0u, 0u, 0u, 0u};
-  if (gr < nrows) v = *(const u32x4_t*)(src + (size_t)gr * ld + c);
-  *(u32x4_t*)(tr + r * LD_ROW + c) = v;
-  if (tt) {
-    const bf16_t* e = (const bf16_t*)&v;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) tt[(c + i) * LD_T + r] = e[i];
-  }
+  const int gr = row0 + r;
+  return gr < nrows ? *(const u32x4_t*)(src + (size_t)gr * ld + c) : u32x4_t{0u, 0u, 0u, 0u};
+}
+__device__ __forceinline__ void store32(const u32x4_t& v, bf16_t* tr) {
+  const int t = threadIdx.x, r = t >> 3;
+  *(u32x4_t*)(tr + r * 64 + (((t & 7) ^ tsw(r)) << 3)) = v;
 }
 
 __device__ __forceinline__ bf16x8_t pack8(const f32x4_t& a, const f32x4_t& b) {
@@ -113,10 +117,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __rest
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ D, float* __restrict__ dk,
                                                             float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) bf16_t sQ[32 * LD_ROW];
-  __shared__ __attribute__((aligned(16))) bf16_t sO[32 * LD_ROW];
-  __shared__ __attribute__((aligned(16))) bf16_t tQ[64 * LD_T];
-  __shared__ __attribute__((aligned(16))) bf16_t tO[64 * LD_T];
+  __shared__ __attribute__((aligned(16))) bf16_t sQ[32 * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t sO[32 * 64];
   __shared__ float sL[32], sD[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int nkb = (S + 63) / 64;
@@ -143,14 +145,22 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __rest
     const bf16_t* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
     const float* lh = lse + ((size_t)b * Hq + h) * S;
     const float* dh = D + ((size_t)b * Hq + h) * S;
+    u32x4_t nq = load32(qh, 64, q_first, S), no = load32(doh, (size_t)Hq * 64, q_first, S);
+    float nl = INFINITY, nd = 0.f;
+    if (tid < 32 && q_first + tid < S) nl = lh[q_first + tid], nd = dh[q_first + tid];
     for (int q0 = q_first; q0 < S; q0 += 32) {
       __syncthreads();
-      stage32(qh, 64, q0, S, sQ, tQ);
-      stage32(doh, (size_t)Hq * 64, q0, S, sO, tO);
-      if (tid < 32) {
-        const int qi = q0 + tid;
-        sL[tid] = qi < S ? lh[qi] : INFINITY;
-        sD[tid] = qi < S ? dh[qi] : 0.f;
+      store32(nq, sQ);
+      store32(no, sO);
+      if (tid < 32) sL[tid] = nl, sD[tid] = nd;
+      if (q0 + 32 < S) {   // the next tile's values under this tile's MFMAs
+        nq = load32(qh, 64, q0 + 32, S);
+        no = load32(doh, (size_t)Hq * 64, q0 + 32, S);
+        if (tid < 32) {
+          const int qi = q0 + 32 + tid;
+          nl = qi < S ? lh[qi] : INFINITY;
+          nd = qi < S ? dh[qi] : 0.f;
+        }
       }
       __syncthreads();
       f32x4_t p[2], ds[2];
@@ -179,8 +189,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __rest
       const bf16x8_t dsf = pack8(ds[0], ds[1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        dva[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, ld_t_frag(tO, dt * 16 + cl, g), dva[dt], 0, 0, 0);
-        dka[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsf, ld_t_frag(tQ, dt * 16 + cl, g), dka[dt], 0, 0, 0);
+        dva[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, ld_t_frag(sO, dt, g, cl), dva[dt], 0, 0, 0);
+        dka[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsf, ld_t_frag(sQ, dt, g, cl), dka[dt], 0, 0, 0);
       }
     }
   }
@@ -208,9 +218,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_kernel(const bf16_t* __restri
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ D, float* __restrict__ dq,
                                                           int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) bf16_t sK[32 * LD_ROW];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[32 * LD_ROW];
-  __shared__ __attribute__((aligned(16))) bf16_t tK[64 * LD_T];
+  __shared__ __attribute__((aligned(16))) bf16_t sK[32 * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[32 * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int nqb = (S + 63) / 64;
   const int qb = nqb - 1 - blockIdx.x / (B * Hq);          // heaviest query blocks first
@@ -234,10 +243,15 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_kernel(const bf16_t* __restri
   for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int kend = min(S, qb * 64 + 64);
+  u32x4_t nk = load32(kh, 64, 0, S), nv = load32(vh, 64, 0, S);
   for (int k0 = 0; k0 < kend; k0 += 32) {
     __syncthreads();
-    stage32(kh, 64, k0, S, sK, tK);
-    stage32(vh, 64, k0, S, sV, nullptr);
+    store32(nk, sK);
+    store32(nv, sV);
+    if (k0 + 32 < kend) {   // the next key tile under this tile's MFMAs
+      nk = load32(kh, 64, k0 + 32, S);
+      nv = load32(vh, 64, k0 + 32, S);
+    }
     __syncthreads();
     f32x4_t ds[2];
 #pragma unroll
@@ -262,7 +276,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_kernel(const bf16_t* __restri
     const bf16x8_t dsf = pack8(ds[0], ds[1]);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
-      acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_t_frag(tK, dt * 16 + cl, g), dsf, acc[dt], 0, 0, 0);
+      acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_t_frag(sK, dt, g, cl), dsf, acc[dt], 0, 0, 0);
   }
   // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
   if (qi < S) {
