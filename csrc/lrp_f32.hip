@@ -407,15 +407,18 @@ __device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8
 // block), heaviest first; wave w owns keys kb 64 + 16 w + cl.  Per 32-query tile: S = Q K^T and dA = dO V^T with the
 // query on the C rows (the lane's K / V planes in registers for the whole sweep), P = exp(S - lse), dS = P (dA/2 - D),
 // then dV += P^T dO and dK += dS^T Q over the tile's 32 queries (P / dS the lane's A fragments, dO / Q from the
-// row-major images by transposing reads).
+// row-major images by transposing reads).  DB: the staging images double-buffered - tile t + 1 is stored into the
+// other buffer before tile t's MFMAs, one barrier per tile instead of two.
+template <bool DB>
 __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                                const float* __restrict__ v,
                                                                const float* __restrict__ dO,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ D, float* __restrict__ dk,
                                                                float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) char sQ[3 * X6P], sO[3 * X6P];
-  __shared__ float sL[32], sD[32];
+  constexpr int NBUF = DB ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) char sQ[NBUF][3 * X6P], sO[NBUF][3 * X6P];
+  __shared__ float sL[NBUF][32], sD[NBUF][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int kb = blockIdx.x / (B * Hq);
   const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
@@ -442,14 +445,34 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
       nd = qi < S ? dh[qi] : 0.f;
     }
   };
+  auto put = [&](int buf) {
+    x6_store(rq, sQ[buf]);
+    x6_store(ro, sO[buf]);
+    if (tid < 32) sL[buf][tid] = nl, sD[buf][tid] = nd;
+  };
   fetch(kb * 64);
-  for (int q0 = kb * 64; q0 < S; q0 += 32) {
+  if constexpr (DB) {
+    put(0);
+    if (kb * 64 + 32 < S) fetch(kb * 64 + 32);
     __syncthreads();
-    x6_store(rq, sQ);
-    x6_store(ro, sO);
-    if (tid < 32) sL[tid] = nl, sD[tid] = nd;
-    if (q0 + 32 < S) fetch(q0 + 32);
-    __syncthreads();
+  }
+  int cur = 0;
+  for (int q0 = kb * 64; q0 < S; q0 += 32, cur ^= (DB ? 1 : 0)) {
+    if constexpr (DB) {
+      if (q0 + 32 < S) {   // tile t + 1 into the other buffer (its readers passed the previous barrier)
+        put(cur ^ 1);
+        if (q0 + 64 < S) fetch(q0 + 64);
+      }
+    } else {
+      __syncthreads();
+      put(0);
+      if (q0 + 32 < S) fetch(q0 + 32);
+      __syncthreads();
+    }
+    const char* bQ = sQ[cur];
+    const char* bO = sO[cur];
+    const float* bL = sL[cur];
+    const float* bD = sD[cur];
     float pv[8], dsv[8];   // k-slot order: j < 4 -> sub-block 0 row 4g + j, j >= 4 -> sub-block 1 row 4g + j - 4
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -457,8 +480,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t qa[3], oa[3];
-        rm_frags(sQ, sub * 16 + cl, 4 * ks + g, qa);
-        rm_frags(sO, sub * 16 + cl, 4 * ks + g, oa);
+        rm_frags(bQ, sub * 16 + cl, 4 * ks + g, qa);
+        rm_frags(bO, sub * 16 + cl, 4 * ks + g, oa);
         sc = x6dot(qa, kf[ks], sc);
         da = x6dot(oa, vf[ks], da);
       }
@@ -466,9 +489,9 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
       for (int r = 0; r < 4; ++r) {
         const int ql = sub * 16 + 4 * g + r, qi = q0 + ql;
         const bool ok = qi < S && key <= qi && key < S;
-        const float pr = ok ? expf(sc[r] - sL[ql]) : 0.f;
+        const float pr = ok ? expf(sc[r] - bL[ql]) : 0.f;
         pv[4 * sub + r] = pr;
-        dsv[4 * sub + r] = pr * (0.5f * da[r] - sD[ql]);
+        dsv[4 * sub + r] = pr * (0.5f * da[r] - bD[ql]);
       }
     }
     bf16x8_t pf[3], dsf[3];
@@ -477,11 +500,12 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x8_t ob[3], qb[3];
-      tr_frags(sO, dt, g, cl, ob);
-      tr_frags(sQ, dt, g, cl, qb);
+      tr_frags(bO, dt, g, cl, ob);
+      tr_frags(bQ, dt, g, cl, qb);
       dva[dt] = x6dot(pf, ob, dva[dt]);
       dka[dt] = x6dot(dsf, qb, dka[dt]);
     }
+    if constexpr (DB) __syncthreads();
   }
   // C[row = key 16w + 4g + r][col = d 16dt + cl]
   float* dkh = dk + ((size_t)b * Hq + h) * S * 64;
@@ -502,12 +526,15 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
 // dQ (inputs and output as lrp_attn_dq_f32_kernel).  Workgroup = (b, h, 64-query block), heaviest (last) first; wave
 // w owns queries qb 64 + 16 w + cl.  Per 32-key tile: S^T = K Q^T and dA^T = V dO^T with the key on the C rows (the
 // lane's Q / dO planes in registers), dS^T = P^T (dA^T/2 - D), then dQ^T += K^T dS^T over the tile's 32 keys.
+// DB as the dK / dV kernel.
+template <bool DB>
 __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                              const float* __restrict__ v, const float* __restrict__ dO,
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ D, float* __restrict__ dq,
                                                              int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) char sK[3 * X6P], sV[3 * X6P];
+  constexpr int NBUF = DB ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) char sK[NBUF][3 * X6P], sV[NBUF][3 * X6P];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int nqb = (S + 63) / 64;
   const int qb = nqb - 1 - blockIdx.x / (B * Hq);
@@ -526,17 +553,34 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
   for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int kend = min(S, qb * 64 + 64);
   X6Regs rk, rv;
-  x6_load(kh, 64, 0, S, rk);
-  x6_load(vh, 64, 0, S, rv);
-  for (int k0 = 0; k0 < kend; k0 += 32) {
+  auto fetch = [&](int k0) {
+    x6_load(kh, 64, k0, S, rk);
+    x6_load(vh, 64, k0, S, rv);
+  };
+  fetch(0);
+  if constexpr (DB) {
+    x6_store(rk, sK[0]);
+    x6_store(rv, sV[0]);
+    if (32 < kend) fetch(32);
     __syncthreads();
-    x6_store(rk, sK);
-    x6_store(rv, sV);
-    if (k0 + 32 < kend) {   // the next key tile's values under this tile's MFMAs
-      x6_load(kh, 64, k0 + 32, S, rk);
-      x6_load(vh, 64, k0 + 32, S, rv);
+  }
+  int cur = 0;
+  for (int k0 = 0; k0 < kend; k0 += 32, cur ^= (DB ? 1 : 0)) {
+    if constexpr (DB) {
+      if (k0 + 32 < kend) {   // tile t + 1 into the other buffer (its readers passed the previous barrier)
+        x6_store(rk, sK[cur ^ 1]);
+        x6_store(rv, sV[cur ^ 1]);
+        if (k0 + 64 < kend) fetch(k0 + 64);
+      }
+    } else {
+      __syncthreads();
+      x6_store(rk, sK[0]);
+      x6_store(rv, sV[0]);
+      if (k0 + 32 < kend) fetch(k0 + 32);   // the next key tile's values under this tile's MFMAs
+      __syncthreads();
     }
-    __syncthreads();
+    const char* bK = sK[cur];
+    const char* bV = sV[cur];
     float dsv[8];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -544,8 +588,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t ka[3], va[3];
-        rm_frags(sK, sub * 16 + cl, 4 * ks + g, ka);
-        rm_frags(sV, sub * 16 + cl, 4 * ks + g, va);
+        rm_frags(bK, sub * 16 + cl, 4 * ks + g, ka);
+        rm_frags(bV, sub * 16 + cl, 4 * ks + g, va);
         sc = x6dot(ka, qf[ks], sc);
         da = x6dot(va, of[ks], da);
       }
@@ -562,9 +606,10 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x8_t kt[3];
-      tr_frags(sK, dt, g, cl, kt);
+      tr_frags(bK, dt, g, cl, kt);
       acc[dt] = x6dot(kt, dsf, acc[dt]);
     }
+    if constexpr (DB) __syncthreads();
   }
   // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
   if (qi < S) {
@@ -982,8 +1027,13 @@ EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* 
   const int nb = (S + 63) / 64;
   lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
   if (g_lrp_attn_x6) {
-    lrp_attn_dkdv_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-    lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+    if (g_lrp_attn_x6 == 2) {   // double-buffered staging
+      lrp_attn_dkdv_x6_kernel<true><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+      lrp_attn_dq_x6_kernel<true><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+    } else {
+      lrp_attn_dkdv_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+      lrp_attn_dq_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+    }
   } else {
     lrp_attn_dkdv_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
     lrp_attn_dq_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);

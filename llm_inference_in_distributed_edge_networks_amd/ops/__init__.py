@@ -692,8 +692,8 @@ def lrp_attn_bwd(q, k, v, o, dO, lse):
 
 
 def set_lrp_attn_x6(on) -> None:
-    """fp32 AttnLRP attention backward: the bf16 matrix-core sweeps on three-plane splits (1, default) or the f32
-    MFMA sweeps (0).  A/B and tests."""
+    """fp32 AttnLRP attention backward: the bf16 matrix-core sweeps on three-plane splits (1, default; 2 the same
+    with double-buffered staging) or the f32 MFMA sweeps (0).  A/B and tests."""
     call("edge_lrp_attn_set_x6", int(on))
 
 
