@@ -301,6 +301,10 @@ __device__ __forceinline__ int x6sw(int r) { return (((r >> 1) & 1) << 1) | ((((
 __device__ __forceinline__ f32x4_t mfma_bf16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// exp(d) for d = score - lse <= ~0 as v_exp_f32(d log2 e): the rounding of the product moves the exponent by
+// |d| 2^-24, so the error relative to the row's largest probability stays below 2^-24 / e (the IEEE expf's range
+// reduction was ~10 VALU per value, a fifth of the sweeps' VALU).  d = -inf (masked / padded rows) gives 0.
+__device__ __forceinline__ float x6_exp(float d) { return __builtin_amdgcn_exp2f(d * 1.4426950408889634f); }
 __device__ __forceinline__ f32x4_t x6dot(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4_t c) {
   c = mfma_bf16(a[2], b[0], c);
   c = mfma_bf16(a[0], b[2], c);
@@ -424,6 +428,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
   const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
   const int key = kb * 64 + wave * 16 + cl;
   const int keyc = key < S ? key : S - 1;
+  const int wkey_max = kb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16 + 15;   // the wave's last key (scalar)
   bf16x8_t kf[2][3], vf[2][3];
   row_frags(k + (((size_t)b * Hkv + hk) * S + keyc) * 64, kf, g);
   row_frags(v + (((size_t)b * Hkv + hk) * S + keyc) * 64, vf, g);
@@ -474,6 +479,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
     const float* bL = sL[cur];
     const float* bD = sD[cur];
     float pv[8], dsv[8];   // k-slot order: j < 4 -> sub-block 0 row 4g + j, j >= 4 -> sub-block 1 row 4g + j - 4
+    // no masking on tiles wholly below the diagonal of this wave's keys (a wave-uniform branch)
+    const bool full = q0 >= wkey_max && q0 + 32 <= S && wkey_max < S;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
@@ -485,13 +492,23 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
         sc = x6dot(qa, kf[ks], sc);
         da = x6dot(oa, vf[ks], da);
       }
+      if (full) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = sub * 16 + 4 * g + r, qi = q0 + ql;
-        const bool ok = qi < S && key <= qi && key < S;
-        const float pr = ok ? expf(sc[r] - bL[ql]) : 0.f;
-        pv[4 * sub + r] = pr;
-        dsv[4 * sub + r] = pr * (0.5f * da[r] - bD[ql]);
+        for (int r = 0; r < 4; ++r) {
+          const int ql = sub * 16 + 4 * g + r;
+          const float pr = x6_exp(sc[r] - bL[ql]);
+          pv[4 * sub + r] = pr;
+          dsv[4 * sub + r] = pr * (0.5f * da[r] - bD[ql]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = sub * 16 + 4 * g + r, qi = q0 + ql;
+          const bool ok = qi < S && key <= qi && key < S;
+          const float pr = ok ? x6_exp(sc[r] - bL[ql]) : 0.f;
+          pv[4 * sub + r] = pr;
+          dsv[4 * sub + r] = pr * (0.5f * da[r] - bD[ql]);
+        }
       }
     }
     bf16x8_t pf[3], dsf[3];
@@ -541,6 +558,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
   const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
   const int qi = qb * 64 + wave * 16 + cl;
   const int qic = qi < S ? qi : S - 1;
+  const int wq_min = qb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16;   // the wave's first query (scalar)
   bf16x8_t qf[2][3], of[2][3];
   row_frags(q + (((size_t)b * Hq + h) * S + qic) * 64, qf, g);
   row_frags(dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64, of, g);
@@ -581,6 +599,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
     }
     const char* bK = sK[cur];
     const char* bV = sV[cur];
+    // no masking on key tiles wholly at or below this wave's first query (a wave-uniform branch)
+    const bool full = k0 + 31 <= wq_min && wq_min + 15 < S;
     float dsv[8];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -593,12 +613,17 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
         sc = x6dot(ka, qf[ks], sc);
         da = x6dot(va, of[ks], da);
       }
+      if (full) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = k0 + sub * 16 + 4 * g + r;
-        const bool ok = qi < S && kj <= qi;
-        const float pr = ok ? expf(sc[r] - lq) : 0.f;
-        dsv[4 * sub + r] = pr * (0.5f * da[r] - dq_);
+        for (int r = 0; r < 4; ++r) dsv[4 * sub + r] = x6_exp(sc[r] - lq) * (0.5f * da[r] - dq_);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kj = k0 + sub * 16 + 4 * g + r;
+          const bool ok = qi < S && kj <= qi;
+          const float pr = ok ? x6_exp(sc[r] - lq) : 0.f;
+          dsv[4 * sub + r] = pr * (0.5f * da[r] - dq_);
+        }
       }
     }
     bf16x8_t dsf[3];
