@@ -411,21 +411,24 @@ __device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8
 // block), heaviest first; wave w owns keys kb 64 + 16 w + cl.  Per 32-query tile: S = Q K^T and dA = dO V^T with the
 // query on the C rows (the lane's K / V planes in registers for the whole sweep), P = exp(S - lse), dS = P (dA/2 - D),
 // then dV += P^T dO and dK += dS^T Q over the tile's 32 queries (P / dS the lane's A fragments, dO / Q from the
-// row-major images by transposing reads).  DB: the staging images double-buffered - tile t + 1 is stored into the
-// other buffer before tile t's MFMAs, one barrier per tile instead of two.
-template <bool DB>
+// row-major images by transposing reads).  GS: one workgroup per (b, kv head, key block) sweeps the G q heads
+// of its group and writes the group's SUM (dk, dv [B, Hkv, S, 64]; the per-q-head partials were 7x the bytes, written
+// here and re-read by the RoPE pack).  History: double-buffered staging (one barrier per tile) measured equal and was
+// dropped (profiles/r04o/ab.txt).
+template <bool GS>
 __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                                const float* __restrict__ v,
                                                                const float* __restrict__ dO,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ D, float* __restrict__ dk,
                                                                float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
-  constexpr int NBUF = DB ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) char sQ[NBUF][3 * X6P], sO[NBUF][3 * X6P];
-  __shared__ float sL[NBUF][32], sD[NBUF][32];
+  __shared__ __attribute__((aligned(16))) char sQ[3 * X6P], sO[3 * X6P];
+  __shared__ float sL[32], sD[32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int kb = blockIdx.x / (B * Hq);
-  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
+  const int G = Hq / Hkv, HH = GS ? Hkv : Hq, NH = GS ? G : 1;   // GS: the workgroup sweeps its kv head's G q heads
+  const int kb = blockIdx.x / (B * HH);
+  const int bh = blockIdx.x % (B * HH), b = bh / HH, hx = bh - b * HH;
+  const int hk = GS ? hx : hx / G, h0 = GS ? hx * G : hx;
   const int key = kb * 64 + wave * 16 + cl;
   const int keyc = key < S ? key : S - 1;
   const int wkey_max = kb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16 + 15;   // the wave's last key (scalar)
@@ -435,49 +438,33 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
   f32x4_t dka[4], dva[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
-  const float* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
-  const float* lh = lse + ((size_t)b * Hq + h) * S;
-  const float* dh = D + ((size_t)b * Hq + h) * S;
+  // (q head, 32-query tile) pairs in one flat sweep, so the prefetch crosses from one q head to the next
+  const int ntile = (S - kb * 64 + 31) / 32, nit = NH * ntile;
   X6Regs rq, ro;
   float nl = INFINITY, nd = 0.f;
-  auto fetch = [&](int q0) {   // the tile's global values into registers (a tile ahead)
-    x6_load(qh, 64, q0, S, rq);
-    x6_load(doh, (size_t)Hq * 64, q0, S, ro);
+  auto fetch = [&](int it) {   // pair it's global values into registers (a tile ahead)
+    const int hh = h0 + it / ntile, q0 = kb * 64 + 32 * (it % ntile);
+    x6_load(q + ((size_t)b * Hq + hh) * S * 64, 64, q0, S, rq);
+    x6_load(dO + (size_t)b * S * (Hq * 64) + hh * 64, (size_t)Hq * 64, q0, S, ro);
     if (tid < 32) {
       const int qi = q0 + tid;
-      nl = qi < S ? lh[qi] : INFINITY;
-      nd = qi < S ? dh[qi] : 0.f;
+      nl = qi < S ? lse[((size_t)b * Hq + hh) * S + qi] : INFINITY;
+      nd = qi < S ? D[((size_t)b * Hq + hh) * S + qi] : 0.f;
     }
   };
-  auto put = [&](int buf) {
-    x6_store(rq, sQ[buf]);
-    x6_store(ro, sO[buf]);
-    if (tid < 32) sL[buf][tid] = nl, sD[buf][tid] = nd;
-  };
-  fetch(kb * 64);
-  if constexpr (DB) {
-    put(0);
-    if (kb * 64 + 32 < S) fetch(kb * 64 + 32);
+  fetch(0);
+  for (int it = 0; it < nit; ++it) {
+    const int q0 = kb * 64 + 32 * (it % ntile);
     __syncthreads();
-  }
-  int cur = 0;
-  for (int q0 = kb * 64; q0 < S; q0 += 32, cur ^= (DB ? 1 : 0)) {
-    if constexpr (DB) {
-      if (q0 + 32 < S) {   // tile t + 1 into the other buffer (its readers passed the previous barrier)
-        put(cur ^ 1);
-        if (q0 + 64 < S) fetch(q0 + 64);
-      }
-    } else {
-      __syncthreads();
-      put(0);
-      if (q0 + 32 < S) fetch(q0 + 32);
-      __syncthreads();
-    }
-    const char* bQ = sQ[cur];
-    const char* bO = sO[cur];
-    const float* bL = sL[cur];
-    const float* bD = sD[cur];
+    x6_store(rq, sQ);
+    x6_store(ro, sO);
+    if (tid < 32) sL[tid] = nl, sD[tid] = nd;
+    if (it + 1 < nit) fetch(it + 1);
+    __syncthreads();
+    const char* bQ = sQ;
+    const char* bO = sO;
+    const float* bL = sL;
+    const float* bD = sD;
     float pv[8], dsv[8];   // k-slot order: j < 4 -> sub-block 0 row 4g + j, j >= 4 -> sub-block 1 row 4g + j - 4
     // no masking on tiles wholly below the diagonal of this wave's keys (a wave-uniform branch)
     const bool full = q0 >= wkey_max && q0 + 32 <= S && wkey_max < S;
@@ -522,11 +509,10 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
       dva[dt] = x6dot(pf, ob, dva[dt]);
       dka[dt] = x6dot(dsf, qb, dka[dt]);
     }
-    if constexpr (DB) __syncthreads();
   }
-  // C[row = key 16w + 4g + r][col = d 16dt + cl]
-  float* dkh = dk + ((size_t)b * Hq + h) * S * 64;
-  float* dvh = dv + ((size_t)b * Hq + h) * S * 64;
+  // C[row = key 16w + 4g + r][col = d 16dt + cl]; GS: the kv head's sum over its q heads, else the q head's partial
+  float* dkh = dk + ((size_t)b * HH + hx) * S * 64;
+  float* dvh = dv + ((size_t)b * HH + hx) * S * 64;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int kr = kb * 64 + wave * 16 + g * 4 + r;
@@ -543,15 +529,12 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
 // dQ (inputs and output as lrp_attn_dq_f32_kernel).  Workgroup = (b, h, 64-query block), heaviest (last) first; wave
 // w owns queries qb 64 + 16 w + cl.  Per 32-key tile: S^T = K Q^T and dA^T = V dO^T with the key on the C rows (the
 // lane's Q / dO planes in registers), dS^T = P^T (dA^T/2 - D), then dQ^T += K^T dS^T over the tile's 32 keys.
-// DB as the dK / dV kernel.
-template <bool DB>
 __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                              const float* __restrict__ v, const float* __restrict__ dO,
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ D, float* __restrict__ dq,
                                                              int B, int Hq, int Hkv, int S) {
-  constexpr int NBUF = DB ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) char sK[NBUF][3 * X6P], sV[NBUF][3 * X6P];
+  __shared__ __attribute__((aligned(16))) char sK[3 * X6P], sV[3 * X6P];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int nqb = (S + 63) / 64;
   const int qb = nqb - 1 - blockIdx.x / (B * Hq);
@@ -576,29 +559,14 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
     x6_load(vh, 64, k0, S, rv);
   };
   fetch(0);
-  if constexpr (DB) {
-    x6_store(rk, sK[0]);
-    x6_store(rv, sV[0]);
-    if (32 < kend) fetch(32);
+  for (int k0 = 0; k0 < kend; k0 += 32) {
     __syncthreads();
-  }
-  int cur = 0;
-  for (int k0 = 0; k0 < kend; k0 += 32, cur ^= (DB ? 1 : 0)) {
-    if constexpr (DB) {
-      if (k0 + 32 < kend) {   // tile t + 1 into the other buffer (its readers passed the previous barrier)
-        x6_store(rk, sK[cur ^ 1]);
-        x6_store(rv, sV[cur ^ 1]);
-        if (k0 + 64 < kend) fetch(k0 + 64);
-      }
-    } else {
-      __syncthreads();
-      x6_store(rk, sK[0]);
-      x6_store(rv, sV[0]);
-      if (k0 + 32 < kend) fetch(k0 + 32);   // the next key tile's values under this tile's MFMAs
-      __syncthreads();
-    }
-    const char* bK = sK[cur];
-    const char* bV = sV[cur];
+    x6_store(rk, sK);
+    x6_store(rv, sV);
+    if (k0 + 32 < kend) fetch(k0 + 32);   // the next key tile's values under this tile's MFMAs
+    __syncthreads();
+    const char* bK = sK;
+    const char* bV = sV;
     // no masking on key tiles wholly at or below this wave's first query (a wave-uniform branch)
     const bool full = k0 + 31 <= wq_min && wq_min + 15 < S;
     float dsv[8];
@@ -634,7 +602,6 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
       tr_frags(bK, dt, g, cl, kt);
       acc[dt] = x6dot(kt, dsf, acc[dt]);
     }
-    if constexpr (DB) __syncthreads();
   }
   // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
   if (qi < S) {
@@ -654,7 +621,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
 __device__ __forceinline__ float rope_pack_value(const float* __restrict__ dq, const float* __restrict__ dk,
                                                  const float* __restrict__ dv, const float* __restrict__ cosT,
                                                  const float* __restrict__ sinT, int b, int s, int c, int S, int Hq,
-                                                 int Hkv, int rot_dim, float q_scale) {
+                                                 int Hkv, int rot_dim, float q_scale, int ksum) {
   const int hh = c >> 6, d = c & 63, G = Hq / Hkv;
   const float* src;
   float scale = 1.f;
@@ -664,11 +631,12 @@ __device__ __forceinline__ float rope_pack_value(const float* __restrict__ dq, c
     src = dq + (((size_t)b * Hq + hh) * S + s) * 64;
     scale = q_scale;
   } else if (hh < Hq + Hkv) {
-    src = dk + (((size_t)b * Hq + (hh - Hq) * G) * S + s) * 64;
-    ng = G;
+    src = ksum ? dk + (((size_t)b * Hkv + (hh - Hq)) * S + s) * 64 : dk + (((size_t)b * Hq + (hh - Hq) * G) * S + s) * 64;
+    ng = ksum ? 1 : G;
   } else {
-    src = dv + (((size_t)b * Hq + (hh - Hq - Hkv) * G) * S + s) * 64;
-    ng = G;
+    src = ksum ? dv + (((size_t)b * Hkv + (hh - Hq - Hkv)) * S + s) * 64
+               : dv + (((size_t)b * Hq + (hh - Hq - Hkv) * G) * S + s) * 64;
+    ng = ksum ? 1 : G;
     rope = false;
   }
   const int half = rot_dim >> 1;
@@ -695,7 +663,7 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_h3_kernel(const float* __re
                                                                const float* __restrict__ sinT, f16_t* __restrict__ out,
                                                                float* __restrict__ rinv,
                                                                const float* __restrict__ post, int B, int S, int Hq,
-                                                               int Hkv, int rot_dim, float q_scale) {
+                                                               int Hkv, int rot_dim, float q_scale, int ksum) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B * S) return;
   const int b = row / S, s = row - b * S, W = (Hq + 2 * Hkv) * 64;
@@ -705,12 +673,12 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_h3_kernel(const float* __re
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int c = lane + 64 * it;
-      cache[it] = c < W ? rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale) : 0.f;
+      cache[it] = c < W ? rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale, ksum) : 0.f;
       mx = fmaxf(mx, fabsf(cache[it]));
     }
   } else {
     for (int c = lane; c < W; c += 64)
-      mx = fmaxf(mx, fabsf(rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale)));
+      mx = fmaxf(mx, fabsf(rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale, ksum)));
   }
   mx = wave_max(mx);
   float inv;
@@ -730,7 +698,7 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_h3_kernel(const float* __re
     }
   } else {
     for (int c = lane; c < W; c += 64)
-      put(c, rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale));
+      put(c, rope_pack_value(dq, dk, dv, cosT, sinT, b, s, c, S, Hq, Hkv, rot_dim, q_scale, ksum));
   }
   if (lane == 0) rinv[row] = inv * (post ? post[row] : 1.f);
 }
@@ -746,7 +714,7 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_h3_v4_kernel(const float* _
                                                                   const float* __restrict__ sinT,
                                                                   f16_t* __restrict__ out, float* __restrict__ rinv,
                                                                   const float* __restrict__ post, int B, int S, int Hq,
-                                                                  int Hkv, int rot_dim, float q_scale) {
+                                                                  int Hkv, int rot_dim, float q_scale, int ksum) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B * S) return;
   const int b = row / S, s = row - b * S, W = (Hq + 2 * Hkv) * 64, G = Hq / Hkv, half = rot_dim >> 1;
@@ -767,11 +735,13 @@ __global__ __launch_bounds__(256) void lrp_rope_pack_h3_v4_kernel(const float* _
       src = dq + (((size_t)b * Hq + hh) * S + s) * 64;
       scale = q_scale;
     } else if (hh < Hq + Hkv) {
-      src = dk + (((size_t)b * Hq + (hh - Hq) * G) * S + s) * 64;
-      ng = G;
+      src = ksum ? dk + (((size_t)b * Hkv + (hh - Hq)) * S + s) * 64
+                 : dk + (((size_t)b * Hq + (hh - Hq) * G) * S + s) * 64;
+      ng = ksum ? 1 : G;
     } else {
-      src = dv + (((size_t)b * Hq + (hh - Hq - Hkv) * G) * S + s) * 64;
-      ng = G;
+      src = ksum ? dv + (((size_t)b * Hkv + (hh - Hq - Hkv)) * S + s) * 64
+                 : dv + (((size_t)b * Hq + (hh - Hq - Hkv) * G) * S + s) * 64;
+      ng = ksum ? 1 : G;
       rope = false;
     }
     const bool rot = rope && d < rot_dim;
@@ -1052,13 +1022,8 @@ EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* 
   const int nb = (S + 63) / 64;
   lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
   if (g_lrp_attn_x6) {
-    if (g_lrp_attn_x6 == 2) {   // double-buffered staging
-      lrp_attn_dkdv_x6_kernel<true><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-      lrp_attn_dq_x6_kernel<true><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
-    } else {
-      lrp_attn_dkdv_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-      lrp_attn_dq_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
-    }
+    lrp_attn_dkdv_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+    lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
   } else {
     lrp_attn_dkdv_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
     lrp_attn_dq_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
@@ -1066,32 +1031,58 @@ EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* 
   return (int)hipGetLastError();
 }
 
+// edge_lrp_attn_bwd_f32 with dk, dv as the GQA group SUMS [B, Hkv, S, 64] (x6 sweeps only: check
+// edge_lrp_attn_gqa_sum_ok first).
+EDGE_API int edge_lrp_attn_bwd_f32_gs(const float* q, const float* k, const float* v, const float* o, const float* dO,
+                                      const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, int B,
+                                      int Hq, int Hkv, int S, hipStream_t st) {
+  if (B <= 0 || S <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv || !g_lrp_attn_x6) return (int)hipErrorInvalidValue;
+  const int nb = (S + 63) / 64;
+  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
+  lrp_attn_dkdv_x6_kernel<true><<<B * Hkv * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+  lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+  return (int)hipGetLastError();
+}
+EDGE_API int edge_lrp_attn_gqa_sum_ok() { return g_lrp_attn_x6 != 0; }
+
 // A/B and tests: 1 = the bf16 matrix-core (x6) sweeps (default), 0 = the f32-MFMA sweeps
 EDGE_API int edge_lrp_attn_set_x6(int on) {
   g_lrp_attn_x6 = on;
   return 0;
 }
 
-EDGE_API int edge_lrp_rope_pack_h3(const float* dq, const float* dk, const float* dv, const float* cosT,
-                                   const float* sinT, void* out, float* rinv, const float* post, int B, int S, int Hq,
-                                   int Hkv, int rot_dim, float q_scale, hipStream_t st) {
+static int rope_pack_h3(const float* dq, const float* dk, const float* dv, const float* cosT, const float* sinT,
+                        void* out, float* rinv, const float* post, int B, int S, int Hq, int Hkv, int rot_dim,
+                        float q_scale, int ksum, hipStream_t st) {
   const int R = B * S;
   if (R <= 0) return 0;
   if (rot_dim > 64 || rot_dim % 2 || Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
   const int W = (Hq + 2 * Hkv) * 64;
   if (rot_dim % 8 == 0 && W <= 1280) {   // Qwen2-0.5B: W = 1152, 5 column groups per lane
     lrp_rope_pack_h3_v4_kernel<5><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S,
-                                                                Hq, Hkv, rot_dim, q_scale);
+                                                                Hq, Hkv, rot_dim, q_scale, ksum);
   } else if (rot_dim % 8 == 0 && W <= 2048) {
     lrp_rope_pack_h3_v4_kernel<8><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S,
-                                                                Hq, Hkv, rot_dim, q_scale);
+                                                                Hq, Hkv, rot_dim, q_scale, ksum);
   } else if (W <= 2048)
     lrp_rope_pack_h3_kernel<32><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S,
-                                                              Hq, Hkv, rot_dim, q_scale);
+                                                              Hq, Hkv, rot_dim, q_scale, ksum);
   else
     lrp_rope_pack_h3_kernel<0><<<(R + 3) / 4, 256, 0, st>>>(dq, dk, dv, cosT, sinT, (f16_t*)out, rinv, post, B, S, Hq,
-                                                             Hkv, rot_dim, q_scale);
+                                                             Hkv, rot_dim, q_scale, ksum);
   return (int)hipGetLastError();
+}
+EDGE_API int edge_lrp_rope_pack_h3(const float* dq, const float* dk, const float* dv, const float* cosT,
+                                   const float* sinT, void* out, float* rinv, const float* post, int B, int S, int Hq,
+                                   int Hkv, int rot_dim, float q_scale, hipStream_t st) {
+  return rope_pack_h3(dq, dk, dv, cosT, sinT, out, rinv, post, B, S, Hq, Hkv, rot_dim, q_scale, 0, st);
+}
+// the same from dk, dv already summed over each GQA group ([B, Hkv, S, 64], edge_lrp_attn_bwd_f32_gs)
+EDGE_API int edge_lrp_rope_pack_h3_gs(const float* dq, const float* dk, const float* dv, const float* cosT,
+                                      const float* sinT, void* out, float* rinv, const float* post, int B, int S,
+                                      int Hq, int Hkv, int rot_dim, float q_scale, hipStream_t st) {
+  return rope_pack_h3(dq, dk, dv, cosT, sinT, out, rinv, post, B, S, Hq, Hkv, rot_dim, q_scale, 1, st);
 }
 
 EDGE_API int edge_split_h3_dyn(const float* x, void* out, float* rinv, const float* post, int R, int K, hipStream_t st) {

@@ -671,29 +671,48 @@ def linear_rowscale(x: torch.Tensor, w: torch.Tensor, rscale: torch.Tensor, resi
     return out
 
 
-def lrp_attn_bwd(q, k, v, o, dO, lse):
+def lrp_gqa_sum_native(t: torch.Tensor) -> bool:
+    """True when ``lrp_attn_bwd(..., gqa_sum=True)`` computes the GQA group sums in the kernel for tensors like ``t``
+    (fp32 on the GPU with the x6 sweeps; False for an A/B build that predates it)."""
+    if not _gpu(t) or t.dtype != torch.float32:
+        return False
+    L = lib()
+    return hasattr(L, "edge_lrp_attn_gqa_sum_ok") and bool(L.edge_lrp_attn_gqa_sum_ok())
+
+
+def lrp_attn_bwd(q, k, v, o, dO, lse, gqa_sum: bool = False):
     """-> (D [B,Hq,S], rel [B,Hq], dq, dk, dv [B,Hq,S,64]) fp32 (dk/dv per-q-head partials); see
-    ``reference.lrp_attn_bwd``."""
-    if not _gpu(q):
-        return ref.lrp_attn_bwd(q, k, v, o, dO, lse)
-    fp32 = q.dtype == torch.float32
-    (_check_f32 if fp32 else _check_bf16)(q, k, v, o, dO)
+    ``reference.lrp_attn_bwd``.  ``gqa_sum``: dk, dv as the sums over each GQA group, [B,Hkv,S,64] (the fp32 x6
+    sweeps compute them directly; elsewhere the partials are summed)."""
     B, Hq, S, D = q.shape
     Hkv = k.shape[1]
+    if not _gpu(q):
+        Dl, rel, dq, dk, dv = ref.lrp_attn_bwd(q, k, v, o, dO, lse)
+        if gqa_sum:
+            dk, dv = (t.view(B, Hkv, Hq // Hkv, S, D).sum(2) for t in (dk, dv))
+        return Dl, rel, dq, dk, dv
+    fp32 = q.dtype == torch.float32
+    (_check_f32 if fp32 else _check_bf16)(q, k, v, o, dO)
     assert D == 64 and k.shape == v.shape == (B, Hkv, S, D) and o.shape == dO.shape == (B * S, Hq * D)
     assert lse.shape == (B, Hq, S) and lse.dtype == torch.float32 and lse.is_contiguous()
     f32 = dict(dtype=torch.float32, device=q.device)
     Dl, rel = torch.empty(B, Hq, S, **f32), torch.empty(B, Hq, **f32)
     dq = torch.empty(B, Hq, S, D, **f32)
+    args = (ptr(q), ptr(k), ptr(v), ptr(o), ptr(dO), ptr(lse), ptr(Dl), ptr(rel), ptr(dq))
+    if gqa_sum and lrp_gqa_sum_native(q):
+        dk, dv = torch.empty(B, Hkv, S, D, **f32), torch.empty(B, Hkv, S, D, **f32)
+        call("edge_lrp_attn_bwd_f32_gs", *args, ptr(dk), ptr(dv), B, Hq, Hkv, S, stream())
+        return Dl, rel, dq, dk, dv
     dk, dv = torch.empty(B, Hq, S, D, **f32), torch.empty(B, Hq, S, D, **f32)
-    call("edge_lrp_attn_bwd_f32" if fp32 else "edge_lrp_attn_bwd", ptr(q), ptr(k), ptr(v), ptr(o), ptr(dO), ptr(lse),
-         ptr(Dl), ptr(rel), ptr(dq), ptr(dk), ptr(dv), B, Hq, Hkv, S, stream())
+    call("edge_lrp_attn_bwd_f32" if fp32 else "edge_lrp_attn_bwd", *args, ptr(dk), ptr(dv), B, Hq, Hkv, S, stream())
+    if gqa_sum:
+        dk, dv = (t.view(B, Hkv, Hq // Hkv, S, D).sum(2) for t in (dk, dv))
     return Dl, rel, dq, dk, dv
 
 
 def set_lrp_attn_x6(on) -> None:
-    """fp32 AttnLRP attention backward: the bf16 matrix-core sweeps on three-plane splits (1, default; 2 the same
-    with double-buffered staging) or the f32 MFMA sweeps (0).  A/B and tests."""
+    """fp32 AttnLRP attention backward: the bf16 matrix-core sweeps on three-plane splits (1, default) or the f32
+    MFMA sweeps (0).  A/B and tests."""
     call("edge_lrp_attn_set_x6", int(on))
 
 
@@ -809,14 +828,16 @@ def lrp_gelu_bwd_h3(dy: torch.Tensor, a: torch.Tensor):
 
 
 def lrp_rope_pack_h3(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, post=None):
-    """Inverse RoPE + q scale + GQA sum + token-major scatter (fp32) -> (h3 d[q|k|v] [B*S, 2(Hq+2Hkv)64], rinv)."""
+    """Inverse RoPE + q scale + GQA sum + token-major scatter (fp32) -> (h3 d[q|k|v] [B*S, 2(Hq+2Hkv)64], rinv).
+    dk, dv: per-q-head partials [B,Hq,S,64] or already the GQA group sums [B,Hkv,S,64]."""
     if not _gpu(dq):
         return ref.lrp_rope_pack_h3(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, post)
     _check_f32(dq, dk, dv, cos, sin)
-    assert dq.shape == dk.shape == dv.shape == (B, Hq, S, 64)
+    assert dq.shape == (B, Hq, S, 64) and dk.shape == dv.shape and dk.shape in ((B, Hq, S, 64), (B, Hkv, S, 64))
+    summed = dk.shape[1] == Hkv and Hq != Hkv
     out, rinv = _rows_out(B * S, (Hq + 2 * Hkv) * 64, dq.device)
-    call("edge_lrp_rope_pack_h3", ptr(dq), ptr(dk), ptr(dv), ptr(cos), ptr(sin), ptr(out), ptr(rinv),
-         ptr(_post(post, B * S)), B, S, Hq, Hkv, rot_dim, float(q_scale), stream())
+    call("edge_lrp_rope_pack_h3_gs" if summed else "edge_lrp_rope_pack_h3", ptr(dq), ptr(dk), ptr(dv), ptr(cos),
+         ptr(sin), ptr(out), ptr(rinv), ptr(_post(post, B * S)), B, S, Hq, Hkv, rot_dim, float(q_scale), stream())
     return out, rinv
 
 

@@ -93,6 +93,9 @@ _SIGS = {
     "edge_lrp_attn_set_x6": [c_i],
     "edge_lrp_attn_bwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_lrp_rope_pack_h3": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
+    "edge_lrp_attn_bwd_f32_gs": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    "edge_lrp_attn_gqa_sum_ok": [],
+    "edge_lrp_rope_pack_h3_gs": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_split_h3_dyn": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_lrp_swiglu_bwd_h3": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_lrp_gelu_bwd_h3": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],

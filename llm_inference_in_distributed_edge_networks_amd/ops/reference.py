@@ -331,12 +331,13 @@ def rope_bwd(dx: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, rot_dim: in
 
 
 def lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, dtype=torch.float32):
-    """Inverse RoPE + q scale + GQA group sum of the dk/dv partials [B,Hq,S,D], scattered to token-major
-    d[q|k|v] [B*S, (Hq+2Hkv)*D]."""
+    """Inverse RoPE + q scale + GQA group sum of the dk/dv partials [B,Hq,S,D] (or dk/dv already summed,
+    [B,Hkv,S,D]), scattered to token-major d[q|k|v] [B*S, (Hq+2Hkv)*D]."""
     c, s_ = cos[:S], sin[:S]
     G = Hq // Hkv
-    dk = _f(dk).view(B, Hkv, G, S, -1).sum(2)
-    dv = _f(dv).view(B, Hkv, G, S, -1).sum(2)
+    if dk.shape[1] == Hq:   # per-q-head partials (else already the group sums [B, Hkv, S, D])
+        dk = _f(dk).view(B, Hkv, G, S, -1).sum(2)
+        dv = _f(dv).view(B, Hkv, G, S, -1).sum(2)
     dqp = rope_bwd(_f(dq) * q_scale, c, s_, rot_dim)
     dkp = rope_bwd(_f(dk), c, s_, rot_dim)
     y = torch.cat([dqp, dkp, _f(dv)], 1)                     # [B, Ht, S, D]

@@ -172,7 +172,9 @@ class RelevanceEngineH3:
                 dy = torch.zeros(B * S, H, dtype=dy.dtype, device=dy.device).index_copy_(0, rows, dy)
                 if not self.qwen:
                     dh2 = torch.zeros(B * S, H, dtype=dh2.dtype, device=dh2.device).index_copy_(0, rows, dh2)
-            _, r, dq, dk, dv = ops.lrp_attn_bwd(sv["q"], sv["k"], sv["v"], sv["o"], dO, sv["lse"])
+            # dk, dv summed over each GQA group in the kernel where it can (else the per-q-head partials)
+            _, r, dq, dk, dv = ops.lrp_attn_bwd(sv["q"], sv["k"], sv["v"], sv["o"], dO, sv["lse"],
+                                                gqa_sum=ops.lrp_gqa_sum_native(sv["q"]))
             rel[:, i] = r
             dqkv3, rinv_q = ops.lrp_rope_pack_h3(dq, dk, dv, m.cos, m.sin, B, S, Hq, Hkv, cfg.rotary_dim, m.q_scale,
                                                  post=sv["rs1"] if self.qwen else None)
