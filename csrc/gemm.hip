@@ -1848,6 +1848,72 @@ __device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[
   }
 }
 
+// bf16 QKV on the 256 x 192 tiles: the same permuted column order and RoPE pairing as qkv192_epilogue, with the fused
+// RMSNorm's row scale rq (from the producer's sum-of-squares partials), the bf16 bias, and the bf16 outputs of the
+// 128 x 128 EPI_QKV_ROPE epilogue: q (scaled) / k [B, H, S, 64], V^T [B, Hkv, 64, s_pad] (2-byte stores: the LDS
+// holds the next tile's staging here).
+template <int RH>
+__device__ __forceinline__ void qkv192_bf16_epilogue(const GemmArgs& a, f32x4_t (&c)[4][6], const float (&rq)[4],
+                                                     int m0, int n0, int lane, int vw, int wn) {
+  static_assert(RH == 0 || RH == 32, "192-wide QKV tiles: full rotary or none");
+  const int g = lane >> 4;
+  const int nw = n0 + wn * 96;
+  u32x2_t bw[6];   // all the epilogue's loads before the first store (vmcnt counts stores too)
+#pragma unroll
+  for (int j = 0; j < 6; ++j) bw[j] = *(const u32x2_t*)(a.bias + q192_feat(nw + j * 16) + g * 4);
+  int bi[4], pi[4];
+  f32x4_t cs[4][2], sn[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = min(m0 + vw * 64 + i * 16 + (lane & 15), a.M - 1);
+    bi[i] = m / a.S;
+    pi[i] = m - bi[i] * a.S;
+    if constexpr (RH == 32) {
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        cs[i][hf] = *(const f32x4_t*)(a.cosT + pi[i] * 32 + hf * 16 + g * 4);
+        sn[i][hf] = *(const f32x4_t*)(a.sinT + pi[i] * 32 + hf * 16 + g * 4);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + vw * 64 + i * 16 + (lane & 15);
+    if (m >= a.M) continue;
+    const int b = bi[i], pos = pi[i];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int col = nw + 32 * p;                       // block 2p: q = 0 or 2 of its head
+      const int head = col >> 6;                         // wave-uniform
+      const int hf = ((col >> 4) & 3) ? 1 : 0;           // low-half dims d .. d+3 (d = 16 hf + 4g), partners d+32
+      const int d = hf * 16 + g * 4;
+      const u32x2_t bl = bw[2 * p], bh = bw[2 * p + 1];
+      f32x4_t lo = c[i][2 * p] * rq[i] + f32x4_t{bf_lo(bl[0]), bf_hi(bl[0]), bf_lo(bl[1]), bf_hi(bl[1])};
+      f32x4_t hi = c[i][2 * p + 1] * rq[i] + f32x4_t{bf_lo(bh[0]), bf_hi(bh[0]), bf_lo(bh[1]), bf_hi(bh[1])};
+      if (head < a.Hq + a.Hkv) {
+        if constexpr (RH == 32) {
+          const f32x4_t cv = hf ? cs[i][1] : cs[i][0], sv = hf ? sn[i][1] : sn[i][0];
+          const f32x4_t l2 = lo * cv - hi * sv;
+          hi = hi * cv + lo * sv;
+          lo = l2;
+        }
+        const float sc = head < a.Hq ? a.q_scale : 1.f;
+        bf16_t* dst = head < a.Hq ? a.qout + (((size_t)b * a.Hq + head) * a.S + pos) * 64
+                                  : a.kout + (((size_t)b * a.Hkv + (head - a.Hq)) * a.S + pos) * 64;
+        *(u32x2_t*)(dst + d) = u32x2_t{pack_bf2(lo[0] * sc, lo[1] * sc), pack_bf2(lo[2] * sc, lo[3] * sc)};
+        *(u32x2_t*)(dst + d + 32) = u32x2_t{pack_bf2(hi[0] * sc, hi[1] * sc), pack_bf2(hi[2] * sc, hi[3] * sc)};
+      } else {
+        bf16_t* dst = a.vtout + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dst[(size_t)(d + r) * a.s_pad] = f2bf(lo[r]);
+          dst[(size_t)(d + 32 + r) * a.s_pad] = f2bf(hi[r]);
+        }
+      }
+    }
+  }
+}
+
 // fp32-output epilogue of the four-wave 256x224 kernel (O-projection / down + fp32 residual): the wave's 128 x 112
 // block in four pairs of 16-row groups, the residual (and row-scale) loads running two pairs ahead of the stores.
 // (vmcnt counts stores too: with each pair's loads issued after the previous pair's stores, every wait drained those
@@ -1927,7 +1993,8 @@ template <int EPI, int RH, int PF, int BN, bool PB = false, bool DS = false>
 __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   static_assert(!DS || PF == 0, "desync: no prefetch stream");
   static_assert(!PB || (epi_f32(EPI) && PF == 0), "paired B: h3 GEMMs without the prefetch stream");
-  static_assert(BN != 192 || (EPI == EPI_F32_QKV_ROPE && (RH == 0 || RH == 32)), "192-wide tiles: fp32 QKV only");
+  static_assert(BN != 192 || ((EPI == EPI_F32_QKV_ROPE || EPI == EPI_QKV_ROPE) && (RH == 0 || RH == 32)),
+                "192-wide tiles: QKV only");
   static_assert(BN == 192 || BN == 224 || BN == 256, "tile width");
   using Gm = w4::Geo<BN>;
   constexpr int NJ = Gm::NJ, NB = Gm::NB, BOFF = Gm::BOFF, TB = Gm::TB, NR = Gm::NR, MF = Gm::MF;
@@ -2173,7 +2240,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   };
   float rs[8];
   auto load_rs = [&](int mt) {
-    if constexpr (BN == 256) {
+    if constexpr (BN == 256 || BN == 192) {
       if constexpr (EPI == EPI_QKV_ROPE) {
         if (a.ssq_in) {   // fused RMSNorm from the producer's sum-of-squares partials (the bf16 QKV GEMM)
           if (a.ssq_parts == 8) rscale_from_partials<8, 128, 8>(a, mt, wm, lane, rs);
@@ -2283,7 +2350,12 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
               c[i][j] = acc[ih * 4 + i][j];
               asm volatile("" : "+v"(c[i][j]));
             }
-          qkv192_epilogue<RH>(a, c, m0, n0, lane, wm * 2 + ih, wn);
+          if constexpr (EPI == EPI_QKV_ROPE) {
+            const float rq[4] = {rs[ih * 4], rs[ih * 4 + 1], rs[ih * 4 + 2], rs[ih * 4 + 3]};
+            qkv192_bf16_epilogue<RH>(a, c, rq, m0, n0, lane, wm * 2 + ih, wn);
+          } else {
+            qkv192_epilogue<RH>(a, c, m0, n0, lane, wm * 2 + ih, wn);
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
       } else if constexpr (epi_f32(EPI)) {
@@ -2668,6 +2740,7 @@ static int launch_4w(const GemmArgs& a, hipStream_t st) {
 static int g_qkv256 = 1;  // QKV+RoPE GEMMs on the four-wave 256x256 kernel when it fills the chip (else 128x128):
                           // 0 never, 1 the fp32-mode QKV, 2 both
 static int g_qkv192 = 1;  // fp32-mode QKV on 256x192 tiles when 192 divides N and 256 does not (A/B: 0 = 256x256)
+static int g_qkv192_bf16 = 0;   // bf16 QKV on the four-wave 256x192 tiles (A/B: 0 = the 128x128 kernel)
 static int g_w7 = 2;  // 256x224 tiles for N % 224 == 0 shapes that 256 does not divide (N = 896): 1 eight-wave
                       // 64x112 wave tiles, 2 four-wave 128x112 wave tiles (default: 10-17 % faster on N = 896)
 
@@ -2732,12 +2805,13 @@ static int launch(const GemmArgs& args, hipStream_t st) {
     // the XCD-chunked tile walk: N = 1152 is 4.5 column tiles, and keeping an XCD's rounds inside one GROUP_M band
     // re-uses its A panels from L2 (h3 QKV at M = 32768: 144 vs 159 us strided, profiles/r02h_gemm_explore.log)
     if (g_walk == 1) a.walk = 2;
-    if constexpr (EPI == EPI_F32_QKV_ROPE && (RH == 0 || RH == 32)) {
+    if constexpr (RH == 0 || RH == 32) {
       // 256x192 tiles when 192 divides N and 256 does not (N = 1152: 768 tiles, 3 full rounds)
       const long long t192 = (long long)((a.M + 255) / 256) * (a.N / 192);
+      const bool on192 = EPI == EPI_F32_QKV_ROPE ? on && g_qkv192 : g_qkv192_bf16 != 0;
       // (tile override 192 forces it at any M, for tests)
       if (a.N % 192 == 0 && a.N % 256 &&
-          (g_tile_override == 192 || (on && g_qkv192 && t192 >= 256 && !g_tile_override)))
+          (g_tile_override == 192 || (on192 && t192 >= 256 && !g_tile_override)))
         return launch_4w<EPI, RH, 0, 192>(a, st);
     }
     if (on && tiles >= 256 && g_tile_override != 128) return launch_4w<EPI, RH>(a, st);
@@ -2819,6 +2893,10 @@ EDGE_API int edge_gemm_set_qkv256(int on) {
   return 0;
 }
 
+EDGE_API int edge_gemm_set_qkv192_bf16(int on) {
+  g_qkv192_bf16 = on;
+  return 0;
+}
 EDGE_API int edge_gemm_set_qkv192(int on) {
   g_qkv192 = on;
   return 0;

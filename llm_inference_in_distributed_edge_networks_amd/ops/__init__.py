@@ -202,6 +202,12 @@ def set_gemm_qkv192(on) -> None:
     call("edge_gemm_set_qkv192", int(on))
 
 
+def set_gemm_qkv192_bf16(on) -> None:
+    """bf16 QKV+RoPE GEMMs on the four-wave 256x192 tiles (fused RMSNorm row scale, bf16 q / k / V^T) when they fill
+    the chip, instead of the 128x128 kernel.  A/B and tests."""
+    call("edge_gemm_set_qkv192_bf16", int(on))
+
+
 def set_gemm_stagger(k: int) -> None:
     """Four-wave GEMMs (A/B): the odd workgroups of each XCD start k x 1024 cycles late, so the chip-wide epilogue
     store bursts split in two (0 = off, the default)."""

@@ -38,6 +38,7 @@ _SIGS = {
     "edge_gemm_set_w7": [c_i],
     "edge_gemm_set_qkv256": [c_i],
     "edge_gemm_set_qkv192": [c_i],
+    "edge_gemm_set_qkv192_bf16": [c_i],
     "edge_gemm_set_skip_epi": [c_i],
     "edge_gemm_set_rs_lds": [c_i],
     "edge_gemm_set_lse256": [c_i],
@@ -138,6 +139,9 @@ def _apply_tuning_env(L) -> None:
     lx = os.environ.get("EDGE_LRP_ATTN_X6")  # fp32 AttnLRP attention backward: 1 bf16-plane sweeps, 0 f32 MFMA
     if lx and hasattr(L, "edge_lrp_attn_set_x6"):
         L.edge_lrp_attn_set_x6(int(lx))
+    qb = os.environ.get("EDGE_GEMM_QKV192_BF16")  # bf16 QKV on the four-wave 256x192 tiles (1) or 128x128 (0)
+    if qb and hasattr(L, "edge_gemm_set_qkv192_bf16"):
+        L.edge_gemm_set_qkv192_bf16(int(qb))
     sp = os.environ.get("EDGE_GEMM_SPLIT")  # four-wave GEMM epilogue desync: -1 auto, 0 off, k K-tiles
     if sp and hasattr(L, "edge_gemm_set_split"):
         L.edge_gemm_set_split(int(sp))

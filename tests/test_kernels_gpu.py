@@ -365,6 +365,34 @@ def test_qkv_rope_fused_norm(B, S, mode, rot):
         ops.set_gemm_qkv256(1)
 
 
+@pytest.mark.parametrize("B,S,norm", [(64, 512, True), (2, 256, True), (2, 512, False), (3, 100, True)])
+def test_qkv_rope_bf16_192(B, S, norm):
+    """bf16 QKV on the four-wave 256x192 tiles (permuted head blocks, RoPE pairs in one lane, fused RMSNorm row scale
+    from the ssq partials, bf16 q / k / V^T): the production shape by the switch, small shapes (partial row tiles,
+    S not a multiple of 64, no norm) by the tile override."""
+    Hq, Hkv, Hd = 14, 2, 896
+    cos, sin = R.rope_tables(1024, 64, 1e6)
+    ops.set_gemm_qkv192_bf16(1)
+    if B * S < 64 * 512:
+        ops.set_gemm_tile(192)
+    try:
+        if norm:
+            _qkv_case(B, S, Hq, Hkv, Hd, cos, sin, 64)
+        else:
+            x = rnd(B * S, Hd, seed=30)
+            N = (Hq + 2 * Hkv) * 64
+            w, b = rnd(N, Hd, s=0.04, seed=31), rnd(N, s=0.3, seed=32)
+            q, k, vt = ops.qkv_rope(x.to(DEV), w.to(DEV), b.to(DEV), cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv, 64, 64,
+                                    0.125)
+            rq, rk, rvt = R.qkv_rope(x, w, b, cos, sin, B, S, Hq, Hkv, 64, 64, 0.125)
+            close(q, rq, atol=2e-2, rtol=2e-2)
+            close(k, rk, atol=3e-2, rtol=2e-2)
+            close(vt, rvt, atol=3e-2, rtol=2e-2)
+    finally:
+        ops.set_gemm_qkv192_bf16(0)
+        ops.set_gemm_tile(0)
+
+
 def _qkv_case(B, S, Hq, Hkv, Hd, cos, sin, rot):
     x = rnd(B * S, Hd, seed=96)
     nw = rnd(Hd, s=0.1, seed=97) + 1
