@@ -126,6 +126,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __rest
   const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
   const int key = kb * 64 + wave * 16 + cl;          // this lane's key (B-operand column / A-operand row)
   const int keyc = key < S ? key : S - 1;
+  const int wkey_max = kb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16 + 15;   // the wave's last key (scalar)
   const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
   const bf16_t* vh = v + ((size_t)b * Hkv + hk) * S * 64;
   bf16x8_t kB[2], vB[2];
@@ -174,15 +175,25 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_kernel(const bf16_t* __rest
           da = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(sO, sub * 16 + cl, ks * 32 + g * 8), vB[ks], da,
                                                         0, 0, 0);
         }
-        // s[r] = score(query = q0 + sub*16 + 4g + r, key)
+        // s[r] = score(query = q0 + sub*16 + 4g + r, key); no masking on tiles wholly below this wave's keys
+        if (q0 >= wkey_max && q0 + 32 <= S && wkey_max < S) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = sub * 16 + g * 4 + r;
-          const int qi = q0 + ql;
-          const bool ok = qi < S && key <= qi && key < S;
-          const float pr = ok ? __expf(s[r] - sL[ql]) : 0.f;
-          p[sub][r] = pr;
-          ds[sub][r] = pr * (0.5f * da[r] - sD[ql]);
+          for (int r = 0; r < 4; ++r) {
+            const int ql = sub * 16 + g * 4 + r;
+            const float pr = __expf(s[r] - sL[ql]);
+            p[sub][r] = pr;
+            ds[sub][r] = pr * (0.5f * da[r] - sD[ql]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = sub * 16 + g * 4 + r;
+            const int qi = q0 + ql;
+            const bool ok = qi < S && key <= qi && key < S;
+            const float pr = ok ? __expf(s[r] - sL[ql]) : 0.f;
+            p[sub][r] = pr;
+            ds[sub][r] = pr * (0.5f * da[r] - sD[ql]);
+          }
         }
       }
       const bf16x8_t pf = pack8(p[0], p[1]);
@@ -226,6 +237,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_kernel(const bf16_t* __restri
   const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
   const int qi = qb * 64 + wave * 16 + cl;
   const int qic = qi < S ? qi : S - 1;
+  const int wq_min = qb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16;   // the wave's first query (scalar)
   const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
   const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
   const bf16_t* vh = v + ((size_t)b * Hkv + hk) * S * 64;
@@ -264,13 +276,18 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_kernel(const bf16_t* __restri
         da = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(sV, sub * 16 + cl, ks * 32 + g * 8), oB[ks], da, 0,
                                                       0, 0);
       }
-      // s[r] = score(key = k0 + sub*16 + 4g + r, query = qi)
+      // s[r] = score(key = k0 + sub*16 + 4g + r, query = qi); no masking on key tiles at or below this wave's queries
+      if (k0 + 31 <= wq_min && wq_min + 15 < S) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = k0 + sub * 16 + g * 4 + r;
-        const bool ok = qi < S && kj <= qi;
-        const float pr = ok ? __expf(s[r] - lq) : 0.f;
-        ds[sub][r] = pr * (0.5f * da[r] - dq_);
+        for (int r = 0; r < 4; ++r) ds[sub][r] = __expf(s[r] - lq) * (0.5f * da[r] - dq_);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kj = k0 + sub * 16 + g * 4 + r;
+          const bool ok = qi < S && kj <= qi;
+          const float pr = ok ? __expf(s[r] - lq) : 0.f;
+          ds[sub][r] = pr * (0.5f * da[r] - dq_);
+        }
       }
     }
     const bf16x8_t dsf = pack8(ds[0], ds[1]);
