@@ -71,22 +71,23 @@ __device__ __forceinline__ float gelu_ratio(float x) { return fabsf(x) > 1e-6f ?
 __global__ __launch_bounds__(256) void lrp_attn_delta_f32_kernel(const float* __restrict__ o,
                                                                  const float* __restrict__ dO, float* __restrict__ D,
                                                                  float* __restrict__ rel, int Hq, int S) {
+  // 16 lanes per token row (4 consecutive values each: every load instruction reads 4 whole 256-byte rows), the
+  // row's dot product reduced over its 16 lanes by xor shuffles
   __shared__ float red[4];
   const int bh = blockIdx.x, b = bh / Hq, h = bh - b * Hq;
+  const int sub = threadIdx.x & 15, r0 = threadIdx.x >> 4;
   float tot = 0.f;
-  for (int i = threadIdx.x; i < S; i += 256) {
-    const size_t off = ((size_t)b * S + i) * (size_t)(Hq * 64) + h * 64;
-    const f32x4_t* po = (const f32x4_t*)(o + off);
-    const f32x4_t* pd = (const f32x4_t*)(dO + off);
-    float s = 0.f;
+  for (int i = r0; i < S; i += 16) {
+    const size_t off = ((size_t)b * S + i) * (size_t)(Hq * 64) + h * 64 + sub * 4;
+    const f32x4_t a = *(const f32x4_t*)(o + off), d = *(const f32x4_t*)(dO + off);
+    float s = fmaf(a[0], d[0], fmaf(a[1], d[1], fmaf(a[2], d[2], a[3] * d[3])));
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const f32x4_t a = po[c], d = pd[c];
-      s = fmaf(a[0], d[0], fmaf(a[1], d[1], fmaf(a[2], d[2], fmaf(a[3], d[3], s))));
-    }
+    for (int x = 1; x < 16; x <<= 1) s += __shfl_xor(s, x, 64);
     s *= 0.5f;
-    D[(size_t)bh * S + i] = s;
-    tot += s;
+    if (sub == 0) {
+      D[(size_t)bh * S + i] = s;
+      tot += s;
+    }
   }
   tot = block_sum<256>(tot, red);
   if (threadIdx.x == 0) rel[bh] = tot;
