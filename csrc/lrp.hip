@@ -85,23 +85,25 @@ __device__ __forceinline__ bf16x8_t pack8(const f32x4_t& a, const f32x4_t& b) {
 __global__ __launch_bounds__(256) void lrp_attn_delta_kernel(const bf16_t* __restrict__ o,
                                                              const bf16_t* __restrict__ dO, float* __restrict__ D,
                                                              float* __restrict__ rel, int Hq, int S) {
+  // 8 lanes per token row (8 consecutive values each: every load instruction reads 8 whole 128-byte rows), the row's
+  // dot product reduced over its 8 lanes by xor shuffles
   __shared__ float red[4];
   const int bh = blockIdx.x, b = bh / Hq, h = bh - b * Hq;
+  const int sub = threadIdx.x & 7, r0 = threadIdx.x >> 3;
   float tot = 0.f;
-  for (int i = threadIdx.x; i < S; i += 256) {
-    const size_t off = ((size_t)b * S + i) * (size_t)(Hq * 64) + h * 64;
-    const u32x4_t* po = (const u32x4_t*)(o + off);
-    const u32x4_t* pd = (const u32x4_t*)(dO + off);
+  for (int i = r0; i < S; i += 32) {
+    const size_t off = ((size_t)b * S + i) * (size_t)(Hq * 64) + h * 64 + sub * 8;
+    const u32x4_t a = *(const u32x4_t*)(o + off), d = *(const u32x4_t*)(dO + off);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const u32x4_t a = po[c], d = pd[c];
+    for (int e = 0; e < 4; ++e) s += bf_lo(a[e]) * bf_lo(d[e]) + bf_hi(a[e]) * bf_hi(d[e]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) s += bf_lo(a[e]) * bf_lo(d[e]) + bf_hi(a[e]) * bf_hi(d[e]);
-    }
+    for (int x = 1; x < 8; x <<= 1) s += __shfl_xor(s, x, 64);
     s *= 0.5f;
-    D[(size_t)bh * S + i] = s;
-    tot += s;
+    if (sub == 0) {
+      D[(size_t)bh * S + i] = s;
+      tot += s;
+    }
   }
   tot = block_sum<256>(tot, red);
   if (threadIdx.x == 0) rel[bh] = tot;
