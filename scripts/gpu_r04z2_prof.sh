@@ -1,0 +1,15 @@
+# Round 4 end: kernel profile of the fp32 bench step (rocprofv3 --kernel-trace --stats), 5 steps, current tree.
+set -o pipefail
+O=gpurun_out/r04z2
+mkdir -p $O
+export TMPDIR=/tmp
+R=$PWD
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof -o run -- \
+  python3 $R/bench.py --steps 5 --warmup 2 --no-bf16 --no-fp32-weights > $R/$O/prof.log 2>&1 \
+  || { echo "profile failed"; tail -20 $R/$O/prof.log; exit 1; }
+cd $R
+python tools/prof_summary.py $(ls $O/prof/*kernel_stats.csv $O/prof/*/*kernel_stats.csv 2>/dev/null | head -1) \
+  "fp32 bench step at the end of round 4 (Qwen2-0.5B 2-stage split, 64-window micro-batches)" > $O/kernel_stats.md || true
+head -16 $O/kernel_stats.md
+exit 0
