@@ -7,7 +7,8 @@ head), computed without autograd and without any S x S tensor:
 * forward with saves: the regular fused layer kernels (QKV+RoPE with the RMSNorm row scale folded in,
   flash attention with its row LSE, O / gate-up / down GEMMs), keeping q, k, v, o, lse, the gate|up
   pre-activations and the norm row scales of every layer;
-* seed: only the B last rows carry gradient (``d hN = mx * W_head[argmax]``, detached final norm);
+* seed: only the B last rows carry gradient (``d hN = mx * W_head[argmax]``, detached final norm), so the last
+  layer runs its O projection and MLP on those rows only, forward and backward;
 * backward per layer, in reverse: input-gradient GEMMs with the transposed weights (norm row scale and
   residual in the epilogue), the SwiGLU / GELU / LayerNorm rules, and the attention backward kernel
   (``csrc/lrp.hip``) that also emits the per-(window, head) relevance ``0.5 sum_i dO_i . O_i``.
@@ -18,11 +19,17 @@ batch of B windows gives B relevance tables in one pass.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
+from ..ops._native import tuning as _tuning
 from ..models.model import DecoderLM
 
+
+# A/B (EDGE_TUNING=1 EDGE_LRP_LAST_ROWS=0): the last layer's O-proj / MLP on every row, as the other layers
+_LAST_ROWS = not (_tuning() and os.environ.get("EDGE_LRP_LAST_ROWS", "1") == "0")
 
 class RelevanceEngine:
     def __init__(self, model: DecoderLM):
@@ -57,6 +64,8 @@ class RelevanceEngine:
         x = m.embed(ids)
         emb = x
         saves = []
+        last = torch.arange(B, device=ids.device) * S + (S - 1)   # the seeded rows
+        nl = len(m.layers)
         for i, L in enumerate(m.layers):
             t = self.T[i]
             sv = {"x": x}
@@ -72,6 +81,11 @@ class RelevanceEngine:
                                         m.q_scale)
             o, lse = ops.attention(q, k, vt, S, need_lse=True)
             sv.update(q=q, k=k, v=vt[..., :S].transpose(-1, -2).contiguous(), o=o, lse=lse.contiguous())
+            if i == nl - 1 and _LAST_ROWS:   # only the seeded rows reach the seed: O-proj and MLP on those rows
+                sv["rows"] = last
+                o, x = o.index_select(0, last), x.index_select(0, last)
+                if not self.qwen:
+                    h2 = h2.index_select(0, last)
             if self.qwen:
                 y = ops.linear(o, L["wo"], residual=x, want_ssq=True)
                 ssq2 = y._edge_ssq
@@ -89,9 +103,10 @@ class RelevanceEngine:
         return emb, x, saves
 
     def _seed(self, x: torch.Tensor, B: int, S: int):
-        """Gradient of ``mx * mx`` w.r.t. the final hidden state (only the last row of each window)."""
+        """Gradient of ``mx * mx`` w.r.t. the final hidden state (x: the last row of each window, [B, H]) -> (the
+        seed gradient [B, H], the seed logits)."""
         m, cfg = self.m, self.m.cfg
-        last = x.view(B, S, -1)[:, -1].float()
+        last = x.float()
         w = m.w["norm_w"].float()
         if self.qwen:
             rstd = torch.rsqrt(last.pow(2).mean(-1, keepdim=True) + cfg.norm_eps)
@@ -107,9 +122,7 @@ class RelevanceEngine:
         g = dhN * rstd * w
         if not self.qwen:
             g = g - g.mean(-1, keepdim=True)
-        dx = torch.zeros_like(x)
-        dx.view(B, S, -1)[:, -1] = g.to(x.dtype)
-        return dx, mx
+        return g.to(x.dtype).contiguous(), mx
 
     @torch.no_grad()
     def head_relevance(self, ids: torch.Tensor, want_channels: bool = False, group: int = 64):
@@ -122,13 +135,19 @@ class RelevanceEngine:
         B, S = ids.shape
         Hq, Hkv = cfg.num_heads, cfg.num_kv_heads
         emb, x, saves = self._forward(ids)
-        dx, mx = self._seed(x, B, S)
+        if saves[-1].get("rows") is None:   # (A/B: the last layer ran on every row) seed its last rows only
+            dx, mx = self._seed(x.view(B, S, -1)[:, -1].contiguous(), B, S)
+            dx = torch.zeros(B * S, x.shape[1], dtype=dx.dtype, device=dx.device).index_copy_(
+                0, torch.arange(B, device=dx.device) * S + (S - 1), dx)
+        else:
+            dx, mx = self._seed(x, B, S)
         rel = torch.zeros(B, cfg.num_layers, Hq, dtype=torch.float32, device=m.device)
         H = cfg.hidden_size
         chan = torch.zeros(B, cfg.num_layers, H // group, dtype=torch.float32, device=m.device) if want_channels \
             else None
         for i in range(cfg.num_layers - 1, -1, -1):
             L, t, sv = m.layers[i], self.T[i], saves[i]
+            rows = sv.get("rows")   # last layer: dx is the seeded rows only [B, H]
             if self.qwen:
                 dm = ops.linear(dx, t["wdT"])
                 dy = ops.linear_rowscale(ops.lrp_swiglu_bwd(dm, sv["gu"]), t["wguT"], sv["rs2"], residual=dx)
@@ -136,6 +155,11 @@ class RelevanceEngine:
                 dh2 = ops.linear(ops.lrp_gelu_bwd(ops.linear(dx, t["wprojT"]), sv["a"]), t["wfcT"])
                 dy = dx
             dO = ops.linear(dy, t["woT"])
+            if rows is not None:   # back to every row: zero outside the seeded rows
+                dO = torch.zeros(B * S, dO.shape[1], dtype=dO.dtype, device=dO.device).index_copy_(0, rows, dO)
+                dy = torch.zeros(B * S, H, dtype=dy.dtype, device=dy.device).index_copy_(0, rows, dy)
+                if not self.qwen:
+                    dh2 = torch.zeros(B * S, H, dtype=dh2.dtype, device=dh2.device).index_copy_(0, rows, dh2)
             _, r, dq, dk, dv = ops.lrp_attn_bwd(sv["q"], sv["k"], sv["v"], sv["o"], dO, sv["lse"])
             rel[:, i] = r
             dqkv = ops.lrp_rope_pack(dq, dk, dv, m.cos, m.sin, B, S, Hq, Hkv, cfg.rotary_dim, m.q_scale,
@@ -144,7 +168,7 @@ class RelevanceEngine:
                 dx = ops.linear_rowscale(dqkv, t["wqkvT"], sv["rs1"], residual=dy)
             else:
                 dh1 = ops.linear(dqkv, t["wqkvT"])
-                dx = ops.lrp_ln_bwd(dh1, sv["rs1"], L["ln1_w"], dh2, sv["rs1"], L["ln2_w"], dx)
+                dx = ops.lrp_ln_bwd(dh1, sv["rs1"], L["ln1_w"], dh2, sv["rs1"], L["ln2_w"], dy)
             if want_channels:
                 chan[:, i] = (sv["x"].float() * dx.float()).abs().view(B, S, H // group, group).sum((1, 3))
             saves[i] = None

@@ -31,11 +31,17 @@ the tests check it against the autograd oracle ``attnlrp.head_relevance_batched`
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
+from ..ops._native import tuning as _tuning
 from ..models.model import DecoderLM
 
+
+# A/B (EDGE_TUNING=1 EDGE_LRP_LAST_ROWS=0): the last layer's O-proj / MLP on every row, as the other layers
+_LAST_ROWS = not (_tuning() and os.environ.get("EDGE_LRP_LAST_ROWS", "1") == "0")
 
 class RelevanceEngineH3:
     def __init__(self, model: DecoderLM):
@@ -93,7 +99,7 @@ class RelevanceEngineH3:
                                        cfg.rotary_dim, m.q_scale)
             o, lse = ops.attention(q, k, vt, S, need_lse=True, in_scales=(sc["att_q"], sc["att_k"], sc["o"]))
             sv.update(q=q, k=k, v=vt[..., :S].transpose(-1, -2).contiguous(), o=o, lse=lse.contiguous())
-            if i == nl - 1:   # only the seeded rows reach the seed: O-proj and MLP on those rows (x -> [B, H])
+            if i == nl - 1 and _LAST_ROWS:   # only the seeded rows reach the seed: O-proj and MLP on those rows
                 sv["rows"] = last
                 x = x.index_select(0, last)
                 if not self.qwen:
@@ -148,7 +154,12 @@ class RelevanceEngineH3:
         B, S = ids.shape
         Hq, Hkv, H = cfg.num_heads, cfg.num_kv_heads, cfg.hidden_size
         emb, x, saves = self._forward(ids)
-        dx, mx = self._seed(x, B, S)
+        if saves[-1].get("rows") is None:   # (A/B: the last layer ran on every row) seed its last rows only
+            dx, mx = self._seed(x.view(B, S, -1)[:, -1].contiguous(), B, S)
+            dx = torch.zeros(B * S, x.shape[1], dtype=dx.dtype, device=dx.device).index_copy_(
+                0, torch.arange(B, device=dx.device) * S + (S - 1), dx)
+        else:
+            dx, mx = self._seed(x, B, S)
         rel = torch.zeros(B, cfg.num_layers, Hq, dtype=torch.float32, device=m.device)
         chan = torch.zeros(B, cfg.num_layers, H // group, dtype=torch.float32, device=m.device) if want_channels \
             else None
