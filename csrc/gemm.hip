@@ -86,6 +86,7 @@ struct GemmArgs {
   int* err = nullptr;       // checked builds (EDGE_GEMM_CHECKS): set to a nonzero code when a bounds check fails
   float* raw = nullptr;     // EPI_H3_SWIGLU, optional: the scaled pre-activations (gate|up interleaved) as fp32 [M, N]
                             // too, bit-identical to EPI_F32 (the AttnLRP forward saves them for the SwiGLU rule)
+  bf16_t* rawb = nullptr;   // EPI_SWIGLU, optional: the same as bf16 [M, N], bit-identical to EPI_NONE
 };
 
 #ifndef EDGE_GEMM_CHECKS
@@ -662,6 +663,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x4_t (&acc)[
     const int m = m0 + wm * CF::WTM + i * 16 + (lane & 15);
     const bool ok = m < a.M;
     if constexpr (EPI == EPI_SWIGLU) {
+      if (a.rawb && ok) {   // the pre-activations as EPI_NONE would store them (columns nw + 16 j + 4 g .. + 3)
+        bf16_t* rp = a.rawb + (size_t)m * a.N + nw + g * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *(u32x2_t*)(rp + j * 16) = u32x2_t{pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3])};
+      }
       u32x2_t w[2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
@@ -2977,6 +2984,21 @@ EDGE_API int edge_gemm(const void* A, const void* B, void* C, int M, int N, int 
   if (bias) return launch<EPI_BIAS>(a, st);
   if (resid) return launch<EPI_RESID>(a, st);
   return launch<EPI_NONE>(a, st);
+}
+
+// EPI_SWIGLU that also stores the (row-scaled) pre-activations raw [M, N] bf16, bit-identical to edge_gemm act 0
+// (the bf16 AttnLRP forward saves them for the SwiGLU rule; one GEMM instead of a GEMM and a SwiGLU pass).
+EDGE_API int edge_gemm_swiglu_raw(const void* A, const void* B, void* C, void* raw, int M, int N, int K, int lda,
+                                  int ldb, int ldc, const float* rscale, hipStream_t st) {
+  GemmArgs a{};
+  a.rscale = rscale;
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = (bf16_t*)C;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.rawb = (bf16_t*)raw;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  if (!raw || ((uintptr_t)raw & 15) || ldc % 8 || ((uintptr_t)C & 15)) return (int)hipErrorInvalidValue;
+  return launch<EPI_SWIGLU>(a, st);
 }
 
 EDGE_API int edge_gemm_qkv_rope(const void* X, const void* W, const void* bias, void* q, void* k, void* vt,

@@ -578,6 +578,27 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
     return out
 
 
+def linear_swiglu_raw(x: torch.Tensor, w: torch.Tensor, norm=None):
+    """``linear(x, w, act="swiglu_il", norm=norm)`` that also returns the pre-activations ``linear(x, w, norm=norm)``
+    (interleaved gate|up [M, N], bit-identical) from the same GEMM -> (activation [M, N/2], pre-activations)."""
+    if not _gpu(x):
+        y = ref.linear(x, w, None, None, None, out_dtype=torch.float32)
+        if norm is not None:
+            y = y * ref.rownorm_scale(norm[0], x.shape[1], norm[1]).view(-1, 1)
+        g, u = ref.deinterleave_gate_up(y)
+        return (torch.nn.functional.silu(g) * u).to(x.dtype), y.to(x.dtype)
+    _check_bf16(x, w)
+    M, K = x.shape
+    N = w.shape[0]
+    act = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+    raw = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    rs = None if norm is None else _norm_scale(norm, K)
+    _gemm_ws(x.device)
+    call("edge_gemm_swiglu_raw", ptr(x), ptr(w), ptr(act), ptr(raw), M, N, K, x.stride(0), w.stride(0), act.stride(0),
+         ptr(rs), stream())
+    return act, raw
+
+
 def linear_h3_swiglu_raw(a3: torch.Tensor, w3: torch.Tensor, alpha: float, out_scale: float, rscale=None):
     """``linear_h3(..., act="swiglu_il", out_scale)`` that also returns the fp32 pre-activations
     ``rscale * (x @ w.T)`` (interleaved gate|up [M, N], bit-identical to ``linear_h3`` without ``act``) from the same

@@ -77,6 +77,7 @@ _SIGS = {
                     c_i, c_i, c_p],
     # fp32 execution mode (h3 split-fp16 GEMM operands, fp32 attention / norms / codec)
     "edge_rmsnorm_f32_rstd": [c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_f, c_p, c_p],
+    "edge_gemm_swiglu_raw": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p],
     "edge_gemm_f32_swiglu_raw": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_f, c_f, c_p],
     "edge_gemm_f32_cs": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_p, c_f, c_p],
     "edge_gemm_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p, c_f, c_f, c_p],

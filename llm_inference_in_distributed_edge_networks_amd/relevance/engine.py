@@ -30,6 +30,8 @@ from ..models.model import DecoderLM
 
 # A/B (EDGE_TUNING=1 EDGE_LRP_LAST_ROWS=0): the last layer's O-proj / MLP on every row, as the other layers
 _LAST_ROWS = not (_tuning() and os.environ.get("EDGE_LRP_LAST_ROWS", "1") == "0")
+# A/B (EDGE_TUNING=1 EDGE_LRP_FUSED_SWIGLU=0): gate|up GEMM, then a separate SwiGLU pass over the saved pre-activations
+_FUSED_SWIGLU = not (_tuning() and os.environ.get("EDGE_LRP_FUSED_SWIGLU", "1") == "0")
 
 class RelevanceEngine:
     def __init__(self, model: DecoderLM):
@@ -90,9 +92,12 @@ class RelevanceEngine:
                 y = ops.linear(o, L["wo"], residual=x, want_ssq=True)
                 ssq2 = y._edge_ssq
                 sv["rs2"] = ops.row_rscale(ssq2, H, cfg.norm_eps)
-                gu = ops.linear(y, t["wgu_n"], norm=(ssq2, cfg.norm_eps))
-                sv["gu"] = gu
-                x = ops.linear(ops.swiglu_il(gu), L["wd"], residual=y)
+                if _FUSED_SWIGLU:   # one GEMM: the SwiGLU activation and the saved pre-activations for its rule
+                    a, sv["gu"] = ops.linear_swiglu_raw(y, t["wgu_n"], norm=(ssq2, cfg.norm_eps))
+                else:
+                    sv["gu"] = ops.linear(y, t["wgu_n"], norm=(ssq2, cfg.norm_eps))
+                    a = ops.swiglu_il(sv["gu"])
+                x = ops.linear(a, L["wd"], residual=y)
             else:
                 a = ops.linear(h2, L["wfc"], L["bfc"])
                 sv["a"] = a

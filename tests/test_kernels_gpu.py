@@ -393,6 +393,18 @@ def test_qkv_rope_bf16_192(B, S, norm):
         ops.set_gemm_tile(0)
 
 
+@pytest.mark.parametrize("M,norm", [(32768, True), (4096, False), (257, True)])
+def test_linear_swiglu_raw(M, norm):
+    """One bf16 GEMM for the SwiGLU activation and the saved pre-activations (bf16 AttnLRP forward): both
+    bit-identical to the separate GEMMs (act="swiglu_il" and act=None), four-wave 256x256 and 128x128 kernels."""
+    K, N = 896, 2 * 4864
+    x, w = rnd(M, K, seed=60).to(DEV), rnd(N, K, s=0.03, seed=61).to(DEV)
+    nm = (R.row_ssq(rnd(M, K, seed=62)).to(DEV), 1e-6) if norm else None
+    a, raw = ops.linear_swiglu_raw(x, w, norm=nm)
+    assert torch.equal(raw, ops.linear(x, w, norm=nm))
+    assert torch.equal(a, ops.linear(x, w, act="swiglu_il", norm=nm))
+
+
 def _qkv_case(B, S, Hq, Hkv, Hd, cos, sin, rot):
     x = rnd(B * S, Hd, seed=96)
     nw = rnd(Hd, s=0.1, seed=97) + 1
