@@ -92,6 +92,8 @@ def parse():
                         "Qwen2-0.5B checkpoint the reference upcasts to fp32 (torch_dtype bfloat16); fp32 = full fp32 "
                         "random values (reported as value_fp32_weights)")
     p.add_argument("--no-fp32-weights", action="store_true", help="skip the fp32-valued-weights measurement")
+    p.add_argument("--no-hf-compare", action="store_true",
+                   help="skip the same-node reference-path measurement (HF transformers + eager, N = 1 only)")
     p.add_argument("--json-out", default="")
     return p.parse_args()
 
@@ -271,6 +273,28 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
     return {"dt": dt, "ppl": ppl, "prov": prov, "stages": stage_reports, "p2p": probe}
 
 
+def same_node_reference(a, cfg, dev) -> dict:
+    """The reference's own computation (HF transformers + PyTorch eager, fp32: importance forward with attention maps,
+    then the layer-wise split forward with the boundary quantized) timed on this GPU right after our run, one window
+    per call as the reference loops and 64 windows batched.  Never fails the bench: an error is recorded instead."""
+    try:
+        from llm_inference_in_distributed_edge_networks_amd.eval.hf_reference import ReferencePath
+        ref = ReferencePath(cfg, dev, seed=a.seed)
+        out = {"what": "reference computation on HF transformers + PyTorch eager, fp32, same GPU, same windows",
+               "layer": a.split, "ratio": a.ratio,
+               "batch1": ref.throughput(batch=1, windows=16, warmup=2, layer=a.split, ratio=a.ratio,
+                                        max_length=a.max_length, stride=a.stride, seed=a.seed),
+               "batch64": ref.throughput(batch=64, windows=128, warmup=1, layer=a.split, ratio=a.ratio,
+                                         max_length=a.max_length, stride=a.stride, seed=a.seed)}
+        ref.close()
+    except Exception as e:   # transformers missing or an HF API change: the headline stands without it
+        out = {"error": f"{type(e).__name__}: {e}"[:300]}
+    gc.collect()
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = parse()
     mode = launch_mode(a)
@@ -311,6 +335,9 @@ def main():
         fp32w = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup, None)
     if not a.no_bf16 and dtype == torch.float32 and env.device.type == "cuda":
         second = measure(a, env, cfg, torch.bfloat16, pp, grid, plan, a.steps, a.warmup, values)
+    hf = None
+    if world == 1 and not a.no_hf_compare and env.device.type == "cuda":
+        hf = same_node_reference(a, cfg, env.device)
     dname = {torch.float32: "fp32", torch.bfloat16: "bf16"}[dtype]
     out = {
         "metric": METRIC,
@@ -349,6 +376,11 @@ def main():
         out["ppl_random_weights_bf16"] = second["ppl"]
         if second["stages"]:
             out["stages_bf16"] = second["stages"]
+    if hf is not None:
+        out["same_node_reference_path"] = hf
+        for k in ("batch1", "batch64"):
+            if k in hf and hf[k]["window_tokens_per_s"] > 0:
+                out[f"vs_same_node_reference_{k}"] = round(value / hf[k]["window_tokens_per_s"], 2)
     fail = os.environ.get("EDGE_BENCH_FAIL_RANK")       # test hook: this rank dies after its measurement
     if fail is not None and int(fail) == env.rank:
         raise RuntimeError(f"EDGE_BENCH_FAIL_RANK: rank {env.rank} fails on purpose")
