@@ -335,7 +335,7 @@ def main():
         fp32w = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup, None)
     if not a.no_bf16 and dtype == torch.float32 and env.device.type == "cuda":
         second = measure(a, env, cfg, torch.bfloat16, pp, grid, plan, a.steps, a.warmup, values)
-    hf = None
+    hf = None   # last, so that nothing of it can touch the framework's own measurements
     if world == 1 and not a.no_hf_compare and env.device.type == "cuda":
         hf = same_node_reference(a, cfg, env.device)
     dname = {torch.float32: "fp32", torch.bfloat16: "bf16"}[dtype]
