@@ -8,12 +8,10 @@ over lines.  Published Pythia-70M values are in BASELINE.md (e.g. JS(0,4) = 0.39
 """
 from __future__ import annotations
 
-import math
 
 import torch
 
 from .. import ops
-from ..importance import ImportanceTracker
 
 
 def js_divergence(p: torch.Tensor, q: torch.Tensor, eps: float = 1e-12) -> float:

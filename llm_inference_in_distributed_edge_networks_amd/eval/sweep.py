@@ -30,10 +30,9 @@ Progress is checkpointed every ``checkpoint_every`` windows and resumed.
 from __future__ import annotations
 
 import json
-import math
 import os
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 import torch
 

@@ -38,10 +38,9 @@ is the faster bf16 mode.
 from __future__ import annotations
 
 import glob
-import json
 import math
 import os
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 import torch
 

@@ -27,7 +27,6 @@ reference's precision (fp32: h3 GEMMs, ``csrc/lrp_f32.hip``) and ``engine.Releva
 """
 from __future__ import annotations
 
-import math
 import os
 
 import torch
@@ -221,7 +220,7 @@ def relevance_main(p) -> list:
     from ..eval.data import token_stream
     from ..eval.windows import sliding_windows
     from ..models import build_model, get_config
-    from ..parallel.dist import all_reduce_sum, get_env, init_distributed
+    from ..parallel.dist import all_reduce_sum, init_distributed
     from ..utils.logging import log, progress_bar
     env = init_distributed(p.device)
     device = str(env.device)
