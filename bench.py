@@ -28,8 +28,11 @@ it to fp32.  Such weights are exact in fp16 after scaling, so their h3 GEMMs nee
 (``value_fp32_weights``, ``--no-fp32-weights`` skips it) and the bf16 mode (``value_bf16``, ``--no-bf16``).
 
 ``value`` = window tokens processed per second over the whole job (every window is a full 512-token forward, as in
-the reference); scored tokens/s, PPL and the measured wire bytes/token are reported alongside, plus a per-stage GPU
-time breakdown for pipelines across GPUs.  Data: synthetic token stream of the WikiText-2 test length, random-init
+the reference, except that the model's last layer, which feeds only the LM head, runs its O-projection / MLP on the
+scored rows: identical NLL, ``config.last_layer_rows``); scored tokens/s, PPL and the wire bytes/token measured by the
+senders' byte counters are reported alongside, plus a per-stage GPU time breakdown for pipelines across GPUs.  At
+N > 1 the headline pp2 x dp(N/2) run is followed by one N-stage pipeline over all the GPUs (``value_ppN``, BASELINE
+configs 4-5), reported beside it.  Data: synthetic token stream of the WikiText-2 test length, random-init
 weights of the exact Qwen2-0.5B architecture (no network / HF cache on the benchmark machines), so the PPL is that
 of random weights (~vocab size) and measures plumbing, not quality.
 """
@@ -94,6 +97,10 @@ def parse():
     p.add_argument("--no-fp32-weights", action="store_true", help="skip the fp32-valued-weights measurement")
     p.add_argument("--no-hf-compare", action="store_true",
                    help="skip the same-node reference-path measurement (HF transformers + eager, N = 1 only)")
+    p.add_argument("--no-deep-pp", action="store_true",
+                   help="N > 1: skip the secondary measurement of one N-stage pipeline over all the GPUs (value_ppN)")
+    p.add_argument("--deep-pp-timeout", type=float, default=300.0,
+                   help="seconds the deep-pipeline measurement may take before it counts as hung")
     p.add_argument("--json-out", default="")
     return p.parse_args()
 
@@ -264,13 +271,22 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
         gathered = [None] * world
         torch.distributed.all_gather_object(gathered, reports[-1] if reports else {})
         stage_reports = [dict(r, rank=i) for i, r in enumerate(gathered)]
+        # measured wire bytes per token of every boundary: the senders' byte counters (warmup + timed region), summed
+        # over the data-parallel replicas of each stage (exact for variable-k top-rho messages too)
+        wires = []
+        for s in range(pp - 1):
+            rs = [r for r in stage_reports if r.get("stage") == s]
+            b, t = sum(r.get("wire_bytes", 0.0) for r in rs), sum(r.get("wire_tokens", 0.0) for r in rs)
+            wires.append(b / t if t else 0.0)
+    else:
+        wires = runner.wire_bytes_per_token()
     if dist_pp:
         runner.close()
     del runner, model
     gc.collect()
     if dev.type == "cuda":
         torch.cuda.empty_cache()
-    return {"dt": dt, "ppl": ppl, "prov": prov, "stages": stage_reports, "p2p": probe}
+    return {"dt": dt, "ppl": ppl, "prov": prov, "stages": stage_reports, "p2p": probe, "wires": wires}
 
 
 def same_node_reference(a, cfg, dev) -> dict:
@@ -328,8 +344,7 @@ def main():
     tok_per_step = grid.dp * a.microbatches * a.batch * a.max_length
     scored_per_step = grid.dp * a.microbatches * a.batch * a.stride
     value = tok_per_step * a.steps / dt
-    wires = [C.message_bytes(spec, a.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
-             / (a.batch * a.max_length)] * (pp - 1)
+    wires = main_run["wires"]
     second = fp32w = None
     if values is not None and not a.no_fp32_weights and dtype == torch.float32 and env.device.type == "cuda":
         fp32w = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup, None)
@@ -352,7 +367,11 @@ def main():
                    "stage_layers": [[r.start, r.stop - 1] for r in (plan.stage_layers(s) for s in range(pp))],
                    "codec": a.codec, "ratio": a.ratio, "importance": a.method,
                    "transport": a.transport if dist_pp else "local", "hip_graphs": not a.no_graphs,
-                   "gemm_precision": "h3 split-fp16 (fp32-accurate)" if dname == "fp32" else "bf16"},
+                   "gemm_precision": "h3 split-fp16 (fp32-accurate)" if dname == "fp32" else "bf16",
+                   # the model's last layer feeds only the LM head: its O-projection / MLP run on the scored rows
+                   # (the NLL is identical); "all" under EDGE_LAST_LAYER_ALL_ROWS=1
+                   "last_layer_rows": "all" if os.environ.get("EDGE_LAST_LAYER_ALL_ROWS", "0") not in ("", "0")
+                   else "scored"},
         "baseline_note": "T4 fp32, 1 eager + 100 split forwards of 512 tokens per window in 16.2 s (BASELINE.md)",
         "scored_tokens_per_s": round(scored_per_step * a.steps / dt, 1),
         "wire_bytes_per_token": [round(w, 2) for w in wires],
@@ -381,21 +400,96 @@ def main():
         for k in ("batch1", "batch64"):
             if k in hf and hf[k]["window_tokens_per_s"] > 0:
                 out[f"vs_same_node_reference_{k}"] = round(value / hf[k]["window_tokens_per_s"], 2)
-    fail = os.environ.get("EDGE_BENCH_FAIL_RANK")       # test hook: this rank dies after its measurement
+    # test hook (tuning mode only, so a stray variable never changes a production run): this rank dies here
+    fail = os.environ.get("EDGE_BENCH_FAIL_RANK") if tuning_mode() else None
     if fail is not None and int(fail) == env.rank:
         raise RuntimeError(f"EDGE_BENCH_FAIL_RANK: rank {env.rank} fails on purpose")
     if env.is_dist:
         # every rank finished its measurement: only then does rank 0 report (a failed rank means no JSON line,
         # and the launcher - or the self-launching parent - exits non-zero)
         torch.distributed.barrier()
-    if env.is_main:
-        print(json.dumps(out), flush=True)
-        if a.json_out:
-            with open(a.json_out, "w") as f:
-                json.dump(out, f, indent=1)
+    emit = Emitter(out, a.json_out if env.is_main else "", env.is_main)
+    if dist_pp and world != pp and not a.no_deep_pp:
+        deep_pipeline(a, env, cfg, dtype, values, spec, emit)
+    emit()
     if env.is_dist:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+
+
+def tuning_mode() -> bool:
+    return os.environ.get("EDGE_TUNING", "0") not in ("", "0")
+
+
+class Emitter:
+    """Prints the one JSON line (rank 0) exactly once: normally at the end of the run, or from the watchdog of the
+    secondary deep-pipeline measurement when that hangs (the headline is never lost; the process then exits 70)."""
+
+    def __init__(self, out: dict, path: str, main: bool):
+        import threading
+        self.out, self.path, self.main = out, path, main
+        self._lock, self._done = threading.Lock(), False
+
+    def __call__(self):
+        with self._lock:
+            if self._done or not self.main:
+                self._done = True
+                return
+            self._done = True
+            print(json.dumps(self.out), flush=True)
+            if self.path:
+                with open(self.path, "w") as f:
+                    json.dump(self.out, f, indent=1)
+
+
+def deep_pipeline(a, env, cfg, dtype, values, spec, emit: Emitter) -> None:
+    """N > 1, after the headline: the same step as ONE N-stage pipeline over all the GPUs (BASELINE config 4 at N = 4,
+    config 5's shape at N = 8: cost-balanced stages, every boundary quantized), on the same process group and
+    transport.  Reported as ``value_pp{N}`` plus its stage breakdown and p2p probe in ``pp{N}``; the primary fields
+    are unchanged.  An exception on any rank is recorded as ``{"error": ...}``; a hang (the measurement
+    still running after ``--deep-pp-timeout`` s) prints the JSON line with the error and exits 70."""
+    from llm_inference_in_distributed_edge_networks_amd.utils.watchdog import Watchdog
+    world = env.world_size
+    key = f"pp{world}"
+    grid = Grid(world, world)
+    plan = PipelinePlan.balanced(cfg, world, a.max_length, a.stride / a.max_length)
+    steps, warm = max(2, a.steps // 2), max(1, a.warmup // 2)
+
+    def on_hang():
+        emit.out[f"value_{key}"] = None
+        emit.out[key] = {"error": f"still running after {a.deep_pp_timeout:.0f} s (rank {env.rank})"}
+        emit()
+        sys.stdout.flush()
+        os._exit(70)
+
+    wd = Watchdog(a.deep_pp_timeout, f"bench-{key}", on_timeout=on_hang).start()
+    err = None
+    res = None
+    sub = argparse.Namespace(**vars(a))
+    sub.microbatches = 4 * world          # weak scaling: every GPU does 4 full-model micro-batches per step
+    try:
+        msg_bytes = C.message_bytes(spec, a.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
+        res = measure(sub, env, cfg, dtype, world, grid, plan, steps, warm, values,
+                      probe_sizes=(1 << 20, int(msg_bytes)))
+    except Exception as e:   # recorded; the headline stands
+        err = f"{type(e).__name__}: {e}"[:300]
+    wd.beat()
+    errs = [None] * world
+    torch.distributed.all_gather_object(errs, err)
+    wd.stop()
+    bad = [f"rank {i}: {e}" for i, e in enumerate(errs) if e]
+    if bad or res is None:
+        emit.out[f"value_{key}"] = None
+        emit.out[key] = {"error": "; ".join(bad)[:600] or "no result"}
+        return
+    tok = sub.microbatches * a.batch * a.max_length   # dp = 1
+    emit.out[f"value_{key}"] = round(tok * steps / res["dt"], 1)
+    emit.out[key] = {
+        "parallelism": f"pp{world}xdp1", "steps": steps, "warmup": warm,
+        "ms_per_step": round(1000 * res["dt"] / steps, 3), "global_batch": sub.microbatches * a.batch,
+        "stage_layers": [[r.start, r.stop - 1] for r in (plan.stage_layers(s) for s in range(world))],
+        "wire_bytes_per_token": [round(w, 2) for w in res["wires"]], "ppl_random_weights": res["ppl"],
+        "stages": res["stages"], "p2p": res["p2p"]}
 
 
 if __name__ == "__main__":

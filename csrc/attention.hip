@@ -2,8 +2,8 @@
 // reference:
 //
 //   flash_attn_fwd : O = softmax(Q K^T) V with online softmax, never materialising S x S; optional
-//                    per-row LSE output (input of the column-sum scorer).  v2 (default) below the v1
-//                    kernel: mask-free interior tiles, exp2 + lazy rescale, 3-stage ring, XCD-aware order.
+//                    per-row LSE output (input of the column-sum scorer): mask-free interior tiles, exp2 + lazy
+//                    rescale, 3-stage ring, XCD-aware order, two query tiles per wave.
 //   attn_lastrow   : P[S-1, :] per head  -> "last_row" importance (Qwen2-0.5B/main.py:80-86).
 //   attn_colsum    : sum_i P[i, j] per head, recomputed from Q, K and the LSE (FA-backward style sweep,
 //                    key block outer / query tiles inner) -> "regular_importance", "weighted_importance",
@@ -41,136 +41,9 @@ __device__ __forceinline__ void stage64(const bf16_t* __restrict__ base, size_t 
 }
 }  // namespace
 
-__global__ __launch_bounds__(256, 2) void flash_attn_fwd_kernel(const bf16_t* __restrict__ q,
-                                                                const bf16_t* __restrict__ k,
-                                                                const bf16_t* __restrict__ vt,
-                                                                bf16_t* __restrict__ o, float* __restrict__ lse,
-                                                                int B, int Hq, int Hkv, int S, int s_pad) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
-  const int nqb = (S + 63) / 64;
-  const int BH = B * Hq;
-  const int qb = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest query blocks first
-  const int bh = blockIdx.x % BH;
-  const int b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
-
-  const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
-  const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
-  const bf16_t* vh = vt + ((size_t)b * Hkv + hk) * 64 * (size_t)s_pad;
-
-  const int q0 = qb * 64 + wave * 16;         // first query row of this wave
-  const int qrow = q0 + ql;                   // the query row this lane's scores belong to
-  const int qld = qrow < S ? qrow : S - 1;
-  bf16x8_t qf[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) qf[ks] = *(const bf16x8_t*)(qh + (size_t)qld * 64 + ks * 32 + g * 8);
-
-  f32x4_t oacc[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
-
-  const int nkb = qb + 1;
-  stage64(kh, 64, 0, S, 0, smem, wave, lane);
-  stage64(vh, s_pad, 0, 64, 0, smem + TILE, wave, lane);
-  wait_vmcnt0();
-  __syncthreads();
-
-  for (int kb = 0; kb < nkb; ++kb) {
-    char* cur = smem + (kb & 1) * 2 * TILE;
-    if (kb + 1 < nkb) {
-      char* nxt = smem + ((kb + 1) & 1) * 2 * TILE;
-      stage64(kh, 64, (kb + 1) * KT, S, 0, nxt, wave, lane);
-      stage64(vh, s_pad, 0, 64, (kb + 1) * KT, nxt + TILE, wave, lane);
-    }
-    const char* lk = cur;
-    const char* lv = cur + TILE;
-
-    // ---- S^T = K Q^T : st[ni][r] = score(key = kb*64 + ni*16 + 4g + r, query = qrow)
-    f32x4_t st[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      st[ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int r = ni * 16 + ql;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8_t kf = *(const bf16x8_t*)(lk + r * 128 + (((ks * 4 + g) ^ aswz(r)) << 4));
-        st[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], st[ni], 0, 0, 0);
-      }
-    }
-    // ---- mask + online softmax
-    const bool diag = (kb * KT + KT > q0);  // tile may contain keys > some query of this wave
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * KT + ni * 16 + g * 4 + r;
-        float s = st[ni][r];
-        if (diag || key >= S) s = (key > qrow || key >= S) ? -INFINITY : s;
-        st[ni][r] = s;
-        mloc = fmaxf(mloc, s);
-      }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float m_new = fmaxf(m_run, mloc);
-    const float alpha = __expf(m_run - m_new);  // m_run = -inf on the first tile -> 0
-    m_run = m_new;
-    float psum = 0.f;
-    bf16x8_t pf[2];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = __expf(st[ni][r] - m_new);
-        psum += p;
-        pf[ni >> 1][(ni & 1) * 4 + r] = (__bf16)p;
-      }
-    l_run = l_run * alpha + psum;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) oacc[d] *= alpha;
-
-    // ---- O^T += V^T P^T, keys permuted as kappa(ks, g, j) = 32ks + 16(j>>2) + 4g + (j&3)
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int row = dt * 16 + ql;
-      const char* rp = lv + row * 128;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int c0 = ks * 4 + (g >> 1);       // chunk of keys 32ks + 4g .. +3
-        const int c1 = c0 + 2;                   // chunk of keys 32ks + 16 + 4g .. +3
-        const int sub = (g & 1) * 8;
-        const u32x2_t lo = *(const u32x2_t*)(rp + ((c0 ^ aswz(row)) << 4) + sub);
-        const u32x2_t hi = *(const u32x2_t*)(rp + ((c1 ^ aswz(row)) << 4) + sub);
-        u32x4_t vv = {lo[0], lo[1], hi[0], hi[1]};
-        const bf16x8_t vf = __builtin_bit_cast(bf16x8_t, vv);
-        oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[ks], oacc[dt], 0, 0, 0);
-      }
-    }
-    wait_vmcnt0();
-    __syncthreads();
-  }
-
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
-  if (qrow < S) {
-    const float inv = 1.f / l_run;
-    bf16_t* orow = o + ((size_t)b * S + qrow) * (size_t)(Hq * 64) + h * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      u32x2_t w;
-      w[0] = pack_bf2(oacc[dt][0] * inv, oacc[dt][1] * inv);
-      w[1] = pack_bf2(oacc[dt][2] * inv, oacc[dt][3] * inv);
-      *(u32x2_t*)(orow + dt * 16 + g * 4) = w;
-    }
-    if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = m_run + logf(l_run);
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
-// v2 forward (default).  Same tile geometry and operand layouts as flash_attn_fwd_kernel; what changed is
-// what the profile of v1 showed (≈210 VALU per wave per 64-key tile against 16 MFMAs, and a 1-tile load
-// lead that left every tile waiting on L2/MALL):
+// Forward tile body (round 1 measured a plain one-tile-per-wave loop at ≈210 VALU per wave per 64-key tile against
+// 16 MFMAs, with a 1-tile load lead that left every tile waiting on L2/MALL):
 //   * masking only on the diagonal tile (kb == qb is the only tile with keys > query or keys >= S);
 //     interior tiles run a mask-free body;
 //   * exp2 domain: p = exp2(fma(s, log2e, -m2)) (one FMA + one v_exp per score);
@@ -186,149 +59,11 @@ constexpr float LOG2E = 1.4426950408889634f;
 constexpr float TAU = 8.f;
 constexpr int NST = 3;
 
-// Key order: MFMA ni, row i reads key 32(ni>>1) + 8(i>>2) + 4(ni&1) + (i&3), so lane group g holds keys
-// 32ks + 8g .. +7 of P in pf[ks] (consecutive), and the V^T operand of P.V is ONE 16-byte row-chunk read.
-template <bool MASK>
-__device__ __forceinline__ void fa2_tile(const char* lk, const char* lv, const bf16x8_t (&qf)[2], f32x4_t (&oacc)[4],
-                                         float& m2, float& l_run, int kb, int qrow, int S, int g, int ql) {
-  f32x4_t st[4];
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    st[ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const int r = 32 * (ni >> 1) + 8 * (ql >> 2) + 4 * (ni & 1) + (ql & 3);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t kf = *(const bf16x8_t*)(lk + r * 128 + (((ks * 4 + g) ^ aswz(r)) << 4));
-      st[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], st[ni], 0, 0, 0);
-    }
-  }
-  if constexpr (MASK) {
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * KT + 32 * (ni >> 1) + 8 * g + 4 * (ni & 1) + r;
-        if (key > qrow || key >= S) st[ni][r] = -INFINITY;
-      }
-  }
-  float mloc = -INFINITY;
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[ni][r]);
-  mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-  mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-  const float mc = mloc * LOG2E;
-  if (__builtin_amdgcn_ballot_w64(mc > m2 + TAU)) {      // wave-uniform: rescale every row exactly
-    const float mn = fmaxf(m2, mc);
-    const float alpha = __builtin_amdgcn_exp2f(m2 - mn);  // m2 = -inf on the first tile -> 0
-    m2 = mn;
-    l_run *= alpha;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) oacc[d] *= alpha;
-  }
-  bf16x8_t pf[2];
-  float ps = 0.f;
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = __builtin_amdgcn_exp2f(fmaf(st[ni][r], LOG2E, -m2));
-      ps += p;
-      pf[ni >> 1][(ni & 1) * 4 + r] = (__bf16)p;
-    }
-  l_run += ps;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    const int row = dt * 16 + ql;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t vf = *(const bf16x8_t*)(lv + row * 128 + (((ks * 4 + g) ^ aswz(row)) << 4));
-      oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[ks], oacc[dt], 0, 0, 0);
-    }
-  }
-}
 }  // namespace
 
-template <int OCC>
-__global__ __launch_bounds__(256, OCC) void flash_attn_fwd2_kernel(const bf16_t* __restrict__ q,
-                                                                 const bf16_t* __restrict__ k,
-                                                                 const bf16_t* __restrict__ vt,
-                                                                 bf16_t* __restrict__ o, float* __restrict__ lse,
-                                                                 const float* __restrict__ n_rows,
-                                                                 int B, int Hq, int Hkv, int S, int s_pad) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
-  const int nqb = (S + 63) / 64;
-  const int G = Hq / Hkv, NG = B * Hkv;
-  // blocks x, x+8, x+16, ... share an XCD (round-robin dispatch): XCD `xcd` owns groups xcd, xcd+8, ...
-  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-  const int cnt = (NG - xcd + 7) >> 3;                 // groups owned by this XCD slot
-  const int per_qb = cnt * G;
-  if (j >= per_qb * nqb) return;
-  const int qb = nqb - 1 - j / per_qb;                  // heavy query blocks first
-  const int rem = j - (nqb - 1 - qb) * per_qb;
-  const int grp = xcd + 8 * (rem / G);
-  const int b = grp / Hkv, hk = grp - b * Hkv, h = hk * G + rem % G;
-  // scored-rows mode (last layer of a model): window b only needs query rows >= S-1-n_rows[b]
-  if (n_rows && qb * 64 + 63 < S - 1 - (int)n_rows[b]) return;
-
-  const bf16_t* qh = q + ((size_t)b * Hq + h) * S * 64;
-  const bf16_t* kh = k + ((size_t)b * Hkv + hk) * S * 64;
-  const bf16_t* vh = vt + ((size_t)b * Hkv + hk) * 64 * (size_t)s_pad;
-
-  const int q0 = qb * 64 + wave * 16;
-  const int qrow = q0 + ql;
-  const int qld = qrow < S ? qrow : S - 1;
-  bf16x8_t qf[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) qf[ks] = *(const bf16x8_t*)(qh + (size_t)qld * 64 + ks * 32 + g * 8);
-
-  f32x4_t oacc[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m2 = -INFINITY, l_run = 0.f;
-
-  const int nkb = qb + 1;
-  stage64(kh, 64, 0, S, 0, smem, wave, lane);
-  stage64(vh, s_pad, 0, 64, 0, smem + TILE, wave, lane);
-  if (nkb > 1) {
-    stage64(kh, 64, KT, S, 0, smem + 2 * TILE, wave, lane);
-    stage64(vh, s_pad, 0, 64, KT, smem + 3 * TILE, wave, lane);
-  }
-  for (int kb = 0; kb < nkb; ++kb) {
-    if (kb + 1 < nkb) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 2 < nkb) {
-      char* nx = smem + ((kb + 2) % NST) * 2 * TILE;
-      stage64(kh, 64, (kb + 2) * KT, S, 0, nx, wave, lane);
-      stage64(vh, s_pad, 0, 64, (kb + 2) * KT, nx + TILE, wave, lane);
-    }
-    const char* cur = smem + (kb % NST) * 2 * TILE;
-    if (kb < qb) fa2_tile<false>(cur, cur + TILE, qf, oacc, m2, l_run, kb, qrow, S, g, ql);
-    else fa2_tile<true>(cur, cur + TILE, qf, oacc, m2, l_run, kb, qrow, S, g, ql);
-  }
-
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
-  if (qrow < S) {
-    const float inv = 1.f / l_run;
-    bf16_t* orow = o + ((size_t)b * S + qrow) * (size_t)(Hq * 64) + h * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      u32x2_t w;
-      w[0] = pack_bf2(oacc[dt][0] * inv, oacc[dt][1] * inv);
-      w[1] = pack_bf2(oacc[dt][2] * inv, oacc[dt][3] * inv);
-      *(u32x2_t*)(orow + dt * 16 + g * 4) = w;
-    }
-    if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = m2 * 0.6931471805599453f + logf(l_run);
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
-// v3 forward: v2's tile body with TWO 16-row query tiles per wave (128 query rows per workgroup).
-// v2 reads 16 ds_read_b128 (8 K + 8 V^T fragments) per 16 MFMAs per wave and tile: at 3 waves per SIMD that
+// The forward: TWO 16-row query tiles per wave (128 query rows per workgroup).
+// One tile per wave reads 16 ds_read_b128 (8 K + 8 V^T fragments) per 16 MFMAs per wave and tile: at 3 waves per SIMD that
 // alone asks ~250 B/clk/CU of the LDS array (peak 256).  Here every K and V^T fragment feeds both row tiles,
 // so the reads per MFMA halve.  Each wave runs the key tiles up to its own last row (wave-uniform skip of
 // the tile past the diagonal) and masks exactly one tile; softmax state is per row tile.
@@ -414,7 +149,7 @@ __global__ __launch_bounds__(256, OCC) void flash_attn_fwd3_kernel(const bf16_t*
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
   const int nqb = (S + 127) / 128;
   const int G = Hq / Hkv, NG = B * Hkv;
-  // XCD-aware order as v2: XCD `xcd` owns (window, kv head) groups xcd, xcd+8, ...; heavy query blocks first
+  // XCD-aware order: XCD `xcd` owns (window, kv head) groups xcd, xcd+8, ...; heavy query blocks first
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
   const int cnt = (NG - xcd + 7) >> 3;
   const int per_qb = cnt * G;
@@ -489,12 +224,6 @@ __global__ __launch_bounds__(256, OCC) void flash_attn_fwd3_kernel(const bf16_t*
       if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = m2[t] * 0.6931471805599453f + logf(l);
     }
   }
-}
-
-static int g_attn_variant = 4;  // v3 at 3 workgroups/CU (58.5 us vs v2's 70.5 at the bench shape)
-EDGE_API int edge_attn_set_variant(int v) {
-  g_attn_variant = (v >= 1 && v <= 5) ? v : 4;
-  return 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -613,36 +342,16 @@ __global__ __launch_bounds__(256) void head_combine_kernel(const float* __restri
 }
 
 // n_rows (nullable, [B] fp32): per-window count of scored rows (the last n_rows[b]+1 positions); query
-// blocks entirely before them are skipped (their O rows are left unwritten).  v2 only; v1 computes all.
+// blocks entirely before them are skipped (their O rows are left unwritten).
 EDGE_API int edge_flash_attn_fwd(const void* q, const void* k, const void* vt, void* o, float* lse, const float* n_rows,
                                  int B, int Hq, int Hkv, int S, int s_pad, hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
   if (Hq % Hkv || s_pad % 64 || s_pad < S) return (int)hipErrorInvalidValue;
-  const int nqb = (S + 63) / 64;
-  if (g_attn_variant >= 4) {  // 4: v3 at 3 workgroups/CU, 5: v3 at 2 workgroups/CU
-    const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
-    const dim3 grid(8 * maxcnt * G * ((S + 127) / 128));
-    if (g_attn_variant == 4)
-      hipLaunchKernelGGL(flash_attn_fwd3_kernel<3>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
-                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
-    else
-      hipLaunchKernelGGL(flash_attn_fwd3_kernel<2>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
-                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
-    return (int)hipGetLastError();
-  }
-  if (g_attn_variant >= 2) {  // 2: v2 at 2 workgroups/CU, 3: v2 at 3 workgroups/CU
-    const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
-    const dim3 grid(8 * maxcnt * G * nqb);
-    if (g_attn_variant == 3)
-      hipLaunchKernelGGL(flash_attn_fwd2_kernel<3>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
-                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
-    else
-      hipLaunchKernelGGL(flash_attn_fwd2_kernel<2>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
-                         (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL(flash_attn_fwd_kernel, dim3(B * Hq * nqb), dim3(256), 4 * TILE, st, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, B, Hq, Hkv, S, s_pad);
+  // 3 workgroups per CU (58.5 us at the bench shape, against 70.5 for the one-tile-per-wave kernel)
+  const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
+  const dim3 grid(8 * maxcnt * G * ((S + 127) / 128));
+  hipLaunchKernelGGL(flash_attn_fwd3_kernel<3>, grid, dim3(256), 2 * NST * TILE, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)vt, (bf16_t*)o, lse, n_rows, B, Hq, Hkv, S, s_pad);
   return (int)hipGetLastError();
 }
 

@@ -2,11 +2,11 @@
 // attention half of the framework's fp32 execution mode (the reference evaluates its models in fp32:
 // Experiments/Qwen2-0.5B/qwen_layer_wise.py:17, Experiments/Pythia-70M/pythia_model.py:25 load without a dtype).
 //
-// flash_attn_fwd_x6 (default) runs the matrix work as split-bf16 products on the bf16 matrix cores (three bf16 planes,
-// six plane products per fp32 product, common.h split3): 1.5x the native f32 kernel, flash_attn_fwd_f32, which runs v_mfma_f32_16x16x4_f32 (exact
-// fp32 products and fp32 accumulation) and stays for A/B and the importance scorers.
+// flash_attn_fwd_x6 runs the matrix work as split products on the matrix cores: scaled fp16 planes (h3, three products
+// per fp32 product) or three bf16 planes (six products, common.h split3); 1.5x (bf16 planes) to 2.5x (fp16 planes) the
+// round-1 kernel on the native v_mfma_f32_16x16x4_f32.  The exact-fp32 importance scorers below keep that MFMA.
 //
-//   flash_attn_fwd_f32 : O = softmax(Q K^T) V, online softmax, optional row LSE; O written as fp32 rows or
+//   flash_attn_fwd_x6  : O = softmax(Q K^T) V, online softmax, optional row LSE; O written as fp32 rows or
 //                        directly in the h3 layout (common.h) the O-projection GEMM consumes.
 //   attn_lastrow_f32   : P[S-1, :] per head.
 //   attn_colsum_f32    : sum_i P[i, j] per head from Q, K and the row LSE (second sweep, key block outer).
@@ -61,151 +61,7 @@ __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <bool MASK>
-__device__ __forceinline__ void f32_tile(const char* lk, const char* lv, const float (&qf)[16], f32x4_t (&oacc)[4],
-                                         float& m2, float& l_run, int kb, int qrow, int S, int g, int ql) {
-  f32x4_t st[4];
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt) {
-    const int row = kt * 16 + ql;
-    f32x4_t kf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) kf[s] = lds_chunk(lk, row, 4 * g + s);
-    st[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) st[kt] = mfma4(kf[kk >> 2][kk & 3], qf[kk], st[kt]);
-  }
-  if constexpr (MASK) {
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * FKT + kt * 16 + 4 * g + r;
-        if (key > qrow || key >= S) st[kt][r] = -INFINITY;
-      }
-  }
-  float mloc = -INFINITY;
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) mloc = fmaxf(mloc, st[kt][r]);
-  mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-  mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-  const float mc = mloc * FLOG2E;
-  if (__builtin_amdgcn_ballot_w64(mc > m2 + FTAU)) {  // wave-uniform lazy rescale (p <= 2^TAU otherwise)
-    const float mn = fmaxf(m2, mc);
-    const float alpha = exp2f(m2 - mn);              // m2 = -inf on the first tile -> 0
-    m2 = mn;
-    l_run *= alpha;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) oacc[d] *= alpha;
-  }
-  float ps = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = exp2f(fmaf(st[kt][r], FLOG2E, -m2));
-      st[kt][r] = p;
-      ps += p;
-    }
-  l_run += ps;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    const int row = dt * 16 + ql;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const f32x4_t vf = lds_chunk(lv, row, 4 * kt + g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) oacc[dt] = mfma4(vf[r], st[kt][r], oacc[dt]);
-    }
-  }
-}
 }  // namespace
-
-// One workgroup = 4 waves = 64 query rows of one (window, head); each wave owns 16 rows.  K / V^T tiles of 64
-// keys are DMA'd to LDS (global_load_lds, swizzled source) and double-buffered; XCD-aware block order as the bf16
-// v2 kernel: the query blocks and heads of one (window, kv head) group run on one XCD, heavy blocks first.
-template <bool H3OUT>
-__global__ __launch_bounds__(256, 2) void flash_attn_fwd_f32_kernel(const float* __restrict__ q,
-                                                                   const float* __restrict__ k,
-                                                                   const float* __restrict__ vt, void* __restrict__ o,
-                                                                   float* __restrict__ lse,
-                                                                   const float* __restrict__ n_rows, int B, int Hq,
-                                                                   int Hkv, int S, int s_pad, float h3s) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, ql = lane & 15;
-  const int nqb = (S + 63) / 64;
-  const int G = Hq / Hkv, NG = B * Hkv;
-  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-  const int cnt = (NG - xcd + 7) >> 3;
-  const int per_qb = cnt * G;
-  if (j >= per_qb * nqb) return;
-  const int qb = nqb - 1 - j / per_qb;
-  const int rem = j - (nqb - 1 - qb) * per_qb;
-  const int grp = xcd + 8 * (rem / G);
-  const int b = grp / Hkv, hk = grp - b * Hkv, h = hk * G + rem % G;
-  if (n_rows && qb * 64 + 63 < S - 1 - (int)n_rows[b]) return;  // scored-rows mode (last layer)
-
-  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
-  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
-  const float* vh = vt + ((size_t)b * Hkv + hk) * 64 * (size_t)s_pad;
-
-  const int q0 = qb * 64 + wave * 16;
-  const int qrow = q0 + ql;
-  const int qld = qrow < S ? qrow : S - 1;
-  float qf[16];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const f32x4_t v = *(const f32x4_t*)(qh + (size_t)qld * 64 + 16 * g + 4 * s);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) qf[4 * s + e] = v[e];
-  }
-  f32x4_t oacc[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) oacc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m2 = -INFINITY, l_run = 0.f;
-
-  const int nkb = qb + 1;
-  const int kmax = (q0 + 15) / FKT;  // last key tile this wave needs (wave-uniform)
-  stage_f32(kh, 64, 0, S, 0, smem, wave, lane);
-  stage_f32(vh, s_pad, 0, 64, 0, smem + FTILE, wave, lane);
-  for (int kb = 0; kb < nkb; ++kb) {
-    wait_vmcnt0();
-    __syncthreads();  // tile kb landed for every wave; every wave's reads of tile kb-1 retired
-    if (kb + 1 < nkb) {
-      char* nx = smem + ((kb + 1) & 1) * 2 * FTILE;
-      stage_f32(kh, 64, (kb + 1) * FKT, S, 0, nx, wave, lane);
-      stage_f32(vh, s_pad, 0, 64, (kb + 1) * FKT, nx + FTILE, wave, lane);
-    }
-    if (kb > kmax) continue;
-    const char* cur = smem + (kb & 1) * 2 * FTILE;
-    if (kb * FKT + FKT - 1 <= q0 && kb * FKT + FKT - 1 < S)
-      f32_tile<false>(cur, cur + FTILE, qf, oacc, m2, l_run, kb, qrow, S, g, ql);
-    else
-      f32_tile<true>(cur, cur + FTILE, qf, oacc, m2, l_run, kb, qrow, S, g, ql);
-  }
-
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
-  if (qrow < S) {
-    const float inv = 1.f / l_run;
-    const int W = Hq * 64;
-    if constexpr (H3OUT) {
-      f16_t* orow = (f16_t*)o + ((size_t)b * S + qrow) * (size_t)(2 * W);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
-        store_h3_4(orow, W, h * 64 + dt * 16 + 4 * g, v, h3s);
-      }
-    } else {
-      float* orow = (float*)o + ((size_t)b * S + qrow) * (size_t)W + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(orow + dt * 16 + 4 * g) = oacc[dt] * inv;
-    }
-    if (lse && g == 0) lse[((size_t)b * Hq + h) * S + qrow] = m2 * 0.6931471805599453f + logf(l_run);
-  }
-}
 
 // ---- split-bf16 ("x6") flash attention: the same fp32-accurate result on the bf16 matrix cores -------------------
 // q, k, v and the probabilities are split into three bf16 planes (common.h split3) and every product is the sum of
@@ -859,13 +715,6 @@ __global__ __launch_bounds__(256) void attn_lastrow_h3_kernel(const float* __res
   }
 }
 
-static int g_attn_f32_variant = 2;   // 0: split-plane MFMA kernel, 64 query rows per workgroup; 2 (default): the same
-                                     // with 128 rows (8 waves); 1: native f32 MFMA kernel (A/B)
-EDGE_API int edge_attn_f32_set_variant(int v) {
-  g_attn_f32_variant = v;
-  return 0;
-}
-
 template <bool H3OUT>
 static void launch_plane_attn(dim3 grid, hipStream_t st, const float* q, const void* kp, const void* vp, void* o,
                               float* lse, const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float h3s,
@@ -893,23 +742,12 @@ EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float
   const bool f16 = sq > 0.f;
   if (f16 && !(sk > 0.f && sv > 0.f)) return (int)hipErrorInvalidValue;
   const bool ho = out_h3_scale > 0.f;
+  // 8 waves, 128 query rows per workgroup (the 4-wave / 64-row form measured slower)
   const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
-  const dim3 grid(8 * maxcnt * G * ((S + 63) / 64));
-  if (g_attn_f32_variant == 0 || g_attn_f32_variant == 2) {   // split-plane matrix cores (0: 64 query rows / WG)
-    const bool w8 = g_attn_f32_variant == 2;
-    const dim3 gx(8 * maxcnt * G * ((S + (w8 ? 127 : 63)) / (w8 ? 128 : 64)));
-    auto* fn = w8 ? (f16 ? (ho ? launch_split_attn<true, 8, true> : launch_split_attn<false, 8, true>)
-                         : (ho ? launch_split_attn<true, 8, false> : launch_split_attn<false, 8, false>))
-                  : (f16 ? (ho ? launch_split_attn<true, 4, true> : launch_split_attn<false, 4, true>)
-                         : (ho ? launch_split_attn<true, 4, false> : launch_split_attn<false, 4, false>));
-    fn(gx, st, q, k, vt, o, lse, n_rows, B, Hq, Hkv, S, s_pad, out_h3_scale, sq, sk, sv);
-  } else if (ho) {             // f32 matrix cores
-    hipLaunchKernelGGL(flash_attn_fwd_f32_kernel<true>, grid, dim3(256), 4 * FTILE, st, q, k, vt, o, lse, n_rows, B,
-                       Hq, Hkv, S, s_pad, out_h3_scale);
-  } else {
-    hipLaunchKernelGGL(flash_attn_fwd_f32_kernel<false>, grid, dim3(256), 4 * FTILE, st, q, k, vt, o, lse, n_rows, B,
-                       Hq, Hkv, S, s_pad, out_h3_scale);
-  }
+  const dim3 gx(8 * maxcnt * G * ((S + 127) / 128));
+  auto* fn = f16 ? (ho ? launch_split_attn<true, 8, true> : launch_split_attn<false, 8, true>)
+                 : (ho ? launch_split_attn<true, 8, false> : launch_split_attn<false, 8, false>);
+  fn(gx, st, q, k, vt, o, lse, n_rows, B, Hq, Hkv, S, s_pad, out_h3_scale, sq, sk, sv);
   return (int)hipGetLastError();
 }
 

@@ -8,10 +8,10 @@
 //
 //   lrp_attn_delta_f32  D[b,h,i] = 0.5 dO_i . O_i (uniform rule on A V) and the per-(window, head) relevance
 //                       rel[b,h] = sum_i D[b,h,i] = sum_{ij} A_ij dA_ij - the reference hook's quantity.
-//   lrp_attn_dkdv_f32   dK, dV partials per (window, q head, 64-key block): P recomputed from Q K^T and the forward
-//                       LSE, dA = 0.5 dO V^T, dS = P (dA - D), dV = 0.5 P^T dO, dK = 0.5 dS^T Q.
-//   lrp_attn_dq_f32     dQ = 0.5 dS K per (window, q head, 64-query block).  Separate sweeps: no atomics.
-//                       All products on v_mfma_f32_16x16x4_f32 (full fp32 operands, no operand rounding).
+//   lrp_attn_dkdv_x6    dK, dV per (window, q head or kv-head group, 64-key block): P recomputed from Q K^T and the
+//                       forward LSE, dA = 0.5 dO V^T, dS = P (dA - D), dV = 0.5 P^T dO, dK = 0.5 dS^T Q.
+//   lrp_attn_dq_x6      dQ = 0.5 dS K per (window, q head, 64-query block).  Separate sweeps: no atomics.
+//                       Products on three-bf16-plane splits (exact fp32 operands, six products).
 //   *_h3 rule kernels   the LRP rules whose output feeds a backward GEMM (SwiGLU / GELU identity rule with the
 //                       uniform product rule, inverse RoPE + GQA sum) write it directly as an h3 activation with a
 //                       per-row power-of-two scale: gradients have no a-priori bound, so each row is scaled to put
@@ -94,197 +94,10 @@ __global__ __launch_bounds__(256) void lrp_attn_delta_f32_kernel(const float* __
 }
 
 // ---------------------------------------------------------------------------------------------
-// dK, dV partials per q head.  q [B,Hq,S,64] (pre-scaled), k, v [B,Hkv,S,64], dO token-major [B*S, Hq*64],
-// lse/D [B,Hq,S] -> dk, dv [B,Hq,S,64] (the GQA group sum happens in the rope/pack kernel).
-// Workgroup = (b, q head, 64-key block), heaviest key blocks (first keys: most causal queries) first; wave w owns keys
-// kb*64 + 16w .. +15 (lane column cl); query tiles of 64 rows staged in LDS, processed as four 16-row sub-tiles.
-__global__ __launch_bounds__(256) void lrp_attn_dkdv_f32_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                                const float* __restrict__ v,
-                                                                const float* __restrict__ dO,
-                                                                const float* __restrict__ lse,
-                                                                const float* __restrict__ D, float* __restrict__ dk,
-                                                                float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) float sQ[64 * LDF];
-  __shared__ __attribute__((aligned(16))) float sO[64 * LDF];
-  __shared__ float sL[64], sD[64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int kb = blockIdx.x / (B * Hq);
-  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
-  const int key = kb * 64 + wave * 16 + cl;
-  const int keyc = key < S ? key : S - 1;
-  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
-  const float* vh = v + ((size_t)b * Hkv + hk) * S * 64;
-  float kB[16], vB[16];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x4_t kv = *(const f32x4_t*)(kh + (size_t)keyc * 64 + 16 * j + 4 * g);
-    const f32x4_t vv = *(const f32x4_t*)(vh + (size_t)keyc * 64 + 16 * j + 4 * g);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      kB[4 * j + e] = kv[e];
-      vB[4 * j + e] = vv[e];
-    }
-  }
-  f32x4_t dka[4], dva[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
-  const float* doh = dO + (size_t)b * S * (Hq * 64) + h * 64;
-  const float* lh = lse + ((size_t)b * Hq + h) * S;
-  const float* dh = D + ((size_t)b * Hq + h) * S;
-  for (int q0 = kb * 64; q0 < S; q0 += 64) {
-    __syncthreads();
-    stage64(qh, 64, q0, S, sQ);
-    stage64(doh, (size_t)Hq * 64, q0, S, sO);
-    if (tid < 64) {
-      const int qi = q0 + tid;
-      sL[tid] = qi < S ? lh[qi] : INFINITY;
-      sD[tid] = qi < S ? dh[qi] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int sub = 0; sub < 4; ++sub) {
-      // scores and dA for queries q0 + sub*16 + 4g + r (C rows) x this lane's key (C column)
-      f32x4_t s = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
-      const float* qa = sQ + (sub * 16 + cl) * LDF + 4 * g;
-      const float* oa = sO + (sub * 16 + cl) * LDF + 4 * g;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4_t qv = *(const f32x4_t*)(qa + 16 * j);
-        const f32x4_t ov = *(const f32x4_t*)(oa + 16 * j);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s = mfma4(qv[e], kB[4 * j + e], s);
-          da = mfma4(ov[e], vB[4 * j + e], da);
-        }
-      }
-      float p[4], ds[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = sub * 16 + g * 4 + r;
-        const int qi = q0 + ql;
-        const bool ok = qi < S && key <= qi && key < S;
-        const float pr = ok ? expf(s[r] - sL[ql]) : 0.f;
-        p[r] = pr;
-        ds[r] = pr * (0.5f * da[r] - sD[ql]);
-      }
-      // dV[key][d] += P^T dO, dK[key][d] += dS^T Q over the 16 queries: MFMA kk takes query 4g + kk of k-slot g
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int row = (sub * 16 + 4 * g + kk) * LDF;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          dva[dt] = mfma4(p[kk], sO[row + dt * 16 + cl], dva[dt]);
-          dka[dt] = mfma4(ds[kk], sQ[row + dt * 16 + cl], dka[dt]);
-        }
-      }
-    }
-  }
-  // C[row = key 16w + 4g + r][col = d 16dt + cl]
-  float* dkh = dk + ((size_t)b * Hq + h) * S * 64;
-  float* dvh = dv + ((size_t)b * Hq + h) * S * 64;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int kr = kb * 64 + wave * 16 + g * 4 + r;
-    if (kr < S) {
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dkh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dka[dt][r];
-        dvh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dva[dt][r];
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// dQ.  Workgroup = (b, h, 64-query block), heaviest (last) query blocks first; wave w owns queries qb*64 + 16w + cl.
-// S^T = K Q^T and dA^T = V dO^T keep the query on the lane column, so dQ^T = K^T dS^T takes dS^T lane-locally.
-__global__ __launch_bounds__(256) void lrp_attn_dq_f32_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                              const float* __restrict__ v, const float* __restrict__ dO,
-                                                              const float* __restrict__ lse,
-                                                              const float* __restrict__ D, float* __restrict__ dq,
-                                                              int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) float sK[64 * LDF];
-  __shared__ __attribute__((aligned(16))) float sV[64 * LDF];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int nqb = (S + 63) / 64;
-  const int qb = nqb - 1 - blockIdx.x / (B * Hq);
-  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
-  const int qi = qb * 64 + wave * 16 + cl;
-  const int qic = qi < S ? qi : S - 1;
-  const float* qh = q + ((size_t)b * Hq + h) * S * 64;
-  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
-  const float* vh = v + ((size_t)b * Hkv + hk) * S * 64;
-  const float* dorow = dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64;
-  float qB[16], oB[16];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x4_t qv = *(const f32x4_t*)(qh + (size_t)qic * 64 + 16 * j + 4 * g);
-    const f32x4_t ov = *(const f32x4_t*)(dorow + 16 * j + 4 * g);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      qB[4 * j + e] = qv[e];
-      oB[4 * j + e] = ov[e];
-    }
-  }
-  const float lq = lse[((size_t)b * Hq + h) * S + qic];
-  const float dq_ = D[((size_t)b * Hq + h) * S + qic];
-  f32x4_t acc[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int kend = min(S, qb * 64 + 64);
-  for (int k0 = 0; k0 < kend; k0 += 64) {
-    __syncthreads();
-    stage64(kh, 64, k0, S, sK);
-    stage64(vh, 64, k0, S, sV);
-    __syncthreads();
-#pragma unroll
-    for (int sub = 0; sub < 4; ++sub) {
-      f32x4_t s = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
-      const float* ka = sK + (sub * 16 + cl) * LDF + 4 * g;
-      const float* va = sV + (sub * 16 + cl) * LDF + 4 * g;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4_t kv = *(const f32x4_t*)(ka + 16 * j);
-        const f32x4_t vv = *(const f32x4_t*)(va + 16 * j);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s = mfma4(kv[e], qB[4 * j + e], s);
-          da = mfma4(vv[e], oB[4 * j + e], da);
-        }
-      }
-      // s[r] = score(key = k0 + sub*16 + 4g + r, query = qi)
-      float ds[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kj = k0 + sub * 16 + g * 4 + r;
-        const bool ok = qi < S && kj <= qi;
-        const float pr = ok ? expf(s[r] - lq) : 0.f;
-        ds[r] = pr * (0.5f * da[r] - dq_);
-      }
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int row = (sub * 16 + 4 * g + kk) * LDF;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma4(sK[row + dt * 16 + cl], ds[kk], acc[dt]);
-      }
-    }
-  }
-  // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
-  if (qi < S) {
-    float* o = dq + (((size_t)b * Hq + h) * S + qi) * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = 0.5f * acc[dt];
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// The same two sweeps on the bf16 matrix cores ("x6", the split of the forward's first fp32 attention): every
+// The dK / dV and dQ sweeps on the bf16 matrix cores ("x6", the split of the forward's first fp32 attention): every
 // operand - q, k, v, dO, and the in-register P and dS - is split into three bf16 planes x = x0 + x1 + x2 (24
 // significant bits, exact: common.h split3), and each product is the six plane products with i + j <= 2, small terms
-// first, on v_mfma_f32_16x16x32_bf16 (1024 FLOP per cycle against the f32 MFMA's 64: 2.7x per useful FLOP).  No
+// first, on v_mfma_f32_16x16x32_bf16 (1024 FLOP per cycle against the f32 MFMA's 64: 2.7x per useful FLOP over the round-3 v_mfma_f32_16x16x4_f32 sweeps).  No
 // scales are needed (bf16 has fp32's exponent range), so the gradients keep their dynamic range with no bounds.
 //
 // 16x16x32 fragments: lane l holds A[row l&15][k 8(l>>4)+j] and B[k 8(l>>4)+j][col l&15], C[row 4(l>>4)+r][col l&15].
@@ -408,7 +221,8 @@ __device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8
 }
 }  // namespace
 
-// dK, dV partials per q head (inputs and outputs as lrp_attn_dkdv_f32_kernel).  Workgroup = (b, q head, 64-key
+// dK, dV partials per q head: q [B,Hq,S,64] (pre-scaled), k, v [B,Hkv,S,64], dO token-major [B*S, Hq*64],
+// lse/D [B,Hq,S] -> dk, dv [B,Hq,S,64] (the GQA group sum happens in the rope/pack kernel).  Workgroup = (b, q head, 64-key
 // block), heaviest first; wave w owns keys kb 64 + 16 w + cl.  Per 32-query tile: S = Q K^T and dA = dO V^T with the
 // query on the C rows (the lane's K / V planes in registers for the whole sweep), P = exp(S - lse), dS = P (dA/2 - D),
 // then dV += P^T dO and dK += dS^T Q over the tile's 32 queries (P / dS the lane's A fragments, dO / Q from the
@@ -527,7 +341,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __re
   }
 }
 
-// dQ (inputs and output as lrp_attn_dq_f32_kernel).  Workgroup = (b, h, 64-query block), heaviest (last) first; wave
+// dQ (inputs as lrp_attn_dkdv_x6_kernel; dq [B,Hq,S,64]).  Workgroup = (b, h, 64-query block), heaviest (last) first; wave
 // w owns queries qb 64 + 16 w + cl.  Per 32-key tile: S^T = K Q^T and dA^T = V dO^T with the key on the C rows (the
 // lane's Q / dO planes in registers), dS^T = P^T (dA^T/2 - D), then dQ^T += K^T dS^T over the tile's 32 keys.
 __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
@@ -1013,8 +827,6 @@ __global__ __launch_bounds__(256) void group_absprod_kernel(const float* __restr
 // ---------------------------------------------------------------------------------------------
 static inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
 
-static int g_lrp_attn_x6 = 1;
-
 EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* v, const float* o, const float* dO,
                                    const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, int B,
                                    int Hq, int Hkv, int S, hipStream_t st) {
@@ -1022,35 +834,22 @@ EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* 
   if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
   const int nb = (S + 63) / 64;
   lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
-  if (g_lrp_attn_x6) {
-    lrp_attn_dkdv_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-    lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
-  } else {
-    lrp_attn_dkdv_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-    lrp_attn_dq_f32_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
-  }
+  lrp_attn_dkdv_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
+  lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
   return (int)hipGetLastError();
 }
 
-// edge_lrp_attn_bwd_f32 with dk, dv as the GQA group SUMS [B, Hkv, S, 64] (x6 sweeps only: check
-// edge_lrp_attn_gqa_sum_ok first).
+// edge_lrp_attn_bwd_f32 with dk, dv as the GQA group SUMS [B, Hkv, S, 64].
 EDGE_API int edge_lrp_attn_bwd_f32_gs(const float* q, const float* k, const float* v, const float* o, const float* dO,
                                       const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, int B,
                                       int Hq, int Hkv, int S, hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
-  if (Hkv <= 0 || Hq % Hkv || !g_lrp_attn_x6) return (int)hipErrorInvalidValue;
+  if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
   const int nb = (S + 63) / 64;
   lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
   lrp_attn_dkdv_x6_kernel<true><<<B * Hkv * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
   lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
   return (int)hipGetLastError();
-}
-EDGE_API int edge_lrp_attn_gqa_sum_ok() { return g_lrp_attn_x6 != 0; }
-
-// A/B and tests: 1 = the bf16 matrix-core (x6) sweeps (default), 0 = the f32-MFMA sweeps
-EDGE_API int edge_lrp_attn_set_x6(int on) {
-  g_lrp_attn_x6 = on;
-  return 0;
 }
 
 static int rope_pack_h3(const float* dq, const float* dk, const float* dv, const float* cosT, const float* sinT,

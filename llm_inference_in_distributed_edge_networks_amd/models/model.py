@@ -57,10 +57,8 @@ class AttnStats:
 
 _H3_KEYS = ("wqkv", "wo", "wgu", "wd", "wfc", "wproj")
 # fp32 mode: the QKV GEMM writes K / V^T also as h3 planes and the attention stages them by LDS DMA (bit-identical
-# result; EDGE_ATTN_KV_PLANES=0 keeps the kernel's own per-tile split, for A/B)
-_KV_PLANES = os.environ.get("EDGE_ATTN_KV_PLANES", "1") != "0"
-# fp32 K from the QKV GEMM only on layers whose importance scorers read it (EDGE_QKV_K32=1: every layer, for A/B)
-_K32_ALWAYS = os.environ.get("EDGE_QKV_K32", "0") == "1"
+# to the kernel's own per-tile split of fp32 K / V^T, which the tests compare against by clearing this flag)
+_KV_PLANES = True
 
 
 def _rownorm(w: torch.Tensor) -> torch.Tensor:
@@ -404,7 +402,7 @@ class DecoderLM:
             q, k, vt, kp, vp = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S,
                                                cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, cfg.rotary_dim,
                                                self.q_scale, kv_scales=(sc["att_k"], sc["o"]),
-                                               need_k=need_k or _K32_ALWAYS)
+                                               need_k=need_k)
             kvp = (kp, vp)
         else:
             q, k, vt = ops.qkv_rope_h3(h3, L["wqkv3"], sc["a_wqkv"], L["bqkv"], self.cos, self.sin, B, S,

@@ -13,7 +13,6 @@ Every op has exactly two implementations with identical layouts and semantics:
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -27,9 +26,8 @@ interleave_gate_up = ref.interleave_gate_up
 deinterleave_gate_up = ref.deinterleave_gate_up
 
 _ACT = {None: 0, "gelu": 1, "swiglu_il": 2}
-from ._native import tuning as _tuning  # noqa: E402
 
-_QKV_ROW_RSCALE = _tuning() and os.environ.get("EDGE_QKV_ROW_RSCALE", "0") not in ("", "0")
+
 
 
 def _gpu(t: torch.Tensor) -> bool:
@@ -160,127 +158,16 @@ def layernorm_dual(x, w1, b1, w2, b2, eps, h3: tuple[float, float] = (0.0, 0.0))
 
 
 def set_gemm_tile(tile: int) -> None:
-    """Force the GEMM block tile (128, 192, 224 or 256; 0 = automatic by shape).  Tuning / tests only.  224 is the
-    256x224 kernel for N % 224 == 0 shapes that 256 does not divide (the Qwen2 hidden size 896); 192 the fp32-mode
-    QKV kernel for N % 192 == 0 (N = 1152)."""
+    """Force the GEMM block tile at any M (tests only): 128 (the 128x128 kernel), 256 / 224 / 192 (the persistent
+    four-wave kernel's 256x256, 256x224 - N % 224 == 0 shapes that 256 does not divide, the Qwen2 hidden size 896 -
+    and 256x192 - the QKV GEMMs with N % 192 == 0 - tiles); 0 = automatic by shape."""
     call("edge_gemm_set_tile", int(tile))
-
-
-# s-a*: timing ablations with wrong results, only in a tuning build of the library (-DEDGE_TUNING_BUILD=1)
-GEMM_VARIANTS = {"p": 0, "": 1, "r": 2, "rp": 3, "s": 4, "s-a1": 5, "s-a2": 6, "s-a3": 7, "s5": 8, "s-a4": 9, "e": 10, "w": 11, "wp": 12}
-
-
-def set_gemm_variant(v: int) -> None:
-    """256x256 GEMM main loop (A/B and tests): 0 K-tile double buffer with compiler-waited fragment loads,
-    1 the same with hand-counted asm reads, 2 the K-half ring, 3 the ring with s_setprio, 4 the ring with
-    wave-group ping-pong, 8 the ping-pong ring with 5 slots, 10 the eight-phase full-line K-tile kernel, 11 the
-    four-wave kernel with 128x128 wave tiles (default), 12 the same with an L2 prefetch stream."""
-    call("edge_gemm_set_variant", int(v))
-
-
-def set_gemm_w7(on) -> None:
-    """Automatic use of the 256x224 tiles for N = 896-like shapes (A/B only): 0 off, 1 / True the eight-wave
-    kernel, 2 the four-wave kernel."""
-    call("edge_gemm_set_w7", int(on))
 
 
 def gemm_ssq_parts(M: int, N: int, K: int, act=None, bias=False, residual=False) -> int:
     """Row sum-of-squares partials ``linear(..., want_ssq=True)`` produces for this shape: N/64 (64-column
     slabs), or N/112 (wave slabs) when the 256x224 kernel runs it."""
     return int(lib().edge_gemm_ssq_parts(M, N, K, _ACT[act], int(bool(bias)), int(bool(residual))))
-
-
-def set_gemm_qkv256(mode: int) -> None:
-    """QKV+RoPE GEMMs on the four-wave 256x256 kernel when the shape fills the chip: 0 never, 1 the fp32-mode (h3)
-    QKV (default), 2 the bf16 QKV too."""
-    call("edge_gemm_set_qkv256", int(mode))
-
-
-def set_gemm_qkv192(on) -> None:
-    """fp32-mode QKV+RoPE GEMMs on 256x192 tiles when 192 divides N and 256 does not (N = 1152: 768 tiles, three
-    full rounds of the chip; default on).  A/B only."""
-    call("edge_gemm_set_qkv192", int(on))
-
-
-def set_gemm_qkv192_bf16(on) -> None:
-    """bf16 QKV+RoPE GEMMs on the four-wave 256x192 tiles (fused RMSNorm row scale, bf16 q / k / V^T) when they fill
-    the chip, instead of the 128x128 kernel.  A/B and tests."""
-    call("edge_gemm_set_qkv192_bf16", int(on))
-
-
-def set_gemm_stagger(k: int) -> None:
-    """Four-wave GEMMs (A/B): the odd workgroups of each XCD start k x 1024 cycles late, so the chip-wide epilogue
-    store bursts split in two (0 = off, the default)."""
-    call("edge_gemm_set_stagger", int(k))
-
-
-def set_gemm_split(k: int) -> None:
-    """Epilogue desync of the four-wave GEMMs: half of each XCD's workgroups run the first k K-tiles of their last
-    tile first (raw accumulators parked in a persistent per-device workspace) and finish it last, so their epilogues
-    fall half a tile after the others' and the chip's store bursts halve.  -1 = auto (half a tile), 0 = off.
-    Bit-identical results either way (same accumulation order)."""
-    global _SPLIT
-    call("edge_gemm_set_split", int(k))
-    _SPLIT = int(k)
-    if _SPLIT and torch.cuda.is_available():
-        _gemm_ws(torch.device("cuda", torch.cuda.current_device()))
-
-
-def get_gemm_split() -> int:
-    return _split()
-
-
-_SPLIT: int | None = None
-_WS: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
-
-
-def _split() -> int:
-    global _SPLIT
-    if _SPLIT is None:
-        L = lib()
-        _SPLIT = int(L.edge_gemm_get_split()) if hasattr(L, "edge_gemm_get_split") else 0
-    return _SPLIT
-
-
-def _gemm_ws(dev: torch.device) -> None:
-    """Register this device's desync workspace with the kernel library, once: a persistent buffer kept in ``_WS``
-    for the life of the process, handed to every four-wave launch as a kernel argument (no per-call allocation, so
-    no lifetime to get wrong).  Nothing to do while the desync is off."""
-    if not _split():
-        return
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    if idx in _WS:
-        return
-    n = int(lib().edge_gemm_ws_floats())
-    with torch.cuda.device(idx):
-        ws = torch.empty(n, dtype=torch.float32, device=f"cuda:{idx}")
-        err = torch.zeros(4, dtype=torch.int32, device=f"cuda:{idx}")
-        call("edge_gemm_set_ws", ws.data_ptr(), n, err.data_ptr())
-    _WS[idx] = (ws, err)
-
-
-def gemm_check_errors(dev=None) -> int:
-    """Checked builds (EDGE_GEMM_CHECKS / the tuning build): the device error word of the desync workspace - 0 when
-    no bounds check failed (1: segment table, 2: workspace offset)."""
-    idx = torch.cuda.current_device() if dev is None else torch.device(dev).index or 0
-    if idx not in _WS:
-        return 0
-    return int(_WS[idx][1][0].item())
-
-
-def set_gemm_walk(chunked) -> None:
-    """Persistent 256x256 GEMMs: XCD-contiguous tile chunks (default) or the grid-strided walk.  A/B only.
-    2 = chunked for the four-wave kernel too (it walks strided otherwise)."""
-    call("edge_gemm_set_walk", int(chunked) if not isinstance(chunked, bool) else int(chunked))
-
-
-def set_gemm_config(spec: str) -> None:
-    """'0' (automatic tile and main loop), '128', or '256' + main-loop suffix ('' asm-read K-tile loop, 'p', 'r',
-    'rp', 's' ping-pong ring, 's5'), e.g. '256s'.  '256' pins variant 1; '0' restores the automatic choice."""
-    digits = len(spec) - len(spec.lstrip("0123456789"))
-    tile, suffix = int(spec[:digits]), spec[digits:]
-    set_gemm_tile(tile)
-    set_gemm_variant(GEMM_VARIANTS[suffix] if (tile == 256 or suffix) else -1)
 
 
 def row_ssq(x: torch.Tensor) -> torch.Tensor:
@@ -349,7 +236,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None,
     rs = None if norm is None else _norm_scale(norm, K)
     ssq_out = torch.empty(M, gemm_ssq_parts(M, N, K, act, bias is not None, residual is not None),
                           dtype=torch.float32, device=x.device) if want_ssq else None
-    _gemm_ws(x.device)
     call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), _ACT[act], ptr(rs), ptr(ssq_out), stream())
     if want_ssq:
@@ -373,13 +259,12 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     vt = torch.zeros(B, Hkv, D, sp, dtype=x.dtype, device=x.device) if sp != S else \
         torch.empty(B, Hkv, D, sp, dtype=x.dtype, device=x.device)
     # fused RMSNorm: with 8 or 14 sum-of-squares partials per row the kernel forms the row scale itself at tile
-    # start (no row_rscale launch; EDGE_QKV_ROW_RSCALE=1 restores it for A/B)
+    # start (no row_rscale launch)
     ssq, eps = norm if norm is not None else (None, 0.0)
     rs = None
     if ssq is not None:
-        if _QKV_ROW_RSCALE or ssq.shape[1] not in (8, 14) or not ssq.is_contiguous() or ssq.data_ptr() % 16:
+        if ssq.shape[1] not in (8, 14) or not ssq.is_contiguous() or ssq.data_ptr() % 16:
             rs, ssq = _norm_scale(norm, K), None
-    _gemm_ws(x.device)
     call("edge_gemm_qkv_rope", ptr(x), ptr(wqkv), ptr(bqkv), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, K, S,
          Hq, Hkv, rot_dim, sp, float(q_scale), ptr(rs), ptr(ssq), 0 if ssq is None else ssq.shape[1], float(eps),
          stream())
@@ -432,12 +317,6 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scal
     call("edge_flash_attn_fwd", ptr(q), ptr(k), ptr(vt), ptr(o), ptr(lse), ptr(nr), B, Hq, Hkv, S, vt.shape[-1],
          stream())
     return o, lse
-
-
-def set_attn_variant(v: int) -> None:
-    """Flash-attention forward kernel: 4 (default: v3, two 16-row query tiles per wave, 3 workgroups/CU), 5 (v3 at
-    2/CU), 3 / 2 (v2 at 3 / 2 workgroups/CU), 1 (the first version).  A/B and tests only."""
-    call("edge_attn_set_variant", int(v))
 
 
 def attn_lastrow(q, k, S, in_scales=None):
@@ -593,7 +472,6 @@ def linear_swiglu_raw(x: torch.Tensor, w: torch.Tensor, norm=None):
     act = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
     raw = torch.empty(M, N, dtype=x.dtype, device=x.device)
     rs = None if norm is None else _norm_scale(norm, K)
-    _gemm_ws(x.device)
     call("edge_gemm_swiglu_raw", ptr(x), ptr(w), ptr(act), ptr(raw), M, N, K, x.stride(0), w.stride(0), act.stride(0),
          ptr(rs), stream())
     return act, raw
@@ -692,7 +570,6 @@ def linear_rowscale(x: torch.Tensor, w: torch.Tensor, rscale: torch.Tensor, resi
     N = w.shape[0]
     out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     rs = rscale.to(torch.float32).contiguous()
-    _gemm_ws(x.device)
     call("edge_gemm", ptr(x), ptr(w), ptr(out), M, N, K, x.stride(0), w.stride(0), out.stride(0), None,
          ptr(residual), 0 if residual is None else residual.stride(0), 0, ptr(rs), None, stream())
     return out
@@ -700,11 +577,8 @@ def linear_rowscale(x: torch.Tensor, w: torch.Tensor, rscale: torch.Tensor, resi
 
 def lrp_gqa_sum_native(t: torch.Tensor) -> bool:
     """True when ``lrp_attn_bwd(..., gqa_sum=True)`` computes the GQA group sums in the kernel for tensors like ``t``
-    (fp32 on the GPU with the x6 sweeps; False for an A/B build that predates it)."""
-    if not _gpu(t) or t.dtype != torch.float32:
-        return False
-    L = lib()
-    return hasattr(L, "edge_lrp_attn_gqa_sum_ok") and bool(L.edge_lrp_attn_gqa_sum_ok())
+    (fp32 on the GPU)."""
+    return _gpu(t) and t.dtype == torch.float32
 
 
 def lrp_attn_bwd(q, k, v, o, dO, lse, gqa_sum: bool = False):
@@ -735,12 +609,6 @@ def lrp_attn_bwd(q, k, v, o, dO, lse, gqa_sum: bool = False):
     if gqa_sum:
         dk, dv = (t.view(B, Hkv, Hq // Hkv, S, D).sum(2) for t in (dk, dv))
     return Dl, rel, dq, dk, dv
-
-
-def set_lrp_attn_x6(on) -> None:
-    """fp32 AttnLRP attention backward: the bf16 matrix-core sweeps on three-plane splits (1, default) or the f32
-    MFMA sweeps (0).  A/B and tests."""
-    call("edge_lrp_attn_set_x6", int(on))
 
 
 def lrp_rope_pack(dq, dk, dv, cos, sin, B, S, Hq, Hkv, rot_dim, q_scale, dtype=torch.bfloat16):

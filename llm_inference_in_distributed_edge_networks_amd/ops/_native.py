@@ -33,30 +33,12 @@ _SIGS = {
     "edge_row_ssq": [c_p, c_p, c_i, c_i, c_p],
     "edge_row_rscale": [c_p, c_p, c_i, c_i, c_i, c_f, c_p],
     "edge_gemm_set_tile": [c_i],
-    "edge_gemm_set_variant": [c_i],
-    "edge_gemm_set_walk": [c_i],
-    "edge_gemm_set_w7": [c_i],
-    "edge_gemm_set_qkv256": [c_i],
-    "edge_gemm_set_qkv192": [c_i],
-    "edge_gemm_set_qkv192_bf16": [c_i],
-    "edge_gemm_set_skip_epi": [c_i],
-    "edge_gemm_set_rs_lds": [c_i],
-    "edge_gemm_set_lse256": [c_i],
-    "edge_gemm_set_w7_mode": [c_i],
-    "edge_gemm_set_stagger": [c_i],
-    "edge_gemm_set_split": [c_i],
-    "edge_gemm_get_split": [],
-    "edge_gemm_set_ws": [c_p, c_ll, c_p],
-    "edge_gemm_ws_floats": [],
-    "edge_gemm_checked_build": [],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],
     "edge_gemm_lse": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_lse_reduce": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_flash_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p],
-    "edge_attn_set_variant": [c_i],
-    "edge_attn_f32_set_variant": [c_i],
     "edge_attn_lastrow": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_attn_colsum": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_head_combine": [c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p],
@@ -92,11 +74,9 @@ _SIGS = {
     "edge_split_h3": [c_p, c_p, c_p, c_i, c_i, c_f, c_p],
     "edge_embedding_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     # fp32 AttnLRP backward (csrc/lrp_f32.hip)
-    "edge_lrp_attn_set_x6": [c_i],
     "edge_lrp_attn_bwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_lrp_rope_pack_h3": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_lrp_attn_bwd_f32_gs": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
-    "edge_lrp_attn_gqa_sum_ok": [],
     "edge_lrp_rope_pack_h3_gs": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_split_h3_dyn": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_lrp_swiglu_bwd_h3": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p],
@@ -116,36 +96,9 @@ class NativeLibraryMissing(RuntimeError):
 
 
 def tuning() -> bool:
-    """Kernel A/B switches (EDGE_GEMM_VARIANT, EDGE_ATTN_VARIANT, ...) are honoured only with EDGE_TUNING=1, so a
-    stray environment variable can never change the production kernel selection."""
+    """Test hooks (EDGE_BENCH_FAIL_RANK) are honoured only with EDGE_TUNING=1, so a stray environment variable can
+    never change a production run."""
     return os.environ.get("EDGE_TUNING", "0") not in ("", "0")
-
-
-def _apply_tuning_env(L) -> None:
-    v = os.environ.get("EDGE_GEMM_VARIANT")  # A/B of the 256x256 main loop (see ops.set_gemm_variant)
-    if v:
-        L.edge_gemm_set_variant(int(v))
-    av = os.environ.get("EDGE_ATTN_VARIANT")  # A/B of the flash-attention forward (see ops.set_attn_variant)
-    if av:
-        L.edge_attn_set_variant(int(av))
-    if os.environ.get("EDGE_GEMM_LSE256", "1") == "0":  # LM-head LSE GEMM on 128x128 tiles
-        L.edge_gemm_set_lse256(0)
-    if os.environ.get("EDGE_GEMM_RS_LDS", "1") == "0":  # row scales by global loads in the epilogue
-        L.edge_gemm_set_rs_lds(0)
-    if os.environ.get("EDGE_GEMM_W7", "1") == "0":  # N = 896 GEMMs back on the 256x256 tiles
-        L.edge_gemm_set_w7(0)
-    st = os.environ.get("EDGE_GEMM_STAGGER")  # four-wave GEMMs: odd workgroups start st x 1024 cycles late
-    if st and hasattr(L, "edge_gemm_set_stagger"):
-        L.edge_gemm_set_stagger(int(st))
-    lx = os.environ.get("EDGE_LRP_ATTN_X6")  # fp32 AttnLRP attention backward: 1 bf16-plane sweeps, 0 f32 MFMA
-    if lx and hasattr(L, "edge_lrp_attn_set_x6"):
-        L.edge_lrp_attn_set_x6(int(lx))
-    qb = os.environ.get("EDGE_GEMM_QKV192_BF16")  # bf16 QKV on the four-wave 256x192 tiles (1) or 128x128 (0)
-    if qb and hasattr(L, "edge_gemm_set_qkv192_bf16"):
-        L.edge_gemm_set_qkv192_bf16(int(qb))
-    sp = os.environ.get("EDGE_GEMM_SPLIT")  # four-wave GEMM epilogue desync: -1 auto, 0 off, k K-tiles
-    if sp and hasattr(L, "edge_gemm_set_split"):
-        L.edge_gemm_set_split(int(sp))
 
 
 def available() -> bool:
@@ -168,8 +121,6 @@ def lib():
             fn.argtypes = argt
             fn.restype = c_ll if name in _LL_RESULT else c_i
         _lib = L
-        if tuning():
-            _apply_tuning_env(L)
     return _lib
 
 

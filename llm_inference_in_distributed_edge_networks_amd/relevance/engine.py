@@ -19,19 +19,13 @@ batch of B windows gives B relevance tables in one pass.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
 from .. import ops
-from ..ops._native import tuning as _tuning
 from ..models.model import DecoderLM
 
 
-# A/B (EDGE_TUNING=1 EDGE_LRP_LAST_ROWS=0): the last layer's O-proj / MLP on every row, as the other layers
-_LAST_ROWS = not (_tuning() and os.environ.get("EDGE_LRP_LAST_ROWS", "1") == "0")
-# A/B (EDGE_TUNING=1 EDGE_LRP_FUSED_SWIGLU=0): gate|up GEMM, then a separate SwiGLU pass over the saved pre-activations
-_FUSED_SWIGLU = not (_tuning() and os.environ.get("EDGE_LRP_FUSED_SWIGLU", "1") == "0")
 
 class RelevanceEngine:
     def __init__(self, model: DecoderLM):
@@ -83,7 +77,7 @@ class RelevanceEngine:
                                         m.q_scale)
             o, lse = ops.attention(q, k, vt, S, need_lse=True)
             sv.update(q=q, k=k, v=vt[..., :S].transpose(-1, -2).contiguous(), o=o, lse=lse.contiguous())
-            if i == nl - 1 and _LAST_ROWS:   # only the seeded rows reach the seed: O-proj and MLP on those rows
+            if i == nl - 1:   # only the seeded rows reach the seed: O-proj and MLP on those rows
                 sv["rows"] = last
                 o, x = o.index_select(0, last), x.index_select(0, last)
                 if not self.qwen:
@@ -92,11 +86,8 @@ class RelevanceEngine:
                 y = ops.linear(o, L["wo"], residual=x, want_ssq=True)
                 ssq2 = y._edge_ssq
                 sv["rs2"] = ops.row_rscale(ssq2, H, cfg.norm_eps)
-                if _FUSED_SWIGLU:   # one GEMM: the SwiGLU activation and the saved pre-activations for its rule
-                    a, sv["gu"] = ops.linear_swiglu_raw(y, t["wgu_n"], norm=(ssq2, cfg.norm_eps))
-                else:
-                    sv["gu"] = ops.linear(y, t["wgu_n"], norm=(ssq2, cfg.norm_eps))
-                    a = ops.swiglu_il(sv["gu"])
+                # one GEMM: the SwiGLU activation and the saved pre-activations for its rule
+                a, sv["gu"] = ops.linear_swiglu_raw(y, t["wgu_n"], norm=(ssq2, cfg.norm_eps))
                 x = ops.linear(a, L["wd"], residual=y)
             else:
                 a = ops.linear(h2, L["wfc"], L["bfc"])

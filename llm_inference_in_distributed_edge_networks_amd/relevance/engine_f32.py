@@ -31,17 +31,13 @@ the tests check it against the autograd oracle ``attnlrp.head_relevance_batched`
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
 from .. import ops
-from ..ops._native import tuning as _tuning
 from ..models.model import DecoderLM
 
 
-# A/B (EDGE_TUNING=1 EDGE_LRP_LAST_ROWS=0): the last layer's O-proj / MLP on every row, as the other layers
-_LAST_ROWS = not (_tuning() and os.environ.get("EDGE_LRP_LAST_ROWS", "1") == "0")
 
 class RelevanceEngineH3:
     def __init__(self, model: DecoderLM):
@@ -99,7 +95,7 @@ class RelevanceEngineH3:
                                        cfg.rotary_dim, m.q_scale)
             o, lse = ops.attention(q, k, vt, S, need_lse=True, in_scales=(sc["att_q"], sc["att_k"], sc["o"]))
             sv.update(q=q, k=k, v=vt[..., :S].transpose(-1, -2).contiguous(), o=o, lse=lse.contiguous())
-            if i == nl - 1 and _LAST_ROWS:   # only the seeded rows reach the seed: O-proj and MLP on those rows
+            if i == nl - 1:   # only the seeded rows reach the seed: O-proj and MLP on those rows
                 sv["rows"] = last
                 x = x.index_select(0, last)
                 if not self.qwen:

@@ -16,20 +16,9 @@ replay i reads; before replaying a slot again the caller makes the stream wait f
 from __future__ import annotations
 
 import gc
-import os
 from typing import Callable
 
 import torch
-
-# A/B (EDGE_TUNING=1 EDGE_GRAPH_GC_OFF=0|1): the collector disabled for the whole capture (round-3 default) or only
-# the collection before it
-_TUNE = os.environ.get("EDGE_TUNING", "0") not in ("", "0")
-_GC_OFF_IN_CAPTURE = not (_TUNE and os.environ.get("EDGE_GRAPH_GC_OFF", "1") == "0")
-# A/B (EDGE_TUNING=1 EDGE_GRAPH_GC_COLLECT=1): an explicit collection before each capture.  Round 3 added one (with
-# the collector off during the capture, which alone keeps a dropped pipeline's CUDAGraph destructor out of a capture);
-# it cost 2.2 % of the fp32 bench and 3.8 % of the bf16 one, same-box, three interleaved rounds
-# (profiles/r04h/gc_ab_and_lrp.txt: fp32 734.1-734.5 k without vs 717.6-719.4 k with, bf16 1.374-1.378 M vs 1.319-1.338 M).
-_GC_COLLECT = _TUNE and os.environ.get("EDGE_GRAPH_GC_COLLECT", "0") == "1"
 
 
 _PRERUN = False
@@ -92,12 +81,10 @@ class GraphCache:
         # a query from another thread aborts the capture.
         # No garbage collection while capturing: a cycle collected mid-capture can hold a dropped CUDAGraph (e.g. of
         # a pipeline rebuilt for another codec), and its destructor is not permitted while a stream captures.  (No
-        # collection forced before it either: measured slower, see _GC_COLLECT.)
-        if _GC_COLLECT:
-            gc.collect()
+        # collection forced before it either: 2.2 % of the fp32 bench and 3.8 % of the bf16 one, same-box, round 4,
+        # profiles/r04h/gc_ab_and_lrp.txt.)
         was = gc.isenabled()
-        if _GC_OFF_IN_CAPTURE:
-            gc.disable()
+        gc.disable()
         try:
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 static_out = self.fn(*static_in)

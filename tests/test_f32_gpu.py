@@ -217,16 +217,13 @@ def test_qkv_rope_h3(B, S, Hq, Hkv, rot, tile, two_term):
     sx = R.h3_scale(x.abs().max().item())
     w3, sw = R.h3_weight(w)
     try:
-        if tile == "192":
-            ops.set_gemm_tile(192)
-        elif tile == "256":
-            ops.set_gemm_qkv192(0)
+        if tile in ("192", "256"):
+            ops.set_gemm_tile(int(tile))
         q, k, vt = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV), cos.to(DEV),
                                    sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125)
         torch.cuda.synchronize()
     finally:
         ops.set_gemm_tile(0)
-        ops.set_gemm_qkv192(1)
     rq, rk, rv = R.qkv_rope(x.double(), w.double(), b.double(), cos.double(), sin.double(), B, S, Hq, Hkv, 64, rot,
                             0.125)
     assert rel_err(q, rq) < 4e-6 and rel_err(k, rk) < 4e-6 and rel_err(vt, rv) < 4e-6
@@ -248,10 +245,8 @@ def test_qkv_kv_planes(B, S, Hq, Hkv, rot, tile):
     w3, sw = R.h3_weight(w)
     sk, sv = 2.0 ** 9, 2.0 ** 11
     try:
-        if tile == "192":
-            ops.set_gemm_tile(192)
-        elif tile == "256":
-            ops.set_gemm_qkv192(0)
+        if tile in ("192", "256"):
+            ops.set_gemm_tile(int(tile))
         q, k, vt, kp, vp = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV),
                                            cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125,
                                            kv_scales=(sk, sv))
@@ -260,7 +255,6 @@ def test_qkv_kv_planes(B, S, Hq, Hkv, rot, tile):
         torch.cuda.synchronize()
     finally:
         ops.set_gemm_tile(0)
-        ops.set_gemm_qkv192(1)
     assert vt is None and torch.equal(q, q2) and torch.equal(k, k2)   # the planes replace the fp32 V^T
     rkp, rvp = R.kv_planes(k.cpu(), vt2.cpu(), sk, sv)
     assert torch.equal(kp.cpu(), rkp)
@@ -298,16 +292,11 @@ def test_attention_kv_planes_bit_identical(B, S, Hq, Hkv, h3):
 
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (3, 100, 14, 2), (1, 2048, 8, 8), (2, 64, 4, 1)])
 @pytest.mark.parametrize("h3", [False, True])
-@pytest.mark.parametrize("variant,planes", [(0, "bf16"), (1, "bf16"), (2, "bf16"), (0, "fp16"), (2, "fp16")])
-def test_attention_f32(B, S, Hq, Hkv, h3, variant, planes):
-    """fp32 attention vs fp64: the split-plane MFMA kernel (variant 0, 64 query rows per workgroup; 2: 128 rows) on
-    three bf16 planes or two scaled fp16 planes (h3), and the native f32 MFMA kernel (1).  The error is dominated by
-    the fp32 exp2 (~5e-6 relative L2 for all; bf16 attention is ~1e-3)."""
-    ops._native.lib().edge_attn_f32_set_variant(variant)
-    try:
-        _attention_f32_case(B, S, Hq, Hkv, h3, planes == "fp16")
-    finally:
-        ops._native.lib().edge_attn_f32_set_variant(2)
+@pytest.mark.parametrize("planes", ["bf16", "fp16"])
+def test_attention_f32(B, S, Hq, Hkv, h3, planes):
+    """fp32 attention vs fp64: the split-plane MFMA kernel (128 query rows per workgroup) on three bf16 planes or two
+    scaled fp16 planes (h3).  The error is dominated by the fp32 exp2 (~5e-6 relative L2; bf16 attention is ~1e-3)."""
+    _attention_f32_case(B, S, Hq, Hkv, h3, planes == "fp16")
 
 
 def _attention_f32_case(B, S, Hq, Hkv, h3, fp16=False, slack=0):
@@ -467,25 +456,24 @@ def test_full_model_kv_planes_identical(name, monkeypatch):
 
 @pytest.mark.parametrize("M,N,K,epi", [(32768, 9728, 896, "swiglu"), (4096, 2048, 512, "gelu"),
                                        (1000, 1024, 896, "resid"), (700, 2048, 512, "bias")])
-@pytest.mark.parametrize("tile", ["256", "256w", "256wp"])
-def test_linear_h3_main_loops(M, N, K, epi, tile):
-    """The h3 (fp32-mode) GEMMs on the C256 (variant 1) and four-wave (variant 11 / 12) main loops."""
-    ops.set_gemm_config(tile)
+def test_linear_h3_four_wave(M, N, K, epi):
+    """The h3 (fp32-mode) GEMMs on the persistent four-wave kernel, forced at every M."""
+    ops.set_gemm_tile(256)
     try:
         test_linear_h3_fp32_accuracy(M, N, K, {"resid": "resid", "gelu": "gelu", "swiglu": "swiglu",
                                                 "bias": "bias"}[epi])
     finally:
-        ops.set_gemm_config("0")
+        ops.set_gemm_tile(0)
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 896, 896), (32768, 896, 896), (32768, 896, 4864), (256 * 3 + 5, 2688, 128)])
 def test_linear_h3_four_wave_224(M, N, K):
     """The fp32-residual O-proj / down GEMMs on the four-wave 256x224 kernel."""
-    ops.set_gemm_config("224w")
+    ops.set_gemm_tile(224)
     try:
         test_linear_h3_fp32_accuracy(M, N, K, "resid")
     finally:
-        ops.set_gemm_config("0")
+        ops.set_gemm_tile(0)
 
 
 @pytest.mark.parametrize("codec", ["mxfp4", "mxfp8", "mixed_mxfp4_mxfp8", "mxfp4_keep"])

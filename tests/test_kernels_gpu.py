@@ -69,48 +69,34 @@ GEMM_CELLS = [(M, N, K, epi, tile)
               for (M, N, K) in [(512, 1152, 896), (300, 896, 896), (1000, 256, 512), (64, 128, 4864),
                                 (700, 1024, 640), (600, 896, 640), (300, 768, 896), (64, 512, 4864)]
               for epi in ["none", "bias", "resid", "bias_resid", "gelu", "swiglu"]
-              for tile in ["128", "256", "256p", "256r", "256s", "256s5"]
+              for tile in ["128", "256"]
               if _tile_fits(N, epi, tile)]
 
 
 @pytest.mark.parametrize("M,N,K,epi,tile", GEMM_CELLS)
 def test_gemm(M, N, K, epi, tile):
-    ops.set_gemm_config(tile)
+    ops.set_gemm_tile(int(tile))
     try:
         _gemm_case(M, N, K, epi)
     finally:
-        ops.set_gemm_config("0")
-
-
-@pytest.mark.parametrize("tile", ["256", "256r", "256rp", "256s", "256s5"])
-@pytest.mark.parametrize("M,N,K,epi", [(4352 + 37, 4096, 192, "resid"), (4352, 4096, 64, "swiglu"),
-                                       (4400, 3968, 128, "bias_resid")])
-def test_gemm_persistent_multi_tile(M, N, K, epi, tile):
-    """More 256x256 tiles than CUs: workgroups walk several tiles, the K-half ring streams across tile
-    boundaries (K=64: two K-halves per tile, the shortest ring), partial last row/column tiles."""
-    ops.set_gemm_config(tile)
-    try:
-        _gemm_case(M, N, K, epi)
-    finally:
-        ops.set_gemm_config("0")
+        ops.set_gemm_tile(0)
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 896, 896), (256 * 70 + 37, 896, 128), (1000, 896, 4864), (64, 896, 192),
                                    (300, 2688, 256)])
 @pytest.mark.parametrize("epi", ["none", "bias", "resid", "bias_resid"])
-@pytest.mark.parametrize("tile", ["224", "224w"])
-def test_gemm_w7(M, N, K, epi, tile):
-    """256x224 tiles (N % 224 == 0, N % 256 != 0), eight-wave and four-wave kernels: partial last row tile, the
-    shortest K loop (two K-tiles, the staging stream crosses tile boundaries every K-tile), more tiles than CUs,
-    several column tiles."""
-    ops.set_gemm_config(tile)
+def test_gemm_224(M, N, K, epi):
+    """256x224 tiles (N % 224 == 0, N % 256 != 0) on the four-wave kernel: partial last row tile, the shortest K loop
+    (two K-tiles, the staging stream crosses tile boundaries every K-tile), more tiles than CUs, several column
+    tiles."""
+    ops.set_gemm_tile(224)
     try:
         _gemm_case(M, N, K, epi)
     finally:
-        ops.set_gemm_config("0")
+        ops.set_gemm_tile(0)
 
 
-def test_gemm_w7_auto_selected_and_inplace():
+def test_gemm_224_auto_selected_and_inplace():
     """The production shape (M = 32768 rows, N = 896) picks the 256x224 kernel by itself (112-column ssq
     partials), in place on the residual stream, with the fused-norm row scale."""
     M, K, N = 32768, 896, 896
@@ -144,15 +130,15 @@ def _gemm_case(M, N, K, epi):
     close(y, ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("tile", ["128", "256", "256r", "256s", "256s5", "256e", "256w"])
+@pytest.mark.parametrize("tile", ["128", "256"])
 def test_gemm_asymmetric_identity(tile):
     # A = I, asymmetric B: catches a transposed C-write
     K = 256
     x = torch.eye(K, dtype=torch.bfloat16)
     w = torch.arange(512 * K, dtype=torch.float32).reshape(512, K).remainder(97).sub(48).to(torch.bfloat16)
-    ops.set_gemm_config(tile)
+    ops.set_gemm_tile(int(tile))
     y = ops.linear(x.to(DEV), w.to(DEV))
-    ops.set_gemm_config("0")
+    ops.set_gemm_tile(0)
     assert torch.equal(y.cpu().float(), w.t().float())
 
 
@@ -191,16 +177,9 @@ def _qkv(B, S, Hq, Hkv, seed):
     return q, k, vt
 
 
-@pytest.fixture(params=[2, 3, 1, 4, 5], ids=["fa2", "fa2occ3", "fa1", "fa3occ3", "fa3"])
-def attn_variant(request):
-    ops.set_attn_variant(request.param)
-    yield request.param
-    ops.set_attn_variant(4)
-
-
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (1, 100, 4, 2), (3, 64, 8, 8), (1, 1000, 2, 1),
                                         (5, 200, 14, 2), (9, 128, 4, 2)])
-def test_flash_attention(B, S, Hq, Hkv, attn_variant):
+def test_flash_attention(B, S, Hq, Hkv):
     q, k, vt = _qkv(B, S, Hq, Hkv, 40)
     o, lse = ops.attention(q.to(DEV), k.to(DEV), vt.to(DEV), S, need_lse=True)
     ro, rlse = R.attention(q, k, vt, S, need_lse=True)
@@ -209,7 +188,7 @@ def test_flash_attention(B, S, Hq, Hkv, attn_variant):
 
 
 @pytest.mark.parametrize("pos", [(200, 230), (3, 250), (70, 71)])
-def test_flash_attention_spike(pos, attn_variant):
+def test_flash_attention_spike(pos):
     # force the online-softmax rescale: one key much larger for one query (early, late, same tile)
     B, S, Hq, Hkv = 1, 256, 2, 1
     q, k, vt = _qkv(B, S, Hq, Hkv, 50)
@@ -222,7 +201,7 @@ def test_flash_attention_spike(pos, attn_variant):
 
 
 @pytest.mark.parametrize("S", [512, 200, 130])
-def test_flash_attention_scored_rows(S, attn_variant):
+def test_flash_attention_scored_rows(S):
     """n_rows mode (last layer): the rows >= S-1-n_rows[b] of every window are exact; others may be skipped."""
     B, Hq, Hkv = 3, 14, 2
     q, k, vt = _qkv(B, S, Hq, Hkv, 41)
@@ -270,11 +249,11 @@ def test_head_nll_vocab_size_tiles(R_):
     t[:4] = torch.tensor([0, V - 1, V - 64, V - 129])   # targets in the first / last (partial) column tiles
     hd, wd, td = h.to(DEV), w.to(DEV), t.to(DEV)
     nll = ops.head_nll(hd, wd, td)
-    ops._native.lib().edge_gemm_set_lse256(0)
+    ops.set_gemm_tile(128)
     try:
         nll128 = ops.head_nll(hd, wd, td)
     finally:
-        ops._native.lib().edge_gemm_set_lse256(1)
+        ops.set_gemm_tile(0)
     close(nll, nll128, atol=2e-3, rtol=1e-3)
     close(nll[:64], R.head_nll(h[:64], w, t[:64]), atol=2e-2, rtol=1e-2)
 
@@ -323,7 +302,7 @@ def test_row_ssq(H):
     close(s, R.row_ssq(x), atol=1e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("tile", ["128", "224", "224w", "256", "256r", "256s", "256s5", "256w"])
+@pytest.mark.parametrize("tile", ["128", "224", "256"])
 @pytest.mark.parametrize("act", [None, "swiglu_il"])
 def test_gemm_fused_norm_and_ssq_out(tile, act):
     M, K, N = 700, 896, 1024
@@ -332,14 +311,14 @@ def test_gemm_fused_norm_and_ssq_out(tile, act):
     nw = rnd(K, s=0.1, seed=93) + 1
     ssq = R.row_ssq(x)
     wn = R.fold_norm_weight(w, nw)
-    ops.set_gemm_config(tile)
+    ops.set_gemm_tile(int(tile))
     try:
         y = ops.linear(x.to(DEV), wn.to(DEV), act=act, norm=(ssq.to(DEV), 1e-6))
         r = rnd(M, 896, seed=94)
         w2 = rnd(896, K, s=1 / math.sqrt(K), seed=95)
         y2 = ops.linear(x.to(DEV), w2.to(DEV), residual=r.to(DEV), want_ssq=True)
     finally:
-        ops.set_gemm_config("0")
+        ops.set_gemm_tile(0)
     ref = R.linear(R.rmsnorm(x, nw, 1e-6), w, act=act, out_dtype=torch.float32)
     close(y, ref, atol=4e-2, rtol=3e-2)
     # producer side: residual GEMM emits the ssq partials of its stored output (64- or 112-column slabs)
@@ -347,34 +326,32 @@ def test_gemm_fused_norm_and_ssq_out(tile, act):
     if y2._edge_ssq.shape == ref_ssq.shape:
         close(y2._edge_ssq, ref_ssq, atol=1e-2, rtol=1e-4)
     else:
-        assert tile.startswith("224") and y2._edge_ssq.shape == (M, 896 // 112)
+        assert tile == "224" and y2._edge_ssq.shape == (M, 896 // 112)
         ref_ssq = y2.cpu().float().pow(2).reshape(M, 8, 112).sum(-1)
         close(y2._edge_ssq, ref_ssq, atol=1e-2, rtol=1e-4)
 
 
-@pytest.mark.parametrize("B,S,mode,rot", [(2, 256, 1, 64), (64, 512, 2, 64), (64, 512, 0, 64), (40, 512, 2, 16)])
-def test_qkv_rope_fused_norm(B, S, mode, rot):
-    """QKV + bias + RoPE + fused RMSNorm (ssq partials): 128x128 tiles, and the four-wave 256x256 kernel (mode 2)
-    at production row counts (partial last column tile N = 1152), full and partial rotary."""
+@pytest.mark.parametrize("B,S,tile,rot", [(2, 256, 0, 64), (64, 512, 256, 64), (64, 512, 0, 64), (40, 512, 256, 16)])
+def test_qkv_rope_fused_norm(B, S, tile, rot):
+    """QKV + bias + RoPE + fused RMSNorm (ssq partials): 128x128 tiles (automatic), and the four-wave 256x256 kernel
+    (forced) at production row counts (partial last column tile N = 1152), full and partial rotary."""
     Hq, Hkv, Hd = 14, 2, 896
     cos, sin = R.rope_tables(1024, max(rot, 2), 1e6)
-    ops.set_gemm_qkv256(mode)
+    ops.set_gemm_tile(tile)
     try:
         _qkv_case(B, S, Hq, Hkv, Hd, cos, sin, rot)
     finally:
-        ops.set_gemm_qkv256(1)
+        ops.set_gemm_tile(0)
 
 
 @pytest.mark.parametrize("B,S,norm", [(64, 512, True), (2, 256, True), (2, 512, False), (3, 100, True)])
 def test_qkv_rope_bf16_192(B, S, norm):
     """bf16 QKV on the four-wave 256x192 tiles (permuted head blocks, RoPE pairs in one lane, fused RMSNorm row scale
-    from the ssq partials, bf16 q / k / V^T): the production shape by the switch, small shapes (partial row tiles,
-    S not a multiple of 64, no norm) by the tile override."""
+    from the ssq partials, bf16 q / k / V^T), forced by the tile override: the production shape and small shapes
+    (partial row tiles, S not a multiple of 64, no norm)."""
     Hq, Hkv, Hd = 14, 2, 896
     cos, sin = R.rope_tables(1024, 64, 1e6)
-    ops.set_gemm_qkv192_bf16(1)
-    if B * S < 64 * 512:
-        ops.set_gemm_tile(192)
+    ops.set_gemm_tile(192)
     try:
         if norm:
             _qkv_case(B, S, Hq, Hkv, Hd, cos, sin, 64)
@@ -389,7 +366,6 @@ def test_qkv_rope_bf16_192(B, S, norm):
             close(k, rk, atol=3e-2, rtol=2e-2)
             close(vt, rvt, atol=3e-2, rtol=2e-2)
     finally:
-        ops.set_gemm_qkv192_bf16(0)
         ops.set_gemm_tile(0)
 
 
@@ -435,16 +411,14 @@ def test_fused_norm_model_matches_unfused():
 @pytest.mark.parametrize("M,N,K,epi", [(4352 + 37, 4096, 192, "resid"), (4352, 4096, 64, "swiglu"),
                                        (4400, 3968, 128, "bias_resid"), (300, 1024, 896, "none"),
                                        (32768, 9728, 896, "swiglu"), (8192, 2048, 4864, "gelu")])
-@pytest.mark.parametrize("tile", ["256e", "256w", "256wp"])
-def test_gemm_eight_phase(M, N, K, epi, tile):
-    """Variant 10 (eight-phase full-line K-tiles, half-tile DMA stream across tile boundaries) and variant 11
-    (four waves of 128x128, K-tile stream across tile boundaries): partial row/column tiles, K = one K-tile (64:
-    the prologue's K-tiles span tiles), more tiles than CUs."""
-    ops.set_gemm_config(tile)
+def test_gemm_four_wave_multi_tile(M, N, K, epi):
+    """The persistent four-wave kernel (128x128 wave tiles, K-tile stream across tile boundaries): partial row /
+    column tiles, K = one K-tile (64: the prologue's K-tiles span tiles), more tiles than CUs."""
+    ops.set_gemm_tile(256)
     try:
         _gemm_case(M, N, K, epi)
     finally:
-        ops.set_gemm_config("0")
+        ops.set_gemm_tile(0)
 
 
 @pytest.mark.parametrize("name", ["rgroup", "mixed_rgroup_int8"])

@@ -60,6 +60,11 @@ def test_bench_contract_cpu(n):
     assert d["config"]["global_batch"] == 2 * 2 * dp
     assert d["ppl_random_weights"] and d["ppl_random_weights"] > 1
     assert d["dtype"] == "fp32" and d["metric"].startswith("WikiText-2 PPL + inter-stage bytes/token")
+    assert d["config"]["last_layer_rows"] == "scored"
+    # the senders' measured byte counters: for a fixed-k codec exactly the wire layout's message size per token
+    from llm_inference_in_distributed_edge_networks_amd import codec as C
+    want = C.message_bytes(C.get_codec("mixed_int4_int8"), 2, 128, 256, 0.5, __import__("torch").float32) / (2 * 128)
+    assert d["wire_bytes_per_token"] == [round(want, 2)]
     if n > 1:   # per-stage GPU-time breakdown rows, one per rank
         assert len(d["stages"]) == n and {s["stage"] for s in d["stages"]} == {0, 1}
         # the p2p probe of every pipeline edge (one per replica), a 1 MiB and a boundary-sized message
@@ -68,6 +73,20 @@ def test_bench_contract_cpu(n):
             assert row["stage"] == 0 and row["edge"][1] == row["edge"][0] + 1
             assert row["p2p_us"] > 0 and row["p2p_GBps"] > 0
         assert {row["bytes"] for row in d["p2p"]} == {1 << 20, round(d["wire_bytes_per_token"][0] * 2 * 128)}
+    if n > 2:   # the secondary measurement: one n-stage pipeline over all the ranks (BASELINE config 4 at n = 4)
+        _check_deep(d, n)
+    else:
+        assert "value_pp2" not in d and "pp2" not in d
+
+
+def _check_deep(d, n):
+    assert d[f"value_pp{n}"] > 0, d.get(f"pp{n}")
+    deep = d[f"pp{n}"]
+    assert deep["parallelism"] == f"pp{n}xdp1" and len(deep["stage_layers"]) == n
+    assert len(deep["stages"]) == n and {s["stage"] for s in deep["stages"]} == set(range(n))
+    assert len(deep["wire_bytes_per_token"]) == n - 1 and all(w > 0 for w in deep["wire_bytes_per_token"])
+    assert len(deep["p2p"]) == 2 * (n - 1) and {r["stage"] for r in deep["p2p"]} == set(range(n - 1))
+    assert deep["ppl_random_weights"] > 1 and deep["ms_per_step"] > 0
 
 
 @pytest.mark.parametrize("pp", [4, 8])
@@ -81,6 +100,17 @@ def test_bench_deep_pipeline_cpu(pp):
     d = _json_line(r.stdout)
     assert d["config"]["parallelism"] == f"pp{pp}xdp1" and len(d["config"]["stage_layers"]) == pp
     assert len(d["wire_bytes_per_token"]) == pp - 1 and len(d["stages"]) == pp
+
+
+def test_bench_eight_ranks_reports_pp8_cpu():
+    """The driver's default 8-GPU run (pp2 x dp4 headline) also times one 8-stage pipeline (BASELINE config 5's
+    shape) and reports it beside the headline."""
+    r = _torchrun(8, ["bench.py", "--model", "byte-qwen2", "--batch", "1", "--steps", "2", "--warmup", "1",
+                      "--max-length", "64", "--split", "3", "--gpus", "8"], timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["config"]["parallelism"] == "pp2xdp4" and d["n_gpus"] == 8
+    _check_deep(d, 8)
 
 
 def test_pipeline_entry_distributed_equals_local(tmp_path):
@@ -149,7 +179,7 @@ def test_bench_refuses_gpus_world_size_mismatch():
 def test_bench_failed_rank_exits_nonzero_without_json(rank):
     """A rank that dies (here on purpose, after its measurement) must leave the self-launching parent with a
     non-zero exit code and NO JSON line: rank 0 reports only after every rank passed the final barrier."""
-    env = dict(_env(), EDGE_BENCH_FAIL_RANK=str(rank))
+    env = dict(_env(), EDGE_BENCH_FAIL_RANK=str(rank), EDGE_TUNING="1")   # a tuning-mode-only test hook
     r = subprocess.run([sys.executable] + BENCH + ["--gpus", "2"], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=600)
     assert r.returncode != 0

@@ -100,16 +100,11 @@ def test_relevance_engine_gpu_vs_cpu(cfg):
     assert rel_err(wg / wg.sum(-1, keepdim=True), wc / wc.sum(-1, keepdim=True)) < 0.04
 
 
-@pytest.mark.parametrize("x6", [1, 0])
 @pytest.mark.parametrize("B,Hq,Hkv,S", [(2, 14, 2, 512), (1, 8, 8, 200), (3, 4, 2, 96), (1, 2, 1, 37)])
-def test_lrp_attn_bwd_f32(B, Hq, Hkv, S, x6):
-    """fp32 attention LRP backward vs the fp64 reference: fp32-rounding agreement for both sweeps - the bf16
-    matrix-core split (x6 = 1, three bf16 planes, six products; the default) and the f32 MFMA (x6 = 0)."""
-    ops.set_lrp_attn_x6(x6)
-    try:
-        _lrp_attn_bwd_f32_case(B, Hq, Hkv, S)
-    finally:
-        ops.set_lrp_attn_x6(1)
+def test_lrp_attn_bwd_f32(B, Hq, Hkv, S):
+    """fp32 attention LRP backward vs the fp64 reference: fp32-rounding agreement of the bf16 matrix-core sweeps on
+    three-bf16-plane splits (six products)."""
+    _lrp_attn_bwd_f32_case(B, Hq, Hkv, S)
 
 
 def test_lrp_attn_bwd_x6_dynamic_range():

@@ -41,12 +41,12 @@ def test_qwen2_production_shapes_w7_vs_256():
     bcfg = BoundaryConfig("mixed_int4_int8", 0.5, "regular_importance")
     assert ops.gemm_ssq_parts(32768, 896, 896, residual=True) == 8   # the 256x224 kernel is selected
     w7 = LocalPipeline(m, plan, bcfg, use_graphs=False).run_batch(b).clone()
-    ops.set_gemm_w7(False)
+    ops.set_gemm_tile(256)   # every GEMM on 256x256 tiles (N = 896: a half-used last column tile)
     try:
         assert ops.gemm_ssq_parts(32768, 896, 896, residual=True) == 14
         c256 = LocalPipeline(m, plan, bcfg, use_graphs=False).run_batch(b).clone()
     finally:
-        ops.set_gemm_w7(2)
+        ops.set_gemm_tile(0)
     assert torch.isfinite(w7).all()
     # same math, different tiling / partial-sum order: bf16-level differences through 24 layers
     assert torch.allclose(w7, c256, rtol=2e-2, atol=2e-2), (w7 - c256).abs().max()

@@ -1,4 +1,4 @@
-"""Flash-attention forward: v1 / v2 / v3 kernels at the bench shape (B windows x 512, 14 q / 2 kv heads, d=64)."""
+"""Flash-attention forward (bf16 and fp32 modes) at the bench shape (B windows x 512, 14 q / 2 kv heads, d=64)."""
 import argparse
 import json
 import os
@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--Hkv", type=int, default=2)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--fp32", action="store_true", help="the fp32-mode kernels: split-plane (bf16 x6 / fp16 h3) vs native f32 MFMA")
+    ap.add_argument("--fp32", action="store_true", help="the fp32-mode kernel: bf16 x6 planes / scaled fp16 h3 planes")
     a = ap.parse_args()
     if a.fp32:
         return bench_fp32(a)
@@ -30,8 +30,7 @@ def main():
     flop = 4.0 * B * Hq * 64 * sum(i + 1 for i in range(S))   # causal QK^T + PV
     res = {}
     for r in range(a.rounds):
-        for v in (1, 2, 3, 4, 5):
-            ops.set_attn_variant(v)
+        for v in (3,):
             for lse in (False, True):
                 ops.attention(q, k, vt, S, need_lse=lse)
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,7 +42,6 @@ def main():
                 us = st.elapsed_time(en) / a.iters * 1e3
                 key = f"v{v}{'_lse' if lse else ''}"
                 res.setdefault(key, []).append(us)
-    ops.set_attn_variant(4)
     out = {k_: {"us": round(min(v), 2), "TFLOPs": round(flop / min(v) * 1e-6, 1)} for k_, v in res.items()}
     print(json.dumps({"shape": [B, S, Hq, Hkv], **out}))
 
@@ -56,12 +54,8 @@ def bench_fp32(a):
     vt = torch.randn(B, Hkv, 64, ops.s_pad(S), generator=g).cuda()
     flop = 4.0 * B * Hq * 64 * sum(i + 1 for i in range(S))
     res = {}
-    lib = ops._native.lib()
     for _ in range(a.rounds):
-        for v, name, sc in ((0, "x6_bf16_mfma", None), (2, "x6_bf16_mfma_128rows", None), (1, "f32_mfma", None),
-                            (0, "h3_fp16_mfma", (1024.0, 1024.0, 1024.0)),
-                            (2, "h3_fp16_mfma_128rows", (1024.0, 1024.0, 1024.0))):
-            lib.edge_attn_f32_set_variant(v)
+        for name, sc in (("x6_bf16_mfma", None), ("h3_fp16_mfma", (1024.0, 1024.0, 1024.0))):
             for h3 in (0.0, 1.0):
                 ops.attention(q, k, vt, S, need_lse=True, h3=h3, in_scales=sc)
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -71,7 +65,6 @@ def bench_fp32(a):
                 en.record()
                 torch.cuda.synchronize()
                 res.setdefault(f"{name}{'_h3out' if h3 else ''}", []).append(st.elapsed_time(en) / a.iters * 1e3)
-    lib.edge_attn_f32_set_variant(2)
     out = {k_: {"us": round(min(v), 2), "TFLOPs_fp32": round(flop / min(v) * 1e-6, 1)} for k_, v in res.items()}
     print(json.dumps({"shape": [B, S, Hq, Hkv], "dtype": "fp32", **out}))
 

@@ -58,8 +58,7 @@ def main():
     ap.add_argument("--m", type=int, default=0, help="override M")
     ap.add_argument("--json", default="")
     ap.add_argument("--only", default="", help="comma list of shapes")
-    ap.add_argument("--tiles", default="0", help="comma list of GEMM configs: 0=auto, 128, 256 + main-loop variant "
-                    "suffix ('' asm reads, p plain loads, r K-half ring, rp ring + setprio), e.g. 256,256r")
+    ap.add_argument("--tiles", default="0", help="comma list of forced tiles: 0 = automatic, 128, 192, 224, 256")
     ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt comparison (profiling)")
     a = ap.parse_args()
     dev = "cuda"
@@ -81,24 +80,9 @@ def main():
         out = torch.empty(M, No, device=dev, dtype=torch.float32 if h3 else torch.bfloat16)
         tiles = a.tiles.split(",")
 
-        def mk(spec):  # spec may end in "/w0" = strided persistent tile walk instead of XCD chunks, or "/noepi" =
-            # timing ablation of the persistent 256x256 loop without its epilogue (wrong results)
-            # "/m<k>": W7 epilogue memory mode k (bit 0 nt stores, bit 1 nt residual loads)
-            # "/nob1": B tiles staged on even K-tiles only, "/nob": no B staging (four-wave kernel, wrong results)
-            # "/notrans": SwiGLU h3 epilogue without its two transcendentals (four-wave kernel, wrong results)
-            last = spec.rpartition("/")[2]
-            # "/novp": QKV epilogue without the V^T plane stores (four-wave 192 kernel, wrong results)
-            noepi = {"/noepi": 1, "/nostore": 2, "/nob1": 3, "/nob": 4, "/notrans": 5, "/novp": 6}.get("/" + last, 0)
-            if noepi:
-                spec = spec.rpartition("/")[0]
-            mode = int(spec.partition("/m")[2] or 0)
-            cfg, _, walk = spec.partition("/m")[0].partition("/w")
-
+        def mk(spec):
             def f():
-                ops.set_gemm_config(cfg)
-                ops.set_gemm_walk(int(walk) if walk else 1)
-                ops._native.lib().edge_gemm_set_skip_epi(int(noepi))
-                ops._native.lib().edge_gemm_set_w7_mode(mode)
+                ops.set_gemm_tile(int(spec))
                 if act == "qkv_rope":
                     ops.qkv_rope(x, w, b, cos, sin, M // 512, 512, 14, 2, 64, 64, 0.125)
                 elif act == "h3_qkv_rope":
@@ -111,8 +95,6 @@ def main():
                     ops.linear_h3(x, w, 1.0, bias=b, residual=r, out=out)
                 else:
                     ops.linear(x, w, bias=b, residual=r, act=act, out=out)
-                ops._native.lib().edge_gemm_set_skip_epi(0)
-                ops._native.lib().edge_gemm_set_w7_mode(0)
             return f
         if act in ("qkv_rope", "h3_qkv_rope", "h3_qkv_rope_kvp"):
             cos, sin = (t.to(dev) for t in ops.rope_tables(512, 64, 1e6))
@@ -132,8 +114,7 @@ def main():
                 t_v[t].append(timeit(f, a.iters))
             t_o.append(min(statistics.median(t_v[t]) for t in tiles))
             t_l.append(timeit(lib, a.iters) if not a.no_lib else 1.0)
-        ops.set_gemm_config("0")
-        ops.set_gemm_walk(True)
+        ops.set_gemm_tile(0)
         fl = 2.0 * M * N * K
         for t, v in t_v.items():
             print(f"   tile={t:>4s}: {statistics.median(v)*1e6:8.1f}us {fl/statistics.median(v)/1e12:7.1f} TF", flush=True)
