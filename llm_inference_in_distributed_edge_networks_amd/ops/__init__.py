@@ -381,7 +381,6 @@ def head_nll(h, w, targets):
     tgt = torch.empty(R, dtype=torch.float32, device=h.device)
     nll = torch.empty(R, dtype=torch.float32, device=h.device)
     t64 = targets.to(torch.int64).contiguous()
-    _gemm_ws(h.device)
     call("edge_gemm_lse", ptr(h), ptr(w), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, K, 0, 0.0, stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
     return nll
@@ -450,7 +449,6 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
         out = torch.empty(M, 2 * No, dtype=torch.float16, device=a3.device)
         ldc = 2 * No
         code = _ACT[act]
-    _gemm_ws(a3.device)
     call("edge_gemm_f32", ptr(a3), ptr(w3), ptr(out), M, N, Kx, kp, a3.stride(0), w3.stride(0), ldc, ptr(bias),
          ptr(residual), 0 if residual is None else residual.stride(0), code, ptr(rscale), float(alpha),
          float(out_scale), stream())
@@ -493,7 +491,6 @@ def linear_h3_swiglu_raw(a3: torch.Tensor, w3: torch.Tensor, alpha: float, out_s
     _check_f32(rscale)
     planes = torch.empty(M, N, dtype=torch.float16, device=a3.device)
     raw = torch.empty(M, N, dtype=torch.float32, device=a3.device)
-    _gemm_ws(a3.device)
     call("edge_gemm_f32_swiglu_raw", ptr(a3), ptr(w3), ptr(planes), ptr(raw), M, N, Kx, kp, a3.stride(0),
          w3.stride(0), N, ptr(rscale), float(alpha), float(out_scale), stream())
     return planes, raw
@@ -528,7 +525,6 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
         kpl = torch.empty(B, Hkv, 2, S, D, **f16)
         vpl = torch.zeros(B, Hkv, 2, D, sp, **f16) if sp != S else torch.empty(B, Hkv, 2, D, sp, **f16)
     sk_, sv_ = kv_scales if kv_scales is not None else (0.0, 0.0)
-    _gemm_ws(a3.device)
     call("edge_gemm_qkv_rope_f32", ptr(a3), ptr(w3), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, kp, S,
          Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), ptr(kpl), ptr(vpl), float(sk_), float(sv_), stream())
     if kv_scales is None:
@@ -549,7 +545,6 @@ def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch
     pmax, psum = torch.empty(R, nparts, **f32), torch.empty(R, nparts, **f32)
     tgt, nll = torch.empty(R, **f32), torch.empty(R, **f32)
     t64 = targets.to(torch.int64).contiguous()
-    _gemm_ws(a3.device)
     call("edge_gemm_lse", ptr(a3), ptr(w3), ptr(t64), ptr(pmax), ptr(psum), ptr(tgt), R, V, Kx, kp, float(alpha),
          stream())
     call("edge_lse_reduce", ptr(pmax), ptr(psum), ptr(tgt), ptr(nll), R, nparts, stream())
