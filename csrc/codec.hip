@@ -18,10 +18,11 @@
 #include "common.h"
 
 enum { FMT_BF16 = 0, FMT_INT8 = 1, FMT_INT4 = 2, FMT_INT2 = 3, FMT_F32 = 4, FMT_MXFP4 = 5, FMT_MXFP8 = 6, FMT_GRP = 7 };
-// Head-group rows (FMT_GRP): every 64-channel group g (one head's width) has its own bit width b_g in {2, 4, 8}
-// (the plan: one byte per group in the message at off_plan, chosen from the boundary's channel-group relevance) and
-// its own max-abs scale s = max|x| / qmax_b (qmax 1 / 7 / 127): row = [group 0 codes (8 b_0 bytes)] ... [group G-1
-// codes][G fp32 scales]; codes are two's-complement int2 / int4 / int8 packed as the uniform formats.
+// Head-group rows (FMT_GRP): every 64-channel group g (one head's width) has its own bit width b_g in {2, 3, 4, 5, 6, 8}
+// (the plan: one byte per group in the message at off_plan, chosen from the boundary's channel-group sensitivity) and
+// its own max-abs scale s = max|x| / qmax_b (qmax = 2^(b-1) - 1: 1 / 3 / 7 / 15 / 31 / 127): row = [group 0 codes
+// (8 b_0 bytes)] ... [group G-1 codes][G fp32 scales]; the group's 64 two's-complement b-bit codes form one
+// little-endian bit stream (code c at bits [b c, b c + b)), so 8 consecutive codes are b whole bytes.
 // OCP microscaling rows (FMT_MXFP4: E2M1 codes, FMT_MXFP8: E4M3 codes): blocks of 32 consecutive channels share one
 // E8M0 scale 2^(floor(log2 max|x|) - emax) (emax 2 / 8), stored after the row's codes: [codes][H/32 scale bytes].
 // Quantize / dequantize with gfx950's scaled converts (v_cvt_scalef32_pk_fp4_f32 / _fp8_f32 and the inverses:
@@ -303,6 +304,38 @@ __device__ __forceinline__ int grp_offset(const uint8_t* __restrict__ plan, int 
   for (int i = 0; i < g; ++i) o += 8 * plan[i];
   return o;
 }
+// The 8 codes of a lane are bytes [sub b, sub b + b) of the group's stream (sub = lane & 7), b-byte aligned: whole
+// 8 / 4 / 2-byte stores for b = 8 / 4 / 2, 2-byte pieces for b = 6, single bytes for b = 3 / 5.
+__device__ __forceinline__ void grp_store(uint8_t* __restrict__ dst, uint64_t w, int bits) {
+  if (bits == 8) {
+    *(u32x2_t*)dst = u32x2_t{(uint32_t)w, (uint32_t)(w >> 32)};
+  } else if (bits == 4) {
+    *(uint32_t*)dst = (uint32_t)w;
+  } else if (bits == 2) {
+    *(uint16_t*)dst = (uint16_t)w;
+  } else if (bits == 6) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ((uint16_t*)dst)[i] = (uint16_t)(w >> (16 * i));
+  } else {
+    for (int i = 0; i < bits; ++i) dst[i] = (uint8_t)(w >> (8 * i));
+  }
+}
+__device__ __forceinline__ uint64_t grp_load(const uint8_t* __restrict__ src, int bits) {
+  if (bits == 8) {
+    const u32x2_t v = *(const u32x2_t*)src;
+    return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+  }
+  if (bits == 4) return *(const uint32_t*)src;
+  if (bits == 2) return *(const uint16_t*)src;
+  uint64_t w = 0;
+  if (bits == 6) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w |= (uint64_t)((const uint16_t*)src)[i] << (16 * i);
+  } else {
+    for (int i = 0; i < bits; ++i) w |= (uint64_t)src[i] << (8 * i);
+  }
+  return w;
+}
 __device__ __forceinline__ void grp_pack8(uint8_t* __restrict__ row, const CodecArgs& a, int col,
                                           const float (&v)[8]) {
   const int lane = threadIdx.x & 63;
@@ -318,27 +351,12 @@ __device__ __forceinline__ void grp_pack8(uint8_t* __restrict__ row, const Codec
   const float s = am / (float)qmax;
   const float inv = am > 0.f ? 1.f / s : 0.f;
   const float qf = (float)qmax;
-  int q[8];
+  const uint64_t mask = (1ull << bits) - 1;
+  uint64_t w = 0;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) q[e] = (int)qround(v[e] * inv, qf, -qf);
-  uint8_t* dst = row + grp_offset(plan, g);
+  for (int e = 0; e < 8; ++e) w |= ((uint64_t)(int64_t)(int)qround(v[e] * inv, qf, -qf) & mask) << (bits * e);
   const int sub = lane & 7;
-  if (bits == 8) {
-    u32x2_t w;
-    w[0] = (q[0] & 255) | ((q[1] & 255) << 8) | ((q[2] & 255) << 16) | ((uint32_t)(q[3] & 255) << 24);
-    w[1] = (q[4] & 255) | ((q[5] & 255) << 8) | ((q[6] & 255) << 16) | ((uint32_t)(q[7] & 255) << 24);
-    *(u32x2_t*)(dst + sub * 8) = w;
-  } else if (bits == 4) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) w |= (uint32_t)(q[e] & 15) << (4 * e);
-    *(uint32_t*)(dst + sub * 4) = w;
-  } else {
-    uint32_t w = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) w |= (uint32_t)(q[e] & 3) << (2 * e);
-    *(uint16_t*)(dst + sub * 2) = (uint16_t)w;
-  }
+  grp_store(row + grp_offset(plan, g) + sub * bits, w, bits);
   if (sub == 0) *(float*)(row + a.grp_code_bytes + 4 * g) = s;
 }
 __device__ __forceinline__ void grp_unpack8(const uint8_t* __restrict__ row, const CodecArgs& a, int col,
@@ -346,28 +364,14 @@ __device__ __forceinline__ void grp_unpack8(const uint8_t* __restrict__ row, con
   const int lane = threadIdx.x & 63;
   const uint8_t* plan = a.msg + a.off_plan;
   const int g = col >> 6, bits = plan[g];
-  const uint8_t* src = row + grp_offset(plan, g);
   const int sub = lane & 7;
+  const uint64_t w = grp_load(row + grp_offset(plan, g) + sub * bits, bits);
   const float s = *(const float*)(row + a.grp_code_bytes + 4 * g);
-  int q[8];
-  if (bits == 8) {
-    const u32x2_t w = *(const u32x2_t*)(src + sub * 8);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      q[e] = (int)(int8_t)((w[0] >> (8 * e)) & 255);
-      q[4 + e] = (int)(int8_t)((w[1] >> (8 * e)) & 255);
-    }
-  } else if (bits == 4) {
-    const uint32_t w = *(const uint32_t*)(src + sub * 4);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = ((int)(w << (28 - 4 * e))) >> 28;
-  } else {
-    const uint32_t w = *(const uint16_t*)(src + sub * 2);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = ((int)(w << (30 - 2 * e))) >> 30;
+  for (int e = 0; e < 8; ++e) {
+    const int q = ((int)((uint32_t)(w >> (bits * e)) << (32 - bits))) >> (32 - bits);   // sign-extend b bits
+    o[e] = (float)q * s;
   }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = (float)q[e] * s;
 }
 
 template <int NCH, class T>

@@ -810,18 +810,37 @@ __global__ __launch_bounds__(256) void lrp_ln_bwd_f32_kernel(const float* __rest
 
 // Channel-group relevance of the residual stream: out[b * ob + g] = sum over the window's S tokens and the group's
 // 64 channels of |x dx|.  One workgroup per (window, group); deterministic (no atomics).
+// sens (optional): the group's quantization sensitivity sum over tokens t of max_c |x_tc|^2 * sum_c dx_tc^2 - the
+// expected squared first-order output change of a max-abs quantizer of step max_c |x_tc| / qmax is that over 12 qmax^2
+// (codec.wire.allocate_group_bits).  Wave w takes tokens w, w + 4, ...; its 64 lanes are the group's channels.
 __global__ __launch_bounds__(256) void group_absprod_kernel(const float* __restrict__ x, const float* __restrict__ dx,
-                                                            float* __restrict__ out, int S, int H, int G, int ob) {
+                                                            float* __restrict__ out, float* __restrict__ sens, int S,
+                                                            int H, int G, int ob) {
   __shared__ float red[4];
   const int b = blockIdx.x / G, gi = blockIdx.x - b * G;
   const int c = threadIdx.x & 63;
-  float acc = 0.f;
+  float acc = 0.f, sacc = 0.f;
   for (int s = threadIdx.x >> 6; s < S; s += 4) {
     const size_t off = ((size_t)b * S + s) * H + gi * 64 + c;
-    acc += fabsf(x[off] * dx[off]);
+    const float xv = x[off], dv = dx[off];
+    acc += fabsf(xv * dv);
+    if (sens) {   // uniform branch: every lane of the wave takes part in the reductions
+      float am = fabsf(xv), d2 = dv * dv;
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) {
+        am = fmaxf(am, __shfl_xor(am, m, 64));
+        d2 += __shfl_xor(d2, m, 64);
+      }
+      if (c == 0) sacc += am * am * d2;
+    }
   }
   acc = block_sum<256>(acc, red);
   if (threadIdx.x == 0) out[(size_t)b * ob + gi] = acc;
+  if (sens) {
+    __syncthreads();
+    sacc = block_sum<256>(sacc, red);
+    if (threadIdx.x == 0) sens[(size_t)b * ob + gi] = sacc;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -934,11 +953,13 @@ EDGE_API int edge_lrp_ln_bwd_f32(const float* dy1, const float* rs, const float*
   return (int)hipGetLastError();
 }
 
-EDGE_API int edge_group_absprod(const float* x, const float* dx, float* out, int B, int S, int H, int out_stride,
-                                hipStream_t st) {
+// out [B, >= H/64] (row stride out_stride): sum |x dx| per window and 64-channel group; sens (nullable, same layout):
+// the quantization sensitivity of group_absprod_kernel
+EDGE_API int edge_group_absprod(const float* x, const float* dx, float* out, float* sens, int B, int S, int H,
+                                int out_stride, hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
   if (H % 64) return (int)hipErrorInvalidValue;
   const int G = H / 64;
-  group_absprod_kernel<<<B * G, 256, 0, st>>>(x, dx, out, S, H, G, out_stride);
+  group_absprod_kernel<<<B * G, 256, 0, st>>>(x, dx, out, sens, S, H, G, out_stride);
   return (int)hipGetLastError();
 }

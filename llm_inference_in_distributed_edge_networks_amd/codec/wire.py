@@ -54,7 +54,7 @@ class CodecSpec:
     ch_kind: int = CH_MAXABS
     uses_ratio: bool = True      # lo class = int(ratio*S) least important tokens
     needs_importance: bool = True
-    plan: tuple | None = None    # FMT_GRP rows: bits (2 / 4 / 8) of every 64-channel group (with_plan)
+    plan: tuple | None = None    # FMT_GRP rows: bits (GROUP_BITS) of every 64-channel group (with_plan)
 
 
 CODECS = {c.name: c for c in [
@@ -80,7 +80,7 @@ CODECS = {c.name: c for c in [
     CodecSpec("mixed_rgroup_int8", 16, FMT_INT8, FMT_GRP, SC_TOKEN, 127, 0),
 ]}
 GROUP = 64                  # channels per group of FMT_GRP rows
-GROUP_BITS = (2, 4, 8)
+GROUP_BITS = (2, 3, 4, 5, 6, 8)
 
 
 def needs_plan(spec: CodecSpec) -> bool:
@@ -88,7 +88,7 @@ def needs_plan(spec: CodecSpec) -> bool:
 
 
 def with_plan(spec: CodecSpec, plan) -> CodecSpec:
-    """The codec with a group bit plan (one entry per 64-channel group, each 2, 4 or 8)."""
+    """The codec with a group bit plan (one entry per 64-channel group, each in GROUP_BITS)."""
     from dataclasses import replace
     plan = tuple(int(b) for b in plan)
     if any(b not in GROUP_BITS for b in plan):
@@ -100,47 +100,96 @@ def boundary_group_relevance(table, boundary: int, groups: int) -> list:
     """The channel-group relevance of the tensor crossing the boundary after layer ``boundary`` from a
     [layers][groups] table of the relevance ENTERING each layer (``channel_group_relevance.json``): row
     ``boundary + 1``.  After the last layer the tensor is the final norm's input, which the table does not hold;
-    its last row (the stream entering the last layer) stands in.  No table: every group equal."""
+    its last row (the stream entering the last layer) stands in.  No table: every group equal.  A dict table
+    ``{"relevance": ..., "sensitivity": ...}`` (``load_group_tables``) gives its relevance."""
+    if isinstance(table, dict):
+        table = table.get("relevance")
     if table is None:
         return [1.0] * groups
     t = torch.as_tensor(table, dtype=torch.float32)
     return [float(v) for v in t[min(boundary + 1, t.shape[0] - 1)]]
 
 
-def allocate_group_bits(relevance, avg_bits: float = 4.0) -> tuple:
-    """Relevance-driven bit allocation over the 64-channel groups of a boundary.
+def boundary_group_plan(table, boundary: int, groups: int, avg_bits: float = 4.0) -> tuple:
+    """The bit plan of the head-group codec at the boundary after layer ``boundary``.
 
-    First-order (LRP) error model: quantizing group g with a max-abs step amax_g / qmax_b moves the output by
-    about sum_c |dx_c| * step / 2, which scales with the group's relevance R_g = sum |x * dx| (the LRP pass,
-    ``channel_group_relevance.json``) over qmax_b (1 / 7 / 127 for 2 / 4 / 8 bits).  Greedy: start every group at
-    2 bits and spend the budget ``avg_bits * G`` on the upgrade with the largest R_g (1/qmax_b - 1/qmax_b') per
-    bit (2 -> 4 -> 8); equal relevance gives the uniform plan."""
-    w = [max(float(r), 0.0) for r in relevance]
+    ``table`` = ``{"relevance": [layers][G], "sensitivity": [layers][G]}`` (``load_group_tables``): the MSE
+    allocation over the groups' quantization sensitivity when it is there (``allocate_group_bits(model="mse")``),
+    else the first-order allocation over the LRP relevance (``model="linear"``, the round-3 allocator); a plain
+    [layers][G] list is a relevance table; None: the uniform plan."""
+    if isinstance(table, dict) and table.get("sensitivity") is not None:
+        w = boundary_group_relevance({"relevance": table["sensitivity"]}, boundary, groups)
+        return allocate_group_bits(w, avg_bits, model="mse")
+    return allocate_group_bits(boundary_group_relevance(table, boundary, groups), avg_bits, model="linear")
+
+
+def _qmax(bits: int) -> int:
+    return (1 << (bits - 1)) - 1
+
+
+def allocate_group_bits(weights, avg_bits: float = 4.0, model: str = "mse", widths=GROUP_BITS) -> tuple:
+    """Bit allocation over the 64-channel groups of a boundary: every group starts at the narrowest width and the
+    budget ``avg_bits * G`` bits goes, one step up the width ladder at a time, to the step with the largest error
+    reduction per bit.  Error models of a group g quantized at b bits (max-abs scale, step amax / qmax_b):
+
+    * ``"mse"``: the expected squared first-order output change, W_g / (12 qmax_b^2) with W_g the group's
+      quantization sensitivity sum_t max_c |x_tc|^2 sum_c dx_tc^2 (``ops.reference.group_sens``: a rounding error
+      uniform in +-step/2 per channel, independent across channels, propagated through the gradient dx).  The
+      error falls 4-9x per added bit, so a group gets a wider code only where its sensitivity is that much larger
+      than the others' - the outlier-heavy groups;
+    * ``"linear"``: R_g / qmax_b with R_g the LRP relevance sum |x dx| (the round-3 allocator: error ~ sum |dx|
+      step / 2), only on the widths 2 / 4 / 8.
+
+    The error reductions per bit fall along the ladder (convex), so the greedy allocation is optimal for the
+    model.  Equal weights give the uniform plan."""
+    w = [max(float(r), 0.0) for r in weights]
     G = len(w)
     if not any(w):
         w = [1.0] * G
-    d = {2: 1.0, 4: 1.0 / 7.0, 8: 1.0 / 127.0}
-    bits = [2] * G
-    budget = int(round(avg_bits * G)) - 2 * G
+    if model == "linear":
+        ladder = (2, 4, 8)
+        err = {b: 1.0 / _qmax(b) for b in ladder}
+    elif model == "mse":
+        ladder = tuple(sorted(widths))
+        err = {b: 1.0 / _qmax(b) ** 2 for b in ladder}
+    else:
+        raise ValueError(f"unknown allocation model {model!r} (mse | linear)")
+    nxt = {ladder[i]: ladder[i + 1] for i in range(len(ladder) - 1)}
+    bits = [ladder[0]] * G
+    budget = int(round(avg_bits * G)) - ladder[0] * G
     while budget > 0:
         best, best_gain = -1, 0.0
         for g in range(G):
             b = bits[g]
-            if b == 8:
+            if b not in nxt:
                 continue
-            nb = 4 if b == 2 else 8
+            nb = nxt[b]
             cost = nb - b
             if cost > budget:
                 continue
-            gain = w[g] * (d[b] - d[nb]) / cost
+            gain = w[g] * (err[b] - err[nb]) / cost
             if gain > best_gain or (gain == best_gain and best >= 0 and w[g] > w[best]):
                 best, best_gain = g, gain
         if best < 0:
             break
-        nb = 4 if bits[best] == 2 else 8
-        budget -= nb - bits[best]
-        bits[best] = nb
+        budget -= nxt[bits[best]] - bits[best]
+        bits[best] = nxt[bits[best]]
     return tuple(bits)
+
+
+def load_group_tables(relevance_path: str):
+    """``channel_group_relevance.json`` and, when the relevance pass wrote it beside, the sensitivity table
+    ``channel_group_sensitivity.json`` -> {"relevance": tensor, "sensitivity": tensor or None}."""
+    import json
+    import os
+    with open(relevance_path) as f:
+        rel = torch.tensor(json.load(f), dtype=torch.float32)
+    sp = os.path.join(os.path.dirname(os.path.abspath(relevance_path)), "channel_group_sensitivity.json")
+    sens = None
+    if os.path.exists(sp):
+        with open(sp) as f:
+            sens = torch.tensor(json.load(f), dtype=torch.float32)
+    return {"relevance": rel, "sensitivity": sens}
 
 
 def get_codec(name: str) -> CodecSpec:
@@ -418,10 +467,27 @@ def _mx_unpack(b: torch.Tensor, fmt: int, n: int, H: int) -> torch.Tensor:
     return (v.reshape(n, H // 32, 32) * _e8m0(sb)[..., None]).reshape(n, H)
 
 
+def _grp_bits_pack(q: torch.Tensor, bits: int) -> torch.Tensor:
+    """Codes [n, 64] (two's complement, |q| < 2^(bits-1)) -> the group's little-endian bit stream [n, 8 bits] bytes:
+    code c at bits [bits c, bits c + bits); 8 consecutive codes are ``bits`` whole bytes (csrc/codec.hip grp_pack8)."""
+    n = q.shape[0]
+    c = (q.to(torch.int64) & ((1 << bits) - 1)).view(n, 8, 8)
+    w = (c << (bits * torch.arange(8, dtype=torch.int64))).sum(-1)                      # [n, 8] words < 2^(8 bits)
+    return ((w[..., None] >> (8 * torch.arange(bits, dtype=torch.int64))) & 255).to(torch.uint8).reshape(n, 8 * bits)
+
+
+def _grp_bits_unpack(b: torch.Tensor, bits: int) -> torch.Tensor:
+    n = b.shape[0]
+    w = (b.to(torch.int64).view(n, 8, bits) << (8 * torch.arange(bits, dtype=torch.int64))).sum(-1)   # [n, 8]
+    c = (w[..., None] >> (bits * torch.arange(8, dtype=torch.int64))) & ((1 << bits) - 1)
+    c = torch.where(c >= (1 << (bits - 1)), c - (1 << bits), c)
+    return c.reshape(n, 64).float()
+
+
 def _grp_pack(rows: torch.Tensor, plan) -> torch.Tensor:
-    """FMT_GRP rows: per 64-channel group g of b_g bits, s = max|x| / qmax_b (qmax 1 / 7 / 127), codes
-    clamp(round(x * (1 / s)), -qmax, qmax) packed as int2 / int4 / int8 (csrc/codec.hip grp_pack8); then the G
-    fp32 scales."""
+    """FMT_GRP rows: per 64-channel group g of b_g bits, s = max|x| / qmax_b (qmax = 2^(b-1) - 1), codes
+    clamp(round(x * (1 / s)), -qmax, qmax) packed as a b-bit stream (csrc/codec.hip grp_pack8); then the G fp32
+    scales."""
     n, H = rows.shape
     parts, scales = [], []
     for g, b in enumerate(plan):
@@ -431,7 +497,7 @@ def _grp_pack(rows: torch.Tensor, plan) -> torch.Tensor:
         s = am / float(qmax)
         inv = torch.where(am > 0, 1.0 / torch.where(am > 0, s, torch.ones_like(s)), torch.zeros_like(s))
         q = torch.round(blk * inv[:, None]).clamp(-qmax, qmax)
-        parts.append(_pack_rows(q, {2: FMT_INT2, 4: FMT_INT4, 8: FMT_INT8}[b]).reshape(n, -1))
+        parts.append(_grp_bits_pack(q, b))
         scales.append(s)
     sc = torch.stack(scales, 1).contiguous().view(torch.uint8).reshape(n, -1)
     return torch.cat(parts + [sc], 1).reshape(-1)
@@ -444,7 +510,7 @@ def _grp_unpack(b: torch.Tensor, plan, n: int, H: int) -> torch.Tensor:
     out, off = [], 0
     for g, bits in enumerate(plan):
         nb = 8 * bits
-        q = _unpack_rows(r[:, off:off + nb].contiguous(), {2: FMT_INT2, 4: FMT_INT4, 8: FMT_INT8}[bits], n, GROUP)
+        q = _grp_bits_unpack(r[:, off:off + nb].contiguous(), bits)
         out.append(q * sc[:, g:g + 1])
         off += nb
     return torch.cat(out, 1)

@@ -45,10 +45,13 @@ def load_wikitext_tokens(hf_id: str, split: str = "test") -> torch.Tensor | None
     return enc.input_ids.to(torch.int64)
 
 
-def local_text_bytes(split: str = "eval", root: str = "") -> torch.Tensor:
+def local_text_bytes(split: str = "eval", root: str = "", max_bytes: int = 256 << 20) -> torch.Tensor:
     """Byte ids [1, N] of real local text: the Python standard-library sources of this image, sorted by path;
     every 10th file is the held-out ``eval`` split, the rest ``train``.  Used with the byte-level model
-    (``byte-qwen2``) for quality experiments, since no pretrained checkpoint or WikiText copy is reachable."""
+    (``byte-qwen2``) for quality experiments, since no pretrained checkpoint or WikiText copy is reachable.
+    ``train-large``: the ``train`` files plus the Python sources of the installed packages (dist-/site-packages,
+    files under 200 KB, sorted by path, up to ``max_bytes``): ~25x the text, so a few minutes of training never
+    revisit a byte and the model does not overfit the 10 MB stdlib split; returned as uint8 [1, N] (cast per batch)."""
     import glob
     import sys
     root = root or os.path.join(sys.base_prefix, "lib", f"python{sys.version_info.major}.{sys.version_info.minor}")
@@ -57,12 +60,23 @@ def local_text_bytes(split: str = "eval", root: str = "") -> torch.Tensor:
     if not files:
         raise FileNotFoundError(f"no python sources under {root}")
     pick = [f for i, f in enumerate(files) if (i % 10 == 0) == (split == "eval")]
+    if split == "train-large":
+        import site
+        roots = [d for d in {*site.getsitepackages(), os.path.join(root, "site-packages")} if os.path.isdir(d)]
+        extra = sorted({f for d in roots for f in glob.glob(os.path.join(d, "**", "*.py"), recursive=True)})
+        pick += [f for f in extra if os.path.getsize(f) < 200_000]
     buf = bytearray()
     for f in pick:
-        with open(f, "rb") as fh:
-            buf += fh.read()
+        if len(buf) >= max_bytes:
+            break
+        try:
+            with open(f, "rb") as fh:
+                buf += fh.read()
+        except OSError:
+            continue
         buf += b"\n\n"
-    return torch.frombuffer(buf, dtype=torch.uint8).to(torch.int64).view(1, -1)
+    t = torch.frombuffer(buf, dtype=torch.uint8).view(1, -1)
+    return t.clone() if split == "train-large" else t.to(torch.int64)
 
 
 class DatasetUnavailable(FileNotFoundError):

@@ -206,8 +206,7 @@ def _group_relevance(p: Params):
     if p.group_relevance and not os.path.exists(path):
         raise FileNotFoundError(f"group_relevance {path} not found (run Experiments/Relevance/main.py)")
     if path and os.path.exists(path):
-        with open(path) as f:
-            return torch.tensor(json.load(f), dtype=torch.float32)
+        return C.wire.load_group_tables(path)   # + channel_group_sensitivity.json when the pass wrote it
     log("head-group codec without channel_group_relevance.json: every group gets the same width")
     return None
 

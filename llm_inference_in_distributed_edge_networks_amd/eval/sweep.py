@@ -64,7 +64,7 @@ class SweepConfig:
     head_weights: torch.Tensor | None = None
     max_fork_tokens: int = 1 << 17     # cap on tokens per stacked suffix forward
     ratio_scale: float = 1.0           # Pythia 'initial' uses ratio in 0..10 meaning 0.1*ratio
-    group_relevance: object = None     # head-group codecs: [layers][H / 64] channel-group relevance (plan source)
+    group_relevance: object = None     # head-group codecs: channel-group tables (plan source, PipelineConfig)
     group_avg_bits: float = 4.0
 
     def rows(self) -> list:
@@ -75,8 +75,11 @@ class SweepConfig:
 
 
 class SweepEngine:
-    def __init__(self, model: DecoderLM, sc: SweepConfig, use_graphs: bool = True):
+    def __init__(self, model: DecoderLM, sc: SweepConfig, use_graphs: bool = True, keep_windows: bool = False):
+        """``keep_windows``: also keep every window's NLL and loss weight (``window_results``: the input of the
+        bootstrap intervals in ``eval.stats``)."""
         self.m, self.sc = model, sc
+        self._kept = [] if keep_windows else None
         self.spec = C.get_codec(sc.codec)
         self.rows = sc.rows()
         self.methods = [r.name for r in self.rows]
@@ -165,8 +168,8 @@ class SweepEngine:
         if not C.wire.needs_plan(spec):
             return spec
         G = self.m.cfg.hidden_size // C.wire.GROUP
-        rel = C.wire.boundary_group_relevance(self.sc.group_relevance, L, G)
-        return C.wire.with_plan(spec, C.wire.allocate_group_bits(rel, self.sc.group_avg_bits))
+        return C.wire.with_plan(spec, C.wire.boundary_group_plan(self.sc.group_relevance, L, G,
+                                                                 self.sc.group_avg_bits))
 
     def _k(self, ratio, S, spec=None):
         return C.wire.num_lo(spec or self.spec, float(ratio) * self.sc.ratio_scale, S)
@@ -233,6 +236,8 @@ class SweepEngine:
                     for (mi, ri) in variants[key]:
                         out[mi, li, ri] = wn[vi]
         w = batch.weights.to(out.device, non_blocking=True)
+        if self._kept is not None:
+            self._kept.append((out.detach().clone(), w.detach().clone()))
         od = out.double()
         if self._dev is None:          # device-side running sums: no host sync per batch (flushed by _flush)
             self._dev = [torch.zeros_like(self.total_nll, device=out.device) for _ in range(2)]
@@ -244,6 +249,15 @@ class SweepEngine:
         return out
 
     # -------------------------------------------------------------- results
+    def window_results(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """(per-window NLL [N, methods, layers, ratios], loss weights [N]) of every window run since construction
+        (``keep_windows``)."""
+        if not self._kept:
+            raise RuntimeError("no windows kept (SweepEngine(..., keep_windows=True))")
+        nll = torch.cat([o.permute(3, 0, 1, 2).float().cpu() for o, _ in self._kept], 0)
+        w = torch.cat([w.float().cpu() for _, w in self._kept], 0)
+        return nll, w
+
     def _flush(self) -> None:
         """Move the device-side NLL sums into the host accumulators (one sync)."""
         if self._dev is not None:

@@ -766,10 +766,14 @@ def lrp_ln_bwd_f32(dy1, rs, w1, dy2, w2, resid):
     return out
 
 
-def group_absprod(x: torch.Tensor, dx: torch.Tensor, B: int, S: int, out: torch.Tensor | None = None):
-    """[B, H/64] sums of |x dx| per window and 64-channel group (into ``out`` [B, >= H/64] rows if given)."""
+def group_absprod(x: torch.Tensor, dx: torch.Tensor, B: int, S: int, out: torch.Tensor | None = None,
+                  sens_out: torch.Tensor | None = None):
+    """[B, H/64] sums of |x dx| per window and 64-channel group (into ``out`` [B, >= H/64] rows if given).
+    ``sens_out`` (same layout as ``out``): also the groups' quantization sensitivity (``reference.group_sens``)."""
     if not _gpu(x):
         r = ref.group_absprod(x, dx, B, S)
+        if sens_out is not None:
+            sens_out.copy_(ref.group_sens(x, dx, B, S))
         if out is not None:
             out.copy_(r)
             return out
@@ -779,5 +783,7 @@ def group_absprod(x: torch.Tensor, dx: torch.Tensor, B: int, S: int, out: torch.
     if out is None:
         out = torch.empty(B, H // 64, dtype=torch.float32, device=x.device)
     assert out.dtype == torch.float32 and out.stride(1) == 1
-    call("edge_group_absprod", ptr(x), ptr(dx), ptr(out), B, S, H, out.stride(0), stream())
+    if sens_out is not None:
+        assert sens_out.dtype == torch.float32 and sens_out.stride() == out.stride() and sens_out.shape == out.shape
+    call("edge_group_absprod", ptr(x), ptr(dx), ptr(out), ptr(sens_out), B, S, H, out.stride(0), stream())
     return out

@@ -84,7 +84,7 @@ _SIGS = {
     "edge_act_h3": [c_p, c_p, c_ll, c_i, c_i, c_f, c_p],
     "edge_row_rstd_f32": [c_p, c_p, c_i, c_i, c_f, c_i, c_p],
     "edge_lrp_ln_bwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p],
-    "edge_group_absprod": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    "edge_group_absprod": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
 }
 
 

@@ -434,3 +434,12 @@ def group_absprod(x: torch.Tensor, dx: torch.Tensor, B: int, S: int, group: int 
     """[B, H / group]: sum over each window's tokens and the group's channels of |x dx|."""
     H = x.shape[-1]
     return (_f(x) * _f(dx)).abs().view(B, S, H // group, group).sum((1, 3))
+
+
+def group_sens(x: torch.Tensor, dx: torch.Tensor, B: int, S: int, group: int = 64) -> torch.Tensor:
+    """[B, H / group]: the quantization sensitivity of each channel group, sum over the window's tokens t of
+    max_c |x_tc|^2 * sum_c dx_tc^2 (c over the group): a max-abs quantizer of step max_c |x_tc| / qmax moves the
+    first-order output by a zero-mean error of variance step^2 / 12 * sum_c dx_tc^2 (codec.wire.allocate_group_bits)."""
+    H = x.shape[-1]
+    xg, dg = _f(x).view(B, S, H // group, group), _f(dx).view(B, S, H // group, group)
+    return (xg.abs().amax(-1).pow(2) * dg.pow(2).sum(-1)).sum(1)

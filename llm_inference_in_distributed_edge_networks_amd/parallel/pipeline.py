@@ -42,9 +42,9 @@ class BoundaryConfig:
     method: str = "last_row"
     head_weights: torch.Tensor | None = None
     selection: str = "ratio"      # "ratio": int(ratio*S) least important; "top_rho": keep mass 1 - ratio
-    # head-group codecs (rgroup, mixed_rgroup_int8): channel-group relevance [layers][H / 64] of the residual stream
-    # entering each layer (channel_group_relevance.json of the relevance pass) and the average bits per channel;
-    # without a table every group gets the same width
+    # head-group codecs (rgroup, mixed_rgroup_int8): the relevance pass's channel-group tables of the residual stream
+    # entering each layer - {"relevance", "sensitivity"} (codec.wire.load_group_tables) or a plain [layers][H / 64]
+    # relevance list - and the average bits per channel; without a table every group gets the same width
     group_relevance: object = None
     group_avg_bits: float = 4.0
 
@@ -59,8 +59,8 @@ class BoundaryConfig:
         if boundary is None or not C.wire.needs_plan(spec):
             return spec
         G = hidden // C.wire.GROUP
-        rel = C.wire.boundary_group_relevance(self.group_relevance, boundary, G)
-        return C.wire.with_plan(spec, C.wire.allocate_group_bits(rel, self.group_avg_bits))
+        return C.wire.with_plan(spec, C.wire.boundary_group_plan(self.group_relevance, boundary, G,
+                                                                 self.group_avg_bits))
 
     @property
     def kvar(self) -> bool:

@@ -186,13 +186,14 @@ def head_relevance(model, ids: torch.Tensor, dtype=torch.float32, via_probs: boo
     return rel, in_rel, mx.detach()
 
 
-def head_relevance_batched(model, ids: torch.Tensor, dtype=torch.float32, group: int = 64):
+def head_relevance_batched(model, ids: torch.Tensor, dtype=torch.float32, group: int = 64, want_sens: bool = False):
     """``head_relevance`` for B windows at once (windows are independent: each seeds its own max logit), plus the
     relevance of the residual stream entering every layer per ``group``-channel block (head-sized groups):
     chan[b, l, g] = sum over tokens and the group's channels of |x * dx| (LRP Gradient x Input, magnitude: the
     bit-allocation signal of the head-group boundary codec).  Returns (rel [B, layers, heads], in_rel [B],
-    seed logit [B], chan [B, layers, H / group]).  Plain PyTorch ops (autograd, library GEMMs): the reference-
-    precision path of the offline calibration on any device."""
+    seed logit [B], chan [B, layers, H / group][, sens [B, layers, H / group]]: ``want_sens``, the groups'
+    quantization sensitivity, ``ops.reference.group_sens``).  Plain PyTorch ops (autograd, library GEMMs): the
+    reference-precision path of the offline calibration on any device."""
     B, S = ids.shape
     with torch.enable_grad():
         logits, emb, outs, xs = lrp_forward(model, ids, dtype, keep_probs=False, keep_x=True)
@@ -202,7 +203,11 @@ def head_relevance_batched(model, ids: torch.Tensor, dtype=torch.float32, group:
     in_rel = (emb * emb.grad).view(B, S, -1).sum((1, 2)).detach()
     H = emb.shape[-1]
     chan = torch.stack([(x * x.grad).abs().view(B, S, H // group, group).sum((1, 3)) for x in xs], 1).detach()
-    return rel.float(), in_rel.float(), mx.detach().float(), chan.float()
+    out = (rel.float(), in_rel.float(), mx.detach().float(), chan.float())
+    if want_sens:
+        from ..ops import reference as R
+        out += (torch.stack([R.group_sens(x.detach(), x.grad, B, S, group) for x in xs], 1).float(),)
+    return out
 
 
 def normalize_per_layer(rel: torch.Tensor) -> torch.Tensor:
@@ -257,26 +262,33 @@ def relevance_main(p) -> list:
     G = cfg.hidden_size // 64
     acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=device)
     cacc = torch.zeros(cfg.num_layers, G, dtype=torch.float64, device=device)
+    sacc = torch.zeros(cfg.num_layers, G, dtype=torch.float64, device=device)
     pb = progress_bar(len(wins), env.is_main)
     for bi, b in enumerate(batches(ids, wins, max(1, p.window_batch))):
         if bi % env.world_size != env.rank:
             continue
         if eng is not None:
-            rel, _, _, chan = eng.head_relevance(b.ids, want_channels=True)
+            rel, _, _, chan, sens = eng.head_relevance(b.ids, want_channels=True, want_sens=True)
         else:
-            rel, _, _, chan = head_relevance_batched(model, b.ids.to(device), dtype)
+            rel, _, _, chan, sens = head_relevance_batched(model, b.ids.to(device), dtype, want_sens=True)
         acc += rel.double().sum(0)
         cacc += chan.double().sum(0)
+        sacc += sens.double().sum(0)
         pb.update(b.B * env.world_size)
     pb.close()
     all_reduce_sum(acc)
     all_reduce_sum(cacc)
+    all_reduce_sum(sacc)
     weights = normalize_per_layer(acc).float().cpu().tolist()
     chan_w = normalize_per_layer(cacc).float().cpu().tolist()
+    # the groups' quantization sensitivity, per layer relative to its mean (the allocation only compares the groups
+    # of one boundary)
+    sens_w = (sacc / sacc.mean(-1, keepdim=True).clamp_min(1e-300)).float().cpu().tolist()
     if env.is_main:
         out = os.path.join(p.output_dir, "attention_head_weights.json")
         dump_json(weights, out)
         cout = os.path.join(p.output_dir, "channel_group_relevance.json")
         dump_json(chan_w, cout)
+        dump_json(sens_w, os.path.join(p.output_dir, "channel_group_sensitivity.json"))
         log(f"wrote {out} and {cout}")
     return weights

@@ -23,6 +23,7 @@ from __future__ import annotations
 import torch
 
 from .. import ops
+from ..ops import reference as R
 from ..models.model import DecoderLM
 
 
@@ -121,11 +122,13 @@ class RelevanceEngine:
         return g.to(x.dtype).contiguous(), mx
 
     @torch.no_grad()
-    def head_relevance(self, ids: torch.Tensor, want_channels: bool = False, group: int = 64):
+    def head_relevance(self, ids: torch.Tensor, want_channels: bool = False, group: int = 64,
+                       want_sens: bool = False):
         """ids [B, S] (B windows of equal length) -> (rel [B, layers, heads] fp32, input relevance [B],
-        seed logit [B][, chan [B, layers, H / group]]).  rel[b, l, h] = sum_{i,j} A_ij dA_ij of head h, layer l,
-        window b; chan (``want_channels``) = sum over tokens and the group's channels of |x * dx| of the residual
-        stream entering layer l (as ``attnlrp.head_relevance_batched``)."""
+        seed logit [B][, chan [B, layers, H / group]][, sens [B, layers, H / group]]).  rel[b, l, h] = sum_{i,j}
+        A_ij dA_ij of head h, layer l, window b; chan (``want_channels``) = sum over tokens and the group's channels
+        of |x * dx| of the residual stream entering layer l (as ``attnlrp.head_relevance_batched``); sens
+        (``want_sens``) = the groups' quantization sensitivity (``ops.reference.group_sens``)."""
         m, cfg = self.m, self.m.cfg
         ids = ids.to(m.device)
         B, S = ids.shape
@@ -141,6 +144,7 @@ class RelevanceEngine:
         H = cfg.hidden_size
         chan = torch.zeros(B, cfg.num_layers, H // group, dtype=torch.float32, device=m.device) if want_channels \
             else None
+        sens = torch.zeros(B, cfg.num_layers, H // group, dtype=torch.float32, device=m.device) if want_sens else None
         for i in range(cfg.num_layers - 1, -1, -1):
             L, t, sv = m.layers[i], self.T[i], saves[i]
             rows = sv.get("rows")   # last layer: dx is the seeded rows only [B, H]
@@ -167,8 +171,8 @@ class RelevanceEngine:
                 dx = ops.lrp_ln_bwd(dh1, sv["rs1"], L["ln1_w"], dh2, sv["rs1"], L["ln2_w"], dy)
             if want_channels:
                 chan[:, i] = (sv["x"].float() * dx.float()).abs().view(B, S, H // group, group).sum((1, 3))
+            if want_sens:
+                sens[:, i] = R.group_sens(sv["x"], dx, B, S, group)
             saves[i] = None
         in_rel = (emb.float() * dx.float()).view(B, S, -1).sum((1, 2))
-        if want_channels:
-            return rel, in_rel, mx, chan
-        return rel, in_rel, mx
+        return (rel, in_rel, mx) + ((chan,) if want_channels else ()) + ((sens,) if want_sens else ())

@@ -140,9 +140,10 @@ class RelevanceEngineH3:
         return g.contiguous(), mx
 
     @torch.no_grad()
-    def head_relevance(self, ids: torch.Tensor, want_channels: bool = False, group: int = 64):
-        """ids [B, S] -> (rel [B, layers, heads], input relevance [B], seed logit [B][, chan [B, layers, H/64]]),
-        all fp32; the same quantities as ``attnlrp.head_relevance_batched``."""
+    def head_relevance(self, ids: torch.Tensor, want_channels: bool = False, group: int = 64,
+                       want_sens: bool = False):
+        """ids [B, S] -> (rel [B, layers, heads], input relevance [B], seed logit [B][, chan [B, layers, H/64]]
+        [, sens [B, layers, H/64]]), all fp32; the same quantities as ``attnlrp.head_relevance_batched``."""
         if group != 64:
             raise ValueError("channel groups are 64 channels (one head) wide")
         m, cfg = self.m, self.m.cfg
@@ -157,8 +158,9 @@ class RelevanceEngineH3:
         else:
             dx, mx = self._seed(x, B, S)
         rel = torch.zeros(B, cfg.num_layers, Hq, dtype=torch.float32, device=m.device)
-        chan = torch.zeros(B, cfg.num_layers, H // group, dtype=torch.float32, device=m.device) if want_channels \
-            else None
+        chan = torch.zeros(B, cfg.num_layers, H // group, dtype=torch.float32, device=m.device) \
+            if (want_channels or want_sens) else None
+        sens = torch.zeros(B, cfg.num_layers, H // group, dtype=torch.float32, device=m.device) if want_sens else None
         for i in range(cfg.num_layers - 1, -1, -1):
             L, t, sv = m.layers[i], self.T[i], saves[i]
             rows = sv.get("rows")   # last layer: dx is the seeded rows only [B, H]
@@ -190,10 +192,8 @@ class RelevanceEngineH3:
             else:
                 dh1 = ops.linear_h3(dqkv3, t["wqkvT3"], t["a_qkvT"], rscale=rinv_q)
                 dx = ops.lrp_ln_bwd_f32(dh1, sv["rs1"], L["ln1_w"], dh2, L["ln2_w"], dy)
-            if want_channels:
-                ops.group_absprod(sv["x"], dx, B, S, out=chan[:, i])
+            if want_channels or want_sens:
+                ops.group_absprod(sv["x"], dx, B, S, out=chan[:, i], sens_out=None if sens is None else sens[:, i])
             saves[i] = None
         in_rel = (emb * dx).view(B, -1).sum(1)
-        if want_channels:
-            return rel, in_rel, mx, chan
-        return rel, in_rel, mx
+        return (rel, in_rel, mx) + ((chan,) if want_channels else ()) + ((sens,) if want_sens else ())

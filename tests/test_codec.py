@@ -214,17 +214,53 @@ def test_mx_codecs_error_and_bytes(codec):
         assert err < ((yt - x) ** 2).mean() / (x ** 2).mean()
 
 
-def test_group_bits_allocation():
-    from llm_inference_in_distributed_edge_networks_amd.codec.wire import allocate_group_bits
+@pytest.mark.parametrize("model", ["linear", "mse"])
+def test_group_bits_allocation(model):
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import GROUP_BITS, allocate_group_bits
     rel = [0.30, 0.01, 0.20, 0.02, 0.25, 0.01, 0.10, 0.11]
-    bits = allocate_group_bits(rel, 4.0)
-    assert sum(bits) == 4 * len(rel) and set(bits) <= {2, 4, 8}
+    bits = allocate_group_bits(rel, 4.0, model=model)
+    assert sum(bits) == 4 * len(rel) and set(bits) <= ({2, 4, 8} if model == "linear" else set(GROUP_BITS))
     order = sorted(range(len(rel)), key=lambda g: -rel[g])
     # more relevant groups never get fewer bits than less relevant ones
     assert all(bits[order[i]] >= bits[order[i + 1]] for i in range(len(rel) - 1)), bits
-    assert allocate_group_bits([1.0] * 14, 4.0) == (4,) * 14
-    assert allocate_group_bits([0.0] * 6, 2.0) == (2,) * 6
-    assert sum(allocate_group_bits(rel, 3.0)) <= 3 * len(rel)
+    assert allocate_group_bits([1.0] * 14, 4.0, model=model) == (4,) * 14
+    assert allocate_group_bits([0.0] * 6, 2.0, model=model) == (2,) * 6
+    assert sum(allocate_group_bits(rel, 3.0, model=model)) <= 3 * len(rel)
+
+
+def test_group_bits_mse_model():
+    """The MSE allocation: the error of b bits is W / qmax_b^2 (qmax 1, 3, 7, 15, 31, 127), so a step pays where the
+    sensitivity ratio beats the ~5x error drop of the next bit; the plan minimises sum_g W_g / qmax^2 at the budget
+    (checked against every plan of two groups), and a 1.2x spread - the surrogate model's relevance spread - stays
+    uniform at 4 bits while an outlier-sized (100x) group takes bits from the others."""
+    import itertools
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import GROUP_BITS, allocate_group_bits
+    q = {b: (1 << (b - 1)) - 1 for b in GROUP_BITS}
+    assert allocate_group_bits([1.0, 1.2, 1.1, 1.0], 4.0) == (4, 4, 4, 4)
+    hot = allocate_group_bits([100.0, 1.0, 1.0, 1.0], 4.0)
+    assert hot[0] > 4 and min(hot[1:]) < 4 and sum(hot) == 16
+    for w in ([50.0, 1.0], [1.0, 7.0], [3.0, 3.0], [400.0, 0.5]):
+        for avg in (3.0, 4.0, 5.0):
+            got = allocate_group_bits(w, avg)
+            err = lambda p: sum(wi / q[b] ** 2 for wi, b in zip(w, p))   # noqa: E731
+            best = min((p for p in itertools.product(GROUP_BITS, repeat=2) if sum(p) <= avg * 2), key=err)
+            assert err(got) <= err(best) * (1 + 1e-12), (w, avg, got, best)
+
+
+def test_boundary_group_plan_tables(tmp_path):
+    """A sensitivity table beside the relevance table switches the plan to the MSE allocation over it."""
+    import json
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import (allocate_group_bits, boundary_group_plan,
+                                                                            load_group_tables)
+    rel = [[1.0, 1.1, 0.9, 1.0]] * 3
+    sens = [[1.0, 1.0, 1.0, 1.0], [80.0, 1.0, 1.0, 1.0], [1.0, 1.0, 1.0, 90.0]]
+    (tmp_path / "channel_group_relevance.json").write_text(json.dumps(rel))
+    assert load_group_tables(str(tmp_path / "channel_group_relevance.json"))["sensitivity"] is None
+    assert boundary_group_plan(rel, 0, 4) == allocate_group_bits(rel[1], 4.0, model="linear")
+    (tmp_path / "channel_group_sensitivity.json").write_text(json.dumps(sens))
+    t = load_group_tables(str(tmp_path / "channel_group_relevance.json"))
+    assert boundary_group_plan(t, 0, 4) == allocate_group_bits(sens[1], 4.0) and boundary_group_plan(t, 0, 4)[0] > 4
+    assert boundary_group_plan(t, 1, 4)[3] > 4 and boundary_group_plan(None, 1, 4) == (4, 4, 4, 4)
 
 
 def test_boundary_group_relevance_rows():
@@ -240,14 +276,14 @@ def test_boundary_group_relevance_rows():
 
 @pytest.mark.parametrize("name", ["rgroup", "mixed_rgroup_int8"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_group_codec_roundtrip(name, dtype):
+@pytest.mark.parametrize("plan", [(8, 2, 4, 4), (3, 5, 6, 2), (6, 3, 8, 5)])
+def test_group_codec_roundtrip(name, dtype, plan):
     from llm_inference_in_distributed_edge_networks_amd.codec.wire import with_plan
     B, S, H = 2, 48, 256
     g = torch.Generator().manual_seed(5)
     x = (torch.randn(B * S, H, generator=g) * 2).to(dtype)
     x[:, 64:128] *= 10          # a loud group
     imp = torch.rand(B, S, generator=g)
-    plan = (8, 2, 4, 4)
     spec = with_plan(C.get_codec(name), plan)
     msg, L = C.encode(x, spec, B, S, 0.5, imp)
     assert L.plan == plan and L.total == msg.numel()

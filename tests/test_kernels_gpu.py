@@ -423,16 +423,22 @@ def test_gemm_four_wave_multi_tile(M, N, K, epi):
 
 @pytest.mark.parametrize("name", ["rgroup", "mixed_rgroup_int8"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_group_codec_gpu_equals_cpu(name, dtype):
-    """Head-group rows with a non-uniform relevance plan: GPU message bytes == CPU oracle bytes (fp32
-    activations; bf16 activations: same bytes from the bf16-rounded input), decode equal."""
-    from llm_inference_in_distributed_edge_networks_amd.codec.wire import allocate_group_bits, with_plan
+@pytest.mark.parametrize("plan", ["linear", "mse", "all_widths"])
+def test_group_codec_gpu_equals_cpu(name, dtype, plan):
+    """Head-group rows with a non-uniform plan (the round-3 linear allocation on 2 / 4 / 8 bits, the MSE allocation,
+    and every width 2 / 3 / 4 / 5 / 6 / 8 in one row): GPU message bytes == CPU oracle bytes (fp32 activations; bf16
+    activations: same bytes from the bf16-rounded input), decode equal."""
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import GROUP_BITS, allocate_group_bits, with_plan
     B, S, H = 3, 200, 896
     x = (rnd(B * S, H, seed=60) * 2).to(dtype)
     x[:, 128:192] *= 30
     imp = torch.rand(B, S, generator=torch.Generator().manual_seed(61))
-    rel = [1.0 if g % 5 == 0 else 0.01 for g in range(H // 64)]     # a few dominant groups: 8 / 4 / 2 bits
-    spec = with_plan(C.get_codec(name), allocate_group_bits(rel, 4.0))
+    if plan == "all_widths":
+        bits = tuple(GROUP_BITS[g % len(GROUP_BITS)] for g in range(H // 64))
+    else:
+        w = [1.0 if g % 5 == 0 else 0.01 for g in range(H // 64)]     # a few dominant groups
+        bits = allocate_group_bits(w if plan == "linear" else [100 * v for v in w], 4.0, model=plan)
+    spec = with_plan(C.get_codec(name), bits)
     assert len(set(spec.plan)) > 1
     m_cpu, L = C.encode(x.float(), spec, B, S, 0.4, imp)
     m_gpu, L2 = C.encode(x.to(DEV), spec, B, S, 0.4, imp.to(DEV))

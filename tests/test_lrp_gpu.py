@@ -214,6 +214,9 @@ def test_fp32_lrp_rule_kernels():
     xx, dd = rnd(3 * 50, 256, seed=30, dtype=f), rnd(3 * 50, 256, seed=31, dtype=f)
     assert rel_err(ops.group_absprod(xx.to(DEV), dd.to(DEV), 3, 50), R.group_absprod(xx.double(), dd.double(), 3,
                                                                                     50)) < 1e-6
+    sens = torch.empty(3, 4, device=DEV)
+    ops.group_absprod(xx.to(DEV), dd.to(DEV), 3, 50, sens_out=sens)
+    assert rel_err(sens, R.group_sens(xx.double(), dd.double(), 3, 50)) < 1e-6
 
 
 @pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX], ids=lambda c: c.name)
@@ -224,9 +227,9 @@ def test_relevance_engine_h3_tiny_vs_autograd(cfg):
     mg = DecoderLM.random_init(cfg, 3, device=DEV, std=0.05)
     mc = DecoderLM.random_init(cfg, 3, std=0.05)
     ids = torch.randint(0, cfg.vocab_size, (4, 128), generator=torch.Generator().manual_seed(2))
-    rg, ing, mxg, cg = RelevanceEngineH3(mg).head_relevance(ids.to(DEV), want_channels=True)
-    rc, inc, mxc, cc = head_relevance_batched(mc, ids, dtype=torch.float64)
-    for n, a, b in (("rel", rg, rc), ("in_rel", ing, inc), ("seed", mxg, mxc), ("chan", cg, cc)):
+    rg, ing, mxg, cg, sg = RelevanceEngineH3(mg).head_relevance(ids.to(DEV), want_channels=True, want_sens=True)
+    rc, inc, mxc, cc, sc = head_relevance_batched(mc, ids, dtype=torch.float64, want_sens=True)
+    for n, a, b in (("rel", rg, rc), ("in_rel", ing, inc), ("seed", mxg, mxc), ("chan", cg, cc), ("sens", sg, sc)):
         e = rel_err(a, b)
         assert e < 1e-5, f"{n}: {e:.3g}"
 

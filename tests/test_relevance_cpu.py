@@ -107,9 +107,13 @@ def test_batched_autograd_and_channel_relevance():
             assert torch.allclose(rel[b], r0, rtol=1e-4, atol=1e-5)
             assert abs(float(in_rel[b]) - float(in0)) < 1e-3 * max(1.0, abs(float(in0)))
             assert abs(float(mx[b]) - float(mx0)) < 1e-4
-        rel_e, _, _, chan_e = RelevanceEngine(m).head_relevance(ids, want_channels=True)
+        rel_e, _, _, chan_e, sens_e = RelevanceEngine(m).head_relevance(ids, want_channels=True, want_sens=True)
         assert torch.allclose(rel_e, rel, rtol=1e-4, atol=1e-5)
         assert torch.allclose(chan_e, chan, rtol=1e-4, atol=1e-6)
+        # the groups' quantization sensitivity: the explicit engine == autograd, and == its definition
+        *_, sens = head_relevance_batched(m, ids, want_sens=True)
+        assert sens.shape == chan.shape and (sens > 0).all()
+        assert torch.allclose(sens_e, sens, rtol=1e-3, atol=1e-12)
 
 
 @pytest.mark.parametrize("arch", ["qwen2", "neox"])

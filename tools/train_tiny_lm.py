@@ -2,9 +2,15 @@
 
 No pretrained checkpoint or WikiText copy is reachable from this machine, so PPL-vs-compression curves on
 random weights would be meaningless.  This trains a small model of the same architecture family as
-Qwen2-0.5B (GQA, RoPE, RMSNorm, SwiGLU, tied head) on the Python standard-library sources (byte tokens,
-``eval.data.local_text_bytes('train')``), then saves it with ``DecoderLM.save_native``; the experiment
-drivers load it with ``weights=<file>.safetensors``.
+Qwen2-0.5B (GQA, RoPE, RMSNorm, SwiGLU, tied head) on local Python sources (byte tokens: by default
+``eval.data.local_text_bytes('train-large')``, the stdlib's training split plus the installed packages' sources,
+~270 MB, so a few minutes of training never revisit a byte), then saves it with ``DecoderLM.save_native``; the
+experiment drivers load it with ``weights=<file>.safetensors``.
+
+Held-out-driven stop: every ``--eval-every`` seconds the loss on the held-out stdlib split AND on a fixed sample of
+the training stream is measured; the best held-out checkpoint is kept, and training stops once the held-out loss has
+not improved for ``--patience`` evaluations (or the time budget ends).  The last line is a JSON summary with the
+train / held-out gap of the kept checkpoint.
 
 The training forward is plain PyTorch autograd (bf16 autocast, SDPA) over the framework's own weight
 layout (fused qkv, interleaved gate|up), so the checkpoint is exactly what the HIP inference path runs.
@@ -55,6 +61,10 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--warmup", type=int, default=200, help="linear learning-rate warmup steps")
     ap.add_argument("--eval-every", type=float, default=15.0, help="seconds between held-out evaluations")
+    ap.add_argument("--corpus", default="large", choices=["large", "stdlib"],
+                    help="large: stdlib train split + installed packages' sources; stdlib: the 10 MB split alone")
+    ap.add_argument("--patience", type=int, default=4, help="evaluations without a held-out improvement to stop")
+    ap.add_argument("--weight-decay", type=float, default=0.1)
     a = ap.parse_args()
     torch.manual_seed(a.seed)
     dev = "cuda"
@@ -64,16 +74,21 @@ def main():
     for p in params:
         p.requires_grad_(True)
     w = {"embed": m.w["embed"], "norm_w": m.w["norm_w"], "layers": m.layers}
-    data = local_text_bytes("train").view(-1).to(dev)
+    data = local_text_bytes("train-large" if a.corpus == "large" else "train").view(-1).to(dev)
     held = local_text_bytes("eval").view(-1)[: 64 * (a.seq + 1)].view(64, a.seq + 1).to(dev)
-    opt = torch.optim.AdamW(params, lr=a.lr, betas=(0.9, 0.95), weight_decay=0.1)
+    # a fixed sample of the training stream, measured beside the held-out text (the train / held-out gap)
+    gs = torch.Generator().manual_seed(1234)
+    tidx = torch.randint(0, data.numel() - a.seq - 1, (64,), generator=gs).tolist()
+    trs = torch.stack([data[i:i + a.seq + 1] for i in tidx]).long()
+    opt = torch.optim.AdamW(params, lr=a.lr, betas=(0.9, 0.95), weight_decay=a.weight_decay)
     cos, sin = m.cos, m.sin
     print(f"training {cfg.name}: {sum(p.numel() for p in params) / 1e6:.1f}M params, {data.numel() / 1e6:.1f}M train "
           f"bytes, batch {a.batch}x{a.seq}, {a.minutes} min", flush=True)
     t0, step, budget = time.time(), 0, a.minutes * 60
     g = torch.Generator(device=dev).manual_seed(a.seed)
     last_print = 0.0
-    best = (float("inf"), 0, None)  # held-out loss, step, CPU snapshot (early stopping: the corpus is small)
+    best = (float("inf"), 0, None, 0.0)  # held-out loss, step, CPU snapshot, train-sample loss
+    stale = 0
     while True:
         el = time.time() - t0
         if el > budget:
@@ -83,7 +98,7 @@ def main():
         for grp in opt.param_groups:
             grp["lr"] = lr
         idx = torch.randint(0, data.numel() - a.seq - 1, (a.batch,), device=dev, generator=g)
-        chunk = torch.stack([data[i:i + a.seq + 1] for i in idx.tolist()])
+        chunk = torch.stack([data[i:i + a.seq + 1] for i in idx.tolist()]).long()
         with torch.autocast("cuda", dtype=torch.bfloat16):
             logits = forward(w, cfg, chunk[:, :-1], cos, sin)
         loss = F.cross_entropy(logits.float().view(-1, cfg.vocab_size), chunk[:, 1:].reshape(-1))
@@ -97,16 +112,29 @@ def main():
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
                 hl = F.cross_entropy(forward(w, cfg, held[:, :-1], cos, sin).float().view(-1, cfg.vocab_size),
                                      held[:, 1:].reshape(-1))
+                tl = F.cross_entropy(forward(w, cfg, trs[:, :-1], cos, sin).float().view(-1, cfg.vocab_size),
+                                     trs[:, 1:].reshape(-1))
             if hl.item() < best[0]:
-                best = (hl.item(), step, [p.detach().to("cpu", copy=True) for p in params])
-            print(f"step {step} t={el:.0f}s lr={lr:.2e} train {loss.item():.3f} held-out {hl.item():.3f} nats/byte "
-                  f"({hl.item() / math.log(2):.3f} bits/byte)", flush=True)
+                best = (hl.item(), step, [p.detach().to("cpu", copy=True) for p in params], tl.item())
+                stale = 0
+            else:
+                stale += 1
+            print(f"step {step} t={el:.0f}s lr={lr:.2e} batch {loss.item():.3f} train-sample {tl.item():.3f} "
+                  f"held-out {hl.item():.3f} nats/byte ({hl.item() / math.log(2):.3f} bits/byte)", flush=True)
+            if stale >= a.patience:
+                print(f"held-out loss has not improved for {stale} evaluations: stopping", flush=True)
+                break
     for p in params:
         p.requires_grad_(False)
     if best[2] is not None:
         for p, b in zip(params, best[2]):
             p.copy_(b.to(p.device))
         print(f"keeping the best held-out checkpoint: step {best[1]}, {best[0]:.3f} nats/byte", flush=True)
+    import json
+    print(json.dumps({"best_step": best[1], "steps": step, "held_out_nats_per_byte": round(best[0], 4),
+                      "train_sample_nats_per_byte": round(best[3], 4),
+                      "gap": round((best[0] - best[3]) / best[0], 4) if best[0] < float("inf") else None,
+                      "corpus": a.corpus, "train_bytes": int(data.numel()), "seed": a.seed}), flush=True)
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     DecoderLM(cfg, {"embed": m.w["embed"], "norm_w": m.w["norm_w"], "head": m.w["embed"], "layers": m.layers},
               "cpu", torch.float32).save_native(a.out)
