@@ -315,6 +315,11 @@ def pipeline_experiment(p: Params, default_model: str) -> dict:
             else:
                 runner.set_boundary(bcfg)
             part = saved.get("partial") if saved.get("partial", {}).get("key") == [m, str(r)] else None
+            if part is not None and not {"total_nll", "n_tokens", "seconds", "wire_bytes", "wire_tokens",
+                                         "next_batch"} <= set(part):
+                # a checkpoint of an older format (e.g. round 3's wire_sum / wire_n): redo this (method, ratio)
+                log(f"{m} ratio={r}: partial checkpoint of an older format, restarting it from batch 0")
+                part = None
             tot, ntok, sec = (part["total_nll"], part["n_tokens"], part["seconds"]) if part else (0.0, 0.0, 0.0)
             # wire bytes and the tokens they carried, summed over the boundaries (and replicas) and over the chunks,
             # so a resumed run reports the uninterrupted run's bytes per token (variable-k codecs included)

@@ -249,7 +249,11 @@ class LocalPipeline:
 
 
 class DistributedPipeline:
-    """One pipeline stage per rank; ``grid.dp`` replicas share the window batches round-robin."""
+    """One pipeline stage per rank; ``grid.dp`` replicas share the window batches round-robin.
+
+    Construction is COLLECTIVE over the default process group when ``transport`` is ``"rccl"`` (``RcclComm`` draws
+    its store namespace with a broadcast from rank 0) or ``"ipc"`` (the slot rings are exchanged): every rank must
+    build its pipeline at the same point of the program, as ``bench.py`` and the pipeline driver do."""
 
     def __init__(self, model: DecoderLM, plan: PipelinePlan, bcfg: BoundaryConfig, grid: Grid, rank: int,
                  use_graphs: bool = True, transport="torch", check: bool | None = None):

@@ -105,9 +105,11 @@ class RcclComm:
     ``ncclCommInitRank`` calls of a chain of stages cannot wait on each other in a cycle.  ``peers=None`` with
     ``world == 1`` is the single-GPU loopback (``sendrecv`` to itself, ``all_reduce_sum_f64``).
 
-    The store keys of one construction live under a namespace rank 0 draws and broadcasts (construction is
-    collective over the default group, as every rank builds its pipeline), so keys never depend on how many
-    communicators each rank built before; the reader deletes a key once it has the id."""
+    The store keys of one construction live under a namespace rank 0 draws and broadcasts, so keys never depend on
+    how many communicators each rank built before; the reader deletes a key once it has the id.  That broadcast
+    makes construction with ``world > 1`` a COLLECTIVE over the default process group: every rank must construct its
+    ``RcclComm`` at the same point of the program (``DistributedPipeline`` does, at its construction), or the ranks
+    hang in the broadcast."""
 
     def __init__(self, rank: int, world: int, device: int, unique_id: bytes | None = None, peers=None):
         self.rank, self.world, self.device = rank, world, device

@@ -162,3 +162,13 @@ def test_pipeline_driver_resumes_mid_run(tmp_path, monkeypatch):
         assert res["last_row"][r]["n_tokens"] == full["last_row"][r]["n_tokens"]
         assert res["last_row"][r]["wire_bytes_per_token"] == pytest.approx(
             full["last_row"][r]["wire_bytes_per_token"], rel=1e-12)
+    # a partial entry in round 3's format (wire_sum / wire_n instead of wire_bytes / wire_tokens) is not resumed
+    # from: that (method, ratio) restarts from batch 0 and still ends at the uninterrupted result
+    ck = tmp_path / "crash" / "pipeline_results.rank0.ckpt.json"
+    state = json.loads(ck.read_text())
+    state["results"]["last_row"].pop("0.75")
+    state["partial"] = {"key": ["last_row", "0.75"], "total_nll": 123.0, "n_tokens": 7.0, "seconds": 0.1,
+                        "wire_sum": 1.0, "wire_n": 1.0, "next_batch": 4}
+    ck.write_text(json.dumps(state))
+    res = E.pipeline_experiment(p, "qwen2-0.5b")["results"]
+    assert res["last_row"]["0.75"]["ppl"] == pytest.approx(full["last_row"]["0.75"]["ppl"], rel=1e-9)
