@@ -116,7 +116,10 @@ def boundary_group_plan(table, boundary: int, groups: int, avg_bits: float = 4.0
     ``table`` = ``{"relevance": [layers][G], "sensitivity": [layers][G]}`` (``load_group_tables``): the MSE
     allocation over the groups' quantization sensitivity when it is there (``allocate_group_bits(model="mse")``),
     else the first-order allocation over the LRP relevance (``model="linear"``, the round-3 allocator); a plain
-    [layers][G] list is a relevance table; None: the uniform plan."""
+    [layers][G] list is a relevance table; None: the uniform plan (every group at ``avg_bits`` when that is a
+    width, else the MSE allocation of equal weights: the nearest widths, as evenly as the budget allows)."""
+    if table is None:
+        return allocate_group_bits([1.0] * groups, avg_bits, model="mse")
     if isinstance(table, dict) and table.get("sensitivity") is not None:
         w = boundary_group_relevance({"relevance": table["sensitivity"]}, boundary, groups)
         return allocate_group_bits(w, avg_bits, model="mse")

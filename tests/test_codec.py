@@ -261,6 +261,8 @@ def test_boundary_group_plan_tables(tmp_path):
     t = load_group_tables(str(tmp_path / "channel_group_relevance.json"))
     assert boundary_group_plan(t, 0, 4) == allocate_group_bits(sens[1], 4.0) and boundary_group_plan(t, 0, 4)[0] > 4
     assert boundary_group_plan(t, 1, 4)[3] > 4 and boundary_group_plan(None, 1, 4) == (4, 4, 4, 4)
+    # no table: the uniform plan at any width of the ladder (3 bits included, not a 4 / 2 split)
+    assert boundary_group_plan(None, 1, 4, 3.0) == (3, 3, 3, 3)
 
 
 def test_boundary_group_relevance_rows():

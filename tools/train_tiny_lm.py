@@ -76,10 +76,12 @@ def main():
     w = {"embed": m.w["embed"], "norm_w": m.w["norm_w"], "layers": m.layers}
     data = local_text_bytes("train-large" if a.corpus == "large" else "train").view(-1).to(dev)
     held = local_text_bytes("eval").view(-1)[: 64 * (a.seq + 1)].view(64, a.seq + 1).to(dev)
-    # a fixed sample of the training stream, measured beside the held-out text (the train / held-out gap)
+    # a fixed sample of the stdlib TRAINING split (in the training data, and the held-out split's own distribution:
+    # the train / held-out gap measures memorisation, not the packages' sources being easier text)
     gs = torch.Generator().manual_seed(1234)
-    tidx = torch.randint(0, data.numel() - a.seq - 1, (64,), generator=gs).tolist()
-    trs = torch.stack([data[i:i + a.seq + 1] for i in tidx]).long()
+    std = local_text_bytes("train").view(-1)
+    tidx = torch.randint(0, std.numel() - a.seq - 1, (64,), generator=gs).tolist()
+    trs = torch.stack([std[i:i + a.seq + 1] for i in tidx]).long().to(dev)
     opt = torch.optim.AdamW(params, lr=a.lr, betas=(0.9, 0.95), weight_decay=a.weight_decay)
     cos, sin = m.cos, m.sin
     print(f"training {cfg.name}: {sum(p.numel() for p in params) / 1e6:.1f}M params, {data.numel() / 1e6:.1f}M train "
