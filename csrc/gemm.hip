@@ -26,7 +26,12 @@ enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_G
        // fp32 output = colscale[n] * product + fp32 residual: the relevance engine's input gradients through a
        // projection whose RMSNorm weight is applied on the output columns (the transposed weight then stays exact in
        // fp16: two products instead of three)
-       EPI_F32_RESID_CS = 16 };
+       EPI_F32_RESID_CS = 16,
+       // the AttnLRP SwiGLU rule on the product (the MLP backward's dm GEMM): d = alpha (A . B^T) [M, N] with the saved
+       // interleaved pre-activations gu [M, 2N] (residf / ldr) -> h3 planes [M, 2 (2N)] of the interleaved
+       // (0.5 d u sig(g), 0.5 d g sig(g)) at unit scale (alpha carries the caller's bound-derived scale: no row max,
+       // so no separate rule pass over an fp32 dm)
+       EPI_H3_LRP_SWIGLU = 17 };
 constexpr bool epi_f32(int e) { return e >= EPI_F32; }
 constexpr bool epi_plain(int e) {  // none / bias / residual epilogues (the 256x224 kernel's set)
   return e == EPI_NONE || e == EPI_BIAS || e == EPI_RESID || e == EPI_BIAS_RESID || e == EPI_F32 ||
@@ -385,6 +390,28 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
           *(u32x4_t*)dst = H;
           *(u32x4_t*)(dst + a.N) = Lw;
         }
+      }
+      continue;
+    }
+    if constexpr (EPI == EPI_H3_LRP_SWIGLU) {   // a 16-column j group is one interleave block: gate|up = 128 B of gu
+      if (m >= a.M) continue;
+      const float* gr = a.residf + (size_t)m * a.ldr;
+      f16_t* dst = a.C + (size_t)m * a.ldc;
+      const int W = 2 * a.N;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nw + j * 16 + g * 4;
+        const int col = (n >> 4) * 32 + (n & 15);
+        const f32x4_t gv = *(const f32x4_t*)(gr + col), uv = *(const f32x4_t*)(gr + col + 16);
+        float dg[4], du[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sg = fast_sigmoid(gv[r]), h = 0.5f * acc[i][j][r] * sg;
+          dg[r] = h * uv[r];
+          du[r] = h * gv[r];
+        }
+        store_h3_4(dst, W, col, dg, 1.f);
+        store_h3_4(dst, W, col + 16, du, 1.f);
       }
       continue;
     }
@@ -1788,6 +1815,25 @@ EDGE_API int edge_gemm_f32_cs(const void* A, const void* B, float* C, int M, int
   if (((uintptr_t)C & 15) || ldc % 4 || ldr % 4 || ((uintptr_t)resid & 15) || ((uintptr_t)colscale & 15))
     return (int)hipErrorInvalidValue;
   return launch<EPI_F32_RESID_CS>(a, st);
+}
+
+// EPI_H3_LRP_SWIGLU: C = h3 planes [M, 4N] (fp16, row stride 4N) of the SwiGLU LRP rule on d = alpha (A . B^T)
+// [M, N] and the interleaved pre-activations gu [M, 2N] (row stride ldr); A / B as edge_gemm_f32.
+EDGE_API int edge_gemm_f32_lrp_swiglu(const void* A, const void* B, void* C, const float* gu, int M, int N, int Kx,
+                                      int kplane, int lda, int ldb, int ldr, float alpha, hipStream_t st) {
+  GemmArgs a{};
+  a.alpha = alpha;
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = (bf16_t*)C;
+  a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = 4 * N;
+  a.residf = gu; a.ldr = ldr;
+  a.h3k = kplane;
+  a.pairb = Kx == 2 * kplane;
+  if (!gu || !h3_geometry_ok(Kx, kplane) || lda < 2 * kplane || ldb < (a.pairb ? kplane : Kx) || !(alpha > 0.f) ||
+      ldr < 2 * N || ldr % 4 || ((uintptr_t)gu & 15) || ((uintptr_t)C & 7))
+    return (int)hipErrorInvalidValue;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  return launch<EPI_H3_LRP_SWIGLU>(a, st);
 }
 
 // fp32 QKV projection + bias + RoPE + head-major scatter: X [M, 2K] (h3 activation), W [(Hq+2Hkv)*64, 3K] (h3

@@ -14,6 +14,8 @@ Every op has exactly two implementations with identical layouts and semantics:
 from __future__ import annotations
 
 
+import math
+
 import torch
 
 from . import reference as ref
@@ -704,6 +706,42 @@ def lrp_swiglu_bwd_h3(dm: torch.Tensor, gu: torch.Tensor, post: torch.Tensor | N
     out, rinv = _rows_out(T, N2, gu.device)
     call("edge_lrp_swiglu_bwd_h3", ptr(dm), ptr(gu), ptr(out), ptr(rinv), ptr(_post(post, T)), T, N2 // 2, stream())
     return out, rinv
+
+
+def linear_h3_lrp_swiglu(a3: torch.Tensor, w3: torch.Tensor, alpha: float, gu: torch.Tensor, c0: float,
+                         rinv: torch.Tensor, post: torch.Tensor | None = None):
+    """The MLP backward's dm GEMM with the SwiGLU LRP rule in its epilogue: a3 the per-row-scaled h3 gradient
+    (``split_h3_dyn`` -> rinv), w3 the transposed down-projection weight, gu the saved interleaved pre-activations
+    [T, 2I] -> (h3 d[gate|up] [T, 4I], its row scale [T]) - what ``lrp_swiglu_bwd_h3(linear_h3(a3, w3, alpha,
+    rscale=rinv), gu, post)`` returns, without the fp32 dm round trip or the rule's row-max pass.
+
+    The planes are at a fixed scale: the rule runs on c0 x (the product still at a3's row scale, max |row| < 2^15);
+    c0 (a power of two) must keep 2^15 x 0.5 max|dm / dx| x max|gu| under 2^15 (``lrp_swiglu_scale``) - an a-priori
+    bound from the weights replaces the row max that needs every column tile.  The row scale rinv post / c0 is exact
+    (powers of two times the detached norm's rstd)."""
+    rs = rinv / c0 if post is None else rinv * _post(post, rinv.numel()) / c0
+    if not _gpu(a3):
+        return ref.linear_h3_lrp_swiglu(a3, w3, alpha, gu, c0, rinv, post)
+    kp, Kx = _check_h3(a3, w3, alpha)
+    _check_f32(gu)
+    M, N = a3.shape[0], w3.shape[0]
+    assert gu.shape == (M, 2 * N) and gu.stride(1) == 1
+    out = torch.empty(M, 4 * N, dtype=torch.float16, device=a3.device)
+    call("edge_gemm_f32_lrp_swiglu", ptr(a3), ptr(w3), ptr(out), ptr(gu), M, N, Kx, kp, a3.stride(0), w3.stride(0),
+         gu.stride(0), float(alpha * c0), stream())
+    return out, rs
+
+
+def lrp_swiglu_scale(wd: torch.Tensor, wgu: torch.Tensor, norm_w: torch.Tensor) -> float:
+    """c0 of ``linear_h3_lrp_swiglu`` for a Qwen2 MLP (wd [H, I] down, wgu [2I, H] interleaved gate|up, norm_w [H]
+    the post-attention RMSNorm weight): |dm_c| <= max|dx| max_c sum_k |wd[k, c]| and |g|, |u| <= sqrt(H)
+    max_j ||wgu_j * norm_w||_2 (the normalised row has ||x_hat||_2 <= sqrt(H)); |dg|, |du| <= 0.5 |dm| max(|g|, |u|).
+    The largest power of two with 2^15 x that bound x c0 <= 2^15."""
+    H = wd.shape[0]
+    cd = float(wd.float().abs().sum(0).max())
+    bgu = float((wgu.float() * norm_w.float().view(1, -1)).norm(dim=1).max()) * H ** 0.5
+    bound = 0.5 * cd * bgu * (1 + 2 ** -10)   # margin for the product's own rounding
+    return 2.0 ** -math.ceil(math.log2(bound)) if bound > 0 else 1.0
 
 
 def lrp_gelu_bwd_h3(dy: torch.Tensor, a: torch.Tensor):

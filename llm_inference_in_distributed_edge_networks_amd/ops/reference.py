@@ -409,6 +409,22 @@ def lrp_swiglu_bwd_h3(dm, gu, post=None):
     return split_h3_dyn(lrp_swiglu_bwd(_f(dm), _f(gu)), post)
 
 
+def h3_unit(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [R, K] -> the 2-plane h3 activation [R, 2K] at scale 1 (the caller bounds |x| below 2^15)."""
+    hi = _f(x).to(torch.float16)
+    lo = (_f(x) - hi.float()).to(torch.float16)
+    return torch.cat([hi, lo], -1).contiguous()
+
+
+def linear_h3_lrp_swiglu(a3, w3, alpha, gu, c0, rinv, post=None):
+    """``lrp_swiglu_bwd_h3`` of the dm GEMM's product with a bound-derived scale instead of the row max: the rule on
+    d = c0 alpha (a3 . w3^T) (the GEMM input's own row scale not undone) as unit-scale h3 planes, and the row scale
+    rinv post / c0 that undoes both (gemm.hip EPI_H3_LRP_SWIGLU)."""
+    d = h3_matmul(a3, w3, alpha * c0)
+    rs = rinv / c0 if post is None else rinv * _f(post) / c0
+    return h3_unit(lrp_swiglu_bwd(d, _f(gu))), rs
+
+
 def lrp_gelu_bwd_h3(dy, a):
     return split_h3_dyn(lrp_gelu_bwd(_f(dy), _f(a)))
 

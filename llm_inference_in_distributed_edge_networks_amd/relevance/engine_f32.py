@@ -16,7 +16,9 @@ and runs every matrix product at fp32 accuracy on the matrix cores:
     GEMM input row is split with its own power-of-two scale (max |row| just under 2^15) and the GEMM's per-row
     epilogue scale multiplies by the exact inverse - times the detached norm's rstd where a norm sits between;
   - the LRP rules that feed a GEMM (SwiGLU / GELU identity + uniform rules, inverse RoPE + GQA sum) write that
-    scaled split directly (csrc/lrp_f32.hip), with the residual add in the GEMM epilogue;
+    scaled split directly (csrc/lrp_f32.hip), with the residual add in the GEMM epilogue; the SwiGLU rule runs in
+    the epilogue of the GEMM producing its input (dm), at a power-of-two scale from an a-priori bound of the
+    weights (``ops.lrp_swiglu_scale``) instead of the row max, which would need every column tile of dm;
   - the attention rule (uniform on Q K^T and A V, plain softmax gradient) on fp32 matrix cores
     (``v_mfma_f32_16x16x4_f32``), emitting rel[b, h] = sum_ij A_ij dA_ij = 0.5 sum_i dO_i . O_i;
   - the channel-group relevance sum |x dx| of the residual stream entering every layer (``group_absprod``).
@@ -64,6 +66,7 @@ class RelevanceEngineH3:
                 t["wqkvT3"], t["a_qkvT"] = t3(L["wqkv"])
                 t["wguT3"], t["a_guT"] = t3(L["wgu"])
                 t["wdT3"], t["a_dT"] = t3(L["wd"])
+                t["c_swiglu"] = ops.lrp_swiglu_scale(L["wd"], L["wgu"], L["ln2_w"])
             else:
                 t["wqkvT3"], t["a_qkvT"] = t3(L["wqkv"])
                 t["wfcT3"], t["a_fcT"] = t3(L["wfc"])
@@ -166,8 +169,9 @@ class RelevanceEngineH3:
             rows = sv.get("rows")   # last layer: dx is the seeded rows only [B, H]
             dx3, rinv = ops.split_h3_dyn(dx)
             if self.qwen:
-                dm = ops.linear_h3(dx3, t["wdT3"], t["a_dT"], rscale=rinv)
-                dgu3, rinv_gu = ops.lrp_swiglu_bwd_h3(dm, sv["gu"], post=sv["rs2"])
+                # dm GEMM + SwiGLU rule in one kernel (the rule's planes at the weights' a-priori bound)
+                dgu3, rinv_gu = ops.linear_h3_lrp_swiglu(dx3, t["wdT3"], t["a_dT"], sv["gu"], t["c_swiglu"], rinv,
+                                                         post=sv["rs2"])
                 dy = ops.linear_h3(dgu3, t["wguT3"], t["a_guT"], rscale=rinv_gu, residual=dx, colscale=L["ln2_w"])
                 dy3, rinv_y = ops.split_h3_dyn(dy)
             else:

@@ -219,6 +219,42 @@ def test_fp32_lrp_rule_kernels():
     assert rel_err(sens, R.group_sens(xx.double(), dd.double(), 3, 50)) < 1e-6
 
 
+@pytest.mark.parametrize("M,N,K,tile,bf16w", [(300, 512, 256, 0, False), (300, 512, 256, 256, True),
+                                               (520, 640, 192, 0, True), (4096, 1024, 256, 0, True)])
+def test_fp32_lrp_swiglu_gemm_epilogue(M, N, K, tile, bf16w):
+    """dm GEMM + SwiGLU rule in one kernel (EPI_H3_LRP_SWIGLU) vs the fp64 rule on the fp64 product: every row within
+    4e-6 of its own max (rows spanning 12 decades), planes below 2^15 at the weights' bound scale; the 128x128 and
+    the persistent 256x256 kernels, three- and two-product (bf16-valued) weights."""
+    f = torch.float32
+    dx = rnd(M, K, seed=40, dtype=f) * torch.logspace(-6, 6, M).view(-1, 1)
+    wd = rnd(K, N, seed=41, dtype=f) * 0.05      # down projection [H, I]
+    wgu = rnd(2 * N, K, seed=42, dtype=f) * 0.05  # interleaved gate|up [2I, H]
+    if bf16w:
+        wd, wgu = wd.bfloat16().float(), wgu.bfloat16().float()
+    nw = torch.rand(K, generator=torch.Generator().manual_seed(43)) + 0.5
+    x = rnd(M, K, seed=44, dtype=f) * 3
+    gu = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-6) * nw) @ wgu.t()
+    post = torch.rand(M, generator=torch.Generator().manual_seed(45)) + 0.5
+    c0 = ops.lrp_swiglu_scale(wd, wgu, nw)
+    w3, s = R.h3_weight(wd.t().contiguous())
+    a3, rinv = ops.split_h3_dyn(dx.to(DEV))
+    ops.set_gemm_tile(tile)
+    try:
+        d3, rs = ops.linear_h3_lrp_swiglu(a3, w3.to(DEV), 1.0 / s, gu.to(DEV), c0, rinv, post=post.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        ops.set_gemm_tile(0)
+    assert d3.shape == (M, 4 * N) and float(d3.float().abs().max()) < 2 ** 15
+    got = R.h3_to_f32(d3.cpu()).double() * rs.cpu().double().view(-1, 1)
+    want = R.lrp_swiglu_bwd(dx.double() @ wd.double(), gu.double()) * post.double().view(-1, 1)
+    row_err = (got - want).abs().amax(1) / want.abs().amax(1)
+    assert float(row_err.max()) < 4e-6, float(row_err.max())   # the h3 product's own error (K terms)
+    # the CPU route of the same op (the engine's CPU path) agrees
+    c3, crs = R.linear_h3_lrp_swiglu(a3.cpu(), w3, 1.0 / s, gu, c0, rinv.cpu(), post)
+    assert torch.equal(crs, rs.cpu())
+    assert rel_err(R.h3_to_f32(c3) * crs.view(-1, 1), want) < 4e-6
+
+
 @pytest.mark.parametrize("cfg", [TINY_QWEN2, TINY_NEOX], ids=lambda c: c.name)
 def test_relevance_engine_h3_tiny_vs_autograd(cfg):
     """fp32 HIP relevance engine vs the autograd oracle (fp64 on the CPU, same weights)."""

@@ -7,6 +7,8 @@ Shapes: Qwen2-0.5B, one 64-window micro-batch of 512 tokens (M = 32768), bf16-va
   norm    fp32 RMSNorm -> h3 planes
   gateup  h3 gate/up GEMM + SwiGLU -> h3 planes (two products)
   down    h3 down GEMM + fp32 residual (two products)
+  lrpmlp        AttnLRP MLP backward, dm GEMM with the SwiGLU rule in its epilogue (EPI_H3_LRP_SWIGLU)
+  lrpmlp_split  the same as an fp32 dm GEMM + the rule's own pass (lrp_swiglu_bwd_h3_kernel), the round-4 path
 Prints the mean time per call (events) as JSON."""
 import argparse
 import json
@@ -22,7 +24,8 @@ from llm_inference_in_distributed_edge_networks_amd.ops import reference as R  #
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--op", default="attn", choices=["attn", "qkv", "colsum", "norm", "gateup", "down"])
+    ap.add_argument("--op", default="attn", choices=["attn", "qkv", "colsum", "norm", "gateup", "down",
+                                                          "lrpmlp", "lrpmlp_split"])
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--S", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
@@ -71,6 +74,20 @@ def main():
         else:
             res = torch.randn(B * S, N, generator=g).to(dev)
             fn = lambda: ops.linear_h3(x3, w3, 1.0 / (2.0 ** 10 * sw), residual=res)                      # noqa
+    elif a.op.startswith("lrpmlp"):   # dx [T, H] -> d[gate|up] h3 planes [T, 4I] (I = 4864), two-product weights
+        I = 4864
+        wd = (torch.randn(H, I, generator=g) * 0.02).bfloat16().float()
+        wgu = (torch.randn(2 * I, H, generator=g) * 0.02).bfloat16().float()
+        w3, sw = R.h3_weight(wd.t().contiguous())
+        w3 = w3.to(dev)
+        c0 = ops.lrp_swiglu_scale(wd, wgu, torch.ones(H))
+        dx3, rinv = ops.split_h3_dyn(torch.randn(B * S, H, generator=g).to(dev))
+        gu = torch.randn(B * S, 2 * I, generator=g).to(dev)
+        post = torch.rand(B * S, generator=g).to(dev)
+        if a.op == "lrpmlp":
+            fn = lambda: ops.linear_h3_lrp_swiglu(dx3, w3, 1.0 / sw, gu, c0, rinv, post=post)   # noqa: E731
+        else:
+            fn = lambda: ops.lrp_swiglu_bwd_h3(ops.linear_h3(dx3, w3, 1.0 / sw, rscale=rinv), gu, post=post)  # noqa
     else:
         x = torch.randn(B * S, H, generator=g).to(dev)
         w = (1 + 0.05 * torch.randn(H, generator=g)).to(dev)
