@@ -7,10 +7,12 @@ Qwen2-0.5B (GQA, RoPE, RMSNorm, SwiGLU, tied head) on local Python sources (byte
 ~270 MB, so a few minutes of training never revisit a byte), then saves it with ``DecoderLM.save_native``; the
 experiment drivers load it with ``weights=<file>.safetensors``.
 
-Held-out-driven stop: every ``--eval-every`` seconds the loss on the held-out stdlib split AND on a fixed sample of
-the training stream is measured; the best held-out checkpoint is kept, and training stops once the held-out loss has
-not improved for ``--patience`` evaluations (or the time budget ends).  The last line is a JSON summary with the
-train / held-out gap of the kept checkpoint.
+Held-out-driven stop: every ``--eval-every`` seconds the loss on 128 random windows of the held-out stdlib split AND
+on 128 random windows of the stdlib training split (the same distribution) is measured; the best held-out
+checkpoint is kept, and training stops once the held-out loss has not improved for ``--patience`` evaluations (or
+the time budget ends).  The last line is a JSON summary with the train / held-out gap of the kept checkpoint, the
+epochs trained, and a memorisation check: the loss on the first two training batches (seen) against fresh windows
+of the same training stream.
 
 The training forward is plain PyTorch autograd (bf16 autocast, SDPA) over the framework's own weight
 layout (fused qkv, interleaved gate|up), so the checkpoint is exactly what the HIP inference path runs.
@@ -75,13 +77,18 @@ def main():
         p.requires_grad_(True)
     w = {"embed": m.w["embed"], "norm_w": m.w["norm_w"], "layers": m.layers}
     data = local_text_bytes("train-large" if a.corpus == "large" else "train").view(-1).to(dev)
-    held = local_text_bytes("eval").view(-1)[: 64 * (a.seq + 1)].view(64, a.seq + 1).to(dev)
-    # a fixed sample of the stdlib TRAINING split (in the training data, and the held-out split's own distribution:
-    # the train / held-out gap measures memorisation, not the packages' sources being easier text)
-    gs = torch.Generator().manual_seed(1234)
-    std = local_text_bytes("train").view(-1)
-    tidx = torch.randint(0, std.numel() - a.seq - 1, (64,), generator=gs).tolist()
-    trs = torch.stack([std[i:i + a.seq + 1] for i in tidx]).long().to(dev)
+    def sample(stream, n, seed):   # n random windows spread over the whole stream (not its first files)
+        gs = torch.Generator().manual_seed(seed)
+        idx = torch.randint(0, stream.numel() - a.seq - 1, (n,), generator=gs).tolist()
+        return torch.stack([stream[i:i + a.seq + 1] for i in idx]).long().to(dev)
+    # held-out: the stdlib eval split (every 10th file); train sample: the stdlib TRAIN split, the held-out split's own
+    # distribution (the gap between them is a generalisation gap, not the packages' sources being other text)
+    held = sample(local_text_bytes("eval").view(-1), 128, 4321)
+    trs = sample(local_text_bytes("train").view(-1), 128, 1234)
+    # memorisation: the first two training batches (windows the model was trained on) against fresh windows of the
+    # same training stream
+    fresh = sample(data, 2 * a.batch, 999)
+    seen = []
     opt = torch.optim.AdamW(params, lr=a.lr, betas=(0.9, 0.95), weight_decay=a.weight_decay)
     cos, sin = m.cos, m.sin
     print(f"training {cfg.name}: {sum(p.numel() for p in params) / 1e6:.1f}M params, {data.numel() / 1e6:.1f}M train "
@@ -90,6 +97,14 @@ def main():
     g = torch.Generator(device=dev).manual_seed(a.seed)
     last_print = 0.0
     best = (float("inf"), 0, None, 0.0)  # held-out loss, step, CPU snapshot, train-sample loss
+
+    def nll(x):
+        out = 0.0
+        for c in x.split(32):
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+                lg = forward(w, cfg, c[:, :-1], cos, sin).float()
+            out += float(F.cross_entropy(lg.view(-1, cfg.vocab_size), c[:, 1:].reshape(-1), reduction="sum"))
+        return out / (x.shape[0] * (x.shape[1] - 1))
     stale = 0
     while True:
         el = time.time() - t0
@@ -101,6 +116,8 @@ def main():
             grp["lr"] = lr
         idx = torch.randint(0, data.numel() - a.seq - 1, (a.batch,), device=dev, generator=g)
         chunk = torch.stack([data[i:i + a.seq + 1] for i in idx.tolist()]).long()
+        if step < 2:
+            seen.append(chunk)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             logits = forward(w, cfg, chunk[:, :-1], cos, sin)
         loss = F.cross_entropy(logits.float().view(-1, cfg.vocab_size), chunk[:, 1:].reshape(-1))
@@ -111,18 +128,14 @@ def main():
         step += 1
         if el - last_print > a.eval_every:
             last_print = el
-            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-                hl = F.cross_entropy(forward(w, cfg, held[:, :-1], cos, sin).float().view(-1, cfg.vocab_size),
-                                     held[:, 1:].reshape(-1))
-                tl = F.cross_entropy(forward(w, cfg, trs[:, :-1], cos, sin).float().view(-1, cfg.vocab_size),
-                                     trs[:, 1:].reshape(-1))
-            if hl.item() < best[0]:
-                best = (hl.item(), step, [p.detach().to("cpu", copy=True) for p in params], tl.item())
+            hl, tl = nll(held), nll(trs)
+            if hl < best[0]:
+                best = (hl, step, [p.detach().to("cpu", copy=True) for p in params], tl)
                 stale = 0
             else:
                 stale += 1
-            print(f"step {step} t={el:.0f}s lr={lr:.2e} batch {loss.item():.3f} train-sample {tl.item():.3f} "
-                  f"held-out {hl.item():.3f} nats/byte ({hl.item() / math.log(2):.3f} bits/byte)", flush=True)
+            print(f"step {step} t={el:.0f}s lr={lr:.2e} batch {loss.item():.3f} train-sample {tl:.3f} "
+                  f"held-out {hl:.3f} nats/byte ({hl / math.log(2):.3f} bits/byte)", flush=True)
             if stale >= a.patience:
                 print(f"held-out loss has not improved for {stale} evaluations: stopping", flush=True)
                 break
@@ -133,9 +146,13 @@ def main():
             p.copy_(b.to(p.device))
         print(f"keeping the best held-out checkpoint: step {best[1]}, {best[0]:.3f} nats/byte", flush=True)
     import json
+    seen_l, fresh_l = nll(torch.cat(seen)), nll(fresh)
     print(json.dumps({"best_step": best[1], "steps": step, "held_out_nats_per_byte": round(best[0], 4),
                       "train_sample_nats_per_byte": round(best[3], 4),
                       "gap": round((best[0] - best[3]) / best[0], 4) if best[0] < float("inf") else None,
+                      "seen_nats_per_byte": round(seen_l, 4), "fresh_nats_per_byte": round(fresh_l, 4),
+                      "memorisation_gap": round((fresh_l - seen_l) / fresh_l, 4),
+                      "epochs": round(step * a.batch * a.seq / data.numel(), 4),
                       "corpus": a.corpus, "train_bytes": int(data.numel()), "seed": a.seed}), flush=True)
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     DecoderLM(cfg, {"embed": m.w["embed"], "norm_w": m.w["norm_w"], "head": m.w["embed"], "layers": m.layers},
