@@ -243,6 +243,59 @@ __device__ __forceinline__ void swiglu_h3_lines_4w(const GemmArgs& a, f32x4_t (&
   }
 }
 
+// AttnLRP SwiGLU rule epilogue of the four-wave 256x256 kernel (EPI_H3_LRP_SWIGLU): the wave's 128 rows x 128 dm
+// columns are 8 interleave blocks per 16-row group, whose gate|up pre-activations (a 128-byte line per row and block)
+// the rule reads.  Row group i + 1's loads are issued before group i computes and stores, so every wait finds its
+// loads long in flight (the per-slab epilogue waited a full memory round trip per group and made the fused GEMM as
+// slow as the GEMM plus the rule's own pass).
+__device__ __forceinline__ void lrp_swiglu_4w(const GemmArgs& a, f32x4_t (&acc)[8][8], int m0, int n0, int lane,
+                                              int wm, int wn) {
+  if (n0 + wn * 128 >= a.N) return;   // empty half of a partial column tile (wave-uniform)
+  const int r = lane & 15, g = lane >> 4;
+  const int W = 2 * a.N;
+  const int cb = (n0 + wn * 128) * 2 + g * 4;   // gu / plane column of the lane's gate chunk in block 0
+  f32x4_t gb[2][8], ub[2][8];
+  auto load = [&](int i, int b) {
+    const int m = min(m0 + wm * 128 + i * 16 + r, a.M - 1);
+    const float* gr = a.residf + (size_t)m * a.ldr + cb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      gb[b][j] = *(const f32x4_t*)(gr + 32 * j);
+      ub[b][j] = *(const f32x4_t*)(gr + 32 * j + 16);
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int b = i & 1;
+    if (i + 1 < 8) load(i + 1, b ^ 1);
+    f32x4_t c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      c[j] = acc[i][j];
+      asm volatile("" : "+v"(c[j]));
+    }
+    const int m = m0 + wm * 128 + i * 16 + r;
+    if (m < a.M) {
+      f16_t* dst = a.C + (size_t)m * a.ldc + cb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float dg[4], du[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float gv = gb[b][j][q];
+          const float h = 0.5f * a.alpha * c[j][q] * fast_sigmoid(gv);
+          dg[q] = h * ub[b][j][q];
+          du[q] = h * gv;
+        }
+        store_h3_4(dst + 32 * j, W, 0, dg, 1.f);
+        store_h3_4(dst + 32 * j + 16, W, 0, du, 1.f);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // ---- K / V^T h3 planes from the fp32 QKV epilogues (GemmArgs::kp / vp).  split2h of s x: bit-identical to the split
 // flash_attn_fwd_x6_kernel applies to the fp32 K / V^T it stages itself.  V^T keys are stored in the order the
 // kernel's P^T operand holds them: within each 32-key block, lane group g's k-slots 8g..8g+7 are keys
@@ -1452,6 +1505,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (BN == 256 && EPI == EPI_H3_SWIGLU) {
         swiglu_h3_lines_4w<8>(a, acc, rs, m0, n0, lane, wm, wn);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (BN == 256 && EPI == EPI_H3_LRP_SWIGLU) {
+        lrp_swiglu_4w(a, acc, m0, n0, lane, wm, wn);
         __builtin_amdgcn_sched_barrier(0);
       } else if constexpr (BN == 256) {
 #pragma unroll

@@ -2,11 +2,11 @@
 # engine, same-box A/B of the fused vs split MLP backward (kernel_probe), the fp32 AttnLRP throughput and its kernel
 # profile.
 set -o pipefail
-O=gpurun_out/r05d
+O=gpurun_out/${OUT:-r05d}
 mkdir -p $O
 export TMPDIR=/tmp
 R=$PWD
-timeout -k 10 400 python -u -m pytest tests/test_lrp_gpu.py -x -q --timeout 200 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_lrp_gpu.py -x -q ${TESTK:+-k "$TESTK"} --timeout 200 --timeout-method thread \
   -p no:cacheprovider > $O/pytest_lrp.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest_lrp.log; exit 1; }
 tail -2 $O/pytest_lrp.log
 for r in 1 2; do
