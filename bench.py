@@ -467,6 +467,7 @@ def deep_pipeline(a, env, cfg, dtype, values, spec, emit: Emitter) -> None:
     res = None
     sub = argparse.Namespace(**vars(a))
     sub.microbatches = 4 * world          # weak scaling: every GPU does 4 full-model micro-batches per step
+    t0 = time.time()
     try:
         msg_bytes = C.message_bytes(spec, a.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
         res = measure(sub, env, cfg, dtype, world, grid, plan, steps, warm, values,
@@ -489,7 +490,7 @@ def deep_pipeline(a, env, cfg, dtype, values, spec, emit: Emitter) -> None:
         "ms_per_step": round(1000 * res["dt"] / steps, 3), "global_batch": sub.microbatches * a.batch,
         "stage_layers": [[r.start, r.stop - 1] for r in (plan.stage_layers(s) for s in range(world))],
         "wire_bytes_per_token": [round(w, 2) for w in res["wires"]], "ppl_random_weights": res["ppl"],
-        "stages": res["stages"], "p2p": res["p2p"]}
+        "stages": res["stages"], "p2p": res["p2p"], "wall_s": round(time.time() - t0, 2)}
 
 
 if __name__ == "__main__":

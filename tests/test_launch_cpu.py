@@ -86,7 +86,7 @@ def _check_deep(d, n):
     assert len(deep["stages"]) == n and {s["stage"] for s in deep["stages"]} == set(range(n))
     assert len(deep["wire_bytes_per_token"]) == n - 1 and all(w > 0 for w in deep["wire_bytes_per_token"])
     assert len(deep["p2p"]) == 2 * (n - 1) and {r["stage"] for r in deep["p2p"]} == set(range(n - 1))
-    assert deep["ppl_random_weights"] > 1 and deep["ms_per_step"] > 0
+    assert deep["ppl_random_weights"] > 1 and deep["ms_per_step"] > 0 and deep["wall_s"] > 0
 
 
 @pytest.mark.parametrize("pp", [4, 8])

@@ -63,6 +63,19 @@ def test_four_stage_pipeline_one_gpu_equals_local():
     assert len(four["stages"]) == 4 and all("compute_ms" in s for s in four["stages"])
 
 
+def test_deep_pipeline_secondary_one_gpu():
+    """4 ranks sharing cuda:0 with the default parallelism: the headline pp2xdp2 plus the secondary measurement of
+    the same step as one 4-stage pipeline (``value_pp4``, its stages, wire sizes and p2p probe; bench.deep_pipeline)
+    on the CUDA path."""
+    four = _run(4, ["--no-bf16", "--no-fp32-weights"])
+    assert four["config"]["parallelism"] == "pp2xdp2"
+    pp = four["pp4"]
+    assert "error" not in pp and four["value_pp4"] > 0, pp
+    assert pp["parallelism"] == "pp4xdp1" and len(pp["stages"]) == 4 and len(pp["p2p"]) == 6
+    assert len(pp["wire_bytes_per_token"]) == 3 and all(w > 0 for w in pp["wire_bytes_per_token"])
+    assert pp["ppl_random_weights"] > 1 and pp["wall_s"] > 0
+
+
 def test_serialized_kernel_mode_same_result():
     """SURVEY §5.2 race check: with every kernel serialised (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1) the
     2-rank pipeline gives bit-identical PPL to the normal asynchronous run - no result depends on stream overlap."""

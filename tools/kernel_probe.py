@@ -7,6 +7,8 @@ Shapes: Qwen2-0.5B, one 64-window micro-batch of 512 tokens (M = 32768), bf16-va
   norm    fp32 RMSNorm -> h3 planes
   gateup  h3 gate/up GEMM + SwiGLU -> h3 planes (two products)
   down    h3 down GEMM + fp32 residual (two products)
+  gateup_lib / down_lib  hipBLASLt (torch.matmul) on the same fp16 operands and K' (no epilogue): the library's clock
+                and MFMA rate under the same sustained load
   lrpmlp        AttnLRP MLP backward, dm GEMM with the SwiGLU rule in its epilogue (EPI_H3_LRP_SWIGLU)
   lrpmlp_split  the same as an fp32 dm GEMM + the rule's own pass (lrp_swiglu_bwd_h3_kernel), the round-4 path
 Prints the mean time per call (events) as JSON."""
@@ -25,7 +27,7 @@ from llm_inference_in_distributed_edge_networks_amd.ops import reference as R  #
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--op", default="attn", choices=["attn", "qkv", "colsum", "norm", "gateup", "down",
-                                                          "lrpmlp", "lrpmlp_split"])
+                                                          "lrpmlp", "lrpmlp_split", "gateup_lib", "down_lib"])
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--S", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
@@ -62,6 +64,11 @@ def main():
         kvs = (2.0 ** 6, 2.0 ** 6) if a.kv_planes else None   # the K / V^T planes the attention stages by DMA
         fn = lambda: ops.qkv_rope_h3(x3, w3, 1.0 / (2.0 ** 10 * sw), bias, cos, sin, B, S, Hq, Hkv, 64, 64,  # noqa
                                      0.125, kv_scales=kvs)
+    elif a.op in ("gateup_lib", "down_lib"):   # the two-product K' = 2K as one plain fp16 GEMM
+        K, N = (H, 9728) if a.op == "gateup_lib" else (4864, H)
+        x = torch.randn(B * S, 2 * K, generator=g).half().to(dev)
+        w = (torch.randn(N, 2 * K, generator=g) * 0.02).half().to(dev)
+        fn = lambda: torch.matmul(x, w.t())   # noqa: E731
     elif a.op in ("gateup", "down"):   # h3 SwiGLU GEMM -> h3 planes / down GEMM + fp32 residual (two products)
         K, N = (H, 9728) if a.op == "gateup" else (4864, H)
         x = torch.randn(B * S, K, generator=g)
