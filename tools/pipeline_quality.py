@@ -181,18 +181,18 @@ def main():
     if comps:
         lines += ["", "Allocated plan vs the uniform plan (same bits): log PPL(plan) - log PPL(uniform), paired "
                   "window-bootstrap 95 % interval; negative = the allocated plan is better:", "",
-                  "| codec | plan | " + " | ".join(f"r={r:g}" for r in ratios) + " | better at |",
-                  "|---|---|" + "---|" * len(ratios) + "---|"]
+                  "| method | codec | plan | " + " | ".join(f"r={r:g}" for r in ratios) + " | better at |",
+                  "|---|---|---|" + "---|" * len(ratios) + "---|"]
         for c in comps:
             cells = [f"{x['diff']:+.2e} [{x['ci'][0]:+.1e}, {x['ci'][1]:+.1e}]" for x in c["cells"]]
             better = sum(1 for x in c["cells"] if x["ci"][1] < 0)
-            lines.append(f"| {c['codec']} | {c['plan']} | " + " | ".join(cells) +
+            lines.append(f"| {c['method']} | {c['codec']} | {c['plan']} | " + " | ".join(cells) +
                          f" | {better} of {len(ratios)} ratios |")
     plans = [r for r in out["rows"] if r.get("group_plans")]
     if plans:
         lines += ["", "Head-group bit plans per boundary (one digit per 64-channel group, ratio 0.5):", ""]
         for r in plans:
-            lines.append(f"- {r['codec']} / {r['plan']}: " +
+            lines.append(f"- {r['method']} / {r['codec']} / {r['plan']}: " +
                          "; ".join(f"after layer {b}: {''.join(str(x) for x in p)}" for b, p in r["group_plans"].items()))
     out["markdown"] = "\n".join(lines)
     print("\n" + out["markdown"], flush=True)
