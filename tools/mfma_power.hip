@@ -102,7 +102,7 @@ static void run(const _Float16* src, float* out, int grid, int launches, int ite
 
 int main(int argc, char** argv) {
   const int launches = argc > 1 ? atoi(argv[1]) : 40;
-  const int iters = argc > 2 ? atoi(argv[2]) : 400;
+  const int iters = argc > 2 ? atoi(argv[2]) : 200000;
   int dev = 0, cus = 0;
   CHECK(hipGetDevice(&dev));
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
