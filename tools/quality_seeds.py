@@ -67,6 +67,26 @@ def main():
     out += table("one_scale_collapse_at_ratio_1", "One-scale collapse at ratio 1: log PPL(r=1) - log PPL(r=0), last_row,"
                  " Q1 (reference: x23 at L22)", ["layer"], lambda x: x["verdict"] == "a worse" and x["rel"] > 1.0)
 
+    # mechanism: the one-scale damage against the boundary's outlier statistics, every (seed, layer)
+    pts = []
+    for name, _, sw, _ in runs:
+        dmg = {x["layer"]: x["rel"] for x in sw["findings"]["one_scale_collapse_at_ratio_1"]}
+        for L, b in sorted(sw.get("boundary_outliers", {}).items(), key=lambda kv: int(kv[0])):
+            if int(L) in dmg:
+                pts.append((name, int(L), b["peak_over_rms"], b["int4_global_zero_fraction"], dmg[int(L)]))
+    if len(pts) >= 3:
+        from scipy.stats import spearmanr
+        out += ["### What the one-scale damage follows", "",
+                "| seed | layer | boundary peak / RMS | values one global int4 scale rounds to 0 | ratio-1 damage |",
+                "|---|---|---|---|---|"]
+        out += [f"| {n} | {L} | {pk:.1f} | {z:.3f} | {100 * d:+.2f} % |" for n, L, pk, z, d in pts]
+        rz = spearmanr([p[3] for p in pts], [p[4] for p in pts])
+        rp = spearmanr([p[2] for p in pts], [p[4] for p in pts])
+        rl = spearmanr([p[1] for p in pts], [p[4] for p in pts])
+        out += ["", f"Spearman over the {len(pts)} (seed, layer) points: zeroed fraction vs damage "
+                f"{rz.statistic:.2f} (p = {rz.pvalue:.1e}); peak / RMS vs damage {rp.statistic:.2f} "
+                f"(p = {rp.pvalue:.1e}); depth vs damage {rl.statistic:.2f} (p = {rl.pvalue:.1e}).", ""]
+
     # config 5: allocated head-group plans against the uniform plan
     out += ["## Head-group plans against the uniform plan (pipeline, 7 boundaries)", "",
             "Ratios at which the allocated plan is better (interval below 0) / worse (interval above 0), of the 4 "
