@@ -76,6 +76,17 @@ def test_deep_pipeline_secondary_one_gpu():
     assert pp["ppl_random_weights"] > 1 and pp["wall_s"] > 0
 
 
+def test_eight_ranks_one_gpu_headline_and_pp8():
+    """The driver's 8-GPU shape rehearsed on one GPU: 8 ranks (gloo, host-staged p2p) run the pp2xdp4 headline and
+    then the 8-stage secondary (one layer per stage on the 8-layer byte model), both through the CUDA-graph path."""
+    r = _run(8, ["--model", "byte-qwen2", "--batch", "2", "--microbatches", "2", "--max-length", "128", "--split", "3",
+                 "--no-bf16", "--no-fp32-weights"])
+    assert r["config"]["parallelism"] == "pp2xdp4" and r["n_gpus"] == 8
+    pp = r["pp8"]
+    assert "error" not in pp and r["value_pp8"] > 0, pp
+    assert pp["parallelism"] == "pp8xdp1" and len(pp["stages"]) == 8 and len(pp["wire_bytes_per_token"]) == 7
+
+
 def test_serialized_kernel_mode_same_result():
     """SURVEY §5.2 race check: with every kernel serialised (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1) the
     2-rank pipeline gives bit-identical PPL to the normal asynchronous run - no result depends on stream overlap."""
