@@ -12,6 +12,6 @@ timeout -s KILL 120 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_
   --output-format csv -d $R/$O/pmc -o run -- $R/tools/bin/mfma_power 20 200000 > $R/$O/pmc.log 2>&1 \
   || { echo "pmc failed"; tail -3 $R/$O/pmc.log; exit 1; }
 cd $R
-{ python tools/clock_pmc.py $O/pmc "mfma_burnILi0" && python tools/clock_pmc.py $O/pmc "mfma_burnILi1"; } > $O/clock.md
+{ python tools/clock_pmc.py $O/pmc "mfma_burnILi0" && python tools/clock_pmc.py $O/pmc "mfma_burnILi1" && python tools/clock_pmc.py $O/pmc "mfma_burnILi2"; } > $O/clock.md
 grep -E "median|dispatches" $O/clock.md
 exit 0
