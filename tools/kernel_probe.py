@@ -7,6 +7,7 @@ Shapes: Qwen2-0.5B, one 64-window micro-batch of 512 tokens (M = 32768), bf16-va
   norm    fp32 RMSNorm -> h3 planes
   gateup  h3 gate/up GEMM + SwiGLU -> h3 planes (two products)
   down    h3 down GEMM + fp32 residual (two products)
+  gateupraw     the AttnLRP forward's gate/up: SwiGLU planes + the fp32 pre-activations from one GEMM
   gateup_lib / down_lib  hipBLASLt (torch.matmul) on the same fp16 operands and K' (no epilogue): the library's clock
                 and MFMA rate under the same sustained load
   lrpmlp        AttnLRP MLP backward, dm GEMM with the SwiGLU rule in its epilogue (EPI_H3_LRP_SWIGLU)
@@ -27,7 +28,7 @@ from llm_inference_in_distributed_edge_networks_amd.ops import reference as R  #
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--op", default="attn", choices=["attn", "qkv", "colsum", "norm", "gateup", "down",
-                                                          "lrpmlp", "lrpmlp_split", "gateup_lib", "down_lib"])
+                                                          "lrpmlp", "lrpmlp_split", "gateup_lib", "down_lib", "gateupraw"])
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--S", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
@@ -69,6 +70,12 @@ def main():
         x = torch.randn(B * S, 2 * K, generator=g).half().to(dev)
         w = (torch.randn(N, 2 * K, generator=g) * 0.02).half().to(dev)
         fn = lambda: torch.matmul(x, w.t())   # noqa: E731
+    elif a.op == "gateupraw":
+        x = torch.randn(B * S, H, generator=g)
+        w = (torch.randn(9728, H, generator=g) * 0.02).bfloat16().float()
+        w3, sw = R.h3_weight(w)
+        x3, w3 = ops.split_h3(x.to(dev), 2.0 ** 10), w3.to(dev)
+        fn = lambda: ops.linear_h3_swiglu_raw(x3, w3, 1.0 / (2.0 ** 10 * sw), 2.0 ** 6)   # noqa: E731
     elif a.op in ("gateup", "down"):   # h3 SwiGLU GEMM -> h3 planes / down GEMM + fp32 residual (two products)
         K, N = (H, 9728) if a.op == "gateup" else (4864, H)
         x = torch.randn(B * S, K, generator=g)
