@@ -46,6 +46,7 @@ struct GemmArgs {
   // ldc = 2 * width
   float* Cf; const float* biasf; const float* residf;
   float* qf; float* kf; float* vtf;
+  float* vf;   // fp32 QKV, optional: V row-major [B, Hkv, S, 64] (the AttnLRP backward's operand) next to V^T / planes
   // QKV_ROPE
   bf16_t* qout; bf16_t* kout; bf16_t* vtout;
   const float* cosT; const float* sinT;
@@ -409,6 +410,11 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
           for (int j = 0; j < 4; ++j) store_k_planes4(a, b, head - a.Hq, pos, j * 16 + g * 4, v[j]);
         }
       } else {
+        if (a.vf) {
+          float* dst = a.vf + (((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * a.S + pos) * 64;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) *(f32x4_t*)(dst + j * 16 + g * 4) = f32x4_t{v[j][0], v[j][1], v[j][2], v[j][3]};
+        }
         if (a.vtf) {
           float* dst = a.vtf + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
 #pragma unroll
@@ -1166,6 +1172,11 @@ __device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[
           store_k_planes4(a, b, head - a.Hq, pos, d + 32, h4);
         }
       } else {
+        if (a.vf) {
+          float* dst = a.vf + (((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * a.S + pos) * 64;
+          *(f32x4_t*)(dst + d) = lo;
+          *(f32x4_t*)(dst + d + 32) = hi;
+        }
         if (a.vtf) {
           float* dst = a.vtf + ((size_t)b * a.Hkv + (head - a.Hq - a.Hkv)) * 64 * (size_t)a.s_pad + pos;
 #pragma unroll
@@ -1913,11 +1924,12 @@ EDGE_API int edge_gemm_f32_lrp_swiglu(const void* A, const void* B, void* C, con
 // weight), alpha = 1 / (s_x s_w), fp32 bias, fp32 outputs q [B,Hq,S,64] (x q_scale), k [B,Hkv,S,64],
 // vt [B,Hkv,64,s_pad].
 // kp / vp (optional, both or neither): K and V^T also as scaled fp16 h3 planes at scales kv_sk / kv_sv (GemmArgs);
-// with them vt may be null (the plane-staged attention reads no fp32 V^T).
+// with them vt may be null (the plane-staged attention reads no fp32 V^T).  vf (optional): V row-major fp32
+// [B,Hkv,S,64] too (the AttnLRP backward's V).
 EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* bias, float* q, float* k, float* vt,
                                     const float* cosT, const float* sinT, int M, int Kx, int kplane, int S, int Hq,
                                     int Hkv, int rot_dim, int s_pad, float q_scale, float alpha, void* kp, void* vp,
-                                    float kv_sk, float kv_sv, hipStream_t st) {
+                                    float kv_sk, float kv_sv, float* vf, hipStream_t st) {
   GemmArgs a{};
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)W;
   a.pairb = Kx == 2 * kplane;
@@ -1928,6 +1940,8 @@ EDGE_API int edge_gemm_qkv_rope_f32(const void* X, const void* W, const float* b
   a.cosT = cosT; a.sinT = sinT; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.s_pad = s_pad;
   a.q_scale = q_scale;
   a.kp = (f16_t*)kp; a.vp = (f16_t*)vp; a.kv_sk = kv_sk; a.kv_sv = kv_sv;
+  a.vf = vf;
+  if (vf && ((uintptr_t)vf & 15)) return (int)hipErrorInvalidValue;
   if (!bias || M % S || !h3_geometry_ok(Kx, kplane) || ((uintptr_t)bias & 15) || !(alpha > 0.f))
     return (int)hipErrorInvalidValue;
   if ((kp == nullptr) != (vp == nullptr) || (kp && (!(kv_sk > 0.f) || !(kv_sv > 0.f) || ((uintptr_t)kp & 7))))

@@ -498,19 +498,20 @@ def linear_h3_swiglu_raw(a3: torch.Tensor, w3: torch.Tensor, alpha: float, out_s
     return planes, raw
 
 
-def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, kv_scales=None, need_k=True):
+def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, kv_scales=None, need_k=True,
+                v_rows=False):
     """fp32 fused QKV projection + bias + RoPE + head-major scatter from h3 operands -> fp32 (q, k, vt).
 
     ``kv_scales`` = (s_k, s_v): also the K / V^T h3 planes at those scales for ``attention(kv_planes=...)`` ->
     (q, k, vt, kp, vp); on the GPU ``vt`` is then None (the planes replace it), and with ``need_k=False`` so is the
-    fp32 ``k`` (the attention stages the planes; only the importance scorers read fp32 K)."""
+    fp32 ``k`` (the attention stages the planes; only the importance scorers read fp32 K).  ``v_rows``: V row-major
+    fp32 [B, Hkv, S, 64] appended to the outputs (the AttnLRP backward's V, from the same epilogue)."""
     if not _gpu(a3):
         y = ref.h3_matmul(a3, w3, alpha)            # x @ w.T, then the rest of the fused op on fp32
         eye = torch.eye(y.shape[1], dtype=torch.float32)
         q, k, vt = ref.qkv_rope(y, eye, bias.float(), cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale)
-        if kv_scales is None:
-            return q, k, vt
-        return (q, k, vt) + ref.kv_planes(k, vt, *kv_scales)   # vt is zero-padded to s_pad(S) already
+        out = (q, k, vt) if kv_scales is None else (q, k, vt) + ref.kv_planes(k, vt, *kv_scales)
+        return out + ((vt[..., :S].transpose(-1, -2).contiguous(),) if v_rows else ())
     kp, Kx = _check_h3(a3, w3, alpha)
     _check_f32(bias)
     assert D == 64, "HIP attention path is specialised for head_dim 64"
@@ -526,12 +527,13 @@ def qkv_rope_h3(a3, w3, alpha, bias, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scal
         f16 = dict(dtype=torch.float16, device=a3.device)
         kpl = torch.empty(B, Hkv, 2, S, D, **f16)
         vpl = torch.zeros(B, Hkv, 2, D, sp, **f16) if sp != S else torch.empty(B, Hkv, 2, D, sp, **f16)
+    v = torch.empty(B, Hkv, S, D, **f32) if v_rows else None
     sk_, sv_ = kv_scales if kv_scales is not None else (0.0, 0.0)
     call("edge_gemm_qkv_rope_f32", ptr(a3), ptr(w3), ptr(bias), ptr(q), ptr(k), ptr(vt), ptr(cos), ptr(sin), M, Kx, kp, S,
-         Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), ptr(kpl), ptr(vpl), float(sk_), float(sv_), stream())
-    if kv_scales is None:
-        return q, k, vt
-    return q, k, vt, kpl, vpl
+         Hq, Hkv, rot_dim, sp, float(q_scale), float(alpha), ptr(kpl), ptr(vpl), float(sk_), float(sv_), ptr(v),
+         stream())
+    out = (q, k, vt) if kv_scales is None else (q, k, vt, kpl, vpl)
+    return out + ((v,) if v_rows else ())
 
 
 def head_nll_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, targets: torch.Tensor) -> torch.Tensor:

@@ -94,10 +94,14 @@ class RelevanceEngineH3:
                 sv["rs1"] = ops.row_rstd(x, eps, center=True)
                 h13, h23 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], eps,
                                               h3=(sc["qkv"], sc["mlp"]))
-            q, k, vt = ops.qkv_rope_h3(h13, L["wqkv3"], sc["a_wqkv"], L["bqkv"], m.cos, m.sin, B, S, Hq, Hkv, D,
-                                       cfg.rotary_dim, m.q_scale)
-            o, lse = ops.attention(q, k, vt, S, need_lse=True, in_scales=(sc["att_q"], sc["att_k"], sc["o"]))
-            sv.update(q=q, k=k, v=vt[..., :S].transpose(-1, -2).contiguous(), o=o, lse=lse.contiguous())
+            # the QKV epilogue also writes the K / V^T planes the attention stages by LDS DMA and V row-major for the
+            # backward (no transpose pass)
+            q, k, vt, kp, vp, v = ops.qkv_rope_h3(h13, L["wqkv3"], sc["a_wqkv"], L["bqkv"], m.cos, m.sin, B, S, Hq,
+                                                  Hkv, D, cfg.rotary_dim, m.q_scale, kv_scales=(sc["att_k"], sc["o"]),
+                                                  v_rows=True)
+            o, lse = ops.attention(q, k, vt, S, need_lse=True, in_scales=(sc["att_q"], sc["att_k"], sc["o"]),
+                                   kv_planes=(kp, vp) if q.is_cuda else None)
+            sv.update(q=q, k=k, v=v, o=o, lse=lse.contiguous())
             if i == nl - 1:   # only the seeded rows reach the seed: O-proj and MLP on those rows
                 sv["rows"] = last
                 x = x.index_select(0, last)

@@ -5,7 +5,8 @@ set -o pipefail
 O=gpurun_out/r05m
 mkdir -p $O
 PREV=$PWD/build/ab_raw/libedge_kernels_prev.so
-timeout -k 10 300 python -u -m pytest tests/test_f32_gpu.py -x -q -k "swiglu_raw" --timeout 120 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_f32_gpu.py tests/test_lrp_gpu.py -x -q \
+  -k "swiglu_raw or qkv_kv_planes or engine_h3 or calibration" --timeout 200 --timeout-method thread \
   -p no:cacheprovider > $O/pytest.log 2>&1 || { echo "tests failed"; tail -20 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for r in 1 2 3; do

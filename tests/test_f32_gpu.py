@@ -234,7 +234,8 @@ def test_qkv_rope_h3(B, S, Hq, Hkv, rot, tile, two_term):
 @pytest.mark.parametrize("tile", ["auto", "192", "256"])
 def test_qkv_kv_planes(B, S, Hq, Hkv, rot, tile):
     """K / V^T h3 planes from the fp32 QKV epilogues (128x128, 256x192 and 256x256 tiles) are the split of the fp32
-    K / V^T, bit for bit, V^T keys in the attention kernel's P^T order and zero key padding; q and K unchanged."""
+    K / V^T, bit for bit, V^T keys in the attention kernel's P^T order and zero key padding; q and K unchanged; the
+    optional row-major V equals the fp32 V^T."""
     H = 896 if Hq == 14 else 512
     Nq = (Hq + 2 * Hkv) * 64
     x = rnd(B * S, H, seed=33)
@@ -247,9 +248,9 @@ def test_qkv_kv_planes(B, S, Hq, Hkv, rot, tile):
     try:
         if tile in ("192", "256"):
             ops.set_gemm_tile(int(tile))
-        q, k, vt, kp, vp = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV),
-                                           cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125,
-                                           kv_scales=(sk, sv))
+        q, k, vt, kp, vp, v = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV),
+                                              cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125,
+                                              kv_scales=(sk, sv), v_rows=True)
         q2, k2, vt2 = ops.qkv_rope_h3(R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV), cos.to(DEV),
                                       sin.to(DEV), B, S, Hq, Hkv, 64, rot, 0.125)
         torch.cuda.synchronize()
@@ -259,6 +260,7 @@ def test_qkv_kv_planes(B, S, Hq, Hkv, rot, tile):
     rkp, rvp = R.kv_planes(k.cpu(), vt2.cpu(), sk, sv)
     assert torch.equal(kp.cpu(), rkp)
     assert torch.equal(vp.cpu(), rvp)
+    assert torch.equal(v, vt2[..., :S].transpose(-1, -2))   # V row-major (AttnLRP), the same values as V^T
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (3, 100, 14, 2), (1, 2048, 8, 8), (2, 64, 4, 1),
