@@ -199,27 +199,6 @@ __device__ __forceinline__ void line_exchange8(const u32x4_t& X, const u32x4_t& 
   }
 }
 
-// GemmArgs::raw of one 16-row group in full 128-byte lines: the 16-column groups (2p, 2p + 1) of a row are one line of
-// 32 fp32; lanes r and r ^ 8 exchange their halves (line_exchange8) so each store writes 8 rows x 128 B instead of
-// 16 rows x 64 B.  ma = the group's row (r & 7), n = the first column of c0 (c1: n + 64).
-__device__ __forceinline__ void swiglu_raw_lines(const GemmArgs& a, const f32x4_t (&c0)[4], const f32x4_t (&c1)[4],
-                                                 float f, int ma, int n, bool lo8, int g) {
-  float* const base = a.raw + n + (lo8 ? 0 : 16) + 4 * g;
-  const int mb = ma + 8;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const f32x4_t x = (h ? c1[2 * p] : c0[2 * p]) * f, y = (h ? c1[2 * p + 1] : c0[2 * p + 1]) * f;
-      u32x4_t A, B;
-      line_exchange8(__builtin_bit_cast(u32x4_t, x), __builtin_bit_cast(u32x4_t, y), lo8, A, B);
-      const int col = 64 * h + 32 * p;
-      if (ma < a.M) *(u32x4_t*)(base + (size_t)ma * a.N + col) = A;
-      if (mb < a.M) *(u32x4_t*)(base + (size_t)mb * a.N + col) = B;
-    }
-  }
-}
-
 // SwiGLU h3 epilogue of the four-wave 256x256 kernel with full-line stores: the wave's 128 accumulator columns are 64
 // output columns = one 128-byte line per plane and row, written 8 rows x 128 bytes per store instruction (the two
 // 64-column slabs of a row group exchanged between lanes r and r ^ 8) instead of 16 rows x 64 bytes - half the
@@ -241,7 +220,11 @@ __device__ __forceinline__ void swiglu_h3_lines_4w(const GemmArgs& a, f32x4_t (&
       asm volatile("" : "+v"(c0[j]), "+v"(c1[j]));
     }
     const float f = rs[i] * a.alpha;
-    if (a.raw) swiglu_raw_lines(a, c0, c1, f, m0 + wm * 128 + i * 16 + (r & 7), n0 + wn * 128, lo8, g);
+    if (a.raw) {   // (full-line stores here, as for the planes, measured equal: profiles/r05/raw_store_ab.log)
+      const int m = m0 + wm * 128 + i * 16 + r;
+      swiglu_raw_store(a, c0, f, m, n0 + wn * 128, g);
+      swiglu_raw_store(a, c1, f, m, n0 + wn * 128 + 64, g);
+    }
     u32x4_t H0, L0, H1, L1;
     swiglu_h3_rowgroup(a, c0, f, H0, L0);
     swiglu_h3_rowgroup(a, c1, f, H1, L1);
