@@ -306,3 +306,41 @@ def test_group_codec_roundtrip(name, dtype, plan):
     # default plan without relevance: 4 bits everywhere
     L4 = C.layout(C.get_codec(name), B, S, H, S // 2 if name != "rgroup" else 0, dtype)
     assert L4.plan == (4, 4, 4, 4)
+
+
+# sha1 prefixes of the CPU oracle's messages for a fixed input (B 2, S 128, H 896, ratio 0.5; head-group plan
+# 2,4,8,4,4,2,8,4,4,4,2,8,4,4): the wire format of every codec, pinned - identical to round 4's tree when taken
+WIRE_FINGERPRINTS = {
+    "channel_1_max": (64576, "7dd6daea9df2e70e"),
+    "channel_1_mean": (64576, "e6e44f6621c8a0da"),
+    "channel_4": (121920, "53e7214e1d216a68"),
+    "channel_8": (236608, "8b3fc6c69b72de9b"),
+    "int4_token": (517184, "fff48e3c9ad2e77b"),
+    "int8_token": (230464, "aabcbc228d1b0ee3"),
+    "int8_token_keep": (574528, "6f7852e159488c62"),
+    "mixed_int2_int8": (144448, "c1e854f4598cae86"),
+    "mixed_int4_int8": (173120, "9fea4432e6d76a0c"),
+    "mixed_mxfp4_mxfp8": (179264, "6b22e50680302847"),
+    "mixed_rgroup_int8": (186448, "deaeac663805b663"),
+    "mxfp4": (121920, "5c658c6ec1c707ad"),
+    "mxfp4_keep": (519744, "e1df63008ca1bf20"),
+    "mxfp8": (236608, "9f69368d50b1cc8d"),
+    "passthrough": (917568, "9565e5c72b2b360c"),
+    "ref_int4_global": (516176, "0b749fe758cea6cf"),
+    "rgroup": (141392, "9adc7787e6ad8fa1"),
+}
+
+
+def test_wire_format_fingerprints():
+    import hashlib
+    from llm_inference_in_distributed_edge_networks_amd.codec import wire as W
+    torch.manual_seed(0)
+    B, S, H = 2, 128, 896
+    x = (torch.randn(B * S, H) * torch.logspace(-2, 2, H)).float()
+    imp = torch.rand(B, S)
+    for name, (n, h) in WIRE_FINGERPRINTS.items():
+        spec = W.CODECS[name]
+        if W.needs_plan(spec):
+            spec = W.with_plan(spec, (2, 4, 8, 4, 4, 2, 8, 4, 4, 4, 2, 8, 4, 4))
+        msg, _ = W.encode(x, spec, B, S, 0.5, imp)
+        assert msg.numel() == n and hashlib.sha1(msg.numpy().tobytes()).hexdigest()[:16] == h, name
