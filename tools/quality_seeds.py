@@ -65,7 +65,7 @@ def main():
     out += table("last_row_beats_column_mean", "last_row beats the column mean: log PPL(column-mean) - log PPL(last_row),"
                  " Q1", ["layer", "ratio"], lambda x: x["verdict"] == "a worse")
     out += table("one_scale_collapse_at_ratio_1", "One-scale collapse at ratio 1: log PPL(r=1) - log PPL(r=0), last_row,"
-                 " Q1 (reference: x23 at L22)", ["layer"], lambda x: x["verdict"] == "a worse" and x["rel"] > 1.0)
+                 " Q1 (reference, BASELINE.md: 13.3 -> 382 at L22, 8.7e6 at L3)", ["layer"], lambda x: x["verdict"] == "a worse" and x["rel"] > 1.0)
 
     # mechanism: the one-scale damage against the boundary's outlier statistics, every (seed, layer)
     pts = []
