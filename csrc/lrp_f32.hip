@@ -70,16 +70,18 @@ __device__ __forceinline__ float gelu_ratio(float x) { return fabsf(x) > 1e-6f ?
 // D and per-(window, head) relevance.  o, dO token-major fp32 [B*S, Hq*64]; D [B,Hq,S]; rel [B,Hq].
 __global__ __launch_bounds__(256) void lrp_attn_delta_f32_kernel(const float* __restrict__ o,
                                                                  const float* __restrict__ dO, float* __restrict__ D,
-                                                                 float* __restrict__ rel, int Hq, int S) {
+                                                                 float* __restrict__ rel, int Hq, int S,
+                                                                 float* __restrict__ dmax) {
   // 16 lanes per token row (4 consecutive values each: every load instruction reads 4 whole 256-byte rows), the
   // row's dot product reduced over its 16 lanes by xor shuffles
   __shared__ float red[4];
   const int bh = blockIdx.x, b = bh / Hq, h = bh - b * Hq;
   const int sub = threadIdx.x & 15, r0 = threadIdx.x >> 4;
-  float tot = 0.f;
+  float tot = 0.f, mx = 0.f;
   for (int i = r0; i < S; i += 16) {
     const size_t off = ((size_t)b * S + i) * (size_t)(Hq * 64) + h * 64 + sub * 4;
     const f32x4_t a = *(const f32x4_t*)(o + off), d = *(const f32x4_t*)(dO + off);
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(d[0]), fabsf(d[1])), fmaxf(fabsf(d[2]), fabsf(d[3]))));
     float s = fmaf(a[0], d[0], fmaf(a[1], d[1], fmaf(a[2], d[2], a[3] * d[3])));
 #pragma unroll
     for (int x = 1; x < 16; x <<= 1) s += __shfl_xor(s, x, 64);
@@ -91,6 +93,11 @@ __global__ __launch_bounds__(256) void lrp_attn_delta_f32_kernel(const float* __
   }
   tot = block_sum<256>(tot, red);
   if (threadIdx.x == 0) rel[bh] = tot;
+  if (dmax) {   // (uniform branch: every thread takes part in the reduction)
+    __syncthreads();
+    mx = block_max<256>(mx, red);
+    if (threadIdx.x == 0) dmax[bh] = mx;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -423,6 +430,285 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __rest
     float* o = dq + (((size_t)b * Hq + h) * S + qi) * 64;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = 0.5f * acc[dt];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The same two sweeps on scaled fp16 planes ("h3", the forward attention's scheme): every operand is scaled by a
+// power of two and split into two fp16 planes, and each product is the three plane products lo x hi + hi x lo + hi x
+// hi on v_mfma_f32_16x16x32_f16 - half the MFMAs of the six-product bf16 split, two planes to stage instead of three,
+// and a 3-VALU split per value pair.  The scales keep every plane inside the fp16 range:
+//   q, k, v  sq, sk, sv: the forward attention's model bounds (s |x| <= 2^15, models/model.py h3 scales)
+//   dO       so = 2^(15 - E) from the max |dO| over the kv head's q heads (the delta kernel's per-head maxima)
+//   P        sp = 2^14 (P <= 1)
+//   dS       sd = so sv 2^-21: |dS| <= |P| (|dA| / 2 + |D|) <= 64 max|dO| max|v| < 2^15 / sd
+// Values far below their scale keep an absolute error of ~2^-25 / s (fp16's subnormal step): relative to the largest
+// value of the same operand ~2^-40, where the bf16 planes kept fp32's relative precision on every element.
+namespace {
+constexpr int H3P = 32 * 64 * 2;   // one fp16 plane of a 32 x 64 tile (bytes)
+__device__ __forceinline__ f32x4_t mfma_f16r(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                0, 0, 0);
+}
+__device__ __forceinline__ f32x4_t h3dot(const bf16x8_t (&a)[2], const bf16x8_t (&b)[2], f32x4_t c) {
+  c = mfma_f16r(a[1], b[0], c);
+  c = mfma_f16r(a[0], b[1], c);
+  return mfma_f16r(a[0], b[0], c);
+}
+// s * v[0..7] as the two fp16 planes of one fragment
+__device__ __forceinline__ void split_frag_s(const float (&v)[8], float s, bf16x8_t (&p)[2]) {
+  u32x4_t H, L;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const u32x2_t t = split2h_pk(v[2 * e] * s, v[2 * e + 1] * s);
+    H[e] = t[0];
+    L[e] = t[1];
+  }
+  p[0] = __builtin_bit_cast(bf16x8_t, H);
+  p[1] = __builtin_bit_cast(bf16x8_t, L);
+}
+// x6_store's layout with two fp16 planes of s * x
+__device__ __forceinline__ void h3_store(const X6Regs& R, char* rm, float s) {
+  int r, c4;
+  x6_own(threadIdx.x, r, c4);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const u32x2_t t0 = split2h_pk(R.v[i][0] * s, R.v[i][1] * s), t1 = split2h_pk(R.v[i][2] * s, R.v[i][3] * s);
+    const int row = r + i;
+    const int off = row * 128 + (((c4 >> 1) ^ x6sw(row)) << 4) + (c4 & 1) * 8;
+    *(u32x2_t*)(rm + off) = u32x2_t{t0[0], t1[0]};
+    *(u32x2_t*)(rm + H3P + off) = u32x2_t{t0[1], t1[1]};
+  }
+}
+__device__ __forceinline__ void rm_frags_h(const char* img, int row, int chunk, bf16x8_t (&f)[2]) {
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * H3P + row * 128 + ((chunk ^ x6sw(row)) << 4));
+}
+__device__ __forceinline__ void tr_frags_h(const char* img, int dt, int g, int cl, bf16x8_t (&f)[2]) {
+  const int q = cl >> 2, p = cl & 3, ch = 2 * dt + (p >> 1);
+  const int r0 = 4 * g + q, r1 = 16 + 4 * g + q;
+  const int o0 = r0 * 128 + ((ch ^ x6sw(r0)) << 4) + (p & 1) * 8;
+  const int o1 = r1 * 128 + ((ch ^ x6sw(r1)) << 4) + (p & 1) * 8;
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl) {
+    typedef __attribute__((address_space(3))) x6s4_t lds_s4;
+    const x6s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * H3P + o0));
+    const x6s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * H3P + o1));
+    const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    f[pl] = __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+__device__ __forceinline__ void row_frags_h(const float* __restrict__ rowp, bf16x8_t (&f)[2][2], int g, float s) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const f32x4_t a = *(const f32x4_t*)(rowp + 32 * ks + 8 * g);
+    const f32x4_t b = *(const f32x4_t*)(rowp + 32 * ks + 8 * g + 4);
+    const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    split_frag_s(v, s, f[ks]);
+  }
+}
+// the dO scale of kv head hk of window b: 2^(15 - E) for the max over its G q heads' max |dO| = m 2^E
+__device__ __forceinline__ float dO_scale(const float* __restrict__ dmax, int b, int Hq, int hk, int G) {
+  float mx = 0.f;
+  for (int j = 0; j < G; ++j) mx = fmaxf(mx, dmax[(size_t)b * Hq + hk * G + j]);
+  float inv;
+  return row_pow2_scale(mx, inv);
+}
+}  // namespace
+
+template <bool GS>
+__global__ __launch_bounds__(256) void lrp_attn_dkdv_h3_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                               const float* __restrict__ v,
+                                                               const float* __restrict__ dO,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ D,
+                                                               const float* __restrict__ dmax, float* __restrict__ dk,
+                                                               float* __restrict__ dv, int B, int Hq, int Hkv, int S,
+                                                               float sq, float sk, float sv) {
+  __shared__ __attribute__((aligned(16))) char sQ[2 * H3P], sO[2 * H3P];
+  __shared__ float sL[32], sD[32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int G = Hq / Hkv, HH = GS ? Hkv : Hq, NH = GS ? G : 1;
+  const int kb = blockIdx.x / (B * HH);
+  const int bh = blockIdx.x % (B * HH), b = bh / HH, hx = bh - b * HH;
+  const int hk = GS ? hx : hx / G, h0 = GS ? hx * G : hx;
+  const int key = kb * 64 + wave * 16 + cl;
+  const int keyc = key < S ? key : S - 1;
+  const int wkey_max = kb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16 + 15;
+  const float so = dO_scale(dmax, b, Hq, hk, G);
+  const float sp = 16384.f, sd = so * sv * 0x1p-21f;
+  // P = 2^(sc c1 - lse log2 e), dS = P (da c2 - D): the product scales folded into c1, c2
+  const float c1 = 1.4426950408889634f / (sq * sk), c2 = 0.5f / (so * sv);
+  bf16x8_t kf[2][2], vf[2][2];
+  row_frags_h(k + (((size_t)b * Hkv + hk) * S + keyc) * 64, kf, g, sk);
+  row_frags_h(v + (((size_t)b * Hkv + hk) * S + keyc) * 64, vf, g, sv);
+  f32x4_t dka[4], dva[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int ntile = (S - kb * 64 + 31) / 32, nit = NH * ntile;
+  X6Regs rq, ro;
+  float nl = INFINITY, nd = 0.f;
+  auto fetch = [&](int it) {
+    const int hh = h0 + it / ntile, q0 = kb * 64 + 32 * (it % ntile);
+    x6_load(q + ((size_t)b * Hq + hh) * S * 64, 64, q0, S, rq);
+    x6_load(dO + (size_t)b * S * (Hq * 64) + hh * 64, (size_t)Hq * 64, q0, S, ro);
+    if (tid < 32) {
+      const int qi = q0 + tid;
+      nl = qi < S ? lse[((size_t)b * Hq + hh) * S + qi] * 1.4426950408889634f : INFINITY;
+      nd = qi < S ? D[((size_t)b * Hq + hh) * S + qi] : 0.f;
+    }
+  };
+  fetch(0);
+  for (int it = 0; it < nit; ++it) {
+    const int q0 = kb * 64 + 32 * (it % ntile);
+    __syncthreads();
+    h3_store(rq, sQ, sq);
+    h3_store(ro, sO, so);
+    if (tid < 32) sL[tid] = nl, sD[tid] = nd;
+    if (it + 1 < nit) fetch(it + 1);
+    __syncthreads();
+    float pv[8], dsv[8];
+    const bool full = q0 >= wkey_max && q0 + 32 <= S && wkey_max < S;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t qa[2], oa[2];
+        rm_frags_h(sQ, sub * 16 + cl, 4 * ks + g, qa);
+        rm_frags_h(sO, sub * 16 + cl, 4 * ks + g, oa);
+        sc = h3dot(qa, kf[ks], sc);
+        da = h3dot(oa, vf[ks], da);
+      }
+      if (full) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = sub * 16 + 4 * g + r;
+          const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], c1, -sL[ql]));
+          pv[4 * sub + r] = pr;
+          dsv[4 * sub + r] = pr * fmaf(da[r], c2, -sD[ql]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = sub * 16 + 4 * g + r, qi = q0 + ql;
+          const bool ok = qi < S && key <= qi && key < S;
+          const float pr = ok ? __builtin_amdgcn_exp2f(fmaf(sc[r], c1, -sL[ql])) : 0.f;
+          pv[4 * sub + r] = pr;
+          dsv[4 * sub + r] = pr * fmaf(da[r], c2, -sD[ql]);
+        }
+      }
+    }
+    bf16x8_t pf[2], dsf[2];
+    split_frag_s(pv, sp, pf);
+    split_frag_s(dsv, sd, dsf);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x8_t ob[2], qb[2];
+      tr_frags_h(sO, dt, g, cl, ob);
+      tr_frags_h(sQ, dt, g, cl, qb);
+      dva[dt] = h3dot(pf, ob, dva[dt]);
+      dka[dt] = h3dot(dsf, qb, dka[dt]);
+    }
+  }
+  float* dkh = dk + ((size_t)b * HH + hx) * S * 64;
+  float* dvh = dv + ((size_t)b * HH + hx) * S * 64;
+  const float fk = 0.5f / (sd * sq), fv = 0.5f / (sp * so);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int kr = kb * 64 + wave * 16 + g * 4 + r;
+    if (kr < S) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dkh[(size_t)kr * 64 + dt * 16 + cl] = fk * dka[dt][r];
+        dvh[(size_t)kr * 64 + dt * 16 + cl] = fv * dva[dt][r];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void lrp_attn_dq_h3_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                             const float* __restrict__ v, const float* __restrict__ dO,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ D,
+                                                             const float* __restrict__ dmax, float* __restrict__ dq,
+                                                             int B, int Hq, int Hkv, int S, float sq, float sk,
+                                                             float sv) {
+  __shared__ __attribute__((aligned(16))) char sK[2 * H3P], sV[2 * H3P];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int nqb = (S + 63) / 64;
+  const int qb = nqb - 1 - blockIdx.x / (B * Hq);
+  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, G = Hq / Hkv, hk = h / G;
+  const int qi = qb * 64 + wave * 16 + cl;
+  const int qic = qi < S ? qi : S - 1;
+  const int wq_min = qb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16;
+  const float so = dO_scale(dmax, b, Hq, hk, G);
+  const float sd = so * sv * 0x1p-21f;
+  const float c1 = 1.4426950408889634f / (sq * sk), c2 = 0.5f / (so * sv);
+  bf16x8_t qf[2][2], of[2][2];
+  row_frags_h(q + (((size_t)b * Hq + h) * S + qic) * 64, qf, g, sq);
+  row_frags_h(dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64, of, g, so);
+  const float lq = lse[((size_t)b * Hq + h) * S + qic] * 1.4426950408889634f;
+  const float dq_ = D[((size_t)b * Hq + h) * S + qic];
+  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
+  const float* vh = v + ((size_t)b * Hkv + hk) * S * 64;
+  f32x4_t acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int kend = min(S, qb * 64 + 64);
+  X6Regs rk, rv;
+  auto fetch = [&](int k0) {
+    x6_load(kh, 64, k0, S, rk);
+    x6_load(vh, 64, k0, S, rv);
+  };
+  fetch(0);
+  for (int k0 = 0; k0 < kend; k0 += 32) {
+    __syncthreads();
+    h3_store(rk, sK, sk);
+    h3_store(rv, sV, sv);
+    if (k0 + 32 < kend) fetch(k0 + 32);
+    __syncthreads();
+    const bool full = k0 + 31 <= wq_min && wq_min + 15 < S;
+    float dsv[8];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t ka[2], va[2];
+        rm_frags_h(sK, sub * 16 + cl, 4 * ks + g, ka);
+        rm_frags_h(sV, sub * 16 + cl, 4 * ks + g, va);
+        sc = h3dot(ka, qf[ks], sc);
+        da = h3dot(va, of[ks], da);
+      }
+      if (full) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          dsv[4 * sub + r] = __builtin_amdgcn_exp2f(fmaf(sc[r], c1, -lq)) * fmaf(da[r], c2, -dq_);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kj = k0 + sub * 16 + 4 * g + r;
+          const bool ok = qi < S && kj <= qi;
+          const float pr = ok ? __builtin_amdgcn_exp2f(fmaf(sc[r], c1, -lq)) : 0.f;
+          dsv[4 * sub + r] = pr * fmaf(da[r], c2, -dq_);
+        }
+      }
+    }
+    bf16x8_t dsf[2];
+    split_frag_s(dsv, sd, dsf);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x8_t kt[2];
+      tr_frags_h(sK, dt, g, cl, kt);
+      acc[dt] = h3dot(kt, dsf, acc[dt]);
+    }
+  }
+  if (qi < S) {
+    const float f = 0.5f / (sk * sd);
+    float* o = dq + (((size_t)b * Hq + h) * S + qi) * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = f * acc[dt];
   }
 }
 
@@ -852,7 +1138,7 @@ EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* 
   if (B <= 0 || S <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
   const int nb = (S + 63) / 64;
-  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
+  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S, nullptr);
   lrp_attn_dkdv_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
   lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
   return (int)hipGetLastError();
@@ -865,9 +1151,29 @@ EDGE_API int edge_lrp_attn_bwd_f32_gs(const float* q, const float* k, const floa
   if (B <= 0 || S <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
   const int nb = (S + 63) / 64;
-  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S);
+  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S, nullptr);
   lrp_attn_dkdv_x6_kernel<true><<<B * Hkv * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
   lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
+  return (int)hipGetLastError();
+}
+
+// The h3-plane sweeps (lrp_attn_dkdv_h3 / dq_h3): q, k, v at the forward attention's plane scales sq, sk, sv (powers
+// of two with s |x| <= 2^15); dmax [B * Hq] workspace (the per-head max |dO| the delta kernel writes).  gs: dk, dv as
+// the GQA group sums [B, Hkv, S, 64], else per-q-head partials.
+EDGE_API int edge_lrp_attn_bwd_h3(const float* q, const float* k, const float* v, const float* o, const float* dO,
+                                  const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, float* dmax,
+                                  int B, int Hq, int Hkv, int S, int gs, float sq, float sk, float sv, hipStream_t st) {
+  if (B <= 0 || S <= 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv || !dmax || !(sq > 0.f && sk > 0.f && sv > 0.f)) return (int)hipErrorInvalidValue;
+  const int nb = (S + 63) / 64;
+  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S, dmax);
+  if (gs)
+    lrp_attn_dkdv_h3_kernel<true><<<B * Hkv * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dmax, dk, dv, B, Hq, Hkv, S, sq,
+                                                                 sk, sv);
+  else
+    lrp_attn_dkdv_h3_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dmax, dk, dv, B, Hq, Hkv, S, sq,
+                                                                 sk, sv);
+  lrp_attn_dq_h3_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dmax, dq, B, Hq, Hkv, S, sq, sk, sv);
   return (int)hipGetLastError();
 }
 

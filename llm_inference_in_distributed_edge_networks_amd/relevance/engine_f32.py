@@ -190,8 +190,10 @@ class RelevanceEngineH3:
                 if not self.qwen:
                     dh2 = torch.zeros(B * S, H, dtype=dh2.dtype, device=dh2.device).index_copy_(0, rows, dh2)
             # dk, dv summed over each GQA group in the kernel where it can (else the per-q-head partials)
+            sc = m.h3_layer[i]   # the forward attention's plane scales: the sweeps run on the same scaled fp16 planes
             _, r, dq, dk, dv = ops.lrp_attn_bwd(sv["q"], sv["k"], sv["v"], sv["o"], dO, sv["lse"],
-                                                gqa_sum=ops.lrp_gqa_sum_native(sv["q"]))
+                                                gqa_sum=ops.lrp_gqa_sum_native(sv["q"]),
+                                                in_scales=(sc["att_q"], sc["att_k"], sc["o"]))
             rel[:, i] = r
             dqkv3, rinv_q = ops.lrp_rope_pack_h3(dq, dk, dv, m.cos, m.sin, B, S, Hq, Hkv, cfg.rotary_dim, m.q_scale,
                                                  post=sv["rs1"] if self.qwen else None)

@@ -101,16 +101,19 @@ def test_relevance_engine_gpu_vs_cpu(cfg):
 
 
 @pytest.mark.parametrize("B,Hq,Hkv,S", [(2, 14, 2, 512), (1, 8, 8, 200), (3, 4, 2, 96), (1, 2, 1, 37)])
-def test_lrp_attn_bwd_f32(B, Hq, Hkv, S):
-    """fp32 attention LRP backward vs the fp64 reference: fp32-rounding agreement of the bf16 matrix-core sweeps on
-    three-bf16-plane splits (six products)."""
-    _lrp_attn_bwd_f32_case(B, Hq, Hkv, S)
+@pytest.mark.parametrize("planes", ["x6", "h3"])
+def test_lrp_attn_bwd_f32(B, Hq, Hkv, S, planes):
+    """fp32 attention LRP backward vs the fp64 reference: fp32-rounding agreement of the matrix-core sweeps on three
+    bf16 planes (x6, six products) and on scaled fp16 planes (h3, three products, the engine's path)."""
+    _lrp_attn_bwd_f32_case(B, Hq, Hkv, S, planes == "h3")
 
 
-def test_lrp_attn_bwd_x6_dynamic_range():
-    """Gradients have no a-priori bound.  The bf16 planes carry fp32's exponent range (no scales), so every output is
-    exactly equivariant under a power-of-two scaling of dO (2^-40 and 2^+40: bit-identical after unscaling), and rows
-    of dO spread over 24 binades keep the fp32-level error of the unit-scale case."""
+@pytest.mark.parametrize("planes", ["x6", "h3"])
+def test_lrp_attn_bwd_dynamic_range(planes):
+    """Gradients have no a-priori bound.  x6: the bf16 planes carry fp32's exponent range (no scales); h3: dO's plane
+    scale is a power of two from its per-head maxima.  Either way every output is exactly equivariant under a
+    power-of-two scaling of dO (2^-40 and 2^+40: bit-identical after unscaling), and rows of dO spread over 80
+    binades keep the fp32-level error (on the global scale) of the unit-scale case."""
     B, Hq, Hkv, S = 1, 4, 2, 160
     f = torch.float32
     q = rnd(B, Hq, S, 64, s=0.5, seed=11, dtype=f) * 0.125
@@ -122,20 +125,21 @@ def test_lrp_attn_bwd_x6_dynamic_range():
     o, lse = R.attention(q, k, vt, S, need_lse=True)
     dev = [t.to(DEV) for t in (q, k, v, o)]
     lse_d = lse.float().contiguous().to(DEV)
-    base = ops.lrp_attn_bwd(*dev, dO.to(DEV), lse_d)
+    sc = tuple(R.h3_scale(t.abs().max().item()) for t in (q, k, v)) if planes == "h3" else None
+    base = ops.lrp_attn_bwd(*dev, dO.to(DEV), lse_d, in_scales=sc)
     for e in (-40, 40):
-        got = ops.lrp_attn_bwd(*dev, (dO * 2.0 ** e).to(DEV), lse_d)
+        got = ops.lrp_attn_bwd(*dev, (dO * 2.0 ** e).to(DEV), lse_d, in_scales=sc)
         for n, g_, b_ in zip(["D", "rel", "dq", "dk", "dv"], got, base):
             assert torch.equal(g_ * 2.0 ** -e, b_), f"{n}: not equivariant under dO x 2^{e}"
     # mixed magnitudes: dO rows over 2^-40 .. 2^40; the error measured against fp64 on the global scale
     dOm = dO * (2.0 ** torch.linspace(-40, 40, B * S).round()).view(-1, 1)
     ref = R.lrp_attn_bwd(q.double(), k.double(), v.double(), o.double(), dOm.double(), lse.double())
-    got = ops.lrp_attn_bwd(*dev, dOm.to(DEV), lse_d)
+    got = ops.lrp_attn_bwd(*dev, dOm.to(DEV), lse_d, in_scales=sc)
     for n, g_, r_ in zip(["D", "rel", "dq", "dk", "dv"], got, ref):
         assert rel_err(g_, r_) < 2e-6, n
 
 
-def _lrp_attn_bwd_f32_case(B, Hq, Hkv, S):
+def _lrp_attn_bwd_f32_case(B, Hq, Hkv, S, h3=False):
     f = torch.float32
     q = rnd(B, Hq, S, 64, s=0.5, seed=1, dtype=f) * 0.125
     k = rnd(B, Hkv, S, 64, s=0.5, seed=2, dtype=f)
@@ -145,13 +149,15 @@ def _lrp_attn_bwd_f32_case(B, Hq, Hkv, S):
     vt[..., :S] = v.transpose(-1, -2)
     o, lse = R.attention(q, k, vt, S, need_lse=True)
     ref = R.lrp_attn_bwd(q.double(), k.double(), v.double(), o.double(), dO.double(), lse.double())
-    got = ops.lrp_attn_bwd(*(t.to(DEV) for t in (q, k, v, o, dO)), lse.float().contiguous().to(DEV))
+    sc = tuple(R.h3_scale(t.abs().max().item()) for t in (q, k, v)) if h3 else None
+    got = ops.lrp_attn_bwd(*(t.to(DEV) for t in (q, k, v, o, dO)), lse.float().contiguous().to(DEV), in_scales=sc)
     for n, g_, r_ in zip(["D", "rel", "dq", "dk", "dv"], got, ref):
         assert g_.shape == r_.shape and g_.dtype == torch.float32, n
         e = rel_err(g_, r_)
         assert e < 2e-6, f"{n}: rel err {e:.3g}"
     # dk, dv summed over each GQA group (the x6 sweeps: one workgroup per kv head sweeping its q heads)
-    got = ops.lrp_attn_bwd(*(t.to(DEV) for t in (q, k, v, o, dO)), lse.float().contiguous().to(DEV), gqa_sum=True)
+    got = ops.lrp_attn_bwd(*(t.to(DEV) for t in (q, k, v, o, dO)), lse.float().contiguous().to(DEV), gqa_sum=True,
+                           in_scales=sc)
     for n, g_, r_ in zip(["dk", "dv"], got[3:], ref[3:]):
         r_ = r_.view(B, Hkv, Hq // Hkv, S, 64).sum(2)
         assert g_.shape == r_.shape, n
