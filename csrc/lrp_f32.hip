@@ -8,10 +8,10 @@
 //
 //   lrp_attn_delta_f32  D[b,h,i] = 0.5 dO_i . O_i (uniform rule on A V) and the per-(window, head) relevance
 //                       rel[b,h] = sum_i D[b,h,i] = sum_{ij} A_ij dA_ij - the reference hook's quantity.
-//   lrp_attn_dkdv_x6    dK, dV per (window, q head or kv-head group, 64-key block): P recomputed from Q K^T and the
+//   lrp_attn_dkdv_h3    dK, dV per (window, q head or kv-head group, 64-key block): P recomputed from Q K^T and the
 //                       forward LSE, dA = 0.5 dO V^T, dS = P (dA - D), dV = 0.5 P^T dO, dK = 0.5 dS^T Q.
-//   lrp_attn_dq_x6      dQ = 0.5 dS K per (window, q head, 64-query block).  Separate sweeps: no atomics.
-//                       Products on three-bf16-plane splits (exact fp32 operands, six products).
+//   lrp_attn_dq_h3      dQ = 0.5 dS K per (window, q head, 64-query block).  Separate sweeps: no atomics.
+//                       Products on scaled two-fp16-plane splits (three products).
 //   *_h3 rule kernels   the LRP rules whose output feeds a backward GEMM (SwiGLU / GELU identity rule with the
 //                       uniform product rule, inverse RoPE + GQA sum) write it directly as an h3 activation with a
 //                       per-row power-of-two scale: gradients have no a-priori bound, so each row is scaled to put
@@ -101,66 +101,42 @@ __global__ __launch_bounds__(256) void lrp_attn_delta_f32_kernel(const float* __
 }
 
 // ---------------------------------------------------------------------------------------------
-// The dK / dV and dQ sweeps on the bf16 matrix cores ("x6", the split of the forward's first fp32 attention): every
-// operand - q, k, v, dO, and the in-register P and dS - is split into three bf16 planes x = x0 + x1 + x2 (24
-// significant bits, exact: common.h split3), and each product is the six plane products with i + j <= 2, small terms
-// first, on v_mfma_f32_16x16x32_bf16 (1024 FLOP per cycle against the f32 MFMA's 64: 2.7x per useful FLOP over the round-3 v_mfma_f32_16x16x4_f32 sweeps).  No
-// scales are needed (bf16 has fp32's exponent range), so the gradients keep their dynamic range with no bounds.
+// The dK / dV and dQ sweeps on scaled fp16 planes ("h3", the forward attention's scheme): every operand - q, k, v,
+// dO, and the in-register P and dS - is scaled by a power of two and split into two fp16 planes, and each product is
+// the three plane products lo x hi + hi x lo + hi x hi on v_mfma_f32_16x16x32_f16.  The scales keep every plane inside
+// the fp16 range:
+//   q, k, v  sq, sk, sv: the forward attention's model bounds (s |x| <= 2^15, models/model.py h3 scales)
+//   dO       so = 2^(15 - E) from the max |dO| over the kv head's q heads (the delta kernel's per-head maxima)
+//   P        sp = 2^14 (P <= 1)
+//   dS       sd = so sv 2^-21: |dS| <= |P| (|dA| / 2 + |D|) <= 64 max|dO| max|v| < 2^15 / sd
+// Values far below their scale keep an absolute error of ~2^-25 / s (fp16's subnormal step): ~2^-40 relative to the
+// largest value of the same operand.  Round 4's form split every operand into three bf16 planes instead (six
+// products, no scales, fp32's exponent range on every element): 1.34x the time of these sweeps
+// (profiles/r05/lrp_attn_h3/probe.log), removed.
 //
 // 16x16x32 fragments: lane l holds A[row l&15][k 8(l>>4)+j] and B[k 8(l>>4)+j][col l&15], C[row 4(l>>4)+r][col l&15].
 // A score tile computed with the query (dkdv) or the key (dq) on the C rows puts 4 rows of a 16-row block on a lane;
 // two such blocks give the lane the 8 k-slots of a 32-deep reduction over those rows, in the order
 // slot 8g + j <-> row perm(g, j) = (j < 4 ? 4g + j : 16 + 4g + j - 4): the probabilities / dS are then the lane's own
-// A / B fragments, and the other operand is read from its row-major LDS image in that row order by transposing reads.
+// A / B fragments, and the other operand is read from its row-major LDS image in that row order by transposing reads
+// (ds_read_b64_tr_b16).  A 32 x 64 tile is staged row-major only ([32][64] per plane, 16-byte chunks swizzled):
+// thread t owns the row pair 2 rp, 2 rp + 1 and columns 4 c4 .. +3 (tile_own): two 16-byte global loads (tile_load,
+// issued a tile ahead so their latency hides under the previous tile's MFMAs) and one 8-byte write per row and plane.
 namespace {
-constexpr int X6P = 32 * 64 * 2;   // one bf16 plane of a 32 x 64 tile (bytes)
-
 // 16-byte chunk swizzle of the row-major images (128-byte rows): conflict-free for the b64 staging writes, the b128
 // row-fragment reads and the ds_read_b64_tr_b16 transposed reads alike (searched over the XOR maps of the row bits
 // with the bank model of MI355X_MICROARCH §LDS; the plain (r >> 1) & 7 is 2-way on the writes and the tr reads)
-__device__ __forceinline__ int x6sw(int r) { return (((r >> 1) & 1) << 1) | ((((r >> 1) ^ (r >> 2)) & 1) << 2); }
-__device__ __forceinline__ f32x4_t mfma_bf16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-// exp(d) for d = score - lse <= ~0 as v_exp_f32(d log2 e): the rounding of the product moves the exponent by
-// |d| 2^-24, so the error relative to the row's largest probability stays below 2^-24 / e (the IEEE expf's range
-// reduction was ~10 VALU per value, a fifth of the sweeps' VALU).  d = -inf (masked / padded rows) gives 0.
-__device__ __forceinline__ float x6_exp(float d) { return __builtin_amdgcn_exp2f(d * 1.4426950408889634f); }
-__device__ __forceinline__ f32x4_t x6dot(const bf16x8_t (&a)[3], const bf16x8_t (&b)[3], f32x4_t c) {
-  c = mfma_bf16(a[2], b[0], c);
-  c = mfma_bf16(a[0], b[2], c);
-  c = mfma_bf16(a[1], b[1], c);
-  c = mfma_bf16(a[1], b[0], c);
-  c = mfma_bf16(a[0], b[1], c);
-  return mfma_bf16(a[0], b[0], c);
-}
-__device__ __forceinline__ void split3_frag(const float (&v)[8], bf16x8_t (&p)[3]) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    float p0, p1, p2;
-    split3(v[e], p0, p1, p2);
-    p[0][e] = (__bf16)p0;
-    p[1][e] = (__bf16)p1;
-    p[2][e] = (__bf16)p2;
-  }
-}
-
-// A 32 x 64 fp32 tile staged as three bf16 planes, row-major only ([32][64], 16-byte chunks swizzled by x6sw(row)):
-// A / B fragments by one ds_read_b128 (rm_frags), and the fragments of a reduction over the tile's rows straight from
-// the same image by the hardware-transposing ds_read_b64_tr_b16 (tr_frags).  Thread t owns the row pair 2 rp, 2 rp + 1
-// and columns 4 c4 .. +3 (x6_own): two 16-byte global loads (x6_load, issued a tile ahead so their latency hides under
-// the previous tile's MFMAs) and one 8-byte write per row and plane (x6_store).  History: the first version also wrote
-// a transposed image ([64][32 slots], 4-byte bf16 pairs) whose writes were 16-way bank conflicts; conflict-free, it
-// still cost 24 of the 36 staging writes per thread and tile.
-struct X6Regs { f32x4_t v[2]; };
-__device__ __forceinline__ void x6_own(int t, int& r, int& c4) {
+__device__ __forceinline__ int tile_sw(int r) { return (((r >> 1) & 1) << 1) | ((((r >> 1) ^ (r >> 2)) & 1) << 2); }
+typedef short s4_t __attribute__((ext_vector_type(4)));
+struct TileRegs { f32x4_t v[2]; };
+__device__ __forceinline__ void tile_own(int t, int& r, int& c4) {
   const int w = t >> 6, l = t & 63, q = (l >> 3) & 3;
   r = 2 * (2 * w + (q & 1) + 8 * (q >> 1));
   c4 = (l & 7) + 8 * (l >> 5);
 }
-__device__ __forceinline__ void x6_load(const float* __restrict__ src, size_t ld, int row0, int nrows, X6Regs& R) {
+__device__ __forceinline__ void tile_load(const float* __restrict__ src, size_t ld, int row0, int nrows, TileRegs& R) {
   int r, c4;
-  x6_own(threadIdx.x, r, c4);
+  tile_own(threadIdx.x, r, c4);
   const int c = 4 * c4;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -168,283 +144,6 @@ __device__ __forceinline__ void x6_load(const float* __restrict__ src, size_t ld
     R.v[i] = gr < nrows ? *(const f32x4_t*)(src + (size_t)gr * ld + c) : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
 }
-__device__ __forceinline__ void x6_store(const X6Regs& R, char* rm) {
-  int r, c4;
-  x6_own(threadIdx.x, r, c4);
-  uint32_t w[2][3][2];   // [row][plane][column pair]: packed bf16 pairs
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; e += 2) {
-      float a0, a1, a2, b0, b1, b2;
-      split3(R.v[i][e], a0, a1, a2);
-      split3(R.v[i][e + 1], b0, b1, b2);
-      w[i][0][e >> 1] = pack_bf2(a0, b0);
-      w[i][1][e >> 1] = pack_bf2(a1, b1);
-      w[i][2][e >> 1] = pack_bf2(a2, b2);
-    }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = r + i;
-    const int off = row * 128 + (((c4 >> 1) ^ x6sw(row)) << 4) + (c4 & 1) * 8;
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) *(u32x2_t*)(rm + pl * X6P + off) = u32x2_t{w[i][pl][0], w[i][pl][1]};
-  }
-}
-__device__ __forceinline__ void rm_frags(const char* img, int row, int chunk, bf16x8_t (&f)[3]) {
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * X6P + row * 128 + ((chunk ^ x6sw(row)) << 4));
-}
-// B (or A) fragment of a reduction over the image's 32 rows in the permuted k order (slot 8g + j <-> row perm(g, j)), for columns 16 dt .. + 15: lane
-// (cl, g) gets column 16 dt + cl of rows 4g .. 4g + 3 (slots 8g .. 8g + 3) and 16 + 4g .. + 3 (slots 8g + 4 .. + 7),
-// two ds_read_b64_tr_b16 per plane (lane 4q + p of a 16-lane group addresses row q of the 4-row block, columns
-// 4p .. 4p + 3; every lane of the wave must execute it).
-typedef short x6s4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void tr_frags(const char* img, int dt, int g, int cl, bf16x8_t (&f)[3]) {
-  const int q = cl >> 2, p = cl & 3, ch = 2 * dt + (p >> 1);
-  const int r0 = 4 * g + q, r1 = 16 + 4 * g + q;
-  const int o0 = r0 * 128 + ((ch ^ x6sw(r0)) << 4) + (p & 1) * 8;
-  const int o1 = r1 * 128 + ((ch ^ x6sw(r1)) << 4) + (p & 1) * 8;
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl) {
-    typedef __attribute__((address_space(3))) x6s4_t lds_s4;
-    const x6s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * X6P + o0));
-    const x6s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * X6P + o1));
-    const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    f[pl] = __builtin_bit_cast(bf16x8_t, v);
-  }
-}
-// the lane's 8 values of row `row` (its key / query), columns 8 kg + 32 ks .. +7, split into planes
-__device__ __forceinline__ void row_frags(const float* __restrict__ rowp, bf16x8_t (&f)[2][3], int g) {
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const f32x4_t a = *(const f32x4_t*)(rowp + 32 * ks + 8 * g);
-    const f32x4_t b = *(const f32x4_t*)(rowp + 32 * ks + 8 * g + 4);
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = a[e], v[4 + e] = b[e];
-    split3_frag(v, f[ks]);
-  }
-}
-}  // namespace
-
-// dK, dV partials per q head: q [B,Hq,S,64] (pre-scaled), k, v [B,Hkv,S,64], dO token-major [B*S, Hq*64],
-// lse/D [B,Hq,S] -> dk, dv [B,Hq,S,64] (the GQA group sum happens in the rope/pack kernel).  Workgroup = (b, q head, 64-key
-// block), heaviest first; wave w owns keys kb 64 + 16 w + cl.  Per 32-query tile: S = Q K^T and dA = dO V^T with the
-// query on the C rows (the lane's K / V planes in registers for the whole sweep), P = exp(S - lse), dS = P (dA/2 - D),
-// then dV += P^T dO and dK += dS^T Q over the tile's 32 queries (P / dS the lane's A fragments, dO / Q from the
-// row-major images by transposing reads).  GS: one workgroup per (b, kv head, key block) sweeps the G q heads
-// of its group and writes the group's SUM (dk, dv [B, Hkv, S, 64]; the per-q-head partials were 7x the bytes, written
-// here and re-read by the RoPE pack).  History: double-buffered staging (one barrier per tile) measured equal and was
-// dropped (profiles/r04o/ab.txt).
-template <bool GS>
-__global__ __launch_bounds__(256) void lrp_attn_dkdv_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                               const float* __restrict__ v,
-                                                               const float* __restrict__ dO,
-                                                               const float* __restrict__ lse,
-                                                               const float* __restrict__ D, float* __restrict__ dk,
-                                                               float* __restrict__ dv, int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) char sQ[3 * X6P], sO[3 * X6P];
-  __shared__ float sL[32], sD[32];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int G = Hq / Hkv, HH = GS ? Hkv : Hq, NH = GS ? G : 1;   // GS: the workgroup sweeps its kv head's G q heads
-  const int kb = blockIdx.x / (B * HH);
-  const int bh = blockIdx.x % (B * HH), b = bh / HH, hx = bh - b * HH;
-  const int hk = GS ? hx : hx / G, h0 = GS ? hx * G : hx;
-  const int key = kb * 64 + wave * 16 + cl;
-  const int keyc = key < S ? key : S - 1;
-  const int wkey_max = kb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16 + 15;   // the wave's last key (scalar)
-  bf16x8_t kf[2][3], vf[2][3];
-  row_frags(k + (((size_t)b * Hkv + hk) * S + keyc) * 64, kf, g);
-  row_frags(v + (((size_t)b * Hkv + hk) * S + keyc) * 64, vf, g);
-  f32x4_t dka[4], dva[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  // (q head, 32-query tile) pairs in one flat sweep, so the prefetch crosses from one q head to the next
-  const int ntile = (S - kb * 64 + 31) / 32, nit = NH * ntile;
-  X6Regs rq, ro;
-  float nl = INFINITY, nd = 0.f;
-  auto fetch = [&](int it) {   // pair it's global values into registers (a tile ahead)
-    const int hh = h0 + it / ntile, q0 = kb * 64 + 32 * (it % ntile);
-    x6_load(q + ((size_t)b * Hq + hh) * S * 64, 64, q0, S, rq);
-    x6_load(dO + (size_t)b * S * (Hq * 64) + hh * 64, (size_t)Hq * 64, q0, S, ro);
-    if (tid < 32) {
-      const int qi = q0 + tid;
-      nl = qi < S ? lse[((size_t)b * Hq + hh) * S + qi] : INFINITY;
-      nd = qi < S ? D[((size_t)b * Hq + hh) * S + qi] : 0.f;
-    }
-  };
-  fetch(0);
-  for (int it = 0; it < nit; ++it) {
-    const int q0 = kb * 64 + 32 * (it % ntile);
-    __syncthreads();
-    x6_store(rq, sQ);
-    x6_store(ro, sO);
-    if (tid < 32) sL[tid] = nl, sD[tid] = nd;
-    if (it + 1 < nit) fetch(it + 1);
-    __syncthreads();
-    const char* bQ = sQ;
-    const char* bO = sO;
-    const float* bL = sL;
-    const float* bD = sD;
-    float pv[8], dsv[8];   // k-slot order: j < 4 -> sub-block 0 row 4g + j, j >= 4 -> sub-block 1 row 4g + j - 4
-    // no masking on tiles wholly below the diagonal of this wave's keys (a wave-uniform branch)
-    const bool full = q0 >= wkey_max && q0 + 32 <= S && wkey_max < S;
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t qa[3], oa[3];
-        rm_frags(bQ, sub * 16 + cl, 4 * ks + g, qa);
-        rm_frags(bO, sub * 16 + cl, 4 * ks + g, oa);
-        sc = x6dot(qa, kf[ks], sc);
-        da = x6dot(oa, vf[ks], da);
-      }
-      if (full) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = sub * 16 + 4 * g + r;
-          const float pr = x6_exp(sc[r] - bL[ql]);
-          pv[4 * sub + r] = pr;
-          dsv[4 * sub + r] = pr * (0.5f * da[r] - bD[ql]);
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = sub * 16 + 4 * g + r, qi = q0 + ql;
-          const bool ok = qi < S && key <= qi && key < S;
-          const float pr = ok ? x6_exp(sc[r] - bL[ql]) : 0.f;
-          pv[4 * sub + r] = pr;
-          dsv[4 * sub + r] = pr * (0.5f * da[r] - bD[ql]);
-        }
-      }
-    }
-    bf16x8_t pf[3], dsf[3];
-    split3_frag(pv, pf);
-    split3_frag(dsv, dsf);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      bf16x8_t ob[3], qb[3];
-      tr_frags(bO, dt, g, cl, ob);
-      tr_frags(bQ, dt, g, cl, qb);
-      dva[dt] = x6dot(pf, ob, dva[dt]);
-      dka[dt] = x6dot(dsf, qb, dka[dt]);
-    }
-  }
-  // C[row = key 16w + 4g + r][col = d 16dt + cl]; GS: the kv head's sum over its q heads, else the q head's partial
-  float* dkh = dk + ((size_t)b * HH + hx) * S * 64;
-  float* dvh = dv + ((size_t)b * HH + hx) * S * 64;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int kr = kb * 64 + wave * 16 + g * 4 + r;
-    if (kr < S) {
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dkh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dka[dt][r];
-        dvh[(size_t)kr * 64 + dt * 16 + cl] = 0.5f * dva[dt][r];
-      }
-    }
-  }
-}
-
-// dQ (inputs as lrp_attn_dkdv_x6_kernel; dq [B,Hq,S,64]).  Workgroup = (b, h, 64-query block), heaviest (last) first; wave
-// w owns queries qb 64 + 16 w + cl.  Per 32-key tile: S^T = K Q^T and dA^T = V dO^T with the key on the C rows (the
-// lane's Q / dO planes in registers), dS^T = P^T (dA^T/2 - D), then dQ^T += K^T dS^T over the tile's 32 keys.
-__global__ __launch_bounds__(256) void lrp_attn_dq_x6_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                             const float* __restrict__ v, const float* __restrict__ dO,
-                                                             const float* __restrict__ lse,
-                                                             const float* __restrict__ D, float* __restrict__ dq,
-                                                             int B, int Hq, int Hkv, int S) {
-  __shared__ __attribute__((aligned(16))) char sK[3 * X6P], sV[3 * X6P];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int nqb = (S + 63) / 64;
-  const int qb = nqb - 1 - blockIdx.x / (B * Hq);
-  const int bh = blockIdx.x % (B * Hq), b = bh / Hq, h = bh - b * Hq, hk = h / (Hq / Hkv);
-  const int qi = qb * 64 + wave * 16 + cl;
-  const int qic = qi < S ? qi : S - 1;
-  const int wq_min = qb * 64 + __builtin_amdgcn_readfirstlane(wave) * 16;   // the wave's first query (scalar)
-  bf16x8_t qf[2][3], of[2][3];
-  row_frags(q + (((size_t)b * Hq + h) * S + qic) * 64, qf, g);
-  row_frags(dO + ((size_t)b * S + qic) * (size_t)(Hq * 64) + h * 64, of, g);
-  const float lq = lse[((size_t)b * Hq + h) * S + qic];
-  const float dq_ = D[((size_t)b * Hq + h) * S + qic];
-  const float* kh = k + ((size_t)b * Hkv + hk) * S * 64;
-  const float* vh = v + ((size_t)b * Hkv + hk) * S * 64;
-  f32x4_t acc[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int kend = min(S, qb * 64 + 64);
-  X6Regs rk, rv;
-  auto fetch = [&](int k0) {
-    x6_load(kh, 64, k0, S, rk);
-    x6_load(vh, 64, k0, S, rv);
-  };
-  fetch(0);
-  for (int k0 = 0; k0 < kend; k0 += 32) {
-    __syncthreads();
-    x6_store(rk, sK);
-    x6_store(rv, sV);
-    if (k0 + 32 < kend) fetch(k0 + 32);   // the next key tile's values under this tile's MFMAs
-    __syncthreads();
-    const char* bK = sK;
-    const char* bV = sV;
-    // no masking on key tiles wholly at or below this wave's first query (a wave-uniform branch)
-    const bool full = k0 + 31 <= wq_min && wq_min + 15 < S;
-    float dsv[8];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      f32x4_t sc = {0.f, 0.f, 0.f, 0.f}, da = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t ka[3], va[3];
-        rm_frags(bK, sub * 16 + cl, 4 * ks + g, ka);
-        rm_frags(bV, sub * 16 + cl, 4 * ks + g, va);
-        sc = x6dot(ka, qf[ks], sc);
-        da = x6dot(va, of[ks], da);
-      }
-      if (full) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dsv[4 * sub + r] = x6_exp(sc[r] - lq) * (0.5f * da[r] - dq_);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int kj = k0 + sub * 16 + 4 * g + r;
-          const bool ok = qi < S && kj <= qi;
-          const float pr = ok ? x6_exp(sc[r] - lq) : 0.f;
-          dsv[4 * sub + r] = pr * (0.5f * da[r] - dq_);
-        }
-      }
-    }
-    bf16x8_t dsf[3];
-    split3_frag(dsv, dsf);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      bf16x8_t kt[3];
-      tr_frags(bK, dt, g, cl, kt);
-      acc[dt] = x6dot(kt, dsf, acc[dt]);
-    }
-  }
-  // acc[dt][r] = dQ^T[d = 16dt + 4g + r][query qi]
-  if (qi < S) {
-    float* o = dq + (((size_t)b * Hq + h) * S + qi) * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(o + dt * 16 + g * 4) = 0.5f * acc[dt];
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// The same two sweeps on scaled fp16 planes ("h3", the forward attention's scheme): every operand is scaled by a
-// power of two and split into two fp16 planes, and each product is the three plane products lo x hi + hi x lo + hi x
-// hi on v_mfma_f32_16x16x32_f16 - half the MFMAs of the six-product bf16 split, two planes to stage instead of three,
-// and a 3-VALU split per value pair.  The scales keep every plane inside the fp16 range:
-//   q, k, v  sq, sk, sv: the forward attention's model bounds (s |x| <= 2^15, models/model.py h3 scales)
-//   dO       so = 2^(15 - E) from the max |dO| over the kv head's q heads (the delta kernel's per-head maxima)
-//   P        sp = 2^14 (P <= 1)
-//   dS       sd = so sv 2^-21: |dS| <= |P| (|dA| / 2 + |D|) <= 64 max|dO| max|v| < 2^15 / sd
-// Values far below their scale keep an absolute error of ~2^-25 / s (fp16's subnormal step): relative to the largest
-// value of the same operand ~2^-40, where the bf16 planes kept fp32's relative precision on every element.
-namespace {
 constexpr int H3P = 32 * 64 * 2;   // one fp16 plane of a 32 x 64 tile (bytes)
 __device__ __forceinline__ f32x4_t mfma_f16r(bf16x8_t a, bf16x8_t b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
@@ -467,33 +166,33 @@ __device__ __forceinline__ void split_frag_s(const float (&v)[8], float s, bf16x
   p[0] = __builtin_bit_cast(bf16x8_t, H);
   p[1] = __builtin_bit_cast(bf16x8_t, L);
 }
-// x6_store's layout with two fp16 planes of s * x
-__device__ __forceinline__ void h3_store(const X6Regs& R, char* rm, float s) {
+// the staged tile's two fp16 planes of s * x
+__device__ __forceinline__ void h3_store(const TileRegs& R, char* rm, float s) {
   int r, c4;
-  x6_own(threadIdx.x, r, c4);
+  tile_own(threadIdx.x, r, c4);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const u32x2_t t0 = split2h_pk(R.v[i][0] * s, R.v[i][1] * s), t1 = split2h_pk(R.v[i][2] * s, R.v[i][3] * s);
     const int row = r + i;
-    const int off = row * 128 + (((c4 >> 1) ^ x6sw(row)) << 4) + (c4 & 1) * 8;
+    const int off = row * 128 + (((c4 >> 1) ^ tile_sw(row)) << 4) + (c4 & 1) * 8;
     *(u32x2_t*)(rm + off) = u32x2_t{t0[0], t1[0]};
     *(u32x2_t*)(rm + H3P + off) = u32x2_t{t0[1], t1[1]};
   }
 }
 __device__ __forceinline__ void rm_frags_h(const char* img, int row, int chunk, bf16x8_t (&f)[2]) {
 #pragma unroll
-  for (int pl = 0; pl < 2; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * H3P + row * 128 + ((chunk ^ x6sw(row)) << 4));
+  for (int pl = 0; pl < 2; ++pl) f[pl] = *(const bf16x8_t*)(img + pl * H3P + row * 128 + ((chunk ^ tile_sw(row)) << 4));
 }
 __device__ __forceinline__ void tr_frags_h(const char* img, int dt, int g, int cl, bf16x8_t (&f)[2]) {
   const int q = cl >> 2, p = cl & 3, ch = 2 * dt + (p >> 1);
   const int r0 = 4 * g + q, r1 = 16 + 4 * g + q;
-  const int o0 = r0 * 128 + ((ch ^ x6sw(r0)) << 4) + (p & 1) * 8;
-  const int o1 = r1 * 128 + ((ch ^ x6sw(r1)) << 4) + (p & 1) * 8;
+  const int o0 = r0 * 128 + ((ch ^ tile_sw(r0)) << 4) + (p & 1) * 8;
+  const int o1 = r1 * 128 + ((ch ^ tile_sw(r1)) << 4) + (p & 1) * 8;
 #pragma unroll
   for (int pl = 0; pl < 2; ++pl) {
-    typedef __attribute__((address_space(3))) x6s4_t lds_s4;
-    const x6s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * H3P + o0));
-    const x6s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * H3P + o1));
+    typedef __attribute__((address_space(3))) s4_t lds_s4;
+    const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * H3P + o0));
+    const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + pl * H3P + o1));
     const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     f[pl] = __builtin_bit_cast(bf16x8_t, v);
   }
@@ -546,12 +245,12 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_h3_kernel(const float* __re
 #pragma unroll
   for (int d = 0; d < 4; ++d) dka[d] = dva[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int ntile = (S - kb * 64 + 31) / 32, nit = NH * ntile;
-  X6Regs rq, ro;
+  TileRegs rq, ro;
   float nl = INFINITY, nd = 0.f;
   auto fetch = [&](int it) {
     const int hh = h0 + it / ntile, q0 = kb * 64 + 32 * (it % ntile);
-    x6_load(q + ((size_t)b * Hq + hh) * S * 64, 64, q0, S, rq);
-    x6_load(dO + (size_t)b * S * (Hq * 64) + hh * 64, (size_t)Hq * 64, q0, S, ro);
+    tile_load(q + ((size_t)b * Hq + hh) * S * 64, 64, q0, S, rq);
+    tile_load(dO + (size_t)b * S * (Hq * 64) + hh * 64, (size_t)Hq * 64, q0, S, ro);
     if (tid < 32) {
       const int qi = q0 + tid;
       nl = qi < S ? lse[((size_t)b * Hq + hh) * S + qi] * 1.4426950408889634f : INFINITY;
@@ -656,10 +355,10 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_h3_kernel(const float* __rest
 #pragma unroll
   for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int kend = min(S, qb * 64 + 64);
-  X6Regs rk, rv;
+  TileRegs rk, rv;
   auto fetch = [&](int k0) {
-    x6_load(kh, 64, k0, S, rk);
-    x6_load(vh, 64, k0, S, rv);
+    tile_load(kh, 64, k0, S, rk);
+    tile_load(vh, 64, k0, S, rv);
   };
   fetch(0);
   for (int k0 = 0; k0 < kend; k0 += 32) {
@@ -1132,31 +831,6 @@ __global__ __launch_bounds__(256) void group_absprod_kernel(const float* __restr
 // ---------------------------------------------------------------------------------------------
 static inline unsigned nblk(size_t n) { return (unsigned)((n + 255) / 256); }
 
-EDGE_API int edge_lrp_attn_bwd_f32(const float* q, const float* k, const float* v, const float* o, const float* dO,
-                                   const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, int B,
-                                   int Hq, int Hkv, int S, hipStream_t st) {
-  if (B <= 0 || S <= 0) return 0;
-  if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
-  const int nb = (S + 63) / 64;
-  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S, nullptr);
-  lrp_attn_dkdv_x6_kernel<false><<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-  lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
-  return (int)hipGetLastError();
-}
-
-// edge_lrp_attn_bwd_f32 with dk, dv as the GQA group SUMS [B, Hkv, S, 64].
-EDGE_API int edge_lrp_attn_bwd_f32_gs(const float* q, const float* k, const float* v, const float* o, const float* dO,
-                                      const float* lse, float* D, float* rel, float* dq, float* dk, float* dv, int B,
-                                      int Hq, int Hkv, int S, hipStream_t st) {
-  if (B <= 0 || S <= 0) return 0;
-  if (Hkv <= 0 || Hq % Hkv) return (int)hipErrorInvalidValue;
-  const int nb = (S + 63) / 64;
-  lrp_attn_delta_f32_kernel<<<B * Hq, 256, 0, st>>>(o, dO, D, rel, Hq, S, nullptr);
-  lrp_attn_dkdv_x6_kernel<true><<<B * Hkv * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dk, dv, B, Hq, Hkv, S);
-  lrp_attn_dq_x6_kernel<<<B * Hq * nb, 256, 0, st>>>(q, k, v, dO, lse, D, dq, B, Hq, Hkv, S);
-  return (int)hipGetLastError();
-}
-
 // The h3-plane sweeps (lrp_attn_dkdv_h3 / dq_h3): q, k, v at the forward attention's plane scales sq, sk, sv (powers
 // of two with s |x| <= 2^15); dmax [B * Hq] workspace (the per-head max |dO| the delta kernel writes).  gs: dk, dv as
 // the GQA group sums [B, Hkv, S, 64], else per-q-head partials.
@@ -1203,7 +877,7 @@ EDGE_API int edge_lrp_rope_pack_h3(const float* dq, const float* dk, const float
                                    int Hkv, int rot_dim, float q_scale, hipStream_t st) {
   return rope_pack_h3(dq, dk, dv, cosT, sinT, out, rinv, post, B, S, Hq, Hkv, rot_dim, q_scale, 0, st);
 }
-// the same from dk, dv already summed over each GQA group ([B, Hkv, S, 64], edge_lrp_attn_bwd_f32_gs)
+// the same from dk, dv already summed over each GQA group ([B, Hkv, S, 64], edge_lrp_attn_bwd_h3 with gs)
 EDGE_API int edge_lrp_rope_pack_h3_gs(const float* dq, const float* dk, const float* dv, const float* cosT,
                                       const float* sinT, void* out, float* rinv, const float* post, int B, int S,
                                       int Hq, int Hkv, int rot_dim, float q_scale, hipStream_t st) {

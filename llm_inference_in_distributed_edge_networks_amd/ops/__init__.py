@@ -583,9 +583,10 @@ def lrp_gqa_sum_native(t: torch.Tensor) -> bool:
 def lrp_attn_bwd(q, k, v, o, dO, lse, gqa_sum: bool = False, in_scales=None):
     """-> (D [B,Hq,S], rel [B,Hq], dq, dk, dv [B,Hq,S,64]) fp32 (dk/dv per-q-head partials); see
     ``reference.lrp_attn_bwd``.  ``gqa_sum``: dk, dv as the sums over each GQA group, [B,Hkv,S,64] (the fp32 sweeps
-    compute them directly; elsewhere the partials are summed).  fp32 with ``in_scales`` = (s_q, s_k, s_v), the
-    forward attention's plane scales (powers of two, s |x| <= 2^15): the sweeps run on scaled fp16 planes (three
-    products, csrc/lrp_f32.hip lrp_attn_*_h3; dO's scale from its per-head maxima); without: three bf16 planes (x6)."""
+    compute them directly; elsewhere the partials are summed).  fp32: the sweeps run on scaled fp16 planes (three
+    products, csrc/lrp_f32.hip lrp_attn_*_h3; dO's scale from its per-head maxima) at ``in_scales`` = (s_q, s_k,
+    s_v), the forward attention's plane scales (powers of two, s |x| <= 2^15); without them the scales are taken
+    from the tensors' maxima."""
     B, Hq, S, D = q.shape
     Hkv = k.shape[1]
     if not _gpu(q):
@@ -601,7 +602,9 @@ def lrp_attn_bwd(q, k, v, o, dO, lse, gqa_sum: bool = False, in_scales=None):
     Dl, rel = torch.empty(B, Hq, S, **f32), torch.empty(B, Hq, **f32)
     dq = torch.empty(B, Hq, S, D, **f32)
     args = (ptr(q), ptr(k), ptr(v), ptr(o), ptr(dO), ptr(lse), ptr(Dl), ptr(rel), ptr(dq))
-    if fp32 and in_scales is not None:
+    if fp32:
+        if in_scales is None:
+            in_scales = tuple(ref.h3_scale(t.abs().max().item()) for t in (q, k, v))
         gs = bool(gqa_sum)
         Hk = Hkv if gs else Hq
         dk, dv = torch.empty(B, Hk, S, D, **f32), torch.empty(B, Hk, S, D, **f32)
@@ -609,12 +612,8 @@ def lrp_attn_bwd(q, k, v, o, dO, lse, gqa_sum: bool = False, in_scales=None):
         sq, sk, sv = (float(x) for x in in_scales)
         call("edge_lrp_attn_bwd_h3", *args, ptr(dk), ptr(dv), ptr(dmax), B, Hq, Hkv, S, int(gs), sq, sk, sv, stream())
         return Dl, rel, dq, dk, dv
-    if gqa_sum and lrp_gqa_sum_native(q):
-        dk, dv = torch.empty(B, Hkv, S, D, **f32), torch.empty(B, Hkv, S, D, **f32)
-        call("edge_lrp_attn_bwd_f32_gs", *args, ptr(dk), ptr(dv), B, Hq, Hkv, S, stream())
-        return Dl, rel, dq, dk, dv
     dk, dv = torch.empty(B, Hq, S, D, **f32), torch.empty(B, Hq, S, D, **f32)
-    call("edge_lrp_attn_bwd_f32" if fp32 else "edge_lrp_attn_bwd", *args, ptr(dk), ptr(dv), B, Hq, Hkv, S, stream())
+    call("edge_lrp_attn_bwd", *args, ptr(dk), ptr(dv), B, Hq, Hkv, S, stream())
     if gqa_sum:
         dk, dv = (t.view(B, Hkv, Hq // Hkv, S, D).sum(2) for t in (dk, dv))
     return Dl, rel, dq, dk, dv

@@ -76,9 +76,7 @@ _SIGS = {
     "edge_split_h3": [c_p, c_p, c_p, c_i, c_i, c_f, c_p],
     "edge_embedding_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     # fp32 AttnLRP backward (csrc/lrp_f32.hip)
-    "edge_lrp_attn_bwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_lrp_rope_pack_h3": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
-    "edge_lrp_attn_bwd_f32_gs": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
     "edge_lrp_rope_pack_h3_gs": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_split_h3_dyn": [c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_lrp_swiglu_bwd_h3": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p],

@@ -1,5 +1,5 @@
 # Round 5: the AttnLRP attention backward on scaled fp16 planes (h3) - tests against fp64 / autograd, the full-Qwen2
-# table against CPU fp32, a same-process A/B of the sweeps (h3 vs x6) and the fp32 AttnLRP throughput.
+# table against CPU fp32, the sweeps' time (the x6 A/B: profiles/r05/lrp_attn_h3/probe.log) and the fp32 AttnLRP throughput.
 set -o pipefail
 O=gpurun_out/r05n
 mkdir -p $O
@@ -7,7 +7,7 @@ timeout -k 10 500 python -u -m pytest tests/test_lrp_gpu.py -x -q --timeout 300 
   -p no:cacheprovider > $O/pytest_lrp.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest_lrp.log; exit 1; }
 tail -1 $O/pytest_lrp.log
 for r in 1 2; do
-  for op in lrpattn_x6 lrpattn; do
+  for op in lrpattn; do
     timeout -k 10 120 python tools/kernel_probe.py --op $op --iters 10 2>/dev/null >> $O/probe.log || exit 1
   done
 done

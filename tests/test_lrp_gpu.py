@@ -101,19 +101,18 @@ def test_relevance_engine_gpu_vs_cpu(cfg):
 
 
 @pytest.mark.parametrize("B,Hq,Hkv,S", [(2, 14, 2, 512), (1, 8, 8, 200), (3, 4, 2, 96), (1, 2, 1, 37)])
-@pytest.mark.parametrize("planes", ["x6", "h3"])
-def test_lrp_attn_bwd_f32(B, Hq, Hkv, S, planes):
-    """fp32 attention LRP backward vs the fp64 reference: fp32-rounding agreement of the matrix-core sweeps on three
-    bf16 planes (x6, six products) and on scaled fp16 planes (h3, three products, the engine's path)."""
-    _lrp_attn_bwd_f32_case(B, Hq, Hkv, S, planes == "h3")
+@pytest.mark.parametrize("scales", ["given", "derived"])
+def test_lrp_attn_bwd_f32(B, Hq, Hkv, S, scales):
+    """fp32 attention LRP backward vs the fp64 reference: fp32-rounding agreement of the matrix-core sweeps on scaled
+    fp16 planes (three products), at the given plane scales (the engine's path: the forward attention's) or at
+    scales derived from the tensors' maxima."""
+    _lrp_attn_bwd_f32_case(B, Hq, Hkv, S, scales == "given")
 
 
-@pytest.mark.parametrize("planes", ["x6", "h3"])
-def test_lrp_attn_bwd_dynamic_range(planes):
-    """Gradients have no a-priori bound.  x6: the bf16 planes carry fp32's exponent range (no scales); h3: dO's plane
-    scale is a power of two from its per-head maxima.  Either way every output is exactly equivariant under a
-    power-of-two scaling of dO (2^-40 and 2^+40: bit-identical after unscaling), and rows of dO spread over 80
-    binades keep the fp32-level error (on the global scale) of the unit-scale case."""
+def test_lrp_attn_bwd_dynamic_range():
+    """Gradients have no a-priori bound: dO's plane scale is a power of two from its per-head maxima, so every output is
+    exactly equivariant under a power-of-two scaling of dO (2^-40 and 2^+40: bit-identical after unscaling), and rows
+    of dO spread over 80 binades keep the fp32-level error (on the global scale) of the unit-scale case."""
     B, Hq, Hkv, S = 1, 4, 2, 160
     f = torch.float32
     q = rnd(B, Hq, S, 64, s=0.5, seed=11, dtype=f) * 0.125
@@ -125,7 +124,7 @@ def test_lrp_attn_bwd_dynamic_range(planes):
     o, lse = R.attention(q, k, vt, S, need_lse=True)
     dev = [t.to(DEV) for t in (q, k, v, o)]
     lse_d = lse.float().contiguous().to(DEV)
-    sc = tuple(R.h3_scale(t.abs().max().item()) for t in (q, k, v)) if planes == "h3" else None
+    sc = tuple(R.h3_scale(t.abs().max().item()) for t in (q, k, v))
     base = ops.lrp_attn_bwd(*dev, dO.to(DEV), lse_d, in_scales=sc)
     for e in (-40, 40):
         got = ops.lrp_attn_bwd(*dev, (dO * 2.0 ** e).to(DEV), lse_d, in_scales=sc)
@@ -155,7 +154,7 @@ def _lrp_attn_bwd_f32_case(B, Hq, Hkv, S, h3=False):
         assert g_.shape == r_.shape and g_.dtype == torch.float32, n
         e = rel_err(g_, r_)
         assert e < 2e-6, f"{n}: rel err {e:.3g}"
-    # dk, dv summed over each GQA group (the x6 sweeps: one workgroup per kv head sweeping its q heads)
+    # dk, dv summed over each GQA group (one workgroup per kv head sweeping its q heads)
     got = ops.lrp_attn_bwd(*(t.to(DEV) for t in (q, k, v, o, dO)), lse.float().contiguous().to(DEV), gqa_sum=True,
                            in_scales=sc)
     for n, g_, r_ in zip(["dk", "dv"], got[3:], ref[3:]):

@@ -8,7 +8,6 @@ Shapes: Qwen2-0.5B, one 64-window micro-batch of 512 tokens (M = 32768), bf16-va
   gateup  h3 gate/up GEMM + SwiGLU -> h3 planes (two products)
   down    h3 down GEMM + fp32 residual (two products)
   lrpattn       AttnLRP attention backward (delta + dK/dV with the GQA sum + dQ) on scaled fp16 planes (h3)
-  lrpattn_x6    the same on three bf16 planes (six products)
   gateupraw     the AttnLRP forward's gate/up: SwiGLU planes + the fp32 pre-activations from one GEMM
   gateup_lib / down_lib  hipBLASLt (torch.matmul) on the same fp16 operands and K' (no epilogue): the library's clock
                 and MFMA rate under the same sustained load
@@ -31,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--op", default="attn", choices=["attn", "qkv", "colsum", "norm", "gateup", "down",
                                                           "lrpmlp", "lrpmlp_split", "gateup_lib", "down_lib", "gateupraw",
-                                                          "lrpattn", "lrpattn_x6"])
+                                                          "lrpattn"])
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--S", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
@@ -73,7 +72,7 @@ def main():
         x = torch.randn(B * S, 2 * K, generator=g).half().to(dev)
         w = (torch.randn(N, 2 * K, generator=g) * 0.02).half().to(dev)
         fn = lambda: torch.matmul(x, w.t())   # noqa: E731
-    elif a.op.startswith("lrpattn"):
+    elif a.op == "lrpattn":
         q = (torch.randn(B, Hq, S, 64, generator=g) * 0.125).to(dev)
         k = torch.randn(B, Hkv, S, 64, generator=g).to(dev)
         v = torch.randn(B, Hkv, S, 64, generator=g).to(dev)
@@ -82,8 +81,7 @@ def main():
         sc = (2.0 ** 12, 2.0 ** 12, 2.0 ** 12)
         o, lse = ops.attention(q, k, vt, S, need_lse=True, in_scales=sc)
         dO = torch.randn(B * S, Hq * 64, generator=g).to(dev)
-        isc = sc if a.op == "lrpattn" else None
-        fn = lambda: ops.lrp_attn_bwd(q, k, v, o, dO, lse, gqa_sum=True, in_scales=isc)   # noqa: E731
+        fn = lambda: ops.lrp_attn_bwd(q, k, v, o, dO, lse, gqa_sum=True, in_scales=sc)   # noqa: E731
     elif a.op == "gateupraw":
         x = torch.randn(B * S, H, generator=g)
         w = (torch.randn(9728, H, generator=g) * 0.02).bfloat16().float()
