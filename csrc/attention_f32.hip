@@ -193,7 +193,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
                                                                   float* __restrict__ lse,
                                                                   const float* __restrict__ n_rows, int B, int Hq,
                                                                   int Hkv, int S, int s_pad, float h3s, float sq,
-                                                                  float sk, float sv) {
+                                                                  float sk, float sv, float* __restrict__ o32) {
+  // o32 (H3OUT, optional): O also as fp32 rows [B*S, Hq*64] (the AttnLRP forward saves it next to the planes)
   static_assert(!KVP || (F16 && NW == 8), "plane staging: h3 planes, 8 waves (8 KiB per DMA round)");
   constexpr int NPL = F16 ? 2 : 3;
   const float* __restrict__ k = (const float*)kin;
@@ -434,6 +435,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
   }
   if (qrow < S) {
     if constexpr (H3OUT) {
+      if (o32) {
+        float* r32 = o32 + ((size_t)b * S + qrow) * (size_t)W + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) *(f32x4_t*)(r32 + dt * 16 + 4 * g) = oacc[dt] * inv;
+      }
       f16_t* orow = (f16_t*)o + ((size_t)b * S + qrow) * (size_t)(2 * W) + h * 64;
 #pragma unroll
       for (int q2 = 0; q2 < 2; ++q2) {
@@ -718,9 +724,9 @@ __global__ __launch_bounds__(256) void attn_lastrow_h3_kernel(const float* __res
 template <bool H3OUT>
 static void launch_plane_attn(dim3 grid, hipStream_t st, const float* q, const void* kp, const void* vp, void* o,
                               float* lse, const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float h3s,
-                              float sq, float sk, float sv) {
+                              float sq, float sk, float sv, float* o32) {
   hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<H3OUT, 8, true, true>), grid, dim3(512), 8 * XPL, st, q, kp, vp, o,
-                     lse, n_rows, B, Hq, Hkv, S, s_pad, h3s, sq, sk, sv);
+                     lse, n_rows, B, Hq, Hkv, S, s_pad, h3s, sq, sk, sv, o32);
 }
 
 template <bool H3OUT, int NW, bool F16>
@@ -728,7 +734,7 @@ static void launch_split_attn(dim3 grid, hipStream_t st, const float* q, const f
                               float* lse, const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float h3s,
                               float sq, float sk, float sv) {
   hipLaunchKernelGGL((flash_attn_fwd_x6_kernel<H3OUT, NW, F16>), grid, dim3(NW * 64), (F16 ? 4 : 6) * XPL, st, q, k,
-                     vt, o, lse, n_rows, B, Hq, Hkv, S, s_pad, h3s, sq, sk, sv);
+                     vt, o, lse, n_rows, B, Hq, Hkv, S, s_pad, h3s, sq, sk, sv, nullptr);
 }
 
 // out_h3_scale > 0: O as a 2-plane h3 activation [B*S, 2*Hq*64] (fp16 planes at that scale) for the O-projection;
@@ -752,18 +758,21 @@ EDGE_API int edge_flash_attn_fwd_f32(const float* q, const float* k, const float
 }
 
 // fp32 attention from the K / V^T h3 planes of edge_gemm_qkv_rope_f32 (kp / vp at scales sk / sv; q fp32, split at
-// sq): the KVP kernel.  Same arguments and outputs as edge_flash_attn_fwd_f32 otherwise.
+// sq): the KVP kernel.  Same arguments and outputs as edge_flash_attn_fwd_f32 otherwise; o32 (optional, with the h3
+// output): O as fp32 rows too.
 EDGE_API int edge_flash_attn_fwd_h3p(const float* q, const void* kp, const void* vp, void* o, float* lse,
                                     const float* n_rows, int B, int Hq, int Hkv, int S, int s_pad, float out_h3_scale,
-                                    float sq, float sk, float sv, hipStream_t st) {
+                                    float sq, float sk, float sv, float* o32, hipStream_t st) {
   if (B <= 0 || S <= 0) return 0;
   if (Hkv <= 0 || Hq % Hkv || s_pad % 64 || s_pad < S || out_h3_scale < 0.f) return (int)hipErrorInvalidValue;
   if (!(sq > 0.f && sk > 0.f && sv > 0.f) || ((uintptr_t)kp & 15) || ((uintptr_t)vp & 15))
     return (int)hipErrorInvalidValue;
   const int G = Hq / Hkv, maxcnt = (B * Hkv + 7) / 8;
   const dim3 gx(8 * maxcnt * G * ((S + 127) / 128));
+  if (o32 && !(out_h3_scale > 0.f)) return (int)hipErrorInvalidValue;
   (out_h3_scale > 0.f ? launch_plane_attn<true> : launch_plane_attn<false>)(gx, st, q, kp, vp, o, lse, n_rows, B, Hq,
-                                                                            Hkv, S, s_pad, out_h3_scale, sq, sk, sv);
+                                                                            Hkv, S, s_pad, out_h3_scale, sq, sk, sv,
+                                                                            o32);
   return (int)hipGetLastError();
 }
 

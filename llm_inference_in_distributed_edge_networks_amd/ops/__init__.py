@@ -273,7 +273,8 @@ def qkv_rope(x, wqkv, bqkv, cos, sin, B, S, Hq, Hkv, D, rot_dim, q_scale, norm=N
     return q, k, vt
 
 
-def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scales=None, kv_planes=None):
+def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scales=None, kv_planes=None,
+              f32_out=False):
     """Causal GQA flash attention -> (o [B*S, Hq*64], lse [B,Hq,S] or None).
 
     ``n_rows`` ([B] fp32, scored rows per window as in ``WindowBatch.n_rows``): only query rows
@@ -283,9 +284,12 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scal
     with s |x| <= 2^15 for every element of q, k and v: the matrix work runs on scaled fp16 planes (three products;
     the model derives them from weight bounds), else on three bf16 planes (six products).  ``kv_planes`` = (kp, vp)
     from ``qkv_rope_h3(kv_scales=(s_k, s_v))`` (with ``in_scales``): the kernel stages those planes by LDS DMA
-    instead of splitting the fp32 K / V^T itself (the same result bit for bit)."""
+    instead of splitting the fp32 K / V^T itself (the same result bit for bit).  ``f32_out`` (with ``h3`` and
+    ``kv_planes``): O as fp32 rows too -> (o planes, lse, o fp32)."""
     if not _gpu(q):
         o, lse = ref.attention(q, k, vt, S, need_lse)
+        if f32_out:
+            return ref.h3_act(o, h3), lse, o
         return (ref.h3_act(o, h3) if h3 else o), lse
     B, Hq, _, D = q.shape
     Hkv = k.shape[1] if k is not None else kv_planes[0].shape[1]   # (k may be None when its planes are given)
@@ -302,10 +306,12 @@ def attention(q, k, vt, S, need_lse=False, n_rows=None, h3: float = 0.0, in_scal
         assert kp.shape == (B, Hkv, 2, S, D) and vp.shape == (B, Hkv, 2, D, sp) and sp % 64 == 0 and sp >= S
         assert kp.is_contiguous() and vp.is_contiguous() and kp.is_cuda and vp.is_cuda
         o = _out_f32_or_h3(B * S, Hq * D, h3, q.device)
+        o32 = torch.empty(B * S, Hq * D, dtype=torch.float32, device=q.device) if f32_out else None
+        assert not f32_out or h3, "f32_out: the fp32 rows next to the h3 planes"
         sq, sk, sv = in_scales
         call("edge_flash_attn_fwd_h3p", ptr(q), ptr(kp), ptr(vp), ptr(o), ptr(lse), ptr(nr), B, Hq, Hkv, S, sp,
-             float(h3), float(sq), float(sk), float(sv), stream())
-        return o, lse
+             float(h3), float(sq), float(sk), float(sv), ptr(o32), stream())
+        return (o, lse, o32) if f32_out else (o, lse)
     if q.dtype == torch.float32:
         _check_f32(q, k, vt)
         assert D == 64 and vt.shape[-1] % 64 == 0 and vt.shape[-1] >= S

@@ -67,7 +67,7 @@ _SIGS = {
     "edge_gemm_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p, c_f, c_f, c_p],
     "edge_gemm_qkv_rope_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f,
                                c_f, c_p, c_p, c_f, c_f, c_p, c_p],
-    "edge_flash_attn_fwd_h3p": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_f, c_f, c_f, c_p],
+    "edge_flash_attn_fwd_h3p": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_f, c_f, c_f, c_p, c_p],
     "edge_flash_attn_fwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_f, c_f, c_f, c_f, c_p],
     "edge_attn_lastrow_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_f, c_p],
     "edge_attn_colsum_f32": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_f, c_f, c_p],

@@ -99,17 +99,17 @@ class RelevanceEngineH3:
             q, k, vt, kp, vp, v = ops.qkv_rope_h3(h13, L["wqkv3"], sc["a_wqkv"], L["bqkv"], m.cos, m.sin, B, S, Hq,
                                                   Hkv, D, cfg.rotary_dim, m.q_scale, kv_scales=(sc["att_k"], sc["o"]),
                                                   v_rows=True)
-            o, lse = ops.attention(q, k, vt, S, need_lse=True, in_scales=(sc["att_q"], sc["att_k"], sc["o"]),
-                                   kv_planes=(kp, vp) if q.is_cuda else None)
+            # O as the O-projection's h3 planes and, for the backward, as fp32 rows - both from the attention kernel
+            o3, lse, o = ops.attention(q, k, vt, S, need_lse=True, h3=sc["o"],
+                                       in_scales=(sc["att_q"], sc["att_k"], sc["o"]),
+                                       kv_planes=(kp, vp) if q.is_cuda else None, f32_out=True)
             sv.update(q=q, k=k, v=v, o=o, lse=lse.contiguous())
             if i == nl - 1:   # only the seeded rows reach the seed: O-proj and MLP on those rows
                 sv["rows"] = last
                 x = x.index_select(0, last)
                 if not self.qwen:
                     h23 = h23.index_select(0, last)
-                o3 = ops.split_h3(o, sc["o"], rows=last)
-            else:
-                o3 = ops.split_h3(o, sc["o"])
+                o3 = o3.index_select(0, last)
             if self.qwen:
                 y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], residual=x)
                 sv["rs2"] = torch.empty(y.shape[0], dtype=torch.float32, device=y.device)

@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/${OUT:-r05n}
 mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_lrp_gpu.py -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 500 python -u -m pytest tests/test_lrp_gpu.py tests/test_f32_gpu.py -x -q --timeout 300 --timeout-method thread \
   -p no:cacheprovider > $O/pytest_lrp.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest_lrp.log; exit 1; }
 tail -1 $O/pytest_lrp.log
 for r in 1 2; do

@@ -284,6 +284,12 @@ def test_attention_kv_planes_bit_identical(B, S, Hq, Hkv, h3):
     o1, l1 = ops.attention(*args, need_lse=True, h3=s, in_scales=sc)
     o2, l2 = ops.attention(q.to(DEV), k.to(DEV), None, S, need_lse=True, h3=s, in_scales=sc, kv_planes=planes)
     assert torch.equal(o1, o2) and torch.equal(l1, l2)
+    if h3:   # the planes plus fp32 rows (AttnLRP forward): the planes unchanged, the rows = the fp32 kernel's output
+        o4, l4, o32 = ops.attention(q.to(DEV), k.to(DEV), None, S, need_lse=True, h3=s, in_scales=sc,
+                                    kv_planes=planes, f32_out=True)
+        of, _ = ops.attention(*args, need_lse=True, in_scales=sc, kv_planes=planes)
+        assert torch.equal(o4, o1) and torch.equal(l4, l1) and torch.equal(o32, of)
+        assert torch.equal(ops.split_h3(o32, s), o1)   # the planes are the split of those rows
     n_rows = torch.tensor([float(min(31 + 40 * i, S - 2)) for i in range(B)], device=DEV)
     o3, _ = ops.attention(*args, n_rows=n_rows, h3=s, in_scales=sc, kv_planes=planes)
     W = o1.shape[1]
