@@ -224,8 +224,9 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_h3_kernel(const float* __re
                                                                const float* __restrict__ dmax, float* __restrict__ dk,
                                                                float* __restrict__ dv, int B, int Hq, int Hkv, int S,
                                                                float sq, float sk, float sv) {
-  __shared__ __attribute__((aligned(16))) char sQ[2 * H3P], sO[2 * H3P];
-  __shared__ float sL[32], sD[32];
+  // double-buffered tiles: tile it + 1 is staged while tile it is computed, one barrier per tile
+  __shared__ __attribute__((aligned(16))) char sQ[2][2 * H3P], sO[2][2 * H3P];
+  __shared__ float sL[2][32], sD[2][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int G = Hq / Hkv, HH = GS ? Hkv : Hq, NH = GS ? G : 1;
   const int kb = blockIdx.x / (B * HH);
@@ -257,15 +258,21 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_h3_kernel(const float* __re
       nd = qi < S ? D[((size_t)b * Hq + hh) * S + qi] : 0.f;
     }
   };
+  auto stage = [&](int buf) {
+    h3_store(rq, sQ[buf], sq);
+    h3_store(ro, sO[buf], so);
+    if (tid < 32) sL[buf][tid] = nl, sD[buf][tid] = nd;
+  };
   fetch(0);
+  stage(0);
+  if (nit > 1) fetch(1);
+  __syncthreads();
   for (int it = 0; it < nit; ++it) {
-    const int q0 = kb * 64 + 32 * (it % ntile);
-    __syncthreads();
-    h3_store(rq, sQ, sq);
-    h3_store(ro, sO, so);
-    if (tid < 32) sL[tid] = nl, sD[tid] = nd;
-    if (it + 1 < nit) fetch(it + 1);
-    __syncthreads();
+    const int q0 = kb * 64 + 32 * (it % ntile), cb = it & 1;
+    const char* bQ = sQ[cb];
+    const char* bO = sO[cb];
+    const float* bL = sL[cb];
+    const float* bD = sD[cb];
     float pv[8], dsv[8];
     const bool full = q0 >= wkey_max && q0 + 32 <= S && wkey_max < S;
 #pragma unroll
@@ -274,8 +281,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_h3_kernel(const float* __re
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t qa[2], oa[2];
-        rm_frags_h(sQ, sub * 16 + cl, 4 * ks + g, qa);
-        rm_frags_h(sO, sub * 16 + cl, 4 * ks + g, oa);
+        rm_frags_h(bQ, sub * 16 + cl, 4 * ks + g, qa);
+        rm_frags_h(bO, sub * 16 + cl, 4 * ks + g, oa);
         sc = h3dot(qa, kf[ks], sc);
         da = h3dot(oa, vf[ks], da);
       }
@@ -283,18 +290,18 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_h3_kernel(const float* __re
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ql = sub * 16 + 4 * g + r;
-          const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], c1, -sL[ql]));
+          const float pr = __builtin_amdgcn_exp2f(fmaf(sc[r], c1, -bL[ql]));
           pv[4 * sub + r] = pr;
-          dsv[4 * sub + r] = pr * fmaf(da[r], c2, -sD[ql]);
+          dsv[4 * sub + r] = pr * fmaf(da[r], c2, -bD[ql]);
         }
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ql = sub * 16 + 4 * g + r, qi = q0 + ql;
           const bool ok = qi < S && key <= qi && key < S;
-          const float pr = ok ? __builtin_amdgcn_exp2f(fmaf(sc[r], c1, -sL[ql])) : 0.f;
+          const float pr = ok ? __builtin_amdgcn_exp2f(fmaf(sc[r], c1, -bL[ql])) : 0.f;
           pv[4 * sub + r] = pr;
-          dsv[4 * sub + r] = pr * fmaf(da[r], c2, -sD[ql]);
+          dsv[4 * sub + r] = pr * fmaf(da[r], c2, -bD[ql]);
         }
       }
     }
@@ -304,11 +311,18 @@ __global__ __launch_bounds__(256) void lrp_attn_dkdv_h3_kernel(const float* __re
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x8_t ob[2], qb[2];
-      tr_frags_h(sO, dt, g, cl, ob);
-      tr_frags_h(sQ, dt, g, cl, qb);
+      tr_frags_h(bO, dt, g, cl, ob);
+      tr_frags_h(bQ, dt, g, cl, qb);
       dva[dt] = h3dot(pf, ob, dva[dt]);
       dka[dt] = h3dot(dsf, qb, dka[dt]);
     }
+    // stage tile it + 1 into the other buffer (its last readers finished before the previous barrier) and fetch
+    // tile it + 2 into the registers the staging just consumed
+    if (it + 1 < nit) {
+      stage(cb ^ 1);
+      if (it + 2 < nit) fetch(it + 2);
+    }
+    __syncthreads();
   }
   float* dkh = dk + ((size_t)b * HH + hx) * S * 64;
   float* dvh = dv + ((size_t)b * HH + hx) * S * 64;
@@ -333,7 +347,7 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_h3_kernel(const float* __rest
                                                              const float* __restrict__ dmax, float* __restrict__ dq,
                                                              int B, int Hq, int Hkv, int S, float sq, float sk,
                                                              float sv) {
-  __shared__ __attribute__((aligned(16))) char sK[2 * H3P], sV[2 * H3P];
+  __shared__ __attribute__((aligned(16))) char sK[2][2 * H3P], sV[2][2 * H3P];   // double-buffered, as dkdv
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int nqb = (S + 63) / 64;
   const int qb = nqb - 1 - blockIdx.x / (B * Hq);
@@ -361,12 +375,14 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_h3_kernel(const float* __rest
     tile_load(vh, 64, k0, S, rv);
   };
   fetch(0);
+  h3_store(rk, sK[0], sk);
+  h3_store(rv, sV[0], sv);
+  if (32 < kend) fetch(32);
+  __syncthreads();
   for (int k0 = 0; k0 < kend; k0 += 32) {
-    __syncthreads();
-    h3_store(rk, sK, sk);
-    h3_store(rv, sV, sv);
-    if (k0 + 32 < kend) fetch(k0 + 32);
-    __syncthreads();
+    const int cb = (k0 >> 5) & 1;
+    const char* bK = sK[cb];
+    const char* bV = sV[cb];
     const bool full = k0 + 31 <= wq_min && wq_min + 15 < S;
     float dsv[8];
 #pragma unroll
@@ -375,8 +391,8 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_h3_kernel(const float* __rest
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8_t ka[2], va[2];
-        rm_frags_h(sK, sub * 16 + cl, 4 * ks + g, ka);
-        rm_frags_h(sV, sub * 16 + cl, 4 * ks + g, va);
+        rm_frags_h(bK, sub * 16 + cl, 4 * ks + g, ka);
+        rm_frags_h(bV, sub * 16 + cl, 4 * ks + g, va);
         sc = h3dot(ka, qf[ks], sc);
         da = h3dot(va, of[ks], da);
       }
@@ -399,9 +415,15 @@ __global__ __launch_bounds__(256) void lrp_attn_dq_h3_kernel(const float* __rest
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       bf16x8_t kt[2];
-      tr_frags_h(sK, dt, g, cl, kt);
+      tr_frags_h(bK, dt, g, cl, kt);
       acc[dt] = h3dot(kt, dsf, acc[dt]);
     }
+    if (k0 + 32 < kend) {
+      h3_store(rk, sK[cb ^ 1], sk);
+      h3_store(rv, sV[cb ^ 1], sv);
+      if (k0 + 64 < kend) fetch(k0 + 64);
+    }
+    __syncthreads();
   }
   if (qi < S) {
     const float f = 0.5f / (sk * sd);
