@@ -47,6 +47,10 @@ struct GemmArgs {
   float* Cf; const float* biasf; const float* residf;
   float* qf; float* kf; float* vtf;
   float* vf;   // fp32 QKV, optional: V row-major [B, Hkv, S, 64] (the AttnLRP backward's operand) next to V^T / planes
+  // EPI_F32_RESID_CS, optional: C also as the 2-plane h3 activation [M, 2N] (planes) of s_m C at the power-of-two row
+  // scale s_m from the caller's bound 2^15 (bnd_a[m] + bnd_b[m] bnd_c) on |C row m|, and prinv[m] = 1 / s_m - the
+  // next backward GEMM's input without a row-max pass (plane_scale)
+  f16_t* planes; float* prinv; const float* bnd_a; const float* bnd_b; float bnd_c;
   // QKV_ROPE
   bf16_t* qout; bf16_t* kout; bf16_t* vtout;
   const float* cosT; const float* sinT;
@@ -316,6 +320,13 @@ __device__ __forceinline__ void store_vt_plane1(const GemmArgs& a, int b, int hv
   a.vp[o + (size_t)64 * a.s_pad] = __builtin_bit_cast(uint16_t, (_Float16)lo);
 }
 
+// s_m of GemmArgs::planes: 2^(15 - E) for the bound 2^15 (bnd_a[m] + bnd_b[m] bnd_c) = f 2^E, f in [0.5, 1)
+__device__ __forceinline__ float plane_scale(const GemmArgs& a, int m) {
+  int e;
+  (void)frexpf(32768.f * (a.bnd_a[m] + a.bnd_b[m] * a.bnd_c), &e);
+  return ldexpf(1.f, 15 - e);
+}
+
 // ---- fp32-execution epilogues (EPI >= EPI_F32).  Same ownership as gemm_epilogue below: lane owns rows
 // m0 + wm*WTM + i*16 + (lane&15) and columns nw + j*16 + 4*(lane>>4) + r of the wave's 64-column slab, so every
 // output is 4 consecutive fp32 values (one 16-byte store) or 4 consecutive values of each of the two h3 planes.
@@ -476,6 +487,13 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
     }
     if (m >= a.M) continue;
     {
+      float ps = 0.f;
+      if constexpr (EPI == EPI_F32_RESID_CS) {
+        if (a.planes) {
+          ps = plane_scale(a, m);
+          if (nw == 0 && g == 0) a.prinv[m] = 1.f / ps;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = nw + j * 16 + g * 4;
@@ -496,6 +514,9 @@ __device__ __forceinline__ void gemm_epilogue_f32(const GemmArgs& a, f32x4_t (&a
           for (int r = 0; r < 4; ++r) o[r] += rw[r];
         }
         *(f32x4_t*)(a.Cf + (size_t)m * a.ldc + n) = f32x4_t{o[0], o[1], o[2], o[3]};
+        if constexpr (EPI == EPI_F32_RESID_CS) {
+          if (a.planes) store_h3_4(a.planes + (size_t)m * (2 * a.N), a.N, n, o, ps);
+        }
       }
     }
   }
@@ -959,42 +980,7 @@ __device__ __forceinline__ void w7_epilogue(const GemmArgs& a, f32x4_t (&acc)[w7
   const int g = lane >> 4;
   const int nw = n0 + wn * 112;
   const int P = a.N / 112;
-  if constexpr (epi_f32(EPI)) {
-    // fp32 execution: fp32 bias / residual / output.  Residuals are loaded two row groups at a time (all four
-    // would be 112 VGPRs and spill at this kernel's 256-register budget), each pair before that pair's stores.
-    constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID || EPI == EPI_F32_RESID_CS;
-#pragma unroll
-    for (int ih = 0; ih < w7::MI; ih += 2) {
-      f32x4_t rv[2][w7::NJ];
-      if constexpr (RESF) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          int mr = m0 + wm * 64 + (ih + i) * 16 + (lane & 15);
-          mr = mr < a.M ? mr : a.M - 1;
-          const float* rrow = a.residf + (size_t)mr * a.ldr + nw + g * 4;
-#pragma unroll
-          for (int j = 0; j < w7::NJ; ++j) rv[i][j] = *(const f32x4_t*)(rrow + j * 16);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int m = m0 + wm * 64 + (ih + i) * 16 + (lane & 15);
-        if (m >= a.M) continue;
-        float* row = a.Cf + (size_t)m * a.ldc + nw + g * 4;
-        const float rsm = (a.rscale ? a.rscale[m] : 1.f) * a.alpha;
-#pragma unroll
-        for (int j = 0; j < w7::NJ; ++j) {
-          f32x4_t o = acc[ih + i][j] * rsm;
-          if constexpr (EPI == EPI_F32_RESID_CS) o *= *(const f32x4_t*)(a.colscale + nw + j * 16 + g * 4);
-          if constexpr (EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID)
-            o += *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
-          if constexpr (RESF) o += rv[i][j];
-          *(f32x4_t*)(row + j * 16) = o;
-        }
-      }
-    }
-    return;
-  }
+  static_assert(!epi_f32(EPI), "fp32 epilogues of the 224-wide tiles: w4_f32_epilogue_224");
   constexpr bool RES = EPI == EPI_RESID || EPI == EPI_BIAS_RESID;
   // every residual load of the slab is issued up front (4 x 7 x 8 B per lane): one global round trip instead of
   // one per 16-row group (the per-group load -> wait -> use chain cost ~30 % of the O-proj GEMM's time)
@@ -1270,12 +1256,13 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
     for (int j = 0; j < 7; ++j) bw[j] = *(const f32x4_t*)(a.colscale + nw + j * 16 + g * 4);
   }
   f32x4_t rv[2][2][RESF ? 7 : 1];
-  float rsv[2][2];
+  float rsv[2][2], psv[2][2];
   auto load = [&](int pr, int buf) {
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2) {
       const int mr = min(rbase + (2 * pr + i2) * 16, a.M - 1);
       rsv[buf][i2] = (a.rscale ? a.rscale[mr] : 1.f) * a.alpha;
+      if constexpr (CS) psv[buf][i2] = a.planes ? plane_scale(a, mr) : 0.f;
       if constexpr (RESF) {
         const float* rrow = a.residf + (size_t)mr * a.ldr + nw + g * 4;
 #pragma unroll
@@ -1308,6 +1295,15 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
           if constexpr (BIAS) o += bw[j];
           if constexpr (RESF) o += rv[buf][i2][j];
           *(f32x4_t*)(row + j * 16) = o;
+          if constexpr (CS) {
+            if (a.planes) {
+              const float v4[4] = {o[0], o[1], o[2], o[3]};
+              store_h3_4(a.planes + (size_t)m * (2 * a.N), a.N, nw + j * 16 + g * 4, v4, psv[buf][i2]);
+            }
+          }
+        }
+        if constexpr (CS) {
+          if (a.planes && nw == 0 && g == 0) a.prinv[m] = 1.f / psv[buf][i2];
         }
       }
     }
@@ -1862,9 +1858,12 @@ EDGE_API int edge_gemm_f32_swiglu_raw(const void* A, const void* B, void* C, flo
 
 // EPI_F32_RESID_CS: C = colscale[n] * rscale[m] * alpha * (A . B^T) + resid (h3 operands as edge_gemm_f32; C may
 // alias resid).
+// planes / prinv / bnd_a / bnd_b / bnd_c (all or none): C also as the h3 activation [M, 2N] at the bound-derived
+// row scales (GemmArgs::planes).
 EDGE_API int edge_gemm_f32_cs(const void* A, const void* B, float* C, int M, int N, int Kx, int kplane, int lda, int ldb,
                               int ldc, const float* colscale, const float* resid, int ldr, const float* rscale,
-                              float alpha, hipStream_t st) {
+                              float alpha, void* planes, float* prinv, const float* bnd_a, const float* bnd_b,
+                              float bnd_c, hipStream_t st) {
   GemmArgs a{};
   a.rscale = rscale;
   a.colscale = colscale;
@@ -1874,8 +1873,11 @@ EDGE_API int edge_gemm_f32_cs(const void* A, const void* B, float* C, int M, int
   a.residf = resid; a.ldr = ldr; a.Cf = C;
   a.h3k = kplane;
   a.pairb = Kx == 2 * kplane;
+  a.planes = (f16_t*)planes; a.prinv = prinv; a.bnd_a = bnd_a; a.bnd_b = bnd_b; a.bnd_c = bnd_c;
   if (!colscale || !resid || !h3_geometry_ok(Kx, kplane) || lda < 2 * kplane || ldb < (a.pairb ? kplane : Kx) ||
       !(alpha > 0.f))
+    return (int)hipErrorInvalidValue;
+  if (planes && (!prinv || !bnd_a || !bnd_b || !(bnd_c >= 0.f) || ((uintptr_t)planes & 7)))
     return (int)hipErrorInvalidValue;
   const int chk = check_shapes(a);
   if (chk) return chk < 0 ? 0 : chk;

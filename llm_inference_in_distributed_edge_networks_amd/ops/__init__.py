@@ -408,14 +408,17 @@ def split_h3(x: torch.Tensor, s: float, rows: torch.Tensor | None = None) -> tor
 
 
 def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, residual=None, act=None, out=None,
-              rscale=None, out_scale: float = 1.0, colscale=None) -> torch.Tensor:
+              rscale=None, out_scale: float = 1.0, colscale=None, planes_bound=None):
     """fp32-accurate ``act(rscale * (x @ w.T) + bias) + residual`` from h3 operands (a3 [M, 2K] the 2-plane
     activation of s_a x, w3 [N, 3K] the h3 weight of w at scale s_w, alpha = 1 / (s_a s_w)).
 
     act None -> fp32 [M, N] (``residual`` fp32, may alias ``out``); act "gelu" / "swiglu_il" -> the activation as
     the 2-plane h3 activation of ``out_scale`` * act(...) ([M, 2N] / [M, N]) for the next GEMM.
     ``colscale`` [N] (with a residual, no bias / act): ``colscale * rscale * (x @ w.T) + residual`` - a norm weight on
-    the output columns instead of folded into w, which then keeps a weight exact in fp16 on two products."""
+    the output columns instead of folded into w, which then keeps a weight exact in fp16 on two products.
+    ``planes_bound`` = (bnd_a [M], bnd_b [M], c) with ``colscale``: the result also as the h3 activation of the next
+    backward GEMM, at per-row powers of two from the caller's bound 2^15 (bnd_a + bnd_b c) on |row| (no row-max pass)
+    -> (out, planes [M, 2N], rinv [M])."""
     M = a3.shape[0]
     N = w3.shape[0]
     if not _gpu(a3):
@@ -435,7 +438,9 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
             y = y + residual.float()
         if out is not None:
             out.copy_(y)
-            return out
+            y = out
+        if planes_bound is not None:
+            return (y,) + ref.bound_planes(y, *planes_bound)
         return y
     kp, Kx = _check_h3(a3, w3, alpha)
     _check_f32(bias, residual, rscale, colscale)
@@ -444,9 +449,18 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
             raise ValueError("colscale: a residual GEMM without bias / activation")
         if out is None:
             out = torch.empty(M, N, dtype=torch.float32, device=a3.device)
+        pl = pr = ba = bb = None
+        bc = 0.0
+        if planes_bound is not None:
+            ba, bb, bc = planes_bound
+            _check_f32(ba, bb)
+            assert ba.numel() == M and bb.numel() == M
+            pl = torch.empty(M, 2 * N, dtype=torch.float16, device=a3.device)
+            pr = torch.empty(M, dtype=torch.float32, device=a3.device)
         call("edge_gemm_f32_cs", ptr(a3), ptr(w3), ptr(out), M, N, Kx, kp, a3.stride(0), w3.stride(0), out.stride(0),
-             ptr(colscale), ptr(residual), residual.stride(0), ptr(rscale), float(alpha), stream())
-        return out
+             ptr(colscale), ptr(residual), residual.stride(0), ptr(rscale), float(alpha), ptr(pl), ptr(pr), ptr(ba),
+             ptr(bb), float(bc), stream())
+        return out if planes_bound is None else (out, pl, pr)
     if act is None:
         if out is None:
             out = torch.empty(M, N, dtype=torch.float32, device=a3.device)

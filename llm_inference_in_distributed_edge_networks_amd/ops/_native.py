@@ -61,7 +61,8 @@ _SIGS = {
     "edge_rmsnorm_f32_rstd": [c_p, c_p, c_p, c_p, c_i, c_i, c_f, c_f, c_p, c_p],
     "edge_gemm_swiglu_raw": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p],
     "edge_gemm_f32_swiglu_raw": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_f, c_f, c_p],
-    "edge_gemm_f32_cs": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_p, c_f, c_p],
+    "edge_gemm_f32_cs": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_p, c_f,
+                         c_p, c_p, c_p, c_p, c_f, c_p],
     "edge_lrp_attn_bwd_h3": [c_p] * 12 + [c_i] * 5 + [c_f] * 3 + [c_p],
     "edge_gemm_f32_lrp_swiglu": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
     "edge_gemm_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p, c_f, c_f, c_p],

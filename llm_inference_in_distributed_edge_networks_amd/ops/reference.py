@@ -409,6 +409,18 @@ def lrp_swiglu_bwd_h3(dm, gu, post=None):
     return split_h3_dyn(lrp_swiglu_bwd(_f(dm), _f(gu)), post)
 
 
+def bound_planes(y: torch.Tensor, bnd_a, bnd_b, bnd_c: float):
+    """(h3 activation [M, 2N] of s_m y_m, 1 / s_m) with s_m = 2^(15 - E) for the bound 2^15 (bnd_a[m] + bnd_b[m]
+    bnd_c) = f 2^E, f in [0.5, 1) (gemm.hip GemmArgs::planes)."""
+    bound = 32768.0 * (_f(bnd_a) + _f(bnd_b) * float(bnd_c))
+    _, e = torch.frexp(bound)
+    s = torch.exp2((15 - e).to(torch.float32))
+    ys = _f(y) * s.view(-1, 1)
+    hi = ys.to(torch.float16)
+    lo = (ys - hi.float()).to(torch.float16)
+    return torch.cat([hi, lo], -1).contiguous(), 1.0 / s
+
+
 def h3_unit(x: torch.Tensor) -> torch.Tensor:
     """fp32 [R, K] -> the 2-plane h3 activation [R, 2K] at scale 1 (the caller bounds |x| below 2^15)."""
     hi = _f(x).to(torch.float16)

@@ -67,6 +67,9 @@ class RelevanceEngineH3:
                 t["wguT3"], t["a_guT"] = t3(L["wgu"])
                 t["wdT3"], t["a_dT"] = t3(L["wd"])
                 t["c_swiglu"] = ops.lrp_swiglu_scale(L["wd"], L["wgu"], L["ln2_w"])
+                # bound of the gate|up input-gradient GEMM's product per unit of its input row scale:
+                # max_c |norm_w[c]| sum_k |W[k, c]| (dy's h3 planes come from that GEMM's epilogue)
+                t["c_gu"] = float((L["wgu"].float().abs().sum(0) * L["ln2_w"].float().abs()).max())
             else:
                 t["wqkvT3"], t["a_qkvT"] = t3(L["wqkv"])
                 t["wfcT3"], t["a_fcT"] = t3(L["wfc"])
@@ -176,8 +179,9 @@ class RelevanceEngineH3:
                 # dm GEMM + SwiGLU rule in one kernel (the rule's planes at the weights' a-priori bound)
                 dgu3, rinv_gu = ops.linear_h3_lrp_swiglu(dx3, t["wdT3"], t["a_dT"], sv["gu"], t["c_swiglu"], rinv,
                                                          post=sv["rs2"])
-                dy = ops.linear_h3(dgu3, t["wguT3"], t["a_guT"], rscale=rinv_gu, residual=dx, colscale=L["ln2_w"])
-                dy3, rinv_y = ops.split_h3_dyn(dy)
+                # dy and its h3 planes in one GEMM: |dy| <= |dx| + rinv_gu 2^15 c_gu, |dx| < 2^15 rinv
+                dy, dy3, rinv_y = ops.linear_h3(dgu3, t["wguT3"], t["a_guT"], rscale=rinv_gu, residual=dx,
+                                                colscale=L["ln2_w"], planes_bound=(rinv, rinv_gu, t["c_gu"]))
             else:
                 dp = ops.linear_h3(dx3, t["wprojT3"], t["a_projT"], rscale=rinv)
                 dfc3, rinv_fc = ops.lrp_gelu_bwd_h3(dp, sv["a"])
@@ -198,6 +202,8 @@ class RelevanceEngineH3:
             dqkv3, rinv_q = ops.lrp_rope_pack_h3(dq, dk, dv, m.cos, m.sin, B, S, Hq, Hkv, cfg.rotary_dim, m.q_scale,
                                                  post=sv["rs1"] if self.qwen else None)
             if self.qwen:
+                # (dx is re-split from its own row maxima at the next layer: bound-derived scales would compound -
+                # rinv_q, rinv_gu are themselves a-priori bounds - and lose the planes' range within a few layers)
                 dx = ops.linear_h3(dqkv3, t["wqkvT3"], t["a_qkvT"], rscale=rinv_q, residual=dy, colscale=L["ln1_w"])
             else:
                 dh1 = ops.linear_h3(dqkv3, t["wqkvT3"], t["a_qkvT"], rscale=rinv_q)

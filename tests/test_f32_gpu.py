@@ -162,6 +162,33 @@ def test_linear_h3_colscale(M, N, K):
     assert rel_err(y, ref) < 4e-6     # fp32 level at K up to 9728 (a CPU fp32 GEMM: ~2e-6 there)
 
 
+@pytest.mark.parametrize("M,N,K", [(32768, 896, 9728), (300, 896, 896), (2048, 1024, 640)])
+def test_linear_h3_colscale_planes(M, N, K):
+    """The column-scaled GEMM that also writes its result as h3 planes at bound-derived row scales (the AttnLRP dy):
+    the fp32 output unchanged, the planes the exact split of s_m * row m with s_m from the bound (CPU oracle), below
+    2^15, and rinv = 1 / s_m - the 256x224 kernel, the 128x128 kernel and the 256-wide generic path."""
+    x, w, r = rnd(M, K, seed=40), rnd(N, K, s=0.03, seed=41).bfloat16().float(), rnd(M, N, seed=42)
+    cs, rs = 1 + 0.3 * rnd(N, seed=43), torch.rand(M, generator=torch.Generator().manual_seed(44)) + 0.5
+    sx = R.h3_scale(x.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    a3, w3d = R.h3_act(x, sx).to(DEV), w3.to(DEV)
+    g = torch.Generator().manual_seed(45)
+    ba = (r.abs().amax(1) * (1 + torch.rand(M, generator=g))) / 32768   # |resid row| < 2^15 ba
+    bb = rs.clone()
+    bc = float(((x.abs().amax() * sx) * w.abs().sum(1).max() * cs.abs().max()) / sx)   # |product| / rs per row
+    args = dict(residual=r.to(DEV), rscale=rs.to(DEV), colscale=cs.to(DEV))
+    y0 = ops.linear_h3(a3, w3d, 1.0 / (sx * sw), **args)
+    y, pl, pr = ops.linear_h3(a3, w3d, 1.0 / (sx * sw), planes_bound=(ba.to(DEV), bb.to(DEV), bc), **args)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    _, want_pr = R.bound_planes(y.cpu(), ba, bb, bc)
+    # the bound may be formed with an fma on the device: a row exactly at a power of two may land one binade over
+    assert (pr.cpu() == want_pr).float().mean() > 0.999
+    assert torch.all((pr.cpu() == want_pr) | (pr.cpu() == 2 * want_pr) | (pr.cpu() == want_pr / 2))
+    assert torch.equal(pl.cpu(), R.h3_act(y.cpu() / pr.cpu().view(-1, 1), 1.0))
+    assert float(pl.float().abs().max()) < 2 ** 15
+
+
 @pytest.mark.parametrize("M,two_term", [(32768, True), (32768, False), (1000, True), (257, False)])
 def test_linear_h3_swiglu_raw(M, two_term):
     """One GEMM for the SwiGLU planes and the saved pre-activations (AttnLRP forward): the planes bit-identical to
