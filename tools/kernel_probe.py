@@ -37,7 +37,10 @@ def main():
     ap.add_argument("--kv-planes", type=int, default=0, help="attn: stage K / V^T h3 planes by LDS DMA")
     ap.add_argument("--save", default="", help="save the op's output tensors here (bit-exact A/B of two builds)")
     ap.add_argument("--compare", default="", help="compare the op's output bit for bit with a --save file")
+    ap.add_argument("--tile", type=int, default=0, help="force the GEMM tile (ops.set_gemm_tile; 0 = by shape)")
     a = ap.parse_args()
+    if a.tile:
+        ops.set_gemm_tile(a.tile)
     B, S, Hq, Hkv, H = a.B, a.S, 14, 2, 896
     g = torch.Generator().manual_seed(0)
     dev = "cuda"
@@ -134,7 +137,7 @@ def main():
         fn()
     en.record()
     torch.cuda.synchronize()
-    print(json.dumps({"op": a.op, "kv_planes": a.kv_planes, "B": B, "S": S,
+    print(json.dumps({"op": a.op, "kv_planes": a.kv_planes, "tile": a.tile, "B": B, "S": S,
                       "us_per_call": round(st.elapsed_time(en) / a.iters * 1e3, 2)}))
 
 
