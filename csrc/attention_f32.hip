@@ -341,16 +341,37 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
     if (kb > kmax) continue;
     // S^T = K Q^T over the 4 key blocks of 16
     f32x4_t st[4];
+    if constexpr (F16) {
+      // product-major over the four independent key blocks (each accumulator sees h3_dot's product order, so the
+      // scores are bit-identical to the block-major loop): consecutive MFMAs never wait on each other's result
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const int row = kt * 16 + ql;
-      st[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int kt = 0; kt < 4; ++kt) st[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t kf[NPL];
+        bf16x8_t kf[4][2];
 #pragma unroll
-        for (int pl = 0; pl < NPL; ++pl) kf[pl] = xfrag(lk + pl * XPL, row, 4 * ks + g);
-        st[kt] = plane_dot<F16>(kf, qp[ks], st[kt]);
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl) kf[kt][pl] = xfrag(lk + pl * XPL, kt * 16 + ql, 4 * ks + g);
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) st[kt] = mfma_h(kf[kt][1], qp[ks][0], st[kt]);
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) st[kt] = mfma_h(kf[kt][0], qp[ks][1], st[kt]);
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) st[kt] = mfma_h(kf[kt][0], qp[ks][0], st[kt]);
+      }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const int row = kt * 16 + ql;
+        st[kt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8_t kf[NPL];
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) kf[pl] = xfrag(lk + pl * XPL, row, 4 * ks + g);
+          st[kt] = plane_dot<F16>(kf, qp[ks], st[kt]);
+        }
       }
     }
     if (__builtin_expect(kb * 64 + 63 > q0 || kb * 64 + 63 >= S, 0)) {   // causal / sequence-end mask (scalar branch)
@@ -396,15 +417,29 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flash_attn_fwd_x6_kernel(cons
 #pragma unroll
       for (int r = 0; r < 4; ++r) { pv8[r] = st[2 * sk][r]; pv8[4 + r] = st[2 * sk + 1][r]; }
       bf16x8_t pp[NPL];
-      if constexpr (F16) split_frag_h1(pv8, pp[0], pp[1]);
-      else split_planes<F16>(pv8, 1.f, pp);
+      if constexpr (F16) {
+        split_frag_h1(pv8, pp[0], pp[1]);
+        bf16x8_t vf[4][2];   // product-major over the four d-blocks, as the scores above
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int row = dt * 16 + ql;
-        bf16x8_t vf[NPL];
+        for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-        for (int pl = 0; pl < NPL; ++pl) vf[pl] = xfrag(lv + pl * XPL, row, 4 * sk + g);
-        oacc[dt] = plane_dot<F16>(vf, pp, oacc[dt]);
+          for (int pl = 0; pl < 2; ++pl) vf[dt][pl] = xfrag(lv + pl * XPL, dt * 16 + ql, 4 * sk + g);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma_h(vf[dt][1], pp[0], oacc[dt]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma_h(vf[dt][0], pp[1], oacc[dt]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma_h(vf[dt][0], pp[0], oacc[dt]);
+      } else {
+        split_planes<F16>(pv8, 1.f, pp);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int row = dt * 16 + ql;
+          bf16x8_t vf[NPL];
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) vf[pl] = xfrag(lv + pl * XPL, row, 4 * sk + g);
+          oacc[dt] = plane_dot<F16>(vf, pp, oacc[dt]);
+        }
       }
     }
   }
