@@ -77,6 +77,13 @@ __device__ __forceinline__ int h3_acol(int kp, int K) {
   return (j == 0 ? K : 0) + (kp - j * K);
 }
 // Store s * v[0..3] at column `col` of an h3 activation row (plane width K): two 8-byte stores.
+// Nontemporal store (global_store ... nt) for the large streamed outputs that overflow the 256 MB Infinity Cache
+// anyway (the SwiGLU planes: 637 MB per bench GEMM): measured 2 % faster than plain stores on the power-limited
+// gate/up GEMM (profiles/r05/gemm_epilogue/probe_store_policy.log), bit-identical.
+template <class T>
+__device__ __forceinline__ void store_nt(T* p, const T& v) {
+  __builtin_nontemporal_store(v, p);
+}
 __device__ __forceinline__ void store_h3_4(f16_t* __restrict__ row, int K, int col, const float (&v)[4], float s) {
   const float x0 = v[0] * s, x1 = v[1] * s, x2 = v[2] * s, x3 = v[3] * s;
   const u32x2_t t0 = split2h_pk(x0, x1), t1 = split2h_pk(x2, x3);

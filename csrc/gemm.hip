@@ -186,7 +186,7 @@ __device__ __forceinline__ void swiglu_raw_store(const GemmArgs& a, const f32x4_
   if (m >= a.M) return;
   float* dst = a.raw + (size_t)m * a.N + n + 4 * g;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) *(f32x4_t*)(dst + 16 * j) = acc4[j] * f;
+  for (int j = 0; j < 4; ++j) store_nt((f32x4_t*)(dst + 16 * j), acc4[j] * f);   // 1.27 GB, read in the backward
 }
 
 // Exchange of two 16-byte chunks between lanes r and r ^ 8 of each 16-lane row (DPP row_ror:8): lanes r < 8 keep X
@@ -237,12 +237,12 @@ __device__ __forceinline__ void swiglu_h3_lines_4w(const GemmArgs& a, f32x4_t (&
     line_exchange8(L0, L1, lo8, LA, LB);
     const int ma = m0 + wm * 128 + i * 16 + (r & 7), mb = ma + 8;
     if (ma < a.M) {
-      *(u32x4_t*)(base + (size_t)ma * a.ldc) = HA;
-      *(u32x4_t*)(base + (size_t)ma * a.ldc + a.N / 2) = LA;
+      store_nt((u32x4_t*)(base + (size_t)ma * a.ldc), HA);
+      store_nt((u32x4_t*)(base + (size_t)ma * a.ldc + a.N / 2), LA);
     }
     if (mb < a.M) {
-      *(u32x4_t*)(base + (size_t)mb * a.ldc) = HB;
-      *(u32x4_t*)(base + (size_t)mb * a.ldc + a.N / 2) = LB;
+      store_nt((u32x4_t*)(base + (size_t)mb * a.ldc), HB);
+      store_nt((u32x4_t*)(base + (size_t)mb * a.ldc + a.N / 2), LB);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
