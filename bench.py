@@ -100,7 +100,10 @@ def parse():
     p.add_argument("--no-deep-pp", action="store_true",
                    help="N > 1: skip the secondary measurement of one N-stage pipeline over all the GPUs (value_ppN)")
     p.add_argument("--deep-pp-timeout", type=float, default=300.0,
-                   help="seconds the deep-pipeline measurement may take before it counts as hung")
+                   help="N > 1: seconds a secondary measurement (deep pipeline, transports) or the shutdown may go "
+                        "without progress before it counts as hung")
+    p.add_argument("--no-transports", action="store_true",
+                   help="N > 1: skip the short per-transport check (torch p2p / native RCCL / IPC peer copies)")
     p.add_argument("--json-out", default="")
     return p.parse_args()
 
@@ -189,20 +192,27 @@ def rank_devices(env) -> list:
     return out
 
 
-def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None, probe_sizes=()):
-    """Build the model/pipeline for ``dtype`` (random weights with ``values`` precision) and time ``timed_steps``
-    steps after ``warmup``.  Returns a dict."""
+def build_stage_model(a, env, cfg, dtype, pp, grid, plan, values=None):
+    """(model, provenance) of this rank: the whole model (one process) or its pipeline stage's layers."""
+    if not (env.world_size > 1 and pp > 1):
+        return build_model(cfg, env.device, dtype, seed=a.seed, values=values)
+    _, stage = grid.coords(env.rank)
+    return build_model(cfg, env.device, dtype, seed=a.seed, layers=plan.stage_layers(stage),
+                       with_embed=(stage == 0), with_head=(stage == pp - 1), values=values)
+
+
+def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None, probe_sizes=(), built=None):
+    """Build the model/pipeline for ``dtype`` (random weights with ``values`` precision; or use ``built`` =
+    ``build_stage_model``'s result, kept alive for the caller) and time ``timed_steps`` steps after ``warmup``.
+    Returns a dict."""
     dev = env.device
     world = env.world_size
     dist_pp = world > 1 and pp > 1
     bcfg = BoundaryConfig(a.codec, a.ratio, a.method)
+    model, prov = built if built is not None else build_stage_model(a, env, cfg, dtype, pp, grid, plan, values)
     if not dist_pp:
-        model, prov = build_model(cfg, dev, dtype, seed=a.seed, values=values)
         runner = LocalPipeline(model, plan, bcfg, use_graphs=not a.no_graphs)
     else:
-        _, stage = grid.coords(env.rank)
-        model, prov = build_model(cfg, dev, dtype, seed=a.seed, layers=plan.stage_layers(stage),
-                                  with_embed=(stage == 0), with_head=(stage == pp - 1), values=values)
         runner = DistributedPipeline(model, plan, bcfg, grid, env.rank, use_graphs=not a.no_graphs,
                                      transport=a.transport)
     probe = None
@@ -230,10 +240,16 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
         through the local stages."""
         idx = [(first_step * per_step + i) % len(pool) for i in range(nsteps * per_step)]
         if not dist_pp:
+            dump = [] if os.environ.get("EDGE_DUMP_NLL") else None
             for j in idx:
                 wn = runner.run_batch(pool[j])
                 nll_acc[0] += (wn.double() * pool_w[j]).sum()   # device-side accumulation: no host sync
                 nll_acc[1] += pool_w[j].sum()
+                if dump is not None:
+                    dump.append(wn.detach().double().clone())
+            if dump:   # debug: per-micro-batch per-window NLL, named like DistributedPipeline's dumps
+                n = run_steps.dumps = getattr(run_steps, "dumps", 0) + 1
+                torch.save(torch.stack([d.cpu() for d in dump]), f"{os.environ['EDGE_DUMP_NLL']}.local.{n - 1}.pt")
         else:
             acc, rep = runner.evaluate([pool[j] for j in idx], timing=timing)
             nll_acc[0] += acc.total_nll
@@ -282,7 +298,7 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
         wires = runner.wire_bytes_per_token()
     if dist_pp:
         runner.close()
-    del runner, model
+    del runner, model, built
     gc.collect()
     if dev.type == "cuda":
         torch.cuda.empty_cache()
@@ -409,12 +425,21 @@ def main():
         # and the launcher - or the self-launching parent - exits non-zero)
         torch.distributed.barrier()
     emit = Emitter(out, a.json_out if env.is_main else "", env.is_main)
+    if not env.is_dist:
+        emit()
+        return
+    # N > 1: secondary measurements and the shutdown run under one watchdog; a hang anywhere after this point still
+    # prints the headline (with the hung measurement marked) and exits 70, an exception is recorded in its field
+    guard = Guard(env, emit, a.deep_pp_timeout)
     if dist_pp and world != pp and not a.no_deep_pp:
-        deep_pipeline(a, env, cfg, dtype, values, spec, emit)
+        key = f"pp{world}"
+        res = guard.run(key, lambda: deep_pipeline(a, env, cfg, dtype, values, spec))
+        emit.out[f"value_{key}"] = res.pop("value") if res else None
+        emit.out[key] = res if res else {"error": guard.last_error}
+    if dist_pp and not a.no_transports:
+        emit.out["transports"] = transports_check(a, env, cfg, dtype, values, spec, pp, grid, plan, guard)
     emit()
-    if env.is_dist:
-        torch.distributed.barrier()
-        torch.distributed.destroy_process_group()
+    guard.close()
 
 
 def tuning_mode() -> bool:
@@ -423,7 +448,7 @@ def tuning_mode() -> bool:
 
 class Emitter:
     """Prints the one JSON line (rank 0) exactly once: normally at the end of the run, or from the watchdog of the
-    secondary deep-pipeline measurement when that hangs (the headline is never lost; the process then exits 70)."""
+    secondary measurements when one of them hangs (the headline is never lost; the process then exits 70)."""
 
     def __init__(self, out: dict, path: str, main: bool):
         import threading
@@ -442,55 +467,161 @@ class Emitter:
                     json.dump(self.out, f, indent=1)
 
 
-def deep_pipeline(a, env, cfg, dtype, values, spec, emit: Emitter) -> None:
+class Guard:
+    """Runs the secondary measurements of an N > 1 run (``run``) and the final shutdown (``close``) under ONE
+    watchdog that stays armed until the process group is destroyed.
+
+    * An exception on any rank is recorded, never raised: the ranks agree on the outcome through the store (one key
+      per rank and measurement), not through a collective, so a rank that failed early can never pair its agreement
+      with a collective that the others are still inside (``measure`` gathers stage reports).
+    * A hang (a measurement or the shutdown still running ``timeout`` seconds after its last progress) prints the JSON
+      line - the headline plus ``{"error": ...}`` in the hung measurement's field - and exits: 0 for a secondary
+      measurement (every rank's watchdog fires, the headline is complete), 70 for the shutdown.  A rank that raised
+      while its peers sit in a collective of the same measurement ends this way too: collectives cannot be
+      cancelled, the watchdog bounds the wait."""
+
+    def __init__(self, env, emit: Emitter, timeout: float):
+        from llm_inference_in_distributed_edge_networks_amd.utils.watchdog import Watchdog
+        self.env, self.emit, self.timeout = env, emit, timeout
+        self.current: str | None = None
+        self.last_error = ""
+        self._n = 0
+        self.wd = Watchdog(timeout, "bench-secondary", on_timeout=self._hang).start()
+
+    def _hang(self):
+        """Watchdog: the JSON line with the hung measurement marked, then exit - 0 when a secondary measurement hung
+        (the headline is complete and valid, the failure is in the JSON), 70 when the shutdown did."""
+        key = self.current or "shutdown"
+        msg = f"still running after {self.timeout:.0f} s (rank {self.env.rank})"
+        if key.startswith("pp"):
+            self.emit.out[f"value_{key}"] = None
+        if key.startswith("transports."):
+            self.emit.out.setdefault("transports", {})[key.split(".", 1)[1]] = {"error": msg}
+        else:
+            self.emit.out[key] = {"error": msg}
+        self.emit()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(70 if key == "shutdown" else 0)
+
+    def agree(self, err: str | None) -> list:
+        """Every rank's error (None = ok) for the current measurement, exchanged through the store."""
+        store = torch.distributed.distributed_c10d._get_default_store()
+        base = f"edge_bench/{self._n}/{self.current}"
+        store.set(f"{base}/{self.env.rank}", json.dumps(err))
+        return [json.loads(store.get(f"{base}/{r}")) for r in range(self.env.world_size)]
+
+    def run(self, key: str, fn):
+        """``fn()``'s result, or None (``last_error`` says why) if it failed on any rank."""
+        self.current = key
+        self._n += 1
+        self.wd.beat()
+        err = res = None
+        try:
+            _test_hook(key, self.env.rank)
+            res = fn()
+        except Exception as e:   # recorded; the headline stands
+            err = f"{type(e).__name__}: {e}"[:300]
+        self.wd.beat()
+        errs = self.agree(err)
+        self.current = None
+        bad = [f"rank {i}: {e}" for i, e in enumerate(errs) if e]
+        self.last_error = "; ".join(bad)[:600]
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        return None if bad else res
+
+    def close(self):
+        self.wd.beat()
+        self.current = "shutdown"
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+        self.wd.stop()
+
+
+def _test_hook(key: str, rank: int) -> None:
+    """Tuning-mode-only fault injection into a secondary measurement: EDGE_BENCH_FAIL_SECONDARY / _HANG_SECONDARY =
+    "<key>:<rank>" (rank "*": every rank) makes that rank raise / block inside measurement <key> (tests of Guard's error
+    and hang paths)."""
+    if not tuning_mode():
+        return
+    for var, hang in (("EDGE_BENCH_FAIL_SECONDARY", False), ("EDGE_BENCH_HANG_SECONDARY", True)):
+        v = os.environ.get(var, "")
+        if v and v.rsplit(":", 1)[0] == key and v.rsplit(":", 1)[1] in ("*", str(rank)):
+            if hang:
+                time.sleep(3600)
+            raise RuntimeError(f"{var}: rank {rank} fails {key} on purpose")
+
+
+def deep_pipeline(a, env, cfg, dtype, values, spec) -> dict:
     """N > 1, after the headline: the same step as ONE N-stage pipeline over all the GPUs (BASELINE config 4 at N = 4,
     config 5's shape at N = 8: cost-balanced stages, every boundary quantized), on the same process group and
     transport.  Reported as ``value_pp{N}`` plus its stage breakdown and p2p probe in ``pp{N}``; the primary fields
-    are unchanged.  An exception on any rank is recorded as ``{"error": ...}``; a hang (the measurement
-    still running after ``--deep-pp-timeout`` s) prints the JSON line with the error and exits 70."""
-    from llm_inference_in_distributed_edge_networks_amd.utils.watchdog import Watchdog
+    are unchanged.  Runs under ``Guard`` (errors recorded, hangs reported)."""
     world = env.world_size
-    key = f"pp{world}"
     grid = Grid(world, world)
     plan = PipelinePlan.balanced(cfg, world, a.max_length, a.stride / a.max_length)
     steps, warm = max(2, a.steps // 2), max(1, a.warmup // 2)
-
-    def on_hang():
-        emit.out[f"value_{key}"] = None
-        emit.out[key] = {"error": f"still running after {a.deep_pp_timeout:.0f} s (rank {env.rank})"}
-        emit()
-        sys.stdout.flush()
-        os._exit(70)
-
-    wd = Watchdog(a.deep_pp_timeout, f"bench-{key}", on_timeout=on_hang).start()
-    err = None
-    res = None
     sub = argparse.Namespace(**vars(a))
     sub.microbatches = 4 * world          # weak scaling: every GPU does 4 full-model micro-batches per step
     t0 = time.time()
-    try:
-        msg_bytes = C.message_bytes(spec, a.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
-        res = measure(sub, env, cfg, dtype, world, grid, plan, steps, warm, values,
-                      probe_sizes=(1 << 20, int(msg_bytes)))
-    except Exception as e:   # recorded; the headline stands
-        err = f"{type(e).__name__}: {e}"[:300]
-    wd.beat()
-    errs = [None] * world
-    torch.distributed.all_gather_object(errs, err)
-    wd.stop()
-    bad = [f"rank {i}: {e}" for i, e in enumerate(errs) if e]
-    if bad or res is None:
-        emit.out[f"value_{key}"] = None
-        emit.out[key] = {"error": "; ".join(bad)[:600] or "no result"}
-        return
+    msg_bytes = C.message_bytes(spec, a.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
+    res = measure(sub, env, cfg, dtype, world, grid, plan, steps, warm, values, probe_sizes=(1 << 20, int(msg_bytes)))
     tok = sub.microbatches * a.batch * a.max_length   # dp = 1
-    emit.out[f"value_{key}"] = round(tok * steps / res["dt"], 1)
-    emit.out[key] = {
+    return {
+        "value": round(tok * steps / res["dt"], 1),
         "parallelism": f"pp{world}xdp1", "steps": steps, "warmup": warm,
         "ms_per_step": round(1000 * res["dt"] / steps, 3), "global_batch": sub.microbatches * a.batch,
         "stage_layers": [[r.start, r.stop - 1] for r in (plan.stage_layers(s) for s in range(world))],
         "wire_bytes_per_token": [round(w, 2) for w in res["wires"]], "ppl_random_weights": res["ppl"],
         "stages": res["stages"], "p2p": res["p2p"], "wall_s": round(time.time() - t0, 2)}
+
+
+TRANSPORTS = ("torch", "rccl", "ipc")
+
+
+def transports_check(a, env, cfg, dtype, values, spec, pp, grid, plan, guard: Guard) -> dict:
+    """N > 1: the native stage hand-offs on the real process layout.  One short pp step (the headline's
+    grid and codec, ``--batch`` capped at 8 windows, 1 warmup + 1 timed step) per transport on ONE stage model: first
+    torch.distributed p2p (the reference PPL), then the native RCCL wrapper (``RcclComm``: a 2-rank communicator per
+    pipeline edge bootstrapped through the store) and the peer-copy transport (``IpcP2P``).  Per transport: the p2p
+    probe rows of every edge, ``ms_per_step``, the PPL and whether it equals torch-p2p's (rel 1e-9: the same windows
+    through the same graphs, so any difference is a transport bug).  A transport that fails (RCCL refuses ranks sharing
+    a GPU) or hangs is recorded as ``{"error": ...}``."""
+    t0 = time.time()
+    sub = argparse.Namespace(**vars(a))
+    sub.batch = min(a.batch, 8)
+    sub.microbatches = 2 * pp
+    msg_bytes = C.message_bytes(spec, sub.batch, a.max_length, cfg.hidden_size, a.ratio, dtype)
+    out: dict = {"what": "one short pp step per stage hand-off (torch.distributed p2p = reference PPL); PPL must be "
+                         "equal at rel 1e-9", "batch": sub.batch, "microbatches": sub.microbatches}
+    built = guard.run("transports.model", lambda: build_stage_model(a, env, cfg, dtype, pp, grid, plan, values))
+    if built is None:
+        out["error"] = guard.last_error
+        return out
+    ref_ppl = None
+    for t in TRANSPORTS:
+        if t != "torch" and env.device.type != "cuda":
+            out[t] = {"skipped": "CPU ranks: the native transports need GPUs"}
+            continue
+        sub_t = argparse.Namespace(**vars(sub))
+        sub_t.transport = t
+        r = guard.run(f"transports.{t}", lambda: measure(sub_t, env, cfg, dtype, pp, grid, plan, 1, 1, values,
+                                                         probe_sizes=(1 << 20, int(msg_bytes)), built=built))
+        if r is None:
+            out[t] = {"error": guard.last_error}
+            continue
+        row = {"ms_per_step": round(1000 * r["dt"], 3), "ppl_random_weights": r["ppl"], "p2p": r["p2p"]}
+        if t == "torch":
+            ref_ppl = r["ppl"]
+        elif ref_ppl:
+            row["rel_diff_vs_torch"] = abs(r["ppl"] - ref_ppl) / ref_ppl
+            row["ppl_equal_torch"] = row["rel_diff_vs_torch"] <= 1e-9
+        out[t] = row
+    del built
+    out["wall_s"] = round(time.time() - t0, 2)
+    return out
 
 
 if __name__ == "__main__":

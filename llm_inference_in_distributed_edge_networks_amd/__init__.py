@@ -13,3 +13,7 @@ oracle), ``codec`` (boundary wire format), ``importance`` (scorers),
 sweeps), ``relevance`` (AttnLRP head calibration), ``utils``.
 """
 __version__ = "0.1.0"
+
+from .utils import poison as _poison  # noqa: E402
+
+_poison.from_env()   # EDGE_POISON=1: NaN / 0xFF-filled torch.empty (uninitialised-read detection)

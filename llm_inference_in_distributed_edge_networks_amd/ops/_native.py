@@ -14,6 +14,8 @@ import os
 
 import torch
 
+from ..utils import poison as _poison
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # EDGE_KERNEL_LIB: load another build of the library (A/B of two kernel builds in one GPU session)
 LIB_PATH = os.environ.get("EDGE_KERNEL_LIB") or os.path.join(os.path.dirname(_HERE), "_native", "libedge_kernels.so")
@@ -86,6 +88,9 @@ _SIGS = {
     "edge_row_rstd_f32": [c_p, c_p, c_i, c_i, c_f, c_i, c_p],
     "edge_lrp_ln_bwd_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p],
     "edge_group_absprod": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p],
+    # debug (csrc/debug.hip): LDS + register-file poison before every kernel under EDGE_POISON=2
+    "edge_poison_lds": [c_p],
+    "edge_poison_lds_bytes": [],
 }
 
 
@@ -133,7 +138,15 @@ def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
 
+_NO_LAUNCH = {"edge_gemm_set_tile", "edge_gemm_ssq_parts", "edge_poison_lds", "edge_poison_lds_bytes"}
+
+
 def call(name: str, *args) -> None:
+    if _poison.level() >= 2 and name not in _NO_LAUNCH:
+        # EDGE_POISON=2: every LDS byte and register of the chip is all-ones (NaN) when this kernel starts
+        rc = lib().edge_poison_lds(stream())
+        if rc != 0:
+            raise RuntimeError(f"edge_poison_lds failed with HIP error {rc}")
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with HIP error {rc}")

@@ -385,6 +385,9 @@ class DistributedPipeline:
         # send of i overlaps the compute of i + 1; before slot i % 2 is replayed again (i + 2) the stream waits
         # for the send that still reads it (GPU-side wait, no host sync, no copy of the message)
         in_flight: list = [None, None]
+        # EDGE_DUMP_NLL=<prefix>: the last stage saves every micro-batch's per-window NLL (debug: a wrong PPL is then
+        # traced to the windows / micro-batches that differ from a reference run)
+        dump = [] if (self.next is None and os.environ.get("EDGE_DUMP_NLL")) else None
         recv_next = self._post_recv(mine[0]) if (self.prev is not None and mine) else None
         t0 = time.perf_counter()
         if timing:
@@ -442,6 +445,8 @@ class DistributedPipeline:
                 w = b.weights.to(self.device)
                 acc_local[0] += (out.double() * w).sum()
                 acc_local[1] += w.sum()
+                if dump is not None:
+                    dump.append(out.detach().double().clone())
         for reqs in in_flight + getattr(self, "_eager_sends", []):
             for r in reqs or ():
                 r.wait()
@@ -460,6 +465,10 @@ class DistributedPipeline:
                           microbatches=len(evs))
         if wd:
             wd.stop()
+        if dump:
+            path = f"{os.environ['EDGE_DUMP_NLL']}.rank{self.rank}.{getattr(self, '_dumps', 0)}.pt"
+            self._dumps = getattr(self, "_dumps", 0) + 1
+            torch.save(torch.stack([d.cpu() for d in dump]), path)
         self.runner.stats.compute_s += time.perf_counter() - t0
         if hasattr(self.tr, "quiesce"):      # peer-copy transport: no flow-control message left unmatched
             self.tr.quiesce()

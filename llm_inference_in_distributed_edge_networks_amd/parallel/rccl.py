@@ -74,8 +74,16 @@ class _Channel:
         L = lib()
         h = ctypes.c_void_p()
         _ok(L.edge_rccl_init(ctypes.byref(h), len(ranks), unique_id, ranks.index(me), device), "ncclCommInitRank")
-        self.h, self.ranks = h, ranks
-        self.stream = torch.cuda.ExternalStream(L.edge_rccl_stream(h), device=torch.device("cuda", device))
+        self.h, self.ranks, self.device = h, ranks, device
+        self._stream = None
+
+    @property
+    def stream(self):
+        """The channel's HIP stream as a torch stream (created on first use)."""
+        if self._stream is None:
+            self._stream = torch.cuda.ExternalStream(lib().edge_rccl_stream(self.h),
+                                                     device=torch.device("cuda", self.device))
+        return self._stream
 
     def peer_index(self, peer: int) -> int:
         return self.ranks.index(peer)

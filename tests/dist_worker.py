@@ -215,3 +215,71 @@ def run_driver(rank, world, port, params, crash_at, out_dir):
     except KeyboardInterrupt:
         pass
     shutdown()
+
+
+class FakeRcclLib:
+    """Stand-in for libedge_comm.so (ctypes): records every call instead of touching RCCL / HIP."""
+
+    def __init__(self, rank):
+        self.rank, self.n_ids, self.inits, self.destroyed = rank, 0, [], []
+
+    def edge_rccl_id_bytes(self):
+        return 128
+
+    def edge_rccl_unique_id(self, buf):
+        self.n_ids += 1
+        buf.value = f"uid-made-by-{self.rank}-#{self.n_ids}".encode()
+        return 0
+
+    def edge_rccl_init(self, href, nranks, uid, idx, device):
+        h = 1000 * self.rank + len(self.inits) + 1
+        href._obj.value = h
+        self.inits.append({"h": h, "nranks": nranks, "uid": uid.rstrip(b"\0").decode(), "idx": idx, "device": device})
+        return 0
+
+    def edge_rccl_destroy(self, h):
+        self.destroyed.append(h.value if hasattr(h, "value") else h)
+        return 0
+
+
+def run_rccl_bootstrap(rank, world, port, out_path):
+    """RcclComm's store bootstrap on a pp chain 0-1-..-(world-1) with the RCCL library mocked: two constructions in a
+    row, every rank reports its namespace, channels (in init order), the ids / comm indices it initialised with, and
+    whether the store keys it read are gone."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from llm_inference_in_distributed_edge_networks_amd.parallel import init_distributed, shutdown
+    from llm_inference_in_distributed_edge_networks_amd.parallel import rccl as R
+    init_distributed("cpu", timeout_s=60)
+    fake = FakeRcclLib(rank)
+    R._lib = fake
+    gens = []
+    orig_ns = R.RcclComm._namespace
+
+    def ns():
+        g = orig_ns()
+        gens.append(g)
+        return g
+
+    R.RcclComm._namespace = staticmethod(ns)
+    prev = rank - 1 if rank > 0 else None
+    nxt = rank + 1 if rank < world - 1 else None
+    report = []
+    for _ in range(2):
+        start = len(fake.inits)
+        comm = R.RcclComm(rank, world, device=rank % 8, peers=[prev, nxt])
+        chans = list(comm.channels.keys())
+        report.append({"gen": gens[-1], "channels": [list(k) for k in chans], "inits": fake.inits[start:],
+                       "peer_index": {str(p): comm.channels[R.channel_key(rank, p)].peer_index(p)
+                                      for p in (prev, nxt) if p is not None},
+                       "h": [comm.channels[k].h.value for k in chans]})
+        dist.barrier()
+        store = dist.distributed_c10d._get_default_store()
+        report[-1]["keys_left"] = [f"{a}-{b}" for a, b in chans
+                                   if store.check([f"edge_rccl/{gens[-1]}/{a}-{b}"])]
+        comm.close()
+        report[-1]["destroyed"] = list(fake.destroyed)
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(report, f)
+    shutdown()

@@ -77,6 +77,14 @@ def test_bench_contract_cpu(n):
         _check_deep(d, n)
     else:
         assert "value_pp2" not in d and "pp2" not in d
+    if n > 1:   # the per-transport check: torch p2p timed with its probe rows; the native ones need GPUs
+        tr = d["transports"]
+        assert tr["torch"]["ppl_random_weights"] > 1 and tr["torch"]["ms_per_step"] > 0
+        assert len(tr["torch"]["p2p"]) == 2 * dp
+        assert tr["rccl"] == tr["ipc"] == {"skipped": "CPU ranks: the native transports need GPUs"}
+        assert tr["wall_s"] >= 0
+    else:
+        assert "transports" not in d
 
 
 def _check_deep(d, n):
@@ -201,3 +209,26 @@ def test_visible_gpu_count_without_hip(monkeypatch):
     src = open(os.path.join(ROOT, "bench.py")).read()
     launch = src[src.index("def launch_mode"):src.index("def self_launch")]
     assert "torch.cuda" not in launch
+
+
+@pytest.mark.parametrize("hook,rc", [("EDGE_BENCH_FAIL_SECONDARY=transports.torch:*", 0),
+                                     ("EDGE_BENCH_HANG_SECONDARY=transports.torch:1", 0)])
+def test_bench_secondary_failure_keeps_headline(hook, rc):
+    """A secondary measurement that raises on every rank is recorded in its field and the run exits 0; one that hangs
+    on one rank (its peers then wait in a collective) ends through the watchdog: the JSON line still carries the
+    headline with the hung measurement marked, and every rank exits (bench.Guard)."""
+    k, v = hook.split("=")
+    env = dict(_env(), EDGE_TUNING="1", **{k: v})
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port())] + BENCH +
+                       ["--gpus", "2", "--deep-pp-timeout", "10"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == rc, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["value"] > 0 and d["ppl_random_weights"] > 1
+    assert "error" in d["transports"]["torch"]
+    if "FAIL" in k:
+        assert "fails transports.torch on purpose" in d["transports"]["torch"]["error"]
+        assert "skipped" in d["transports"]["rccl"]
+    else:
+        assert "still running after 10 s" in d["transports"]["torch"]["error"]
