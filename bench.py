@@ -63,6 +63,7 @@ METRIC = "WikiText-2 PPL + inter-stage bytes/token, Qwen2-0.5B 2-stage split; to
 # Reference throughput on its own hardware: the Qwen2 sweep ran 1 eager + 100 split fp32 forwards of
 # 512 tokens per window at 16.03-16.35 s/window on a T4 = ~3.2k forward tokens/s.
 BASELINE_TOKENS_PER_S = 3200.0
+T4_SWEEP_S_PER_WINDOW = 16.19   # the same notebook's sweep: 16.03-16.35 s per window
 DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
 
 
@@ -95,6 +96,8 @@ def parse():
                         "Qwen2-0.5B checkpoint the reference upcasts to fp32 (torch_dtype bfloat16); fp32 = full fp32 "
                         "random values (reported as value_fp32_weights)")
     p.add_argument("--no-fp32-weights", action="store_true", help="skip the fp32-valued-weights measurement")
+    p.add_argument("--no-sweep", action="store_true",
+                   help="N = 1: skip the timing of the reference's notebook sweep (notebook_sweep)")
     p.add_argument("--no-hf-compare", action="store_true",
                    help="skip the same-node reference-path measurement (HF transformers + eager, N = 1 only)")
     p.add_argument("--no-deep-pp", action="store_true",
@@ -305,6 +308,55 @@ def measure(a, env, cfg, dtype, pp, grid, plan, timed_steps, warmup, values=None
     return {"dt": dt, "ppl": ppl, "prov": prov, "stages": stage_reports, "p2p": probe, "wires": wires}
 
 
+def notebook_sweep(a, env, cfg, dtype, values, windows: int = 64, batch: int = 32) -> dict:
+    """The reference's own workload, timed on this GPU: the Qwen2 notebook sweep (``Notebooks/qwen2-0.5B_experiment.ipynb``
+    cells 8-12, ``Experiments/Qwen2-0.5B/main.py:151-197``): per window 4 importance methods x boundary layers
+    [22, 18, 3, 23, 11] x ratios [0, .25, .5, .75, 1] with the Q1 one-global-scale int4 quantizer, i.e. the 1 eager + 100
+    split forwards the reference runs per window, here through ``SweepEngine`` (one shared prefix forward per window
+    batch, the (method, ratio) variants forked at each boundary) in the bench's precision.  ``windows`` windows after one
+    warmup batch (graph capture); the reference ran 16.03-16.35 s/window on a T4.  Never fails the
+    bench: an error is recorded instead."""
+    from llm_inference_in_distributed_edge_networks_amd.eval.sweep import SweepConfig, SweepEngine
+    t_all = time.time()
+    try:
+        model, _ = build_model(cfg, env.device, dtype, seed=a.seed, values=values)
+        layers = [22, 18, 3, 23, 11] if cfg.num_layers == 24 else sorted({1, cfg.num_layers - 2})
+        hw = torch.full((cfg.num_layers, cfg.num_heads), 1.0 / cfg.num_heads)
+        sc = SweepConfig(["regular_importance", "weighted_importance", "last_row", "aggregate_till"], layers,
+                         [0, 0.25, 0.5, 0.75, 1], codec="ref_int4_global", head_weights=hw)
+        toks = synthetic_stream(299_078, cfg.vocab_size, a.seed + 1)
+        wins = [w for w in sliding_windows(toks.shape[1], a.max_length, a.stride) if w.length == a.max_length]
+        bl = [b.to(env.device) for b in batches(toks, wins[: windows + 2 * batch], batch)]
+        warm = SweepEngine(model, sc)
+        for b in bl[:2]:              # warmup: an eager prefix, then its HIP-graph capture
+            warm.run_batch(b)
+        if env.device.type == "cuda":
+            torch.cuda.synchronize()
+        eng = SweepEngine(model, sc)  # fresh accumulators, the captured prefix graph kept
+        eng._graphs = warm._graphs
+        t0 = time.perf_counter()
+        for b in bl[2:]:
+            eng.run_batch(b)
+        ppl = eng.ppl()               # host sync: every window's 100 configurations done
+        if env.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        n = eng.windows_done
+        out = {"what": f"notebook sweep: 4 methods x layers {layers} x ratios [0,.25,.5,.75,1], ref_int4_global "
+                       f"(Q1): {int(ppl.numel())} split configurations per window + the importance forward",
+               "windows": n, "seconds": round(dt, 3), "windows_per_s": round(n / dt, 2),
+               "s_per_window": round(dt / n, 5), "configs_per_window": int(ppl.numel()),
+               "ppl_ratio0_random_weights": float(ppl.reshape(-1)[0]), "wall_s_incl_build": None}
+        del eng, warm, model, bl
+    except Exception as e:   # the headline stands without it
+        out = {"error": f"{type(e).__name__}: {e}"[:300]}
+    gc.collect()
+    if env.device.type == "cuda":
+        torch.cuda.empty_cache()
+    out["wall_s_incl_build"] = round(time.time() - t_all, 2)
+    return out
+
+
 def same_node_reference(a, cfg, dev) -> dict:
     """The reference's own computation (HF transformers + PyTorch eager, fp32: importance forward with attention maps,
     then the layer-wise split forward with the boundary quantized) timed on this GPU right after our run, one window
@@ -366,6 +418,9 @@ def main():
         fp32w = measure(a, env, cfg, dtype, pp, grid, plan, a.steps, a.warmup, None)
     if not a.no_bf16 and dtype == torch.float32 and env.device.type == "cuda":
         second = measure(a, env, cfg, torch.bfloat16, pp, grid, plan, a.steps, a.warmup, values)
+    sweep = None
+    if world == 1 and not a.no_sweep:
+        sweep = notebook_sweep(a, env, cfg, dtype, values)
     hf = None   # last, so that nothing of it can touch the framework's own measurements
     if world == 1 and not a.no_hf_compare and env.device.type == "cuda":
         hf = same_node_reference(a, cfg, env.device)
@@ -411,6 +466,13 @@ def main():
         out["ppl_random_weights_bf16"] = second["ppl"]
         if second["stages"]:
             out["stages_bf16"] = second["stages"]
+    if sweep is not None:   # the reference's own workload (101 forwards per window), through the sweep engine
+        out["notebook_sweep"] = sweep
+        if "windows_per_s" in sweep:
+            out["sweep_windows_per_s"] = sweep["windows_per_s"]
+            out["sweep_s_per_window"] = sweep["s_per_window"]
+            out["sweep_s_per_window_t4"] = T4_SWEEP_S_PER_WINDOW
+            out["sweep_speedup_vs_t4"] = round(T4_SWEEP_S_PER_WINDOW / sweep["s_per_window"], 1)
     if hf is not None:
         out["same_node_reference_path"] = hf
         for k in ("batch1", "batch64"):

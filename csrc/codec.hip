@@ -359,13 +359,31 @@ __device__ __forceinline__ void grp_pack8(uint8_t* __restrict__ row, const Codec
   grp_store(row + grp_offset(plan, g) + sub * bits, w, bits);
   if (sub == 0) *(float*)(row + a.grp_code_bytes + 4 * g) = s;
 }
+__device__ __forceinline__ bool grp_bits_ok(int b) { return b == 2 || b == 3 || b == 4 || b == 5 || b == 6 || b == 8; }
 __device__ __forceinline__ void grp_unpack8(const uint8_t* __restrict__ row, const CodecArgs& a, int col,
                                             float (&o)[8]) {
   const int lane = threadIdx.x & 63;
   const uint8_t* plan = a.msg + a.off_plan;
-  const int g = col >> 6, bits = plan[g];
+  const int g = col >> 6;
   const int sub = lane & 7;
-  const uint64_t w = grp_load(row + grp_offset(plan, g) + sub * bits, bits);
+  // the plan bytes come from the message: a width outside GROUP_BITS (a corrupt or version-mismatched message) or a
+  // group stream reaching past the row's code bytes decodes to NaN - loud - instead of a shift by 32 or a read past
+  // the row (invalid widths count 0 bytes in the offset)
+  int off = 0;
+  bool bad = false;
+  for (int i = 0; i < g; ++i) {
+    const int b = plan[i];
+    bad |= !grp_bits_ok(b);
+    off += grp_bits_ok(b) ? 8 * b : 0;
+  }
+  const int bits = plan[g];
+  bad |= !grp_bits_ok(bits) || off + 8 * bits > a.grp_code_bytes;
+  if (bad) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = __builtin_nanf("");
+    return;
+  }
+  const uint64_t w = grp_load(row + off + sub * bits, bits);
   const float s = *(const float*)(row + a.grp_code_bytes + 4 * g);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {

@@ -15,6 +15,7 @@ import os
 import torch
 
 WIKITEXT2_TEST_TOKENS = 299_078
+LAST_EXCLUDED = 0   # extra train-large files dropped as copies of held-out (eval) files by the last local_text_bytes
 
 
 def synthetic_stream(num_tokens: int, vocab_size: int, seed: int = 0) -> torch.Tensor:
@@ -61,10 +62,31 @@ def local_text_bytes(split: str = "eval", root: str = "", max_bytes: int = 256 <
         raise FileNotFoundError(f"no python sources under {root}")
     pick = [f for i, f in enumerate(files) if (i % 10 == 0) == (split == "eval")]
     if split == "train-large":
+        import hashlib
         import site
+        global LAST_EXCLUDED
         roots = [d for d in {*site.getsitepackages(), os.path.join(root, "site-packages")} if os.path.isdir(d)]
         extra = sorted({f for d in roots for f in glob.glob(os.path.join(d, "**", "*.py"), recursive=True)})
-        pick += [f for f in extra if os.path.getsize(f) < 200_000]
+        extra = [f for f in extra if os.path.getsize(f) < 200_000]
+        # packages vendor copies of stdlib modules (setuptools/_distutils, pip/_vendor, backports): drop every extra
+        # file whose content equals a held-out (eval) file, or whose path ends in an eval file's stdlib-relative path
+        evf = [f for i, f in enumerate(files) if i % 10 == 0]
+
+        def digest(f):
+            try:
+                with open(f, "rb") as fh:
+                    return hashlib.sha1(fh.read()).hexdigest()
+            except OSError:
+                return None
+        ev_hash = {digest(f) for f in evf} - {None}
+        ev_tail = {os.path.relpath(f, root) for f in evf}
+
+        def tails(f):   # every path suffix of f made of whole components
+            parts = f.split(os.sep)
+            return {os.sep.join(parts[i:]) for i in range(1, len(parts))}
+        keep = [f for f in extra if digest(f) not in ev_hash and not (tails(f) & ev_tail)]
+        LAST_EXCLUDED = len(extra) - len(keep)
+        pick += keep
     buf = bytearray()
     for f in pick:
         if len(buf) >= max_bytes:

@@ -104,16 +104,27 @@ def make_batch(tokens: torch.Tensor, wins: list) -> WindowBatch:
         weights=torch.tensor([w.weight for w in wins], dtype=torch.float64))
 
 
-def batches(tokens: torch.Tensor, wins: list, batch_size: int):
-    """Group consecutive equal-length windows into batches of at most ``batch_size``."""
+def with_bos(batch: WindowBatch, bos: int) -> WindowBatch:
+    """The batch with every window's first input token replaced by ``bos`` (a fixed sink / start-of-window token, as
+    the byte surrogate is trained with: ``tools/train_tiny_lm.py --bos``).  Position 0 is never a target, so the
+    scored rows and their targets are unchanged."""
+    ids = batch.ids.clone()
+    ids[:, 0] = bos
+    return WindowBatch(ids, batch.windows, batch.rows, batch.targets, batch.row_window, batch.n_rows, batch.weights)
+
+
+def batches(tokens: torch.Tensor, wins: list, batch_size: int, bos: int | None = None):
+    """Group consecutive equal-length windows into batches of at most ``batch_size`` (``bos``: see ``with_bos``)."""
     cur = []
     for w in wins:
         if cur and (len(cur) == batch_size or w.length != cur[0].length):
-            yield make_batch(tokens, cur)
+            b = make_batch(tokens, cur)
+            yield b if bos is None else with_bos(b, bos)
             cur = []
         cur.append(w)
     if cur:
-        yield make_batch(tokens, cur)
+        b = make_batch(tokens, cur)
+        yield b if bos is None else with_bos(b, bos)
 
 
 def segment_mean(values: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:

@@ -451,3 +451,22 @@ def test_group_codec_gpu_equals_cpu(name, dtype, plan):
         assert torch.equal(y_gpu, y_cpu)
     else:
         assert (y_gpu - y_cpu).abs().max() <= 1e-5 * y_cpu.abs().max() + 1e-6
+
+
+@pytest.mark.parametrize("bad", [0, 7, 255])
+def test_group_codec_gpu_rejects_corrupt_plan(bad):
+    """A message whose plan byte holds a width outside GROUP_BITS (corrupt / version-mismatched) decodes to NaN from
+    that group on - loudly, without a shift-by-32 or a read past the row - while the groups before it still decode."""
+    from llm_inference_in_distributed_edge_networks_amd.codec.wire import with_plan
+    B, S, H = 2, 128, 896
+    x = rnd(B * S, H, seed=62)
+    bits = tuple([4] * (H // 64))
+    spec = with_plan(C.get_codec("rgroup"), bits)
+    msg, L = C.encode(x.to(DEV), spec, B, S, 0.0, None)
+    good = C.decode(msg, spec, L, torch.float32).cpu()
+    msg = msg.clone()
+    msg[L.off_plan + 3] = bad
+    y = C.decode(msg, spec, L, torch.float32).cpu()
+    torch.cuda.synchronize()
+    assert torch.equal(y[:, :192], good[:, :192])          # groups 0-2: before the corrupt width
+    assert torch.isnan(y[:, 192:]).all()                   # group 3 and every group after it

@@ -40,6 +40,13 @@ def test_two_ranks_one_gpu_equals_single_process():
     two = _run(2)
     assert two["config"]["parallelism"] == "pp2xdp1"
     assert two["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
+    # the N > 1 transports record on the CUDA path: torch p2p is the reference, the peer-copy transport must give the
+    # same PPL, and RCCL - which refuses two ranks on one GPU - is recorded as an error entry, not a crash
+    tr = two["transports"]
+    assert tr["torch"]["ppl_random_weights"] > 1 and len(tr["torch"]["p2p"]) == 2
+    assert tr["ipc"]["ppl_equal_torch"] is True and len(tr["ipc"]["p2p"]) == 2
+    assert "ncclCommInitRank failed" in tr["rccl"]["error"]
+    assert "notebook_sweep" in one and one["notebook_sweep"]["windows_per_s"] > 0
     chk = _run(2, ["--no-graphs"], {"EDGE_P2P_CHECK": "1"})
     assert chk["ppl_random_weights"] == pytest.approx(one["ppl_random_weights"], rel=1e-9)
 

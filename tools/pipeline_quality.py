@@ -79,6 +79,9 @@ def main():
     ap.add_argument("--ratios", default="0,0.25,0.5,0.75,1")
     ap.add_argument("--group-bits", type=float, default=4.0, help="average bits of the head-group codecs")
     ap.add_argument("--relevance-windows", type=int, default=256)
+    ap.add_argument("--bos", type=int, default=-1,
+                    help="start-of-window token put at position 0 of every window (as the model was trained with "
+                         "tools/train_tiny_lm.py --bos); -1: none")
     ap.add_argument("--json-out", default="gpurun_out/pipeline_quality.json")
     ap.add_argument("--splits", default="balanced", choices=["balanced", "bench"],
                     help="stage boundaries: cost-balanced for this model, or the bench's splits for Qwen2-0.5B "
@@ -102,20 +105,20 @@ def main():
         run = lambda ids: eng.head_relevance(ids, want_channels=True, want_sens=True)   # noqa: E731
     else:
         run = lambda ids: head_relevance_batched(m, ids, want_sens=True)                 # noqa: E731
-    for b in batches(tr, wins, 16):
+    for b in batches(tr, wins, 16, bos=a.bos if a.bos >= 0 else None):
         rel, _, _, chan, sens = run(b.ids.to(dev))
         acc += rel.double().sum(0)
         cacc += chan.double().sum(0)
         sacc += sens.double().sum(0)
     hw = normalize_per_layer(acc).float().cpu()
     grel = normalize_per_layer(cacc).float().cpu()
-    gsens = (sacc / sacc.mean(-1, keepdim=True)).float().cpu()
+    gsens = (sacc / sacc.mean(-1, keepdim=True).clamp_min(1e-300)).float().cpu()
     tables = {"sens": {"relevance": grel, "sensitivity": gsens}, "rel": grel, "uniform": None, "-": None}
     print(f"relevance (fp32 engine): {len(wins)} windows in {time.time() - t0:.1f}s", flush=True)
 
     ev = local_text_bytes("eval")
     wins = sliding_windows(ev.shape[1], 512, 32)[: a.windows]
-    bl = [b.to(dev) for b in batches(ev, wins, a.batch)]
+    bl = [b.to(dev) for b in batches(ev, wins, a.batch, bos=a.bos if a.bos >= 0 else None)]
     out = {"model": cfg.name, "weights": a.weights, "dtype": "fp32", "device": dev,
            "data": f"python-stdlib-bytes/eval, {len(wins)} windows (max_length 512, stride 32)",
            "ratios": ratios, "group_avg_bits": a.group_bits, "head_weights": hw.tolist(),

@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--ratios", default="0,0.25,0.5,0.75,1")
     ap.add_argument("--codecs", default="ref_int4_global,int4_token,mixed_int4_int8,mixed_int2_int8")
     ap.add_argument("--relevance-windows", type=int, default=256)
+    ap.add_argument("--bos", type=int, default=-1,
+                    help="start-of-window token put at position 0 of every window (as the model was trained with "
+                         "tools/train_tiny_lm.py --bos); -1: none")
     ap.add_argument("--json-out", default="gpurun_out/quality_sweep.json")
     ap.add_argument("--boot", type=int, default=1000, help="window-bootstrap replicates of the intervals")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
@@ -96,14 +99,14 @@ def main():
     acc = torch.zeros(cfg.num_layers, cfg.num_heads, dtype=torch.float64, device=dev)
     cacc = torch.zeros(cfg.num_layers, cfg.hidden_size // 64, dtype=torch.float64, device=dev)
     sacc = torch.zeros_like(cacc)
-    for b in batches(tr, wins, a.batch):
+    for b in batches(tr, wins, a.batch, bos=a.bos if a.bos >= 0 else None):
         rel, _, _, chan, sens = eng.head_relevance(b.ids, want_channels=True, want_sens=True)
         acc += rel.double().sum(0)
         cacc += chan.double().sum(0)
         sacc += sens.double().sum(0)
     hw = normalize_per_layer(acc).float().cpu()
     grel = normalize_per_layer(cacc).float().cpu()     # channel-group relevance and sensitivity: the head-group
-    gsens = (sacc / sacc.mean(-1, keepdim=True)).float().cpu()   # codecs' bit plans
+    gsens = (sacc / sacc.mean(-1, keepdim=True).clamp_min(1e-300)).float().cpu()   # codecs' bit plans
     print(f"relevance: {len(wins)} windows in {time.time() - t0:.1f}s", flush=True)
 
     ev = local_text_bytes("eval")
@@ -115,7 +118,7 @@ def main():
     # outlier structure of the boundary tensors: what a one-global-scale quantizer (ref_int4_global) is sensitive to.
     # peak/rms = max |x| over the batch / rms of x; token_peak = median over tokens of max_c |x_tc| / rms_t
     with torch.no_grad():
-        b0 = next(iter(batches(ev, wins, a.batch)))
+        b0 = next(iter(batches(ev, wins, a.batch, bos=a.bos if a.bos >= 0 else None)))
         x = m.embed(b0.ids)
         outl = {}
         for i in range(cfg.num_layers):
@@ -144,7 +147,7 @@ def main():
         sc = SweepConfig(METHODS, layers, ratios, codec=base, head_weights=hw, group_relevance=table,
                          group_avg_bits=avg)
         eng_s = SweepEngine(m, sc, keep_windows=True)
-        res = run_sweep(eng_s, batches(ev, wins, a.batch))
+        res = run_sweep(eng_s, batches(ev, wins, a.batch, bos=a.bos if a.bos >= 0 else None))
         nll, wts = eng_s.window_results()            # [N, methods, layers, ratios], [N]
         flat = nll.reshape(nll.shape[0], -1)
         dmg = stats.damage_table(flat, wts, base=0, reps=a.boot, seed=1)   # cell 0 = (method 0, layer 0, ratio 0)
