@@ -79,7 +79,7 @@ __device__ __forceinline__ int h3_acol(int kp, int K) {
 // Store s * v[0..3] at column `col` of an h3 activation row (plane width K): two 8-byte stores.
 // Nontemporal store (global_store ... nt) for the large streamed outputs that overflow the 256 MB Infinity Cache
 // anyway (the SwiGLU planes: 637 MB per bench GEMM): measured 2 % faster than plain stores on the power-limited
-// gate/up GEMM (profiles/r05/gemm_epilogue/probe_store_policy.log), bit-identical.
+// gate/up GEMM (profiles/history/r05/gemm_epilogue/probe_store_policy.log), bit-identical.
 template <class T>
 __device__ __forceinline__ void store_nt(T* p, const T& v) {
   __builtin_nontemporal_store(v, p);

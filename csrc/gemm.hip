@@ -206,7 +206,7 @@ __device__ __forceinline__ void line_exchange8(const u32x4_t& X, const u32x4_t& 
 // SwiGLU h3 epilogue of the four-wave 256x256 kernel with full-line stores: the wave's 128 accumulator columns are 64
 // output columns = one 128-byte line per plane and row, written 8 rows x 128 bytes per store instruction (the two
 // 64-column slabs of a row group exchanged between lanes r and r ^ 8) instead of 16 rows x 64 bytes - half the
-// store cost of the per-slab layout (ablation: 1 KiB-contiguous stores, profiles/r02k_gemm_epilogue_ablations.log).
+// store cost of the per-slab layout (ablation: 1 KiB-contiguous stores, profiles/history/r02k_gemm_epilogue_ablations.log).
 template <int MI8>
 __device__ __forceinline__ void swiglu_h3_lines_4w(const GemmArgs& a, f32x4_t (&acc)[MI8][8], const float (&rs)[MI8],
                                                    int m0, int n0, int lane, int wm, int wn) {
@@ -224,7 +224,7 @@ __device__ __forceinline__ void swiglu_h3_lines_4w(const GemmArgs& a, f32x4_t (&
       asm volatile("" : "+v"(c0[j]), "+v"(c1[j]));
     }
     const float f = rs[i] * a.alpha;
-    if (a.raw) {   // (full-line stores here, as for the planes, measured equal: profiles/r05/raw_store_ab.log)
+    if (a.raw) {   // (full-line stores here, as for the planes, measured equal: profiles/history/r05/raw_store_ab.log)
       const int m = m0 + wm * 128 + i * 16 + r;
       swiglu_raw_store(a, c0, f, m, n0 + wn * 128, g);
       swiglu_raw_store(a, c1, f, m, n0 + wn * 128 + 64, g);
@@ -284,7 +284,7 @@ __device__ __forceinline__ void lrp_swiglu_4w(const GemmArgs& a, f32x4_t (&acc)[
     // the gate half (columns 4g..) and the up half (16 + 4g..) of block j exchanged between lanes l, l ^ 16 (same row:
     // every lane takes part) into 8 consecutive columns pair_col(g): one 16-byte store per plane instead of two 8-byte
     // ones - the fused GEMM 996-1005 against 1098-1104 us; plain stores (nontemporal: 1057-1061 us, the next GEMM reads
-    // these planes; profiles/r05/lrp_epi17/)
+    // these planes; profiles/history/r05/lrp_epi17/)
     f16_t* dst = a.C + (size_t)min(m, a.M - 1) * a.ldc + (n0 + wn * 128) * 2 + pair_col(g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1680,7 +1680,7 @@ static int launch(const GemmArgs& a, hipStream_t st) {
   if constexpr (EPI == EPI_QKV_ROPE || EPI == EPI_F32_QKV_ROPE) {
     // fp32-mode (h3) QKV: 256x192 tiles when 192 divides N and 256 does not (N = 1152: 768 tiles, three full rounds
     // of the chip), else 256x256 when they fill it; the XCD-chunked walk keeps an XCD's rounds inside one GROUP_M
-    // band, re-using its A panels from L2 (h3 QKV at M = 32768: 144 vs 159 us strided, profiles/r02h_gemm_explore.log).
+    // band, re-using its A panels from L2 (h3 QKV at M = 32768: 144 vs 159 us strided, profiles/history/r02h_gemm_explore.log).
     // The bf16 QKV (K = 896, fused RMSNorm row scale) stays on 128x128 tiles unless a test forces a tile.
     const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
     if constexpr (RH == 0 || RH == 32) {

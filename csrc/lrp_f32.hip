@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void lrp_attn_delta_f32_kernel(const float* __
 // Values far below their scale keep an absolute error of ~2^-25 / s (fp16's subnormal step): ~2^-40 relative to the
 // largest value of the same operand.  Round 4's form split every operand into three bf16 planes instead (six
 // products, no scales, fp32's exponent range on every element): 1.34x the time of these sweeps
-// (profiles/r05/lrp_attn_h3/probe.log), removed.
+// (profiles/history/r05/lrp_attn_h3/probe.log), removed.
 //
 // 16x16x32 fragments: lane l holds A[row l&15][k 8(l>>4)+j] and B[k 8(l>>4)+j][col l&15], C[row 4(l>>4)+r][col l&15].
 // A score tile computed with the query (dkdv) or the key (dq) on the C rows puts 4 rows of a 16-row block on a lane;

@@ -82,7 +82,7 @@ class GraphCache:
         # No garbage collection while capturing: a cycle collected mid-capture can hold a dropped CUDAGraph (e.g. of
         # a pipeline rebuilt for another codec), and its destructor is not permitted while a stream captures.  (No
         # collection forced before it either: 2.2 % of the fp32 bench and 3.8 % of the bf16 one, same-box, round 4,
-        # profiles/r04h/gc_ab_and_lrp.txt.)
+        # profiles/history/r04h/gc_ab_and_lrp.txt.)
         was = gc.isenabled()
         gc.disable()
         try:

@@ -1,5 +1,5 @@
 # Round 5 final kernel profiles: the driver-argument fp32 bench step (5 steps) and the fp32 AttnLRP (64 windows, 3
-# passes) under rocprofv3 --kernel-trace --stats; summaries for profiles/r05/final_prof/.  Then the LRP tests.
+# passes) under rocprofv3 --kernel-trace --stats; summaries for profiles/history/r05/final_prof/.  Then the LRP tests.
 set -o pipefail
 O=gpurun_out/${OUT:-r05ah}
 mkdir -p $O

@@ -1,5 +1,5 @@
 # Round 5: per-dispatch clock and MFMA occupancy of the gate/up GEMM with the nontemporal SwiGLU planes (this tree;
-# compare profiles/r05/gemm_epilogue/clock_nostore.md: plain stores 1.625 GHz / 0.671, stores off 1.738 GHz / 0.683).
+# compare profiles/history/r05/gemm_epilogue/clock_nostore.md: plain stores 1.625 GHz / 0.671, stores off 1.738 GHz / 0.683).
 set -o pipefail
 O=gpurun_out/${OUT:-r05aj}
 mkdir -p $O

@@ -1,5 +1,5 @@
 # Round 5: the AttnLRP attention backward on scaled fp16 planes (h3) - tests against fp64 / autograd, the full-Qwen2
-# table against CPU fp32, the sweeps' time (the x6 A/B: profiles/r05/lrp_attn_h3/probe.log) and the fp32 AttnLRP throughput.
+# table against CPU fp32, the sweeps' time (the x6 A/B: profiles/history/r05/lrp_attn_h3/probe.log) and the fp32 AttnLRP throughput.
 set -o pipefail
 O=gpurun_out/${OUT:-r05n}
 mkdir -p $O

@@ -92,7 +92,7 @@ def test_relevance_engine_gpu_vs_cpu(cfg):
     rg, ing, mxg = RelevanceEngine(mg).head_relevance(ids.to(DEV))
     rc, inc, mxc = RelevanceEngine(mc).head_relevance(ids)
     assert rel_err(mxg, mxc) < 1e-2
-    # measured on MI355X (profiles/r03m_lrp_bf16_err.jsonl, seeds 2-4): per-head relevance <= 0.76 %, normalised
+    # measured on MI355X (profiles/history/r03m_lrp_bf16_err.jsonl, seeds 2-4): per-head relevance <= 0.76 %, normalised
     # table <= 2.8 % (the 3.2 % of docs/RESULTS.md is the full-size Qwen2 table)
     assert rel_err(rg, rc) < 0.02, rel_err(rg, rc)
     # the calibrated table (normalised per layer over all windows) is what weighted_importance consumes

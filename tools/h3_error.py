@@ -9,7 +9,7 @@ For the model's GEMM shapes it prints the relative L2 and max errors of
 Products of 16-bit values are exact in fp32, so the plane GEMMs are emulated as fp32 GEMMs over the
 K-concatenated planes, the way the MFMA accumulates them.
 
-    python tools/h3_error.py [--out profiles/r02_h3_error.txt]
+    python tools/h3_error.py [--out profiles/history/r02_h3_error.txt]
 """
 import argparse
 import math
