@@ -379,6 +379,46 @@ def same_node_reference(a, cfg, dev) -> dict:
     return out
 
 
+def box_calibration(dev) -> dict:
+    """Box-speed reference measured right after the framework's runs, so that numbers from different boxes can be
+    compared through the driver's own record (box to box the headline spans ~7 % at equal code): the sustained
+    throughput of a plain library GEMM (hipBLASLt fp16, 8192^3, 40 back-to-back calls: long enough to settle at the
+    chip's power-limited clock, as the bench's GEMMs do) and of a 1 GiB device copy (HBM).  Never fails the bench."""
+    if dev.type != "cuda":
+        return {"skipped": "cpu"}
+    try:
+        n = 8192
+        a = torch.randn(n, n, device=dev, dtype=torch.float16)
+        b = torch.randn(n, n, device=dev, dtype=torch.float16)
+        c = torch.empty(n, n, device=dev, dtype=torch.float16)
+        for _ in range(10):
+            torch.matmul(a, b, out=c)
+        torch.cuda.synchronize()
+        reps = 40
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            torch.matmul(a, b, out=c)
+        torch.cuda.synchronize()
+        tf = 2.0 * n ** 3 * reps / (time.perf_counter() - t0) / 1e12
+        del a, b, c
+        src = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        dst = torch.empty_like(src)
+        for _ in range(3):
+            dst.copy_(src)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            dst.copy_(src)
+        torch.cuda.synchronize()
+        bw = 2.0 * src.numel() * 10 / (time.perf_counter() - t0) / 1e9   # read + write
+        del src, dst
+        torch.cuda.empty_cache()
+        return {"what": "same-box reference: hipBLASLt fp16 8192^3 GEMM (40 back-to-back) and a 1 GiB device copy",
+                "hipblaslt_fp16_tflops": round(tf, 1), "hbm_copy_GBps": round(bw, 1)}
+    except Exception as e:   # the headline stands without it
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+
+
 def main():
     a = parse()
     mode = launch_mode(a)
@@ -424,6 +464,7 @@ def main():
     hf = None   # last, so that nothing of it can touch the framework's own measurements
     if world == 1 and not a.no_hf_compare and env.device.type == "cuda":
         hf = same_node_reference(a, cfg, env.device)
+    calib = box_calibration(env.device) if env.is_main else None
     dname = {torch.float32: "fp32", torch.bfloat16: "bf16"}[dtype]
     out = {
         "metric": METRIC,
@@ -473,6 +514,10 @@ def main():
             out["sweep_s_per_window"] = sweep["s_per_window"]
             out["sweep_s_per_window_t4"] = T4_SWEEP_S_PER_WINDOW
             out["sweep_speedup_vs_t4"] = round(T4_SWEEP_S_PER_WINDOW / sweep["s_per_window"], 1)
+    if calib is not None:
+        out["box_calibration"] = calib
+        if "hipblaslt_fp16_tflops" in calib:   # headline per sustained library TFLOP/s: comparable across boxes
+            out["value_per_box_tflops"] = round(value / calib["hipblaslt_fp16_tflops"], 2)
     if hf is not None:
         out["same_node_reference_path"] = hf
         for k in ("batch1", "batch64"):
@@ -666,6 +711,12 @@ def transports_check(a, env, cfg, dtype, values, spec, pp, grid, plan, guard: Gu
     for t in TRANSPORTS:
         if t != "torch" and env.device.type != "cuda":
             out[t] = {"skipped": "CPU ranks: the native transports need GPUs"}
+            continue
+        if t == "rccl" and shared_gpu():
+            # RCCL refuses ranks that share a device: ncclCommInitRank returns an error, or on some runs blocks until
+            # the watchdog fires (the round-6 full-suite run stalled there); never attempted in the rehearsal
+            out[t] = {"error": "not attempted: ncclCommInitRank refuses ranks sharing one GPU (EDGE_SHARED_GPU "
+                               "rehearsal); the native RCCL channels need one GPU per rank"}
             continue
         sub_t = argparse.Namespace(**vars(sub))
         sub_t.transport = t

@@ -24,7 +24,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["bench.py", "--model", "tiny-qwen2", "--batch", "4", "--microbatches", "2", "--steps", "3", "--warmup", "1",
         "--max-length", "256", "--split", "1", "--pp", "4", "--no-bf16", "--no-fp32-weights", "--no-hf-compare",
-        "--no-transports"]
+        "--no-transports", "--no-sweep", "--no-hf-compare"]
 
 
 def _port():
@@ -54,12 +54,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--runs", type=int, default=8)
     ap.add_argument("--out", default="gpurun_out/rehearsal_stress")
+    ap.add_argument("--hog-seconds", type=float, default=0.0,
+                    help="> 0: the 4-rank runs share the GPU with tools/contention_check.py's hog (2 GiB copies + fp16 "
+                         "GEMMs back to back in a fifth process) for at most this long")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="stress_")
     ref = run(1, os.path.join(tmp, "ref"))
     ref_nll = torch.load(os.path.join(tmp, "ref.local.1.pt"))
     rows = []
+    child = None
+    if a.hog_seconds > 0:
+        child = subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "contention_check.py"), "--hog-child",
+                                  "--hog-seconds", str(a.hog_seconds)], stdout=subprocess.PIPE, text=True)
+        assert child.stdout.readline().strip() == "hog running"
     for k in range(a.runs):
         pre = os.path.join(tmp, f"r{k}")
         r = run(4, pre, {"EDGE_P2P_CHECK": "1"})
@@ -75,7 +83,12 @@ def main():
         print(json.dumps({"run": k, **r}), flush=True)
         if r["rc"] != 0 and r["rc"] in (124, 134, 137, 139, -6, -11):
             break
-    out = {"reference": ref, "runs": rows, "all_identical": all(r.get("bit_identical") for r in rows),
+    if child is not None:
+        r_hog = child.poll()
+        if r_hog is None:
+            child.terminate()
+        child.wait(timeout=60)
+    out = {"reference": ref, "runs": rows, "hog": child is not None and r_hog is None, "all_identical": all(r.get("bit_identical") for r in rows),
            "microbatches_x_windows": list(ref_nll.shape)}
     with open(os.path.join(a.out, "summary.json"), "w") as f:
         json.dump(out, f, indent=1)
