@@ -31,11 +31,17 @@ enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_G
        // interleaved pre-activations gu [M, 2N] (residf / ldr) -> h3 planes [M, 2 (2N)] of the interleaved
        // (0.5 d u sig(g), 0.5 d g sig(g)) at unit scale (alpha carries the caller's bound-derived scale: no row max,
        // so no separate rule pass over an fp32 dm)
-       EPI_H3_LRP_SWIGLU = 17 };
+       EPI_H3_LRP_SWIGLU = 17,
+       // fp32 output = product + fp32 residual, plus the next RMSNorm's producer side (the separate RMSNorm pass goes):
+       // the h3 planes [M, 2N] of p_m (C_m * colscale) at a power-of-two row scale p_m from a bound on |C_m * colscale|,
+       // prinv[m] = 1 / p_m and the row sum-of-squares partials ssq_out[m, N / 112] of C; the consumer GEMM takes
+       // rscale[m] = rsqrt(sum ssq_out[m] / N + eps) * prinv[m] (np_scale)
+       EPI_F32_RESID_NP = 18 };
 constexpr bool epi_f32(int e) { return e >= EPI_F32; }
 constexpr bool epi_plain(int e) {  // none / bias / residual epilogues (the 256x224 kernel's set)
   return e == EPI_NONE || e == EPI_BIAS || e == EPI_RESID || e == EPI_BIAS_RESID || e == EPI_F32 ||
-         e == EPI_F32_BIAS || e == EPI_F32_RESID || e == EPI_F32_BIAS_RESID || e == EPI_F32_RESID_CS;
+         e == EPI_F32_BIAS || e == EPI_F32_RESID || e == EPI_F32_BIAS_RESID || e == EPI_F32_RESID_CS ||
+         e == EPI_F32_RESID_NP;
 }
 
 struct GemmArgs {
@@ -51,6 +57,10 @@ struct GemmArgs {
   // scale s_m from the caller's bound 2^15 (bnd_a[m] + bnd_b[m] bnd_c) on |C row m|, and prinv[m] = 1 / s_m - the
   // next backward GEMM's input without a row-max pass (plane_scale)
   f16_t* planes; float* prinv; const float* bnd_a; const float* bnd_b; float bnd_c;
+  // EPI_F32_RESID_NP: the bound on |C_m * colscale| is np_g (np_rn / bnd_b[m] + bnd_c) with bnd_b the residual input's
+  // RMSNorm normalisers rsqrt(mean(x_m^2) + eps) (np_rn / bnd_b[m] = sqrt(K mean + K eps) >= ||x_m||_2 >= max |x_m|, np_rn =
+  // sqrt(N)), bnd_c a bound on |product| and np_g = max |colscale|
+  float np_g, np_rn;
   // QKV_ROPE
   bf16_t* qout; bf16_t* kout; bf16_t* vtout;
   const float* cosT; const float* sinT;
@@ -333,6 +343,14 @@ __device__ __forceinline__ float plane_scale(const GemmArgs& a, int m) {
   int e;
   (void)frexpf(32768.f * (a.bnd_a[m] + a.bnd_b[m] * a.bnd_c), &e);
   return ldexpf(1.f, 15 - e);
+}
+
+// p_m of EPI_F32_RESID_NP: 2^(14 - E) for the bound u = np_g (np_rn / bnd_b[m] + bnd_c) = f 2^E, f in [0.5, 1), so that
+// p_m |C_m colscale| < 2^14 (fp16 max 65504: 2x headroom for the fp32 rounding of C)
+__device__ __forceinline__ float np_scale(const GemmArgs& a, int m) {
+  int e;
+  (void)frexpf(a.np_g * (a.np_rn / a.bnd_b[m] + a.bnd_c), &e);
+  return ldexpf(1.f, 14 - e);
 }
 
 // ---- fp32-execution epilogues (EPI >= EPI_F32).  Same ownership as gemm_epilogue below: lane owns rows
@@ -1248,18 +1266,19 @@ __device__ __forceinline__ void qkv192_bf16_epilogue(const GemmArgs& a, f32x4_t 
 template <int EPI>
 __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (&acc)[8][7], int m0, int n0,
                                                     int lane, int wm, int wn) {
-  constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID || EPI == EPI_F32_RESID_CS;
+  constexpr bool NP = EPI == EPI_F32_RESID_NP;
+  constexpr bool RESF = EPI == EPI_F32_RESID || EPI == EPI_F32_BIAS_RESID || EPI == EPI_F32_RESID_CS || NP;
   constexpr bool BIAS = EPI == EPI_F32_BIAS || EPI == EPI_F32_BIAS_RESID;
   constexpr bool CS = EPI == EPI_F32_RESID_CS;
   const int g = lane >> 4;
   const int nw = n0 + wn * 112;
   const int rbase = m0 + wm * 128 + (lane & 15);
-  f32x4_t bw[BIAS || CS ? 7 : 1];   // bias, or the column scales (never both)
+  f32x4_t bw[BIAS || CS || NP ? 7 : 1];   // bias, or the column scales / the next norm's weight (never both)
   if constexpr (BIAS) {
 #pragma unroll
     for (int j = 0; j < 7; ++j) bw[j] = *(const f32x4_t*)(a.biasf + nw + j * 16 + g * 4);
   }
-  if constexpr (CS) {
+  if constexpr (CS || NP) {
 #pragma unroll
     for (int j = 0; j < 7; ++j) bw[j] = *(const f32x4_t*)(a.colscale + nw + j * 16 + g * 4);
   }
@@ -1271,6 +1290,7 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
       const int mr = min(rbase + (2 * pr + i2) * 16, a.M - 1);
       rsv[buf][i2] = (a.rscale ? a.rscale[mr] : 1.f) * a.alpha;
       if constexpr (CS) psv[buf][i2] = a.planes ? plane_scale(a, mr) : 0.f;
+      if constexpr (NP) psv[buf][i2] = np_scale(a, mr);
       if constexpr (RESF) {
         const float* rrow = a.residf + (size_t)mr * a.ldr + nw + g * 4;
 #pragma unroll
@@ -1294,6 +1314,7 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2) {
       const int m = rbase + (2 * pr + i2) * 16;
+      float ss = 0.f;
       if (m < a.M) {
         float* row = a.Cf + (size_t)m * a.ldc + nw + g * 4;
 #pragma unroll
@@ -1309,9 +1330,23 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
               store_h3_4(a.planes + (size_t)m * (2 * a.N), a.N, nw + j * 16 + g * 4, v4, psv[buf][i2]);
             }
           }
+          if constexpr (NP) {
+            const f32x4_t n4 = o * bw[j];
+            const float v4[4] = {n4[0], n4[1], n4[2], n4[3]};
+            store_h3_4(a.planes + (size_t)m * (2 * a.N), a.N, nw + j * 16 + g * 4, v4, psv[buf][i2]);
+            ss += o[0] * o[0] + o[1] * o[1] + o[2] * o[2] + o[3] * o[3];
+          }
         }
         if constexpr (CS) {
           if (a.planes && nw == 0 && g == 0) a.prinv[m] = 1.f / psv[buf][i2];
+        }
+      }
+      if constexpr (NP) {   // uniform: every lane takes part in the shuffles (the 4 lanes of a row: g = 0..3)
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        if (m < a.M && g == 0) {
+          a.ssq_out[(size_t)m * (a.N / 112) + nw / 112] = ss;
+          if (nw == 0) a.prinv[m] = 1.f / psv[buf][i2];
         }
       }
     }
@@ -1892,6 +1927,36 @@ EDGE_API int edge_gemm_f32_cs(const void* A, const void* B, float* C, int M, int
   if (((uintptr_t)C & 15) || ldc % 4 || ldr % 4 || ((uintptr_t)resid & 15) || ((uintptr_t)colscale & 15))
     return (int)hipErrorInvalidValue;
   return launch<EPI_F32_RESID_CS>(a, st);
+}
+
+// EPI_F32_RESID_NP (the O-projection / down GEMM with the next RMSNorm's producer side): C = alpha (A . B^T) + resid
+// (fp32, C may alias resid), planes [M, 2N] = h3 of p_m (C_m * g) with p_m from the bound g_max (sqrt(N) / rstd_in[m] +
+// prod_bound) on |C_m * g| (np_scale), prinv[m] = 1 / p_m, ssq_out [M, N / 112] the row sum-of-squares partials of C.
+// 256x224 tiles only (edge_gemm_f32_np_ok); A / B as edge_gemm_f32.
+EDGE_API int edge_gemm_f32_np_ok(int M, int N, int Kx) { return use_224(M, N, Kx, EPI_F32_RESID_NP) ? 1 : 0; }
+
+EDGE_API int edge_gemm_f32_np(const void* A, const void* B, float* C, int M, int N, int Kx, int kplane, int lda, int ldb,
+                              int ldc, const float* resid, int ldr, float alpha, const float* g, const float* rstd_in,
+                              float g_max, float prod_bound, void* planes, float* prinv, float* ssq_out, hipStream_t st) {
+  GemmArgs a{};
+  a.alpha = alpha;
+  a.colscale = g;
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B;
+  a.M = M; a.N = N; a.K = Kx; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.residf = resid; a.ldr = ldr; a.Cf = C;
+  a.h3k = kplane;
+  a.pairb = Kx == 2 * kplane;
+  a.planes = (f16_t*)planes; a.prinv = prinv; a.bnd_b = rstd_in; a.bnd_c = prod_bound; a.ssq_out = ssq_out;
+  a.np_g = g_max; a.np_rn = sqrtf((float)N);
+  if (!g || !resid || !rstd_in || !planes || !prinv || !ssq_out || !h3_geometry_ok(Kx, kplane) || lda < 2 * kplane ||
+      ldb < (a.pairb ? kplane : Kx) || !(alpha > 0.f) || !(g_max > 0.f) || !(prod_bound >= 0.f))
+    return (int)hipErrorInvalidValue;
+  const int chk = check_shapes(a);
+  if (chk) return chk < 0 ? 0 : chk;
+  if (((uintptr_t)C & 15) || ldc % 4 || ldr % 4 || ((uintptr_t)resid & 15) || ((uintptr_t)g & 15) ||
+      ((uintptr_t)planes & 7) || !use_224(M, N, Kx, EPI_F32_RESID_NP))
+    return (int)hipErrorInvalidValue;
+  return launch_4w<EPI_F32_RESID_NP, 0, 224>(a, st);
 }
 
 // EPI_H3_LRP_SWIGLU: C = h3 planes [M, 4N] (fp16, row stride 4N) of the SwiGLU LRP rule on d = alpha (A . B^T)

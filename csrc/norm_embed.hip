@@ -202,18 +202,29 @@ EDGE_API int edge_row_ssq(const void* x, float* ssq, int R, int H, hipStream_t s
 
 // rscale[r] = rsqrt(sum_p ssq[r, p] / H + eps): the per-row RMSNorm factor from the slab partials.
 __global__ __launch_bounds__(256) void row_rscale_kernel(const float* __restrict__ ssq, float* __restrict__ rs, int R,
-                                                         int P, int H, float eps) {
+                                                         int P, int H, float eps, const float* __restrict__ mul) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= R) return;
   const float* p = ssq + (size_t)r * P;
   float s = 0.f;
   for (int i = 0; i < P; ++i) s += p[i];
-  rs[r] = rsqrtf(s / (float)H + eps);
+  const float v = rsqrtf(s / (float)H + eps);
+  rs[r] = mul ? v * mul[r] : v;
 }
 
 EDGE_API int edge_row_rscale(const float* ssq, float* rs, int R, int P, int H, float eps, hipStream_t st) {
   if (R <= 0) return 0;
-  row_rscale_kernel<<<(R + 255) / 256, 256, 0, st>>>(ssq, rs, R, P, H, eps);
+  row_rscale_kernel<<<(R + 255) / 256, 256, 0, st>>>(ssq, rs, R, P, H, eps, nullptr);
+  return (int)hipGetLastError();
+}
+
+// rs[r] = rsqrt(sum_p ssq[r, p] / H + eps) * mul[r]: the consumer row scale of the fp32 fused RMSNorm (mul = the
+// producer's 1 / p_m, gemm.hip EPI_F32_RESID_NP)
+EDGE_API int edge_row_rscale_mul(const float* ssq, const float* mul, float* rs, int R, int P, int H, float eps,
+                                 hipStream_t st) {
+  if (R <= 0) return 0;
+  if (!mul) return (int)hipErrorInvalidValue;
+  row_rscale_kernel<<<(R + 255) / 256, 256, 0, st>>>(ssq, rs, R, P, H, eps, mul);
   return (int)hipGetLastError();
 }
 

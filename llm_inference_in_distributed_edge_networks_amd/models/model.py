@@ -122,12 +122,19 @@ class DecoderLM:
             for i, L in enumerate(self.layers):
                 if L is None:
                     continue
-                sc = {k: S(v) for k, v in _h3_bounds(cfg, L).items()}
+                bd = _h3_bounds(cfg, L)
+                sc = {k: S(v) for k, v in bd.items()}
                 ins = dict(wqkv="qkv", wo="o", wgu="mlp", wd="down", wfc="mlp", wproj="down")
                 for k in _H3_KEYS:
                     if k in L:
                         L[k + "3"], sw = ops.reference.h3_weight(L[k])
                         sc["a_" + k] = 1.0 / (sc[ins[k]] * sw)
+                if cfg.arch == "qwen2":
+                    # fused RMSNorm-2 (the O-projection's epilogue writes the gate/up GEMM's planes, linear_h3_np):
+                    # |o @ Wo^T| <= max|o| max_n ||Wo_n||_1, the gate/up product without the static activation scale
+                    sc["np_po"] = bd["o"] * L["wo"].float().abs().sum(1).max().item()
+                    sc["np_g2"] = L["ln2_w"].float().abs().max().item()
+                    sc["a_wgu_np"] = sc["a_wgu"] * sc["mlp"]
                 self.h3_layer[i] = sc
             if weights.get("head") is not None:
                 g, b = weights["norm_w"], weights.get("norm_b")
@@ -140,6 +147,10 @@ class DecoderLM:
         self.cos = cos.to(self.device).contiguous()
         self.sin = sin.to(self.device).contiguous()
         self.q_scale = 1.0 / math.sqrt(cfg.head_dim)
+        # fp32 (h3) mode, Qwen2: RMSNorm-2 fused into the O-projection's epilogue (linear_h3_np) when the GPU kernel
+        # runs the shape; EDGE_FUSED_NORM_F32=0 keeps the separate norm pass (A/B); tests set it on CPU models too
+        self.fuse_norm_f32 = (self.h3 and cfg.arch == "qwen2" and self.device.type == "cuda"
+                              and os.environ.get("EDGE_FUSED_NORM_F32", "1") not in ("", "0"))
         # GPU fast path for RMSNorm models: the norm weight is folded into the consuming GEMM's weight and
         # the row scale is applied in its epilogue, from sum-of-squares partials the residual GEMMs emit.
         self.fuse_norm = (self.device.type == "cuda" and cfg.arch == "qwen2" and dtype == torch.bfloat16
@@ -387,13 +398,21 @@ class DecoderLM:
                 raise ValueError(kd)
         return kinds
 
-    def _attn_h3(self, i, x, B, S, need_lse=False, n_rows=None, need_k=True):
+    def _np_fused(self, M: int) -> bool:
+        """RMSNorm-2 fused into the O-projection for an M-row layer (linear_h3_np on the GPU's 256x224 tiles)."""
+        if not self.fuse_norm_f32:
+            return False
+        H = self.cfg.hidden_size
+        return self.device.type != "cuda" or ops.gemm_np_supported(M, H, 2 * H)
+
+    def _attn_h3(self, i, x, B, S, need_lse=False, n_rows=None, need_k=True, rstd_out=None):
         """fp32 mode: norm(s) -> h3 QKV GEMM (+bias+RoPE) -> fp32 attention with h3 output (``need_k=False``: no
-        fp32 K on the GPU, only its planes for the attention - k is then None)."""
+        fp32 K on the GPU, only its planes for the attention - k is then None).  ``rstd_out``: RMSNorm-1's row
+        normalisers are written there too (the fused RMSNorm-2's bound)."""
         cfg, L, sc = self.cfg, self.layers[i], self.h3_layer[i]
         h23 = None
         if cfg.arch == "qwen2":
-            h3 = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps, h3=sc["qkv"])
+            h3 = ops.rmsnorm(x, L["ln1_w"], cfg.norm_eps, h3=sc["qkv"], rstd_out=rstd_out)
         else:
             h3, h23 = ops.layernorm_dual(x, L["ln1_w"], L["ln1_b"], L["ln2_w"], L["ln2_b"], cfg.norm_eps,
                                          h3=(sc["qkv"], sc["mlp"]))
@@ -411,8 +430,16 @@ class DecoderLM:
                                 in_scales=(sc["att_q"], sc["att_k"], sc["o"]), kv_planes=kvp)
         return q, k, o3, lse, h23
 
-    def _mlp_h3(self, i, o3, x, h23):
+    def _mlp_h3(self, i, o3, x, h23, rstd1=None):
         cfg, L, sc = self.cfg, self.layers[i], self.h3_layer[i]
+        if cfg.arch == "qwen2" and rstd1 is not None:
+            # RMSNorm-2 in the O-projection's epilogue: its planes of p_m (y_m * ln2_w) feed the gate/up GEMM with the row
+            # scale rsqrt(mean(y_m^2) + eps) / p_m (no separate norm pass over y)
+            y, planes, prinv, ssq = ops.linear_h3_np(o3, L["wo3"], sc["a_wo"], x, L["ln2_w"], rstd1, sc["np_g2"],
+                                                     sc["np_po"])
+            rs = ops.row_rscale_mul(ssq, prinv, cfg.hidden_size, cfg.norm_eps)
+            a3 = ops.linear_h3(planes, L["wgu3"], sc["a_wgu_np"], act="swiglu_il", out_scale=sc["down"], rscale=rs)
+            return ops.linear_h3(a3, L["wd3"], sc["a_wd"], residual=y, out=y)
         if cfg.arch == "qwen2":
             y = ops.linear_h3(o3, L["wo3"], sc["a_wo"], residual=x)
             a3 = ops.linear_h3(ops.rmsnorm(y, L["ln2_w"], cfg.norm_eps, h3=sc["mlp"]), L["wgu3"], sc["a_wgu"],
@@ -424,14 +451,15 @@ class DecoderLM:
 
     def _layer_h3(self, i, x, B, S, stats):
         kinds = self._stat_kinds(stats)
-        q, k, o3, lse, h23 = self._attn_h3(i, x, B, S, need_lse="colsum" in kinds, need_k=bool(kinds))
+        rstd1 = torch.empty(x.shape[0], dtype=torch.float32, device=x.device) if self._np_fused(x.shape[0]) else None
+        q, k, o3, lse, h23 = self._attn_h3(i, x, B, S, need_lse="colsum" in kinds, need_k=bool(kinds), rstd_out=rstd1)
         st = None
         if kinds:   # the scores on the forward's scaled fp16 planes (consistent with its LSE)
             sc = self.h3_layer[i]
             qk = (sc["att_q"], sc["att_k"])
             st = AttnStats(lastrow=ops.attn_lastrow(q, k, S, in_scales=qk) if "lastrow" in kinds else None,
                            colsum=ops.attn_colsum(q, k, lse, S, in_scales=qk) if "colsum" in kinds else None)
-        return self._mlp_h3(i, o3, x, h23), st
+        return self._mlp_h3(i, o3, x, h23, rstd1), st
 
     def layer_rows(self, i: int, x: torch.Tensor, B: int, S: int, rows: torch.Tensor,
                    n_rows: torch.Tensor | None = None) -> torch.Tensor:

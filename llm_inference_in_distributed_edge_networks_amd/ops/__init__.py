@@ -477,6 +477,54 @@ def linear_h3(a3: torch.Tensor, w3: torch.Tensor, alpha: float, bias=None, resid
     return out
 
 
+def gemm_np_supported(M: int, N: int, Kx: int) -> bool:
+    """Whether ``linear_h3_np`` runs this GPU shape (the 256x224 persistent tiles: N % 224 == 0, N % 256 != 0 and at
+    least one tile per CU)."""
+    return bool(lib().edge_gemm_f32_np_ok(int(M), int(N), int(Kx)))
+
+
+def linear_h3_np(a3: torch.Tensor, w3: torch.Tensor, alpha: float, residual: torch.Tensor, g: torch.Tensor,
+                 rstd_in: torch.Tensor, g_max: float, prod_bound: float, out: torch.Tensor | None = None):
+    """The O-projection / down GEMM with the NEXT RMSNorm's producer side fused into its epilogue (no separate norm
+    pass): y = alpha (x @ w.T) + residual (fp32, ``out`` may alias ``residual``) and, for the GEMM that consumes
+    rmsnorm(y) * g, the h3 planes of p_m (y_m * g) at a power-of-two row scale p_m from the bound
+    g_max (sqrt(N) / rstd_in[m] + prod_bound) on |y_m * g| (``rstd_in``: the residual's own RMSNorm normalisers,
+    ``prod_bound``: a bound on |alpha (x @ w.T)|, ``g_max`` = max |g|), 1 / p_m and y's row sum-of-squares partials
+    -> (y, planes [M, 2N], prinv [M], ssq [M, N / 112]).  The consumer takes ``rscale = row_rscale_mul(ssq, prinv)`` and
+    its weight's own product scale (no activation scale)."""
+    M, N = a3.shape[0], w3.shape[0]
+    if not _gpu(a3):
+        y = ref.h3_matmul(a3, w3, alpha) + residual.float()
+        if out is not None:
+            out.copy_(y)
+            y = out
+        return (y,) + ref.np_planes(y, g, rstd_in, g_max, prod_bound)
+    kp, Kx = _check_h3(a3, w3, alpha)
+    _check_f32(residual, g, rstd_in, out)
+    if N % 112:
+        raise ValueError(f"linear_h3_np: N = {N} is not a multiple of the 112-column slabs")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=a3.device)
+    planes = torch.empty(M, 2 * N, dtype=torch.float16, device=a3.device)
+    prinv = torch.empty(M, dtype=torch.float32, device=a3.device)
+    ssq = torch.empty(M, N // 112, dtype=torch.float32, device=a3.device)
+    call("edge_gemm_f32_np", ptr(a3), ptr(w3), ptr(out), M, N, Kx, kp, a3.stride(0), w3.stride(0), out.stride(0),
+         ptr(residual), residual.stride(0), float(alpha), ptr(g), ptr(rstd_in), float(g_max), float(prod_bound),
+         ptr(planes), ptr(prinv), ptr(ssq), stream())
+    return out, planes, prinv, ssq
+
+
+def row_rscale_mul(ssq: torch.Tensor, mul: torch.Tensor, K: int, eps: float) -> torch.Tensor:
+    """rsqrt(sum(ssq_parts) / K + eps) * mul per row: the consumer row scale of ``linear_h3_np``'s fused RMSNorm."""
+    if not ssq.is_cuda:
+        return ref.row_rscale_mul(ssq, mul, K, eps)
+    _check_f32(ssq, mul)
+    T, P = ssq.shape
+    out = torch.empty(T, dtype=torch.float32, device=ssq.device)
+    call("edge_row_rscale_mul", ptr(ssq), ptr(mul), ptr(out), T, P, K, float(eps), stream())
+    return out
+
+
 def linear_swiglu_raw(x: torch.Tensor, w: torch.Tensor, norm=None):
     """``linear(x, w, act="swiglu_il", norm=norm)`` that also returns the pre-activations ``linear(x, w, norm=norm)``
     (interleaved gate|up [M, N], bit-identical) from the same GEMM -> (activation [M, N/2], pre-activations)."""

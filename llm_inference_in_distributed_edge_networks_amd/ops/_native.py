@@ -67,6 +67,10 @@ _SIGS = {
                          c_p, c_p, c_p, c_p, c_f, c_p],
     "edge_lrp_attn_bwd_h3": [c_p] * 12 + [c_i] * 5 + [c_f] * 3 + [c_p],
     "edge_gemm_f32_lrp_swiglu": [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p],
+    "edge_gemm_f32_np_ok": [c_i, c_i, c_i],
+    "edge_gemm_f32_np": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_f, c_p, c_p, c_f, c_f, c_p, c_p,
+                         c_p, c_p],
+    "edge_row_rscale_mul": [c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_p],
     "edge_gemm_f32": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_i, c_p, c_f, c_f, c_p],
     "edge_gemm_qkv_rope_f32": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f,
                                c_f, c_p, c_p, c_f, c_f, c_p, c_p],
@@ -138,7 +142,8 @@ def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
 
-_NO_LAUNCH = {"edge_gemm_set_tile", "edge_gemm_ssq_parts", "edge_poison_lds", "edge_poison_lds_bytes"}
+_NO_LAUNCH = {"edge_gemm_set_tile", "edge_gemm_ssq_parts", "edge_poison_lds", "edge_poison_lds_bytes",
+              "edge_gemm_f32_np_ok"}
 
 
 def call(name: str, *args) -> None:

@@ -421,6 +421,28 @@ def bound_planes(y: torch.Tensor, bnd_a, bnd_b, bnd_c: float):
     return torch.cat([hi, lo], -1).contiguous(), 1.0 / s
 
 
+def np_planes(y: torch.Tensor, g: torch.Tensor, rstd_in: torch.Tensor, g_max: float, prod_bound: float):
+    """The fused-RMSNorm producer outputs of gemm.hip EPI_F32_RESID_NP besides C = y: (planes [M, 2N] = h3 of
+    p_m (y_m * g), prinv [M] = 1 / p_m, ssq [M, N / 112] row sum-of-squares partials of y), with p_m = 2^(14 - E) for
+    the bound u_m = g_max (sqrt(N) / rstd_in[m] + prod_bound) = f 2^E on |y_m * g| (fp32 arithmetic as the kernel's).
+    The consumer GEMM then takes rscale[m] = rsqrt(sum ssq[m] / N + eps) * prinv[m] (``row_rscale_mul``)."""
+    M, N = y.shape
+    yf = _f(y)
+    u = torch.tensor(float(g_max), dtype=torch.float32) * (
+        torch.tensor(math.sqrt(N), dtype=torch.float32) / _f(rstd_in) + torch.tensor(float(prod_bound), dtype=torch.float32))
+    _, e = torch.frexp(u)
+    p = torch.exp2((14 - e).to(torch.float32))
+    ys = (yf * _f(g).view(1, -1)) * p.view(-1, 1)
+    hi = ys.to(torch.float16)
+    lo = (ys - hi.float()).to(torch.float16)
+    ssq = yf.pow(2).reshape(M, N // 112, 112).sum(-1) if N % 112 == 0 else yf.pow(2).sum(-1, keepdim=True)
+    return torch.cat([hi, lo], -1).contiguous(), 1.0 / p, ssq
+
+
+def row_rscale_mul(ssq: torch.Tensor, mul: torch.Tensor, K: int, eps: float) -> torch.Tensor:
+    return torch.rsqrt(_f(ssq).sum(-1) / K + eps) * _f(mul)
+
+
 def h3_unit(x: torch.Tensor) -> torch.Tensor:
     """fp32 [R, K] -> the 2-plane h3 activation [R, 2K] at scale 1 (the caller bounds |x| below 2^15)."""
     hi = _f(x).to(torch.float16)

@@ -189,6 +189,44 @@ def test_linear_h3_colscale_planes(M, N, K):
     assert float(pl.float().abs().max()) < 2 ** 15
 
 
+@pytest.mark.parametrize("M,K,two_term", [(32768, 896, True), (32768, 4864, True), (16384, 896, False)])
+def test_linear_h3_np(M, K, two_term):
+    """The O-projection / down GEMM with the next RMSNorm's producer side in its epilogue (EPI_F32_RESID_NP): the fp32
+    output bit-identical to the plain residual GEMM, the planes the exact split of p_m (y_m * g) and 1 / p_m exactly the
+    CPU oracle's (R.np_planes on the GPU's y: same fp32 bound arithmetic), below 2^14, the sum-of-squares partials the
+    row sums of y^2 per 112-column slab; and the consumer side (row_rscale_mul + the gate/up GEMM on the planes) equal
+    to rmsnorm -> gate/up within fp32 accuracy."""
+    N = 896
+    x, w, r = rnd(M, K, seed=60), rnd(N, K, s=0.03, seed=61), rnd(M, N, seed=62)
+    if two_term:
+        w = w.bfloat16().float()
+    g = 1 + 0.2 * rnd(N, seed=63)
+    g[7] = 9.0                                   # an outlier norm channel
+    sx = R.h3_scale(x.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    a3, w3d, rd = R.h3_act(x, sx).to(DEV), w3.to(DEV), r.to(DEV)
+    rstd = torch.rsqrt(r.pow(2).mean(1) + 1e-6)
+    pb = float(x.abs().max() * w.abs().sum(1).max())          # |x @ w.T| bound
+    assert ops.gemm_np_supported(M, N, 2 * K)
+    al = 1.0 / (sx * sw)
+    y0 = ops.linear_h3(a3, w3d, al, residual=rd)
+    y, pl, pr, ssq = ops.linear_h3_np(a3, w3d, al, rd, g.to(DEV), rstd.to(DEV), float(g.abs().max()), pb)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    want_pl, want_pr, want_ssq = R.np_planes(y.cpu(), g, rstd, float(g.abs().max()), pb)
+    assert torch.equal(pr.cpu(), want_pr) and torch.equal(pl.cpu(), want_pl)
+    assert float(pl.float().abs().max()) < 2 ** 14
+    assert rel_err(ssq, want_ssq.double()) < 1e-6
+    # consumer: the gate/up GEMM on the planes with the fused row scale == on rmsnorm(y) * g planes (fp32 accuracy)
+    wg = rnd(2 * 4864, N, s=0.03, seed=64).bfloat16().float()
+    wg3, swg = R.h3_weight(wg)
+    rs = ops.row_rscale_mul(ssq, pr, N, 1e-6)
+    yd = y.cpu().double()
+    yn = yd * torch.rsqrt(yd.pow(2).mean(1, keepdim=True) + 1e-6) * g.double()
+    got_gu = ops.linear_h3(pl, wg3.to(DEV), 1.0 / swg, rscale=rs)   # the plain GEMM: the pre-activations
+    assert rel_err(got_gu, yn @ wg.double().t()) < 4e-6
+
+
 @pytest.mark.parametrize("M,two_term", [(32768, True), (32768, False), (1000, True), (257, False)])
 def test_linear_h3_swiglu_raw(M, two_term):
     """One GEMM for the SwiGLU planes and the saved pre-activations (AttnLRP forward): the planes bit-identical to
@@ -469,6 +507,27 @@ def test_full_model_nll_matches_cpu_fp32(name, B, S, values):
     assert rel < 1e-4, (rel, cpu.tolist(), gpu.tolist())
 
 
+def test_full_model_fused_norm_equals_separate_pass():
+    """Qwen2-0.5B fp32 mode with RMSNorm-2 fused into the O projection's epilogue (default) vs the separate norm pass:
+    the final hidden state and the row NLL agree to fp32 accuracy (the planes carry a per-row instead of a per-layer
+    scale, and the row sums of squares come from the epilogue's 112-column partials)."""
+    from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
+    from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows
+    from llm_inference_in_distributed_edge_networks_amd.models import DecoderLM, get_config
+    cfg = get_config("qwen2-0.5b")
+    S = 512
+    toks = synthetic_stream(S * 40, cfg.vocab_size, 0)
+    b = next(batches(toks, [w for w in sliding_windows(toks.shape[1], S, 32) if w.length == S][:32], 32)).to(DEV)
+    m = DecoderLM.random_init(cfg, 0, device=DEV, dtype=torch.float32, values=torch.bfloat16)
+    assert m.fuse_norm_f32 and m._np_fused(32 * S)
+    out = {}
+    for flag in (True, False):
+        m.fuse_norm_f32 = flag
+        x = m.forward_hidden(b.ids)
+        out[flag] = (x.double().cpu(), m.row_nll(x, b.rows, b.targets).double().cpu())
+    assert _l2(out[True][0], out[False][0]) < 2e-6 and _l2(out[True][1], out[False][1]) < 1e-6
+
+
 @pytest.mark.parametrize("name", ["qwen2-0.5b", "pythia-70m"])
 def test_full_model_kv_planes_identical(name, monkeypatch):
     """The fp32 model with the plane-staged attention (default) equals the per-tile-split attention bit for bit."""
@@ -591,9 +650,10 @@ def test_full_model_hidden_state_and_peaked_nll(name, B, S, values, monkeypatch)
     xg, ng, wg = _hidden_and_nll(mg, bg)
     e_h, e_n = _l2(xg, xc), _l2(ng, nc)
     spread = float(nc.std())       # nats; ~0 for a near-uniform softmax (random head), tens of nats here
-    # layer 3's O projection: the 2nd fp32 GEMM of a layer (QKV has its own entry point), 3 per Qwen2 layer /
-    # 3 per NeoX layer after the QKV
-    per_layer = 3
+    # the (3 per_layer + 1)-th ops.linear_h3 GEMM of the forward (QKV has its own entry point): 3 per Qwen2 / NeoX
+    # layer after the QKV - layer 3's O projection; 2 with RMSNorm-2 fused into the O projection (ops.linear_h3_np),
+    # the O projection then has its own entry point too - layer 3's gate/up GEMM
+    per_layer = 2 if (cfg.arch == "qwen2" and mg.fuse_norm_f32) else 3
     pert = _PerturbOneGemm(3 * per_layer + 1, 1e-4)
     monkeypatch.setattr(ops, "linear_h3", pert)
     xp, npp, _ = _hidden_and_nll(mg, bg)
