@@ -148,9 +148,12 @@ class DecoderLM:
         self.sin = sin.to(self.device).contiguous()
         self.q_scale = 1.0 / math.sqrt(cfg.head_dim)
         # fp32 (h3) mode, Qwen2: RMSNorm-2 fused into the O-projection's epilogue (linear_h3_np) when the GPU kernel
-        # runs the shape; EDGE_FUSED_NORM_F32=0 keeps the separate norm pass (A/B); tests set it on CPU models too
+        # runs the shape.  Off by default: same-box, the bench step is 0.7-1.3 % SLOWER with it (the epilogue's plane
+        # stores cost the O-projection +28 us, more than the 34 us norm pass they replace once the gate/up GEMM that
+        # follows is counted; docs/RESULTS.md section 6, profiles/r06/fused_norm/).  EDGE_FUSED_NORM_F32=1 turns it on;
+        # tests set the attribute directly (also on CPU models, the oracle of the fused path)
         self.fuse_norm_f32 = (self.h3 and cfg.arch == "qwen2" and self.device.type == "cuda"
-                              and os.environ.get("EDGE_FUSED_NORM_F32", "1") not in ("", "0"))
+                              and os.environ.get("EDGE_FUSED_NORM_F32", "0") not in ("", "0"))
         # GPU fast path for RMSNorm models: the norm weight is folded into the consuming GEMM's weight and
         # the row scale is applied in its epilogue, from sum-of-squares partials the residual GEMMs emit.
         self.fuse_norm = (self.device.type == "cuda" and cfg.arch == "qwen2" and dtype == torch.bfloat16

@@ -508,7 +508,7 @@ def test_full_model_nll_matches_cpu_fp32(name, B, S, values):
 
 
 def test_full_model_fused_norm_equals_separate_pass():
-    """Qwen2-0.5B fp32 mode with RMSNorm-2 fused into the O projection's epilogue (default) vs the separate norm pass:
+    """Qwen2-0.5B fp32 mode with RMSNorm-2 fused into the O projection's epilogue (opt-in) vs the separate norm pass:
     the final hidden state and the row NLL agree to fp32 accuracy (the planes carry a per-row instead of a per-layer
     scale, and the row sums of squares come from the epilogue's 112-column partials)."""
     from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
@@ -519,7 +519,8 @@ def test_full_model_fused_norm_equals_separate_pass():
     toks = synthetic_stream(S * 40, cfg.vocab_size, 0)
     b = next(batches(toks, [w for w in sliding_windows(toks.shape[1], S, 32) if w.length == S][:32], 32)).to(DEV)
     m = DecoderLM.random_init(cfg, 0, device=DEV, dtype=torch.float32, values=torch.bfloat16)
-    assert m.fuse_norm_f32 and m._np_fused(32 * S)
+    m.fuse_norm_f32 = True                       # opt-in (EDGE_FUSED_NORM_F32=1): slower on the bench, kept tested
+    assert m._np_fused(32 * S)
     out = {}
     for flag in (True, False):
         m.fuse_norm_f32 = flag
