@@ -8,9 +8,12 @@ R=$PWD
 timeout -k 10 180 python -c "import time, __graft_entry__ as g; t=time.time(); g.smoke(); print('smoke s', round(time.time()-t, 1))" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
 grep -E "smoke" $O/smoke.log
 if [ "${SUITE:-1}" = 1 ]; then
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
-  > $O/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -40 $O/pytest_gpu.log; exit 1; }
-tail -2 $O/pytest_gpu.log
+( while sleep 30; do date +%T >> $O/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --durations=15 --timeout 300 --timeout-method thread \
+  -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; grep -E "FAILED|ERROR" $O/pytest_gpu.log | head; tail -40 $O/pytest_gpu.log; exit 1; }
+grep -cE " PASSED" $O/pytest_gpu.log; tail -18 $O/pytest_gpu.log
 fi
 timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 --json-out $O/bench.json > $O/bench.log 2>&1 \
   || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
