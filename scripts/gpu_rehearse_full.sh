@@ -5,6 +5,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+( while sleep 30; do date +%T >> gpurun_out/rehearse_heartbeat; done ) &   # long cases print nothing for minutes
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 run() {  # n extra-args...
   local n=$1; shift
   local tag=$n$(echo "$@" | tr -d ' -')
