@@ -120,12 +120,11 @@ def main():
         except subprocess.TimeoutExpired:
             child.kill()
             child.wait()
-    hog_ran = [r for r in rows]
     out = {"what": "per-window NLL bit-identity of the bench step (config 3, HIP graphs) while another process floods "
                    "the GPU with 2 GiB copies and fp16 GEMMs",
            "model": cfg.name, "windows_per_step": a.batch * a.microbatches,
            "idle_identical": {n: r["idle_identical"] for n, r in runs.items()},
-           "under_contention": len(hog_ran), "all_identical": all(r["identical"] for r in rows) and
+           "under_contention": len(rows), "all_identical": all(r["identical"] for r in rows) and
            all(r["idle_identical"] for r in runs.values()) and len(rows) > 0, "rows": rows}
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
