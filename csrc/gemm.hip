@@ -15,6 +15,7 @@
 //   target logit, logits are never written to memory).
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_GELU = 4, EPI_SWIGLU = 5,
        EPI_QKV_ROPE = 6, EPI_LSE = 7,
@@ -1088,6 +1089,9 @@ template <int BN> struct Geo {
   static constexpr int NR = 8 + NJ;                     // fragment reads (and glds) per wave per K-half (K-tile)
   static constexpr int MF = 8 * NJ;                     // MFMAs per wave per K-half
   static constexpr int LDS = 2 * TB;
+  // R3 (paired-B h3 GEMMs): three A slots of 32 KiB in a ring, then the two pair B regions - the DMA runs three K-tiles
+  // ahead instead of two (96 KiB + 2 x BN/8 KiB <= 160 KiB for BN <= 256)
+  static constexpr int LDS_R3 = 3 * 32768 + 2 * BN * 128;
 };
 // position (MFMA index) after which work item r of NR is issued: evenly spread over the MF MFMAs
 template <int MF, int NR>
@@ -1359,14 +1363,26 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
 // against the same weight columns) lives in the B region of buffer p & 1 and is staged with the pair's even K-tile
 // only - a quarter less L2 -> LDS traffic.  The K loop is unrolled by two so that every DMA / read switch stays
 // compile-time (nk is even: pairs never straddle tiles).
-template <int EPI, int RH, int BN, bool PB = false>
+//
+// R3 (with PB): the A tiles live in a ring of three LDS slots (K-tile t in slot t mod 3) and the pair B tiles in two
+// regions after them, so M(t,1) stages K-tile t + 3 instead of t + 2 (into slot t mod 3, whose last reads - K-half 1 of
+// K-tile t in M(t,0) - retired before the barrier) and the wait before M(t,1) leaves the newest K-tile's DMA in flight:
+// vmcnt(8 + NB) after an M(t-1,1) that staged an even K-tile (A and the pair's B), vmcnt(8) after one that staged an odd
+// one (A only).  Every vector-memory op issued after those glds - epilogue loads and stores included - only makes the
+// wait retire more, never less.  Three K-halves of MFMAs instead of two hide each DMA (the short-K QKV and
+// O-projection GEMMs wait on it; tools/glds_wait_audit.py checks the prologue count).
+template <int EPI, int RH, int BN, bool PB = false, bool R3 = false>
 __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   static_assert(!PB || epi_f32(EPI), "paired B: h3 GEMMs");
+  static_assert(!R3 || PB, "the A-slot ring: paired-B GEMMs");
   static_assert(BN != 192 || ((EPI == EPI_F32_QKV_ROPE || EPI == EPI_QKV_ROPE) && (RH == 0 || RH == 32)),
                 "192-wide tiles: QKV only");
   static_assert(BN == 192 || BN == 224 || BN == 256, "tile width");
   using Gm = w4::Geo<BN>;
   constexpr int NJ = Gm::NJ, NB = Gm::NB, BOFF = Gm::BOFF, TB = Gm::TB, NR = Gm::NR, MF = Gm::MF;
+  // LDS geometry: A tile of K-tile q at aslot(q); B tiles at BREG + region * BSTRIDE (PB: region = pair parity)
+  constexpr int BREG = R3 ? 3 * 32768 : BOFF, BSTRIDE = R3 ? BN * 128 : TB;
+  auto aslot = [](int q) -> uint32_t { return R3 ? (uint32_t)(q % 3) * 32768u : (uint32_t)(q & 1) * TB; };
   using CQ = Cfg<256, 256, 4, 4>;   // BN = 256 epilogue view: 64x64 slabs
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1414,8 +1430,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     if (r < 8) {
       glds16(sa + kba + oa[r], buf + (r * 4 + wave) * 1024);
     } else {
-      char* bbuf = PB ? smem + ((st_q >> 1) & 1) * TB : buf;
-      glds16(sb + kb + ob[r - 8], bbuf + BOFF + ((r - 8) * 4 + wave) * 1024);
+      char* bbuf = PB ? smem + BREG + ((st_q >> 1) & 1) * BSTRIDE : buf + BOFF;
+      glds16(sb + kb + ob[r - 8], bbuf + ((r - 8) * 4 + wave) * 1024);
     }
   };
   // byte offsets of the stream K-tile's A and B columns (h3 operands: the plane remap / pair mapping, computed once per
@@ -1434,7 +1450,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     st_kb = b_kcol(a, st_kt * 64) * 2;
   };
   auto stage_all = [&](auto with_b) {
-    char* buf = smem + (st_q & 1) * TB;
+    char* buf = smem + aslot(st_q);
     const int kb = st_kb, kba = st_kba;
 #pragma unroll
     for (int r = 0; r < (decltype(with_b)::value ? NR : 8); ++r) dma_item(r, buf, kba, kb);
@@ -1448,7 +1464,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   for (int ks = 0; ks < 2; ++ks) {
     const int c = ks * 4 + (lane >> 4);
     abase[ks] = lds_addr(smem) + (wm * 128 + (lane & 15)) * 128 + ((c ^ sw) << 4);
-    bbase[ks] = lds_addr(smem) + BOFF + (wn * (BN / 2) + (lane & 15)) * 128 + ((c ^ sw) << 4);
+    bbase[ks] = lds_addr(smem) + BREG + (wn * (BN / 2) + (lane & 15)) * 128 + ((c ^ sw) << 4);
   }
   bf16x8_t XA[8], XB[NJ], YA[8], YB[NJ];
   f32x4_t acc[8][NJ];
@@ -1461,7 +1477,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     constexpr bool first = decltype(first_c)::value, dma_on = decltype(dma_c)::value;
     constexpr bool read_on = decltype(read_c)::value, dma_b = decltype(dmab_c)::value;
     const uint32_t va = abase[ks] + bo, vb = bbase[ks] + boB;
-    char* dbuf = smem + (st_q & 1) * TB;
+    char* dbuf = smem + aslot(st_q);
     const int kb = st_kb, kba = st_kba;
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
@@ -1490,9 +1506,16 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     if constexpr (dma_on) advance_stage();
   };
 
-  // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed and visible, its K-half 0 fragments in X
+  // prologue: K-tiles 0 and 1 (R3: 0, 1 and 2) in flight, K-tile 0 landed and visible, its K-half 0 fragments in X
   stage_all(std::true_type{});
-  if (total > 1) {
+  if constexpr (R3) {
+    // PB: total >= nk >= 2; past the end the stream re-stages its last K-tile into slots nobody reads again
+    stage_all(std::false_type{});   // K-tile 1 (odd): A only
+    stage_all(std::true_type{});    // K-tile 2 (even): A and pair 1's B
+    if constexpr (NB == 8) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");         // K-tiles 1 and 2: 8 + 16
+    else if constexpr (NB == 7) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");    // 8 + 15
+    else asm volatile("s_waitcnt vmcnt(22)" ::: "memory");                          // 8 + 14
+  } else if (total > 1) {
     stage_all(std::integral_constant<bool, !PB>{});
     if constexpr (PB) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-tile 1 staged its 8 A blocks only
     else if constexpr (NR == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -1531,18 +1554,30 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   // K-tile t of the stream; dmab_c: the DMA issued in M(t,1) (K-tile t + 2) includes the B tile; end_c: K-tile t
   // may be its tile's last (with PB only odd K-tiles can be)
   auto ktile = [&](int t, auto dmab_c, auto end_c) {
-    const uint32_t bo = (t & 1) * TB, bn = ((t + 1) & 1) * TB;
-    const uint32_t boB = PB ? ((t >> 1) & 1) * TB : bo, bnB = PB ? (((t + 1) >> 1) & 1) * TB : bn;
+    const uint32_t bo = aslot(t), bn = aslot(t + 1);
+    const uint32_t boB = PB ? ((t >> 1) & 1) * BSTRIDE : bo, bnB = PB ? (((t + 1) >> 1) & 1) * BSTRIDE : bn;
     // M(t,0) on X, K-half 1 of K-tile t -> Y
     __builtin_amdgcn_sched_barrier(0);
     if (kt == 0) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, std::false_type{}, std::true_type{}, dmab_c);
     else mma(XA, XB, YA, YB, bo, boB, 1, std::false_type{}, std::false_type{}, std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < total) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + 1 < total) {
+      if constexpr (R3) {
+        // K-tile t+1 landed; K-tile t+2 (staged in M(t-1,1): A + B when t is even - then this ktile stages an odd one,
+        // dmab off - A only when t is odd) may stay in flight
+        if constexpr (decltype(dmab_c)::value) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else if constexpr (NB == 8) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+        else if constexpr (NB == 7) asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // M(t,1) on Y, K-tile t+2 -> buffer t & 1, K-half 0 of K-tile t+1 -> X.  Unconditional: past the end of the
+    // M(t,1) on Y, K-tile t+2 (R3: t+3) -> buffer t & 1 (R3: slot t mod 3), K-half 0 of K-tile t+1 -> X.  Unconditional: past the end of the
     // stream the DMA re-reads the last K-tile into a buffer nobody reads again and X gets values nobody consumes.
     // (A runtime switch between read / no-read copies of this loop makes the allocator spill the fragments.)
     mma(YA, YB, XA, XB, bn, bnB, 0, std::false_type{}, std::true_type{}, std::true_type{}, dmab_c);
@@ -1634,7 +1669,10 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   };
 #pragma unroll 1
   for (int t = 0; t < total; t += PB ? 2 : 1) {
-    if constexpr (PB) {
+    if constexpr (R3) {
+      ktile(t, std::false_type{}, std::false_type{});      // M(t,1) stages K-tile t+3 (odd): A only
+      ktile(t + 1, std::true_type{}, std::true_type{});    // M(t+1,1) stages K-tile t+4 (even): A and the pair's B
+    } else if constexpr (PB) {
       ktile(t, std::true_type{}, std::false_type{});       // M(t,1) stages K-tile t+2 (even): A and the pair's B
       ktile(t + 1, std::false_type{}, std::true_type{});   // M(t+1,1) stages K-tile t+3 (odd): A only
     } else {
@@ -1670,27 +1708,40 @@ static int launch_cfg(const GemmArgs& a, hipStream_t st) {
 }
 
 // the persistent four-wave kernel: one workgroup per CU walks its tiles (walk 0 strided, 1 XCD-chunked)
-template <int EPI, int RH, int BN, bool PB>
+template <int EPI, int RH, int BN, bool PB, bool R3 = false>
 static int launch_4w_pb(const GemmArgs& args, hipStream_t st, int walk) {
   GemmArgs a = args;
   a.walk = walk;
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   const int grid = std::min(tiles, num_cus());
-  constexpr int lds = w4::Geo<BN>::LDS;
+  constexpr int lds = R3 ? w4::Geo<BN>::LDS_R3 : w4::Geo<BN>::LDS;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, BN, PB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
+    (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, BN, PB, R3>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, BN, PB>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, BN, PB, R3>), dim3(grid), dim3(256), lds, st, a);
   return (int)hipGetLastError();
+}
+
+// the three-slot A ring of the paired-B four-wave kernels (gemm_4w_kernel R3): EDGE_GEMM_RING=1 or edge_gemm_set_ring
+static int g_ring = -1;
+static bool use_ring() {
+  if (g_ring < 0) {
+    const char* e = getenv("EDGE_GEMM_RING");
+    g_ring = (e && e[0] && e[0] != '0') ? 1 : 0;
+  }
+  return g_ring == 1;
 }
 
 template <int EPI, int RH, int BN = 256>
 static int launch_4w(const GemmArgs& a, hipStream_t st, int walk = 0) {
   if constexpr (epi_f32(EPI)) {
-    if (a.pairb) return launch_4w_pb<EPI, RH, BN, true>(a, st, walk);
+    if (a.pairb) {
+      if (use_ring()) return launch_4w_pb<EPI, RH, BN, true, true>(a, st, walk);
+      return launch_4w_pb<EPI, RH, BN, true>(a, st, walk);
+    }
   }
   return launch_4w_pb<EPI, RH, BN, false>(a, st, walk);
 }
@@ -1746,6 +1797,12 @@ static int launch(const GemmArgs& a, hipStream_t st) {
 
 EDGE_API int edge_gemm_set_tile(int t) {
   g_tile_override = t;
+  return 0;
+}
+
+// 1: the paired-B h3 GEMMs run the three-slot A ring (gemm_4w_kernel R3), 0: two buffers; -1: from EDGE_GEMM_RING
+EDGE_API int edge_gemm_set_ring(int on) {
+  g_ring = on;
   return 0;
 }
 

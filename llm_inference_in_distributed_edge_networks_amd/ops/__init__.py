@@ -166,6 +166,12 @@ def set_gemm_tile(tile: int) -> None:
     call("edge_gemm_set_tile", int(tile))
 
 
+def set_gemm_ring(on: int) -> None:
+    """The paired-B h3 (fp32-mode) GEMMs on the three-slot A ring (gemm_4w_kernel R3: the DMA three K-tiles ahead):
+    1 on, 0 off, -1 from EDGE_GEMM_RING (default off)."""
+    call("edge_gemm_set_ring", int(on))
+
+
 def gemm_ssq_parts(M: int, N: int, K: int, act=None, bias=False, residual=False) -> int:
     """Row sum-of-squares partials ``linear(..., want_ssq=True)`` produces for this shape: N/64 (64-column
     slabs), or N/112 (wave slabs) when the 256x224 kernel runs it."""
