@@ -80,7 +80,8 @@ struct GemmArgs {
   // partials, rsqrt(sum_p ssq_in[m, p] * norm_inv_k + norm_eps); takes precedence over rscale
   const float* ssq_in; int ssq_parts; float norm_inv_k, norm_eps;
   int walk;      // persistent four-wave kernel's tile walk: 0 = strided by the grid size, 1 = XCD-contiguous chunks
-  int h3k;       // > 0: A is a 2-plane h3 activation [M, 2 h3k] (common.h h3_acol) of the K' = 3 h3k (or 2 h3k) GEMM
+  int store_wait = 0;  // four-wave kernel: the wait after a full tile's epilogue leaves its last stores in flight
+  int h3k;      // > 0: A is a 2-plane h3 activation [M, 2 h3k] (common.h h3_acol) of the K' = 3 h3k (or 2 h3k) GEMM
   int pairb;     // h3 two-product GEMM (K' = 2 h3k, B the single fp16 plane [N, h3k]): K-tiles interleave the planes,
                  // t -> A plane (t odd: hi, even: lo) column 64 (t >> 1), B column 64 (t >> 1) (b_kcol)
   float alpha = 1.f;      // h3: 1 / (s_a s_b), the product's scale (applied with the row scale)
@@ -1371,6 +1372,27 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
 // one (A only).  Every vector-memory op issued after those glds - epilogue loads and stores included - only makes the
 // wait retire more, never less.  Three K-halves of MFMAs instead of two hide each DMA (the short-K QKV and
 // O-projection GEMMs wait on it; tools/glds_wait_audit.py checks the prologue count).
+//
+// Stores after an epilogue (GemmArgs::store_wait): vmcnt counts stores, and retires in issue order, so the first wait
+// of the next tile - for the K-tile whose DMA M(t,1) issued just before the epilogue - also drained the whole
+// epilogue's stores.  epi_tail_stores<EPI, BN>() is a lower bound on the vector-memory ops every wave issues after the
+// last of its epilogue's own waits, when the tile is full (no guarded row skips a store): vmcnt(that + the DMA
+// issued after K-tile t+1) still retires K-tile t+1's DMA and leaves those stores in flight.
+//   SwiGLU 256x256 (swiglu_h3_lines_4w): no loads; 8 row groups x 4 line stores = 32.
+//   fp32 256x224 (w4_f32_epilogue_224): row pair 3's residual loads are issued after pair 1's stores and waited for
+//   before pair 3 computes; pairs 2 and 3 store 2 x 2 x 7 = 28 after that wait.
+template <int EPI, int BN>
+__device__ constexpr int epi_tail_stores() {
+  if constexpr (BN == 256 && EPI == EPI_H3_SWIGLU) return 32;
+  else if constexpr (BN == 224 && epi_f32(EPI)) return 28;
+  else return 0;
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
 template <int EPI, int RH, int BN, bool PB = false, bool R3 = false>
 __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   static_assert(!PB || epi_f32(EPI), "paired B: h3 GEMMs");
@@ -1532,6 +1554,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
   int tile = tile0, kt = 0, m0, n0;
+  bool epi_full = false;   // the previous tile's epilogue issued its epi_tail_stores (store_wait on, full tile)
   tile_origin(tile, a.M, a.N, 256, BN, m0, n0);
   float rs[8];
   auto load_rs = [&](int mt) {
@@ -1562,15 +1585,16 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     else mma(XA, XB, YA, YB, bo, boB, 1, std::false_type{}, std::false_type{}, std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < total) {
-      if constexpr (R3) {
-        // K-tile t+1 landed; K-tile t+2 (staged in M(t-1,1): A + B when t is even - then this ktile stages an odd one,
-        // dmab off - A only when t is odd) may stay in flight
-        if constexpr (decltype(dmab_c)::value) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-        else if constexpr (NB == 8) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-        else if constexpr (NB == 7) asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
+      // R3: K-tile t+1 landed; K-tile t+2 (staged in M(t-1,1): A + B when t is even - then this ktile stages an odd
+      // one, dmab off - A only when t is odd) may stay in flight.  After a full tile's epilogue its last TS stores
+      // may too (they were issued after M(t-1,1)'s DMA).
+      constexpr int N0 = R3 ? (decltype(dmab_c)::value ? 8 : 8 + NB) : 0;
+      constexpr int TS = epi_tail_stores<EPI, BN>();
+      if constexpr (TS > 0) {
+        if (kt == 0 && epi_full) wait_vm_lgkm0<N0 + TS>();
+        else wait_vm_lgkm0<N0>();
       } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        wait_vm_lgkm0<N0>();
       }
     } else {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1651,6 +1675,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      epi_full = a.store_wait && m0 + 256 <= a.M && n0 + BN <= a.N;
       tile += G;
       kt = 0;
       if (tile < walk.end) {
@@ -1707,11 +1732,22 @@ static int launch_cfg(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// GemmArgs::store_wait for the four-wave kernels: EDGE_GEMM_STORE_WAIT (1 / 0) or edge_gemm_set_store_wait
+static int g_store_wait = -1;
+static int store_wait() {
+  if (g_store_wait < 0) {
+    const char* e = getenv("EDGE_GEMM_STORE_WAIT");
+    g_store_wait = (e && e[0] && e[0] != '0') ? 1 : 0;
+  }
+  return g_store_wait;
+}
+
 // the persistent four-wave kernel: one workgroup per CU walks its tiles (walk 0 strided, 1 XCD-chunked)
 template <int EPI, int RH, int BN, bool PB, bool R3 = false>
 static int launch_4w_pb(const GemmArgs& args, hipStream_t st, int walk) {
   GemmArgs a = args;
   a.walk = walk;
+  a.store_wait = store_wait();
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   const int grid = std::min(tiles, num_cus());
   constexpr int lds = R3 ? w4::Geo<BN>::LDS_R3 : w4::Geo<BN>::LDS;
@@ -1803,6 +1839,13 @@ EDGE_API int edge_gemm_set_tile(int t) {
 // 1: the paired-B h3 GEMMs run the three-slot A ring (gemm_4w_kernel R3), 0: two buffers; -1: from EDGE_GEMM_RING
 EDGE_API int edge_gemm_set_ring(int on) {
   g_ring = on;
+  return 0;
+}
+
+// 1: the four-wave kernels leave a full tile's last epilogue stores in flight across the next tile's first wait
+// (GemmArgs::store_wait), 0: that wait drains them; -1: from EDGE_GEMM_STORE_WAIT
+EDGE_API int edge_gemm_set_store_wait(int on) {
+  g_store_wait = on;
   return 0;
 }
 

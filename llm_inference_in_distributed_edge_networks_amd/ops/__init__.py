@@ -172,6 +172,12 @@ def set_gemm_ring(on: int) -> None:
     call("edge_gemm_set_ring", int(on))
 
 
+def set_gemm_store_wait(on: int) -> None:
+    """The four-wave GEMMs leave a full tile's last epilogue stores in flight across the next tile's first K-tile wait
+    (vmcnt counts stores; without this that wait drains them): 1 on, 0 off, -1 from EDGE_GEMM_STORE_WAIT."""
+    call("edge_gemm_set_store_wait", int(on))
+
+
 def gemm_ssq_parts(M: int, N: int, K: int, act=None, bias=False, residual=False) -> int:
     """Row sum-of-squares partials ``linear(..., want_ssq=True)`` produces for this shape: N/64 (64-column
     slabs), or N/112 (wave slabs) when the 256x224 kernel runs it."""

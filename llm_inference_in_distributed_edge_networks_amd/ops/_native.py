@@ -36,6 +36,7 @@ _SIGS = {
     "edge_row_rscale": [c_p, c_p, c_i, c_i, c_i, c_f, c_p],
     "edge_gemm_set_tile": [c_i],
     "edge_gemm_set_ring": [c_i],
+    "edge_gemm_set_store_wait": [c_i],
     "edge_gemm_ssq_parts": [c_i, c_i, c_i, c_i, c_i, c_i],
     "edge_gemm_qkv_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_f, c_p, c_p,
                            c_i, c_f, c_p],
@@ -143,7 +144,7 @@ def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
 
-_NO_LAUNCH = {"edge_gemm_set_tile", "edge_gemm_set_ring", "edge_gemm_ssq_parts", "edge_poison_lds", "edge_poison_lds_bytes",
+_NO_LAUNCH = {"edge_gemm_set_tile", "edge_gemm_set_ring", "edge_gemm_set_store_wait", "edge_gemm_ssq_parts", "edge_poison_lds", "edge_poison_lds_bytes",
               "edge_gemm_f32_np_ok"}
 
 

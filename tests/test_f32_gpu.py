@@ -575,9 +575,11 @@ def test_linear_h3_four_wave_224(M, N, K):
     (32768, 896, 896, "resid", 0), (32768, 896, 4864, "resid", 0), (4096, 9728, 896, "swiglu", 0),
     (1000, 9728, 896, "swiglu", 256), (257, 896, 896, "resid", 224), (700, 512, 2048, "bias_resid", 256),
     (300, 512, 128, "none", 256), (5000, 896, 128, "resid", 224)])
-def test_linear_h3_ring_bit_identical(M, N, K, epi, tile):
-    """The paired-B h3 GEMMs on the three-slot A ring (DMA three K-tiles ahead, opt-in) equal the two-buffer kernel
-    bit for bit: same MFMA order, only the staging changes (partial tiles, one K pair, many tiles per workgroup)."""
+@pytest.mark.parametrize("knob", ["ring", "store_wait", "ring+store_wait"])
+def test_linear_h3_ring_bit_identical(M, N, K, epi, tile, knob):
+    """The paired-B h3 GEMMs on the three-slot A ring (DMA three K-tiles ahead, opt-in) and / or with a full tile's
+    last epilogue stores left in flight across the next tile's first wait equal the default kernel bit for bit: same
+    MFMA order, only the staging and the waits change (partial tiles, one K pair, many tiles per workgroup)."""
     x = rnd(M, K, seed=20)
     w = rnd(N, K, s=1 / math.sqrt(K), seed=21).to(torch.bfloat16).float()
     b = rnd(N, s=0.1, seed=22).to(DEV) if "bias" in epi else None
@@ -589,19 +591,27 @@ def test_linear_h3_ring_bit_identical(M, N, K, epi, tile):
     out = {}
     ops.set_gemm_tile(tile)
     try:
-        for ring in (0, 1):
-            ops.set_gemm_ring(ring)
-            out[ring] = ops.linear_h3(a3, w3, 1.0 / (sx * sw), b, r, act, out_scale=1.0)
+        for on in (0, 1):
+            _knob(knob, on)
+            out[on] = ops.linear_h3(a3, w3, 1.0 / (sx * sw), b, r, act, out_scale=1.0)
         torch.cuda.synchronize()
     finally:
-        ops.set_gemm_ring(-1)
+        _knob(knob, -1)
         ops.set_gemm_tile(0)
     assert torch.equal(out[0], out[1])
 
 
-def test_full_model_ring_identical():
-    """Qwen2-0.5B fp32 mode (QKV, O-proj, gate/up, down and the LSE head all paired-B): the three-slot A ring equals
-    the two-buffer kernels bit for bit on the final hidden state and the row NLL."""
+def _knob(knob: str, on: int) -> None:
+    if "ring" in knob:
+        ops.set_gemm_ring(on)
+    if "store_wait" in knob:
+        ops.set_gemm_store_wait(on)
+
+
+@pytest.mark.parametrize("knob", ["ring", "store_wait"])
+def test_full_model_ring_identical(knob):
+    """Qwen2-0.5B fp32 mode (QKV, O-proj, gate/up, down and the LSE head all paired-B): the three-slot A ring / the
+    store-tolerant post-epilogue wait equal the default kernels bit for bit on the final hidden state and row NLL."""
     from llm_inference_in_distributed_edge_networks_amd.eval.data import synthetic_stream
     from llm_inference_in_distributed_edge_networks_amd.eval.windows import batches, sliding_windows
     from llm_inference_in_distributed_edge_networks_amd.models import DecoderLM, get_config
@@ -612,12 +622,12 @@ def test_full_model_ring_identical():
     m = DecoderLM.random_init(cfg, 0, device=DEV, dtype=torch.float32, values=torch.bfloat16)
     out = {}
     try:
-        for ring in (0, 1):
-            ops.set_gemm_ring(ring)
+        for on in (0, 1):
+            _knob(knob, on)
             x = m.forward_hidden(b.ids)
-            out[ring] = (x.clone(), m.row_nll(x, b.rows, b.targets).clone())
+            out[on] = (x.clone(), m.row_nll(x, b.rows, b.targets).clone())
     finally:
-        ops.set_gemm_ring(-1)
+        _knob(knob, -1)
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
 
 
