@@ -1090,8 +1090,8 @@ template <int BN> struct Geo {
   static constexpr int NR = 8 + NJ;                     // fragment reads (and glds) per wave per K-half (K-tile)
   static constexpr int MF = 8 * NJ;                     // MFMAs per wave per K-half
   static constexpr int LDS = 2 * TB;
-  // R3 (paired-B h3 GEMMs): three A slots of 32 KiB in a ring, then the two pair B regions - the DMA runs three K-tiles
-  // ahead instead of two (96 KiB + 2 x BN/8 KiB <= 160 KiB for BN <= 256)
+  // R3 (paired-B h3 GEMMs): three A slots of 32 KiB in a ring, then the two pair B regions - a K-tile's DMA spread
+  // over both K-halves (96 KiB + 2 x BN/8 KiB <= 160 KiB for BN <= 256)
   static constexpr int LDS_R3 = 3 * 32768 + 2 * BN * 128;
 };
 // position (MFMA index) after which work item r of NR is issued: evenly spread over the MF MFMAs
@@ -1365,13 +1365,14 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
 // only - a quarter less L2 -> LDS traffic.  The K loop is unrolled by two so that every DMA / read switch stays
 // compile-time (nk is even: pairs never straddle tiles).
 //
-// R3 (with PB): the A tiles live in a ring of three LDS slots (K-tile t in slot t mod 3) and the pair B tiles in two
-// regions after them, so M(t,1) stages K-tile t + 3 instead of t + 2 (into slot t mod 3, whose last reads - K-half 1 of
-// K-tile t in M(t,0) - retired before the barrier) and the wait before M(t,1) leaves the newest K-tile's DMA in flight:
-// vmcnt(8 + NB) after an M(t-1,1) that staged an even K-tile (A and the pair's B), vmcnt(8) after one that staged an odd
-// one (A only).  Every vector-memory op issued after those glds - epilogue loads and stores included - only makes the
-// wait retire more, never less.  Three K-halves of MFMAs instead of two hide each DMA (the short-K QKV and
-// O-projection GEMMs wait on it; tools/glds_wait_audit.py checks the prologue count).
+// R3 (with PB): the A tiles live in a ring of three LDS slots (K-tile q in slot q mod 3) and the pair B tiles in two
+// regions after them, which frees a slot one K-half earlier and lets the DMA be SPREAD over both K-halves instead of
+// issued in one: M(u,0) stages K-tile u+2's 8 A pieces into slot (u+2) mod 3 (K-tile u-1's, whose last reads - K-half 1
+// in M(u-1,0) - retired before ktile(u-1)'s barrier), M(u,1) its NB B pieces when u+2 is even (into the B region of
+// pair (u+2)/2 = pair u/2 - 1's, last read in M(u-1,0) too) and advances the stream.  Per K-half at most 8 or NB pieces
+// instead of 0 and 8+NB: an LDS-DMA piece costs its wave ~60 issue cycles among bare MFMAs and 100-185 in a K-half
+// already carrying 8 pieces and 16 fragment reads (MI355X_MICROARCH constants).  Every wait before M(u,1) is vmcnt(8):
+// K-tile u+1's last piece was issued before M(u,0)'s 8.  The prologue is PB's (K-tile 0, K-tile 1's A, vmcnt(8)).
 //
 // Stores after an epilogue (GemmArgs::store_wait): vmcnt counts stores, and retires in issue order, so the first wait
 // of the next tile - for the K-tile whose DMA M(t,1) issued just before the epilogue - also drained the whole
@@ -1494,9 +1495,12 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   // 8 NJ MFMAs on (FA, FB) with the NR fragment reads of K-half ks of buffer bo into (GA, GB) and, with DMA, the NR
   // glds of the stream's next K-tile spread evenly between them.  The switches are compile-time (runtime-predicated
   // asm register writes make the allocator spill the fragments); first_c: the tile's first MFMAs start from zero.
+  // dm_c: 0 no DMA; 1 the stream K-tile's A pieces and, with dmab, its B pieces, then advance; 2 (R3) its A pieces
+  // only, spread over the NR work items; 3 (R3) its B pieces (with dmab) spread, then advance
   auto mma = [&](const bf16x8_t(&FA)[8], const bf16x8_t(&FB)[NJ], bf16x8_t(&GA)[8], bf16x8_t(&GB)[NJ], uint32_t bo,
-                 uint32_t boB, int ks, auto first_c, auto dma_c, auto read_c, auto dmab_c) {
-    constexpr bool first = decltype(first_c)::value, dma_on = decltype(dma_c)::value;
+                 uint32_t boB, int ks, auto first_c, auto dm_c, auto read_c, auto dmab_c) {
+    constexpr bool first = decltype(first_c)::value;
+    constexpr int dm = decltype(dm_c)::value;
     constexpr bool read_on = decltype(read_c)::value, dma_b = decltype(dmab_c)::value;
     const uint32_t va = abase[ks] + bo, vb = bbase[ks] + boB;
     char* dbuf = smem + aslot(st_q);
@@ -1520,24 +1524,22 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
         if (rr < 8) DS_READ_B128(GA[rr], va, rr * 2048);
         else DS_READ_B128(GB[rr - 8], vb, (rr - 8) * 2048);
       }
-      if constexpr (dma_on) {
-        if (rr < 8 || dma_b) dma_item(rr, dbuf, kba, kb);   // rr is a compile-time index of the unrolled loop
+      // rr is a compile-time index of the unrolled loop; spread pieces: piece floor(rr n / NR) at the rr where it steps
+      if constexpr (dm == 1) {
+        if (rr < 8 || dma_b) dma_item(rr, dbuf, kba, kb);
+      } else if constexpr (dm == 2) {
+        if ((rr * 8) % NR < 8) dma_item(rr * 8 / NR, dbuf, kba, kb);
+      } else if constexpr (dm == 3) {
+        if (dma_b && (rr * NB) % NR < NB) dma_item(8 + rr * NB / NR, dbuf, kba, kb);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (dma_on) advance_stage();
+    if constexpr (dm == 1 || dm == 3) advance_stage();
   };
 
-  // prologue: K-tiles 0 and 1 (R3: 0, 1 and 2) in flight, K-tile 0 landed and visible, its K-half 0 fragments in X
+  // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed and visible, its K-half 0 fragments in X
   stage_all(std::true_type{});
-  if constexpr (R3) {
-    // PB: total >= nk >= 2; past the end the stream re-stages its last K-tile into slots nobody reads again
-    stage_all(std::false_type{});   // K-tile 1 (odd): A only
-    stage_all(std::true_type{});    // K-tile 2 (even): A and pair 1's B
-    if constexpr (NB == 8) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");         // K-tiles 1 and 2: 8 + 16
-    else if constexpr (NB == 7) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");    // 8 + 15
-    else asm volatile("s_waitcnt vmcnt(22)" ::: "memory");                          // 8 + 14
-  } else if (total > 1) {
+  if (total > 1) {
     stage_all(std::integral_constant<bool, !PB>{});
     if constexpr (PB) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-tile 1 staged its 8 A blocks only
     else if constexpr (NR == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -1581,16 +1583,17 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     const uint32_t boB = PB ? ((t >> 1) & 1) * BSTRIDE : bo, bnB = PB ? (((t + 1) >> 1) & 1) * BSTRIDE : bn;
     // M(t,0) on X, K-half 1 of K-tile t -> Y
     __builtin_amdgcn_sched_barrier(0);
-    if (kt == 0) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, std::false_type{}, std::true_type{}, dmab_c);
-    else mma(XA, XB, YA, YB, bo, boB, 1, std::false_type{}, std::false_type{}, std::true_type{}, dmab_c);
+    using DM0 = std::integral_constant<int, R3 ? 2 : 0>;   // R3: K-tile t+2's A pieces
+    if (kt == 0) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, DM0{}, std::true_type{}, dmab_c);
+    else mma(XA, XB, YA, YB, bo, boB, 1, std::false_type{}, DM0{}, std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < total) {
-      // R3: K-tile t+1 landed; K-tile t+2 (staged in M(t-1,1): A + B when t is even - then this ktile stages an odd
-      // one, dmab off - A only when t is odd) may stay in flight.  After a full tile's epilogue its last TS stores
-      // may too (they were issued after M(t-1,1)'s DMA).
-      constexpr int N0 = R3 ? (decltype(dmab_c)::value ? 8 : 8 + NB) : 0;
+      // K-tile t+1 landed (R3: K-tile t+2's 8 A pieces, issued in M(t,0), may stay in flight).  After a full tile's
+      // epilogue its last TS stores may too (issued after M(t-1,1)'s DMA; with R3 they precede M(t,0)'s, so R3 waits
+      // for them)
+      constexpr int N0 = R3 ? 8 : 0;
       constexpr int TS = epi_tail_stores<EPI, BN>();
-      if constexpr (TS > 0) {
+      if constexpr (TS > 0 && !R3) {
         if (kt == 0 && epi_full) wait_vm_lgkm0<N0 + TS>();
         else wait_vm_lgkm0<N0>();
       } else {
@@ -1601,10 +1604,12 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // M(t,1) on Y, K-tile t+2 (R3: t+3) -> buffer t & 1 (R3: slot t mod 3), K-half 0 of K-tile t+1 -> X.  Unconditional: past the end of the
-    // stream the DMA re-reads the last K-tile into a buffer nobody reads again and X gets values nobody consumes.
+    // M(t,1) on Y, K-tile t+2 -> buffer t & 1 (R3: its B pieces), K-half 0 of K-tile t+1 -> X.  Unconditional: past
+    // the end of the stream the DMA re-reads the last K-tile into a buffer nobody reads again and X gets values nobody
+    // consumes.
     // (A runtime switch between read / no-read copies of this loop makes the allocator spill the fragments.)
-    mma(YA, YB, XA, XB, bn, bnB, 0, std::false_type{}, std::true_type{}, std::true_type{}, dmab_c);
+    mma(YA, YB, XA, XB, bn, bnB, 0, std::false_type{}, std::integral_constant<int, R3 ? 3 : 1>{}, std::true_type{},
+        dmab_c);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ++kt;
@@ -1694,10 +1699,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   };
 #pragma unroll 1
   for (int t = 0; t < total; t += PB ? 2 : 1) {
-    if constexpr (R3) {
-      ktile(t, std::false_type{}, std::false_type{});      // M(t,1) stages K-tile t+3 (odd): A only
-      ktile(t + 1, std::true_type{}, std::true_type{});    // M(t+1,1) stages K-tile t+4 (even): A and the pair's B
-    } else if constexpr (PB) {
+    if constexpr (PB) {   // (R3: M(t,0) / M(t,1) stage K-tile t+2's A / B, M(t+1,0) K-tile t+3's A)
       ktile(t, std::true_type{}, std::false_type{});       // M(t,1) stages K-tile t+2 (even): A and the pair's B
       ktile(t + 1, std::false_type{}, std::true_type{});   // M(t+1,1) stages K-tile t+3 (odd): A only
     } else {
@@ -1732,6 +1734,12 @@ static int launch_cfg(const GemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// four-wave tile walk forced for every GEMM (A/B measurements): EDGE_GEMM_WALK=0 / 1, unset or -1 = by GEMM
+static int g_walk_override = [] {
+  const char* e = getenv("EDGE_GEMM_WALK");
+  return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : -1;
+}();
+
 // GemmArgs::store_wait for the four-wave kernels: EDGE_GEMM_STORE_WAIT (1 / 0) or edge_gemm_set_store_wait
 static int g_store_wait = -1;
 static int store_wait() {
@@ -1746,7 +1754,7 @@ static int store_wait() {
 template <int EPI, int RH, int BN, bool PB, bool R3 = false>
 static int launch_4w_pb(const GemmArgs& args, hipStream_t st, int walk) {
   GemmArgs a = args;
-  a.walk = walk;
+  a.walk = g_walk_override >= 0 ? g_walk_override : walk;
   a.store_wait = store_wait();
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   const int grid = std::min(tiles, num_cus());
@@ -1762,20 +1770,22 @@ static int launch_4w_pb(const GemmArgs& args, hipStream_t st, int walk) {
 }
 
 // the three-slot A ring of the paired-B four-wave kernels (gemm_4w_kernel R3): EDGE_GEMM_RING=1 or edge_gemm_set_ring
+// 0 off, 1 every paired-B GEMM, 2 the 256x224 tiles only (O-projection / down; the default: +0.5-0.7 % on the fp32
+// bench, same box, where all-on gave +0.2-0.3 % and all-but-QKV 0 - docs/RESULTS.md section 6), 3 the 224 and 256 tiles
 static int g_ring = -1;
-static bool use_ring() {
+static bool use_ring(int bn) {
   if (g_ring < 0) {
     const char* e = getenv("EDGE_GEMM_RING");
-    g_ring = (e && e[0] && e[0] != '0') ? 1 : 0;
+    g_ring = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
   }
-  return g_ring == 1;
+  return g_ring == 1 || (g_ring == 2 && bn == 224) || (g_ring == 3 && bn != 192);
 }
 
 template <int EPI, int RH, int BN = 256>
 static int launch_4w(const GemmArgs& a, hipStream_t st, int walk = 0) {
   if constexpr (epi_f32(EPI)) {
     if (a.pairb) {
-      if (use_ring()) return launch_4w_pb<EPI, RH, BN, true, true>(a, st, walk);
+      if (use_ring(BN)) return launch_4w_pb<EPI, RH, BN, true, true>(a, st, walk);
       return launch_4w_pb<EPI, RH, BN, true>(a, st, walk);
     }
   }
@@ -1836,7 +1846,8 @@ EDGE_API int edge_gemm_set_tile(int t) {
   return 0;
 }
 
-// 1: the paired-B h3 GEMMs run the three-slot A ring (gemm_4w_kernel R3), 0: two buffers; -1: from EDGE_GEMM_RING
+// the paired-B h3 GEMMs on the three-slot A ring (gemm_4w_kernel R3): 1 all, 2 the 224-wide tiles, 3 the 224- and
+// 256-wide tiles, 0 none (two buffers); -1: from EDGE_GEMM_RING
 EDGE_API int edge_gemm_set_ring(int on) {
   g_ring = on;
   return 0;

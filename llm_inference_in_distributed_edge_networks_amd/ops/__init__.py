@@ -167,8 +167,9 @@ def set_gemm_tile(tile: int) -> None:
 
 
 def set_gemm_ring(on: int) -> None:
-    """The paired-B h3 (fp32-mode) GEMMs on the three-slot A ring (gemm_4w_kernel R3: the DMA three K-tiles ahead):
-    1 on, 0 off, -1 from EDGE_GEMM_RING (default off)."""
+    """The paired-B h3 (fp32-mode) GEMMs on the three-slot A ring (gemm_4w_kernel R3: each K-tile's LDS DMA spread over
+    both K-halves): 1 every paired-B GEMM, 2 the 256x224 tiles only (O-projection / down), 3 the 224- and 256-wide
+    tiles (not the QKV), 0 none, -1 from EDGE_GEMM_RING (default 2)."""
     call("edge_gemm_set_ring", int(on))
 
 
