@@ -16,6 +16,7 @@
 #include "common.h"
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_RESID = 2, EPI_BIAS_RESID = 3, EPI_BIAS_GELU = 4, EPI_SWIGLU = 5,
        EPI_QKV_ROPE = 6, EPI_LSE = 7,
@@ -1373,6 +1374,10 @@ __device__ __forceinline__ void w4_f32_epilogue_224(const GemmArgs& a, f32x4_t (
 // instead of 0 and 8+NB: an LDS-DMA piece costs its wave ~60 issue cycles among bare MFMAs and 100-185 in a K-half
 // already carrying 8 pieces and 16 fragment reads (MI355X_MICROARCH constants).  Every wait before M(u,1) is vmcnt(8):
 // K-tile u+1's last piece was issued before M(u,0)'s 8.  The prologue is PB's (K-tile 0, K-tile 1's A, vmcnt(8)).
+// RING: 0 the two buffers, 1 R3, 2 the two buffers with the B pieces spread (PB): the B region of pair t/2 + 1 (t
+// even) is pair t/2 - 1's, last read in M(t-1,0), so M(t,0) stages K-tile t+2's NB B pieces and M(t,1) its 8 A pieces
+// (per K-half NB, 8, 0, 8 instead of 0, 8+NB, 0, 8; no extra LDS); the wait before M(t,1) is vmcnt(NB), before
+// M(t+1,1) vmcnt(0).
 //
 // Stores after an epilogue (GemmArgs::store_wait): vmcnt counts stores, and retires in issue order, so the first wait
 // of the next tile - for the K-tile whose DMA M(t,1) issued just before the epilogue - also drained the whole
@@ -1394,10 +1399,11 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
 }
 
-template <int EPI, int RH, int BN, bool PB = false, bool R3 = false>
+template <int EPI, int RH, int BN, bool PB = false, int RING = 0>
 __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   static_assert(!PB || epi_f32(EPI), "paired B: h3 GEMMs");
-  static_assert(!R3 || PB, "the A-slot ring: paired-B GEMMs");
+  static_assert(RING == 0 || PB, "spread DMA schedules: paired-B GEMMs");
+  constexpr bool R3 = RING == 1, SP2 = RING == 2;
   static_assert(BN != 192 || ((EPI == EPI_F32_QKV_ROPE || EPI == EPI_QKV_ROPE) && (RH == 0 || RH == 32)),
                 "192-wide tiles: QKV only");
   static_assert(BN == 192 || BN == 224 || BN == 256, "tile width");
@@ -1496,7 +1502,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
   // glds of the stream's next K-tile spread evenly between them.  The switches are compile-time (runtime-predicated
   // asm register writes make the allocator spill the fragments); first_c: the tile's first MFMAs start from zero.
   // dm_c: 0 no DMA; 1 the stream K-tile's A pieces and, with dmab, its B pieces, then advance; 2 (R3) its A pieces
-  // only, spread over the NR work items; 3 (R3) its B pieces (with dmab) spread, then advance
+  // only, spread over the NR work items; 3 (R3) its B pieces (with dmab) spread, then advance; 4 (SP2) its B pieces
+  // (with dmab) spread; 5 (SP2) its A pieces spread, then advance
   auto mma = [&](const bf16x8_t(&FA)[8], const bf16x8_t(&FB)[NJ], bf16x8_t(&GA)[8], bf16x8_t(&GB)[NJ], uint32_t bo,
                  uint32_t boB, int ks, auto first_c, auto dm_c, auto read_c, auto dmab_c) {
     constexpr bool first = decltype(first_c)::value;
@@ -1527,14 +1534,14 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       // rr is a compile-time index of the unrolled loop; spread pieces: piece floor(rr n / NR) at the rr where it steps
       if constexpr (dm == 1) {
         if (rr < 8 || dma_b) dma_item(rr, dbuf, kba, kb);
-      } else if constexpr (dm == 2) {
+      } else if constexpr (dm == 2 || dm == 5) {
         if ((rr * 8) % NR < 8) dma_item(rr * 8 / NR, dbuf, kba, kb);
-      } else if constexpr (dm == 3) {
+      } else if constexpr (dm == 3 || dm == 4) {
         if (dma_b && (rr * NB) % NR < NB) dma_item(8 + rr * NB / NR, dbuf, kba, kb);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (dm == 1 || dm == 3) advance_stage();
+    if constexpr (dm == 1 || dm == 3 || dm == 5) advance_stage();
   };
 
   // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed and visible, its K-half 0 fragments in X
@@ -1583,7 +1590,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     const uint32_t boB = PB ? ((t >> 1) & 1) * BSTRIDE : bo, bnB = PB ? (((t + 1) >> 1) & 1) * BSTRIDE : bn;
     // M(t,0) on X, K-half 1 of K-tile t -> Y
     __builtin_amdgcn_sched_barrier(0);
-    using DM0 = std::integral_constant<int, R3 ? 2 : 0>;   // R3: K-tile t+2's A pieces
+    // R3: K-tile t+2's A pieces; SP2: its B pieces (t even)
+    using DM0 = std::integral_constant<int, R3 ? 2 : (SP2 && decltype(dmab_c)::value) ? 4 : 0>;
     if (kt == 0) mma(XA, XB, YA, YB, bo, boB, 1, std::true_type{}, DM0{}, std::true_type{}, dmab_c);
     else mma(XA, XB, YA, YB, bo, boB, 1, std::false_type{}, DM0{}, std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
@@ -1591,9 +1599,9 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
       // K-tile t+1 landed (R3: K-tile t+2's 8 A pieces, issued in M(t,0), may stay in flight).  After a full tile's
       // epilogue its last TS stores may too (issued after M(t-1,1)'s DMA; with R3 they precede M(t,0)'s, so R3 waits
       // for them)
-      constexpr int N0 = R3 ? 8 : 0;
+      constexpr int N0 = R3 ? 8 : (SP2 && decltype(dmab_c)::value) ? NB : 0;   // SP2: M(t,0)'s B pieces
       constexpr int TS = epi_tail_stores<EPI, BN>();
-      if constexpr (TS > 0 && !R3) {
+      if constexpr (TS > 0 && RING == 0) {
         if (kt == 0 && epi_full) wait_vm_lgkm0<N0 + TS>();
         else wait_vm_lgkm0<N0>();
       } else {
@@ -1602,14 +1610,23 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
     } else {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    if constexpr ((BN == 256 || BN == 192) && (RING == 0 || (SP2 && !decltype(dmab_c)::value))) {
+      // The row scales load_rs issued at the tile's start are older than the DMA the wait above leaves in flight, so
+      // they have landed: hand them to the compiler as fresh values on every path here.  Otherwise its own wait for
+      // them sits at their first use in the epilogue, as vmcnt(0), and also drains the DMA issued just before it.
+      // (The compiler puts its own vmcnt(0) before these asm statements on the first K-tile after load_rs: only where
+      // the wait above is vmcnt(0) anyway - two buffers, SP2's odd K-tiles; with store_wait it voids vmcnt(TS).)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(rs[i]));
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     // M(t,1) on Y, K-tile t+2 -> buffer t & 1 (R3: its B pieces), K-half 0 of K-tile t+1 -> X.  Unconditional: past
     // the end of the stream the DMA re-reads the last K-tile into a buffer nobody reads again and X gets values nobody
     // consumes.
     // (A runtime switch between read / no-read copies of this loop makes the allocator spill the fragments.)
-    mma(YA, YB, XA, XB, bn, bnB, 0, std::false_type{}, std::integral_constant<int, R3 ? 3 : 1>{}, std::true_type{},
-        dmab_c);
+    mma(YA, YB, XA, XB, bn, bnB, 0, std::false_type{}, std::integral_constant<int, R3 ? 3 : SP2 ? 5 : 1>{},
+        std::true_type{}, dmab_c);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ++kt;
@@ -1751,41 +1768,46 @@ static int store_wait() {
 }
 
 // the persistent four-wave kernel: one workgroup per CU walks its tiles (walk 0 strided, 1 XCD-chunked)
-template <int EPI, int RH, int BN, bool PB, bool R3 = false>
+template <int EPI, int RH, int BN, bool PB, int RING = 0>
 static int launch_4w_pb(const GemmArgs& args, hipStream_t st, int walk) {
   GemmArgs a = args;
   a.walk = g_walk_override >= 0 ? g_walk_override : walk;
   a.store_wait = store_wait();
   const int tiles = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN);
   const int grid = std::min(tiles, num_cus());
-  constexpr int lds = R3 ? w4::Geo<BN>::LDS_R3 : w4::Geo<BN>::LDS;
+  constexpr int lds = RING == 1 ? w4::Geo<BN>::LDS_R3 : w4::Geo<BN>::LDS;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, BN, PB, R3>,
+    (void)hipFuncSetAttribute((const void*)gemm_4w_kernel<EPI, RH, BN, PB, RING>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, BN, PB, R3>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((gemm_4w_kernel<EPI, RH, BN, PB, RING>), dim3(grid), dim3(256), lds, st, a);
   return (int)hipGetLastError();
 }
 
-// the three-slot A ring of the paired-B four-wave kernels (gemm_4w_kernel R3): EDGE_GEMM_RING=1 or edge_gemm_set_ring
-// 0 off, 1 every paired-B GEMM, 2 the 256x224 tiles only (O-projection / down; the default: +0.5-0.7 % on the fp32
-// bench, same box, where all-on gave +0.2-0.3 % and all-but-QKV 0 - docs/RESULTS.md section 6), 3 the 224 and 256 tiles
+// DMA schedule of the paired-B four-wave kernels per tile width (gemm_4w_kernel RING): three decimal digits for the
+// 192- (QKV), 224- (O-projection / down) and 256-wide (gate/up, LM head) tiles, each 0 two buffers, 1 the three-slot
+// ring (R3), 2 the two buffers with B spread (SP2).  EDGE_GEMM_RING or edge_gemm_set_ring; default 022 (SP2 on the
+// O-projection / down and gate/up GEMMs: +1.0-1.2 % on the fp32 bench against 010, same box, 3 of 3 rounds; 010 was
+// +0.5-0.7 % against 000; the QKV stays on two plain buffers - docs/RESULTS.md section 6)
 static int g_ring = -1;
-static bool use_ring(int bn) {
+static int ring_mode(int bn) {
   if (g_ring < 0) {
     const char* e = getenv("EDGE_GEMM_RING");
-    g_ring = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
+    g_ring = 22;
+    if (e && strlen(e) == 3 && strspn(e, "012") == 3) g_ring = atoi(e);
   }
-  return g_ring == 1 || (g_ring == 2 && bn == 224) || (g_ring == 3 && bn != 192);
+  return (bn == 192 ? g_ring / 100 : bn == 224 ? g_ring / 10 : g_ring) % 10;
 }
 
 template <int EPI, int RH, int BN = 256>
 static int launch_4w(const GemmArgs& a, hipStream_t st, int walk = 0) {
   if constexpr (epi_f32(EPI)) {
     if (a.pairb) {
-      if (use_ring(BN)) return launch_4w_pb<EPI, RH, BN, true, true>(a, st, walk);
+      const int r = ring_mode(BN);
+      if (r == 1) return launch_4w_pb<EPI, RH, BN, true, 1>(a, st, walk);
+      if (r == 2) return launch_4w_pb<EPI, RH, BN, true, 2>(a, st, walk);
       return launch_4w_pb<EPI, RH, BN, true>(a, st, walk);
     }
   }
@@ -1846,10 +1868,11 @@ EDGE_API int edge_gemm_set_tile(int t) {
   return 0;
 }
 
-// the paired-B h3 GEMMs on the three-slot A ring (gemm_4w_kernel R3): 1 all, 2 the 224-wide tiles, 3 the 224- and
-// 256-wide tiles, 0 none (two buffers); -1: from EDGE_GEMM_RING
-EDGE_API int edge_gemm_set_ring(int on) {
-  g_ring = on;
+// the paired-B GEMMs' DMA schedules (ring_mode): code = 100 x (192 tiles) + 10 x (224) + (256), digits 0 / 1 / 2;
+// -1: from EDGE_GEMM_RING
+EDGE_API int edge_gemm_set_ring(int code) {
+  const bool ok = code >= 0 && code / 100 <= 2 && code / 10 % 10 <= 2 && code % 10 <= 2;
+  g_ring = ok ? code : -1;
   return 0;
 }
 

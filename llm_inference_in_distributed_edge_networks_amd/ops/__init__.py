@@ -166,11 +166,12 @@ def set_gemm_tile(tile: int) -> None:
     call("edge_gemm_set_tile", int(tile))
 
 
-def set_gemm_ring(on: int) -> None:
-    """The paired-B h3 (fp32-mode) GEMMs on the three-slot A ring (gemm_4w_kernel R3: each K-tile's LDS DMA spread over
-    both K-halves): 1 every paired-B GEMM, 2 the 256x224 tiles only (O-projection / down), 3 the 224- and 256-wide
-    tiles (not the QKV), 0 none, -1 from EDGE_GEMM_RING (default 2)."""
-    call("edge_gemm_set_ring", int(on))
+def set_gemm_ring(code: int) -> None:
+    """DMA schedule of the paired-B h3 (fp32-mode) four-wave GEMMs per tile width: code = 100 x (192-wide QKV tiles)
+    + 10 x (224-wide O-projection / down tiles) + (256-wide gate/up / LM-head tiles), each digit 0 two LDS buffers,
+    1 the three-slot A ring (a K-tile's A and B pieces in different K-halves), 2 two buffers with the B pieces staged
+    a K-half early; -1 from EDGE_GEMM_RING (three digits, default 022)."""
+    call("edge_gemm_set_ring", int(code))
 
 
 def set_gemm_store_wait(on: int) -> None:

@@ -575,7 +575,7 @@ def test_linear_h3_four_wave_224(M, N, K):
     (32768, 896, 896, "resid", 0), (32768, 896, 4864, "resid", 0), (4096, 9728, 896, "swiglu", 0),
     (1000, 9728, 896, "swiglu", 256), (257, 896, 896, "resid", 224), (700, 512, 2048, "bias_resid", 256),
     (300, 512, 128, "none", 256), (5000, 896, 128, "resid", 224)])
-@pytest.mark.parametrize("knob", ["ring", "store_wait", "ring+store_wait"])
+@pytest.mark.parametrize("knob", ["ring", "spread2", "store_wait", "ring+store_wait"])
 def test_linear_h3_ring_bit_identical(M, N, K, epi, tile, knob):
     """The paired-B h3 GEMMs on the three-slot A ring (DMA three K-tiles ahead, opt-in) and / or with a full tile's
     last epilogue stores left in flight across the next tile's first wait equal the default kernel bit for bit: same
@@ -602,13 +602,13 @@ def test_linear_h3_ring_bit_identical(M, N, K, epi, tile, knob):
 
 
 def _knob(knob: str, on: int) -> None:
-    if "ring" in knob:
-        ops.set_gemm_ring(on)
-    if "store_wait" in knob:
-        ops.set_gemm_store_wait(on)
+    """on: 1 the variant, 0 the two-buffer kernels with draining waits, -1 the defaults."""
+    ring = {"ring": 111, "ring+store_wait": 111, "spread2": 222}.get(knob)
+    ops.set_gemm_ring(-1 if on < 0 else ring * on if ring else 0)
+    ops.set_gemm_store_wait(on if "store_wait" in knob else (-1 if on < 0 else 0))
 
 
-@pytest.mark.parametrize("knob", ["ring", "store_wait"])
+@pytest.mark.parametrize("knob", ["ring", "spread2", "store_wait"])
 def test_full_model_ring_identical(knob):
     """Qwen2-0.5B fp32 mode (QKV, O-proj, gate/up, down and the LSE head all paired-B): the three-slot A ring / the
     store-tolerant post-epilogue wait equal the default kernels bit for bit on the final hidden state and row NLL."""

@@ -18,7 +18,7 @@ from __future__ import annotations
 import re
 import sys
 
-FUNC = re.compile(r"^(_Z14gemm_4w_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb([01])E(?:Lb([01])E)?Ev8GemmArgs):")
+FUNC = re.compile(r"^(_Z14gemm_4w_kernelILi(\d+)ELi(\d+)ELi(\d+)ELb([01])E(?:L[bi](\d)E)?Ev8GemmArgs):")
 VM = re.compile(r"^\s*(global|buffer|scratch|flat)_\w+")
 WAIT = re.compile(r"^\s*s_waitcnt\s+.*vmcnt\((\d+)\)")
 
