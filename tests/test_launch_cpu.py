@@ -88,6 +88,7 @@ def test_bench_contract_cpu(n):
         # the reference's own workload (the notebook sweep) timed beside the headline
         sw = d["notebook_sweep"]
         assert sw["windows"] == 64 and sw["configs_per_window"] == 4 * 2 * 5 and sw["windows_per_s"] > 0
+        assert len(sw["pass_seconds"]) == 3 and sw["seconds"] == sorted(sw["pass_seconds"])[1]
         assert d["sweep_speedup_vs_t4"] == round(16.19 / sw["s_per_window"], 1)
 
 
