@@ -1112,18 +1112,24 @@ __device__ __forceinline__ int q192_feat(int col) {   // tile column (permuted o
 
 // c: the virtual wave vw's 64 x 96 slab (rows m0 + vw 64 + i 16 + (lane & 15), columns nw + j 16 + 4 g + r); RH = 32
 // (full 64-dim rotary: pair offset 32) or 0 (no rotary)
+// bias of the wave's 96 columns (permuted order), loaded once per tile for both 64-row halves: the second half's
+// reload came after the first half's stores, and waiting for it drained them (bench-shape probe 158.5-161.9 us against
+// 162.5-165.8, same box; docs/RESULTS.md section 6)
+__device__ __forceinline__ void qkv192_bias(const GemmArgs& a, int n0, int lane, int wn, f32x4_t (&bw)[6]) {
+  const int nw = n0 + wn * 96;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) bw[j] = *(const f32x4_t*)(a.biasf + q192_feat(nw + j * 16) + (lane >> 4) * 4);
+}
+
 template <int RH>
-__device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[4][6], int m0, int n0, int lane,
-                                                int vw, int wn) {
+__device__ __forceinline__ void qkv192_epilogue(const GemmArgs& a, f32x4_t (&c)[4][6], const f32x4_t (&bw)[6], int m0,
+                                                int n0, int lane, int vw, int wn) {
   static_assert(RH == 0 || RH == 32, "192-wide QKV tiles: full rotary or none");
   const int g = lane >> 4;
   const int nw = n0 + wn * 96;
-  // every global load of the epilogue (bias, the RoPE tables of all four row groups for both low-half dim groups
-  // 4g and 16 + 4g) is issued before the first store: vmcnt counts stores too, so a load waited between two
-  // groups' stores would drain them
-  f32x4_t bw[6];
-#pragma unroll
-  for (int j = 0; j < 6; ++j) bw[j] = *(const f32x4_t*)(a.biasf + q192_feat(nw + j * 16) + g * 4);
+  // every global load of the epilogue (bias - by the caller, before the first half - and the RoPE tables of all four
+  // row groups for both low-half dim groups 4g and 16 + 4g) is issued before the first store: vmcnt counts stores
+  // too, so a load waited between two groups' stores would drain them
   int bi[4], pi[4];
   f32x4_t cs[4][2], sn[4][2];
 #pragma unroll
@@ -1661,6 +1667,8 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
           __builtin_amdgcn_sched_barrier(0);
         }
       } else if constexpr (BN == 192) {
+        f32x4_t bw[6];
+        if constexpr (EPI != EPI_QKV_ROPE) qkv192_bias(a, n0, lane, wn, bw);
 #pragma unroll
         for (int ih = 0; ih < 2; ++ih) {   // 64 x 96 halves
           f32x4_t c[4][6];
@@ -1675,7 +1683,7 @@ __global__ __launch_bounds__(256, 1) void gemm_4w_kernel(GemmArgs a) {
             const float rq[4] = {rs[ih * 4], rs[ih * 4 + 1], rs[ih * 4 + 2], rs[ih * 4 + 3]};
             qkv192_bf16_epilogue<RH>(a, c, rq, m0, n0, lane, wm * 2 + ih, wn);
           } else {
-            qkv192_epilogue<RH>(a, c, m0, n0, lane, wm * 2 + ih, wn);
+            qkv192_epilogue<RH>(a, c, bw, m0, n0, lane, wm * 2 + ih, wn);
           }
           __builtin_amdgcn_sched_barrier(0);
         }

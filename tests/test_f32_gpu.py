@@ -328,6 +328,33 @@ def test_qkv_kv_planes(B, S, Hq, Hkv, rot, tile):
     assert torch.equal(v, vt2[..., :S].transpose(-1, -2))   # V row-major (AttnLRP), the same values as V^T
 
 
+@pytest.mark.parametrize("B,S,rot", [(2, 512, 64), (3, 98, 64), (64, 512, 64), (3, 200, 0)])
+def test_qkv_planes_only(B, S, rot):
+    """The planes-only QKV of the model's layers (need_k=False: q + K / V^T planes, no fp32 K / V^T / V rows) on the
+    256x192 tiles: q and the planes equal the need_k=True call's bit for bit (partial row tiles, S % 4 != 0, no
+    rotary).  (A separate planes-only instantiation with the unused outputs compiled out was measured 2-4 % slower on
+    the bench-shape probe than this one and removed: docs/RESULTS.md section 6.)"""
+    Hq, Hkv, H = 14, 2, 896
+    Nq = (Hq + 2 * Hkv) * 64
+    x = rnd(B * S, H, seed=36)
+    w = rnd(Nq, H, s=1 / math.sqrt(H), seed=37).to(torch.bfloat16).float()
+    b = rnd(Nq, s=0.1, seed=38)
+    cos, sin = R.rope_tables(4096, max(rot, 2), 1e6)
+    sx = R.h3_scale(x.abs().max().item())
+    w3, sw = R.h3_weight(w)
+    args = (R.h3_act(x, sx).to(DEV), w3.to(DEV), 1.0 / (sx * sw), b.to(DEV), cos.to(DEV), sin.to(DEV), B, S, Hq, Hkv,
+            64, rot, 0.125)
+    try:
+        ops.set_gemm_tile(192)
+        q1, k1, _, kp1, vp1 = ops.qkv_rope_h3(*args, kv_scales=(2.0 ** 9, 2.0 ** 11), need_k=True)
+        q2, k2, _, kp2, vp2 = ops.qkv_rope_h3(*args, kv_scales=(2.0 ** 9, 2.0 ** 11), need_k=False)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_gemm_tile(0)
+    assert k1 is not None and k2 is None
+    assert torch.equal(q1, q2) and torch.equal(kp1, kp2) and torch.equal(vp1, vp2)
+
+
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 14, 2), (3, 100, 14, 2), (1, 2048, 8, 8), (2, 64, 4, 1),
                                          (2, 200, 14, 2)])
 @pytest.mark.parametrize("h3", [False, True])

@@ -34,7 +34,9 @@ def main():
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--S", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--kv-planes", type=int, default=0, help="attn: stage K / V^T h3 planes by LDS DMA")
+    ap.add_argument("--kv-planes", type=int, default=0,
+                    help="attn: stage K / V^T h3 planes by LDS DMA; qkv: 1 emit the planes too, 2 the planes without "
+                         "the fp32 K (the model's layers without importance statistics)")
     ap.add_argument("--save", default="", help="save the op's output tensors here (bit-exact A/B of two builds)")
     ap.add_argument("--compare", default="", help="compare the op's output bit for bit with a --save file")
     ap.add_argument("--tile", type=int, default=0, help="force the GEMM tile (ops.set_gemm_tile; 0 = by shape)")
@@ -68,8 +70,9 @@ def main():
         cos, sin = R.rope_tables(4096, 64, 1e6)
         cos, sin, w3 = cos.to(dev), sin.to(dev), w3.to(dev)
         kvs = (2.0 ** 6, 2.0 ** 6) if a.kv_planes else None   # the K / V^T planes the attention stages by DMA
+        # --kv-planes 2: planes only, no fp32 K (the model's layers that compute no importance statistics)
         fn = lambda: ops.qkv_rope_h3(x3, w3, 1.0 / (2.0 ** 10 * sw), bias, cos, sin, B, S, Hq, Hkv, 64, 64,  # noqa
-                                     0.125, kv_scales=kvs)
+                                     0.125, kv_scales=kvs, need_k=a.kv_planes != 2)
     elif a.op in ("gateup_lib", "down_lib"):   # the two-product K' = 2K as one plain fp16 GEMM
         K, N = (H, 9728) if a.op == "gateup_lib" else (4864, H)
         x = torch.randn(B * S, 2 * K, generator=g).half().to(dev)
